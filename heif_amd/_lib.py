@@ -1,0 +1,123 @@
+"""ctypes binding of include/heifgpu.h (libheifgpu.so, built in-tree).
+
+The product path has no CPU fallback: if the HIP library is missing this
+module raises at import time.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libheifgpu.so"
+
+HEIFGPU_OK = 0
+HEIFGPU_E_INVALID = -1
+HEIFGPU_E_PARSE = -2
+HEIFGPU_E_UNSUPPORTED = -3
+HEIFGPU_E_DEVICE = -4
+HEIFGPU_E_DECODE = -5
+
+STATUS_BITS = {
+    1 << 0: "cabac_init",
+    1 << 1: "substream_end",
+    1 << 2: "overrun",
+    1 << 3: "syntax",
+    1 << 4: "unsupported",
+    1 << 5: "capacity",
+}
+
+
+class ImageInfo(ctypes.Structure):
+    _fields_ = [
+        (name, ctypes.c_uint32)
+        for name in (
+            "width", "height", "chroma_format_idc", "bit_depth", "bytes_per_sample", "grid_rows",
+            "grid_cols", "tile_width", "tile_height", "num_tiles", "rotation", "ispe_width",
+            "ispe_height", "coded_bytes", "primary_item_id", "num_thumbnails", "matrix_coeffs",
+            "full_range",
+        )
+    ]
+
+
+class Planes(ctypes.Structure):
+    _fields_ = [("plane", ctypes.c_void_p * 3), ("pitch", ctypes.c_int32 * 3)]
+
+
+# every symbol include/heifgpu.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "heifgpu_image_parse", "heifgpu_image_get_info", "heifgpu_image_free", "heifgpu_create",
+    "heifgpu_destroy", "heifgpu_last_error", "heifgpu_batch_prepare", "heifgpu_batch_decode",
+    "heifgpu_batch_status", "heifgpu_batch_free", "heifgpu_set_timing", "heifgpu_stage_times",
+    "heifgpu_decode_batch", "heifgpu_remove_emulation_prevention", "heifgpu_read_ue",
+    "heifgpu_read_se", "heifgpu_bins_truncated_rice", "heifgpu_bins_chroma_pred_mode",
+    "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb",
+)
+
+
+class HeifGpuError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"heifgpu error {code}: {msg}")
+        self.code = code
+
+
+class UnsupportedError(HeifGpuError):
+    pass
+
+
+def _load() -> ctypes.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(there is no CPU fallback on the product path)"
+        )
+    lib = ctypes.CDLL(str(LIB_PATH), mode=os.RTLD_LOCAL)
+    P, VP, SZ, I32, U32 = ctypes.POINTER, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32
+    u8p = P(ctypes.c_uint8)
+    sig = {
+        "heifgpu_image_parse": (I32, [u8p, SZ, P(VP)]),
+        "heifgpu_image_get_info": (I32, [VP, P(ImageInfo)]),
+        "heifgpu_image_free": (None, [VP]),
+        "heifgpu_create": (I32, [I32, P(VP)]),
+        "heifgpu_destroy": (None, [VP]),
+        "heifgpu_last_error": (ctypes.c_char_p, []),
+        "heifgpu_batch_prepare": (I32, [VP, P(VP), SZ, P(VP)]),
+        "heifgpu_batch_decode": (I32, [VP, VP, P(Planes), VP]),
+        "heifgpu_batch_status": (I32, [VP, VP, P(U32), VP]),
+        "heifgpu_batch_free": (None, [VP]),
+        "heifgpu_set_timing": (I32, [VP, I32]),
+        "heifgpu_stage_times": (I32, [VP, P(ctypes.c_float)]),
+        "heifgpu_decode_batch": (I32, [VP, P(VP), SZ, P(Planes), VP, P(U32)]),
+        "heifgpu_remove_emulation_prevention": (SZ, [u8p, SZ, u8p]),
+        "heifgpu_read_ue": (I32, [u8p, SZ, P(U32)]),
+        "heifgpu_read_se": (I32, [u8p, SZ, P(ctypes.c_int32)]),
+        "heifgpu_bins_truncated_rice": (I32, [u8p, I32, I32, I32, P(I32)]),
+        "heifgpu_bins_chroma_pred_mode": (I32, [u8p, I32, P(I32)]),
+        "heifgpu_bins_coeff_abs_level_remaining": (I32, [u8p, I32, I32, P(I32)]),
+        "heifgpu_bins_exp_golomb": (I32, [u8p, I32, I32, P(I32)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error() -> str:
+    return lib.heifgpu_last_error().decode(errors="replace")
+
+
+def check(rc: int) -> None:
+    if rc == HEIFGPU_OK:
+        return
+    if rc == HEIFGPU_E_UNSUPPORTED:
+        raise UnsupportedError(rc, last_error())
+    raise HeifGpuError(rc, last_error())
+
+
+def u8buf(data: bytes):
+    return (ctypes.c_uint8 * max(len(data), 1)).from_buffer_copy(data if data else b"\0")

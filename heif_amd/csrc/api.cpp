@@ -1,0 +1,405 @@
+// api.cpp — C ABI (include/heifgpu.h): host parsing, batch flattening, device
+// arenas and the five-stage launch sequence.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/heifgpu.h"
+#include "common/desc.hpp"
+#include "host/batch.hpp"
+#include "host/heic_image.hpp"
+#include "kernels/cabac.hpp"
+#include "kernels/kernels.hpp"
+
+using namespace hg;
+
+struct heifgpu_image {
+    ParsedImage img;
+};
+
+struct heifgpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    hipEvent_t ev[6] = {};
+    float stage_ms[5] = {};
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) return fail(HEIFGPU_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t alloc(size_t count) {
+        n = count;
+        return hipMalloc(reinterpret_cast<void **>(&p), std::max<size_t>(count, 1) * sizeof(T));
+    }
+};
+
+}  // namespace
+
+struct heifgpu_batch {
+    int device = 0;
+    size_t n_images = 0;
+    int n_pics = 0;
+    BatchArgs args{};
+    DevBuf<uint8_t> bits, sf, maps, recon;
+    DevBuf<PicDesc> pics;
+    DevBuf<uint32_t> subs, row_counts, status;
+    DevBuf<SeqParams> seqs;
+    DevBuf<OutImage> outs;
+    DevBuf<TuRec> tus;
+    DevBuf<Coef> coefs;
+    DevBuf<int16_t> resid;
+    DevBuf<SaoParams> sao;
+    std::vector<OutImage> out_host;
+    std::vector<uint32_t> pic_image;  // picture → image
+    std::vector<heifgpu_image_info> infos;
+};
+
+extern "C" {
+
+const char *heifgpu_last_error(void) { return g_err.c_str(); }
+
+int heifgpu_image_parse(const uint8_t *data, size_t len, heifgpu_image **out) {
+    if (!data || !out) return fail(HEIFGPU_E_INVALID, "null argument");
+    *out = nullptr;
+    try {
+        auto im = std::make_unique<heifgpu_image>();
+        im->img = parse_heic(data, len);
+        *out = im.release();
+        return HEIFGPU_OK;
+    } catch (const UnsupportedError &e) {
+        return fail(HEIFGPU_E_UNSUPPORTED, e.what());
+    } catch (const std::exception &e) {
+        return fail(HEIFGPU_E_PARSE, e.what());
+    }
+}
+
+int heifgpu_image_get_info(const heifgpu_image *img, heifgpu_image_info *info) {
+    if (!img || !info) return fail(HEIFGPU_E_INVALID, "null argument");
+    const ParsedImage &p = img->img;
+    const SequenceParameterSet &s = p.params[0].sps;
+    std::memset(info, 0, sizeof(*info));
+    info->width = p.out_width;
+    info->height = p.out_height;
+    info->chroma_format_idc = uint32_t(s.chroma_array_type());
+    info->bit_depth = uint32_t(8 + s.bit_depth_luma_minus8);
+    info->bytes_per_sample = info->bit_depth > 8 ? 2 : 1;
+    info->grid_rows = p.rows;
+    info->grid_cols = p.cols;
+    info->tile_width = p.tile_width;
+    info->tile_height = p.tile_height;
+    info->num_tiles = uint32_t(p.tiles.size());
+    info->rotation = p.rotation;
+    info->ispe_width = p.ispe_width;
+    info->ispe_height = p.ispe_height;
+    info->coded_bytes = p.coded_bytes;
+    info->primary_item_id = p.primary_item_id;
+    info->num_thumbnails = p.num_thumbnails;
+    info->matrix_coeffs = uint32_t(s.matrix_coeffs);
+    info->full_range = s.video_full_range_flag ? 1u : 0u;
+    return HEIFGPU_OK;
+}
+
+void heifgpu_image_free(heifgpu_image *img) { delete img; }
+
+int heifgpu_create(int device, heifgpu_ctx **out) {
+    if (!out) return fail(HEIFGPU_E_INVALID, "null argument");
+    *out = nullptr;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(HEIFGPU_E_DEVICE, "no such HIP device");
+    HIP_TRY(hipSetDevice(device));
+    auto c = std::make_unique<heifgpu_ctx>();
+    c->device = device;
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
+    *out = c.release();
+    return HEIFGPU_OK;
+}
+
+void heifgpu_destroy(heifgpu_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    for (auto &e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int heifgpu_set_timing(heifgpu_ctx *ctx, int enable) {
+    if (!ctx) return fail(HEIFGPU_E_INVALID, "null ctx");
+    ctx->timing = enable != 0;
+    return HEIFGPU_OK;
+}
+
+int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[5]) {
+    if (!ctx || !ms) return fail(HEIFGPU_E_INVALID, "null argument");
+    if (!ctx->timing) return fail(HEIFGPU_E_INVALID, "timing disabled");
+    HIP_TRY(hipEventSynchronize(ctx->ev[5]));
+    for (int i = 0; i < 5; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], ctx->ev[i], ctx->ev[i + 1]));
+    return HEIFGPU_OK;
+}
+
+int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, heifgpu_batch **out) {
+    if (!ctx || !imgs || !out || n == 0) return fail(HEIFGPU_E_INVALID, "invalid argument");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto b = std::make_unique<heifgpu_batch>();
+    b->device = ctx->device;
+    b->n_images = n;
+    std::vector<const ParsedImage *> parsed;
+    for (size_t i = 0; i < n; ++i) {
+        if (!imgs[i]) return fail(HEIFGPU_E_INVALID, "null image");
+        parsed.push_back(&imgs[i]->img);
+        heifgpu_image_info info;
+        heifgpu_image_get_info(imgs[i], &info);
+        b->infos.push_back(info);
+    }
+    HostBatch hb;
+    try {
+        hb = build_batch(parsed.data(), n);
+    } catch (const UnsupportedError &e) {
+        return fail(HEIFGPU_E_UNSUPPORTED, e.what());
+    } catch (const std::exception &e) {
+        return fail(HEIFGPU_E_PARSE, e.what());
+    }
+    std::vector<uint8_t> &h_bits = hb.bits;
+    std::vector<PicDesc> &h_pics = hb.pics;
+    std::vector<uint32_t> &h_subs = hb.subs;
+    std::vector<SeqParams> &h_seqs = hb.seqs;
+    std::vector<uint8_t> &h_sf = hb.sf;
+    const uint64_t recon_bytes = hb.recon_bytes, resid_elems = hb.resid_elems, map_bytes = hb.map_bytes,
+                   sao_n = hb.sao_n, tu_n = hb.tu_n, coef_n = hb.coef_n;
+    const uint32_t rows = hb.rows;
+    const int max_w = hb.max_w, max_wctb = hb.max_wctb, max_rows = hb.max_rows, bps = hb.bps;
+    b->pic_image = hb.pic_image;
+    b->n_pics = int(h_pics.size());
+    // ---- device arenas
+    HIP_TRY(b->bits.alloc(h_bits.size()));
+    HIP_TRY(b->pics.alloc(h_pics.size()));
+    HIP_TRY(b->subs.alloc(h_subs.size()));
+    HIP_TRY(b->seqs.alloc(h_seqs.size()));
+    HIP_TRY(b->sf.alloc(h_sf.size()));
+    HIP_TRY(b->outs.alloc(n));
+    HIP_TRY(b->tus.alloc(tu_n));
+    HIP_TRY(b->coefs.alloc(coef_n));
+    HIP_TRY(b->row_counts.alloc(size_t(2) * rows));
+    HIP_TRY(b->recon.alloc(recon_bytes));
+    HIP_TRY(b->resid.alloc(resid_elems));
+    HIP_TRY(b->maps.alloc(map_bytes));
+    HIP_TRY(b->sao.alloc(sao_n));
+    HIP_TRY(b->status.alloc(h_pics.size()));
+    HIP_TRY(hipMemcpy(b->bits.p, h_bits.data(), h_bits.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b->pics.p, h_pics.data(), h_pics.size() * sizeof(PicDesc), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b->subs.p, h_subs.data(), h_subs.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b->seqs.p, h_seqs.data(), h_seqs.size() * sizeof(SeqParams), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b->sf.p, h_sf.data(), h_sf.size(), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemset(b->status.p, 0, h_pics.size() * sizeof(uint32_t)));
+    BatchArgs &a = b->args;
+    a.bits = b->bits.p;
+    a.pics = b->pics.p;
+    a.subs = b->subs.p;
+    a.seqs = b->seqs.p;
+    a.sf = b->sf.p;
+    a.outs = b->outs.p;
+    a.tus = b->tus.p;
+    a.coefs = b->coefs.p;
+    a.row_counts = b->row_counts.p;
+    a.recon = b->recon.p;
+    a.resid = b->resid.p;
+    a.maps = b->maps.p;
+    a.sao = b->sao.p;
+    a.status = b->status.p;
+    a.n_pics = b->n_pics;
+    a.max_width = max_w;
+    a.max_wctb = max_wctb;
+    a.max_rows = max_rows;
+    a.total_rows = int(rows);
+    a.bytes_per_sample = bps;
+    b->out_host.assign(n, OutImage{});
+    *out = b.release();
+    return HEIFGPU_OK;
+}
+
+int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_planes *out, void *stream) {
+    if (!ctx || !b || !out) return fail(HEIFGPU_E_INVALID, "invalid argument");
+    if (b->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    HIP_TRY(hipSetDevice(ctx->device));
+    bool changed = false;
+    for (size_t i = 0; i < b->n_images; ++i) {
+        OutImage o{};
+        for (int c = 0; c < 3; ++c) {
+            o.plane[c] = reinterpret_cast<uint64_t>(out[i].plane[c]);
+            o.pitch[c] = out[i].pitch[c];
+        }
+        if (!out[i].plane[0] || (b->infos[i].chroma_format_idc && (!out[i].plane[1] || !out[i].plane[2])))
+            return fail(HEIFGPU_E_INVALID, "missing output plane");
+        o.width = int32_t(b->infos[i].width);
+        o.height = int32_t(b->infos[i].height);
+        if (std::memcmp(&o, &b->out_host[i], sizeof(o)) != 0) {
+            b->out_host[i] = o;
+            changed = true;
+        }
+    }
+    if (changed)
+        HIP_TRY(hipMemcpyAsync(b->outs.p, b->out_host.data(), b->n_images * sizeof(OutImage), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(b->status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), s));
+    const BatchArgs &a = b->args;
+    // bring-up knob: HEIFGPU_STAGES=k launches only the first k stages
+    static const int max_stages = [] {
+        const char *e = std::getenv("HEIFGPU_STAGES");
+        return e ? std::atoi(e) : 5;
+    }();
+    if (max_stages < 5) {
+        hipError_t (*fns[5])(const BatchArgs &, hipStream_t) = {launch_parse, launch_transform, launch_intra,
+                                                                launch_deblock, launch_sao_out};
+        for (int i = 0; i < max_stages; ++i) HIP_TRY(fns[i](a, s));
+        return HEIFGPU_OK;
+    }
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[0], s));
+    HIP_TRY(launch_parse(a, s));
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[1], s));
+    HIP_TRY(launch_transform(a, s));
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[2], s));
+    HIP_TRY(launch_intra(a, s));
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[3], s));
+    HIP_TRY(launch_deblock(a, s));
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[4], s));
+    HIP_TRY(launch_sao_out(a, s));
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[5], s));
+    return HEIFGPU_OK;
+}
+
+int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *b, uint32_t *status, void *stream) {
+    if (!ctx || !b) return fail(HEIFGPU_E_INVALID, "invalid argument");
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    HIP_TRY(hipSetDevice(ctx->device));
+    std::vector<uint32_t> st(size_t(b->n_pics));
+    HIP_TRY(hipMemcpyAsync(st.data(), b->status.p, st.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<uint32_t> per(b->n_images, 0);
+    for (size_t p = 0; p < st.size(); ++p) per[b->pic_image[p]] |= st[p];
+    bool bad = false;
+    for (size_t i = 0; i < b->n_images; ++i) {
+        if (status) status[i] = per[i];
+        bad |= per[i] != 0;
+    }
+    return bad ? fail(HEIFGPU_E_DECODE, "one or more pictures failed the kernel bitstream checks") : HEIFGPU_OK;
+}
+
+void heifgpu_batch_free(heifgpu_batch *b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    delete b;
+}
+
+int heifgpu_decode_batch(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, const heifgpu_planes *out,
+                         void *stream, uint32_t *status) {
+    heifgpu_batch *b = nullptr;
+    int rc = heifgpu_batch_prepare(ctx, imgs, n, &b);
+    if (rc) return rc;
+    rc = heifgpu_batch_decode(ctx, b, out, stream);
+    if (!rc) rc = heifgpu_batch_status(ctx, b, status, stream);
+    heifgpu_batch_free(b);
+    return rc;
+}
+
+// ---------------------------------------------------------------- test hooks
+size_t heifgpu_remove_emulation_prevention(const uint8_t *in, size_t n, uint8_t *out) {
+    std::vector<uint8_t> v = RbspReader::remove_emulation_prevention(in, n);
+    if (!v.empty()) std::memcpy(out, v.data(), v.size());
+    return v.size();
+}
+
+int heifgpu_read_ue(const uint8_t *buf, size_t n, uint32_t *val) {
+    try {
+        RbspReader r(buf, n);
+        *val = r.read_ue();
+        return HEIFGPU_OK;
+    } catch (const std::exception &e) {
+        return fail(HEIFGPU_E_PARSE, e.what());
+    }
+}
+
+int heifgpu_read_se(const uint8_t *buf, size_t n, int32_t *val) {
+    try {
+        RbspReader r(buf, n);
+        *val = r.read_se();
+        return HEIFGPU_OK;
+    } catch (const std::exception &e) {
+        return fail(HEIFGPU_E_PARSE, e.what());
+    }
+}
+
+namespace {
+struct VecBins {
+    const uint8_t *b;
+    int n, i = 0;
+    bool under = false;
+    int operator()() {
+        if (i >= n) {
+            under = true;
+            return 0;
+        }
+        return b[i++] ? 1 : 0;
+    }
+};
+}  // namespace
+
+int heifgpu_bins_truncated_rice(const uint8_t *bins, int n, int c_max, int c_rice, int *used) {
+    VecBins v{bins, n};
+    uint32_t r = bin_truncated_rice(v, uint32_t(c_max), c_rice);
+    if (used) *used = v.i;
+    return v.under ? -1 : int(r);
+}
+
+int heifgpu_bins_chroma_pred_mode(const uint8_t *bins, int n, int *used) {
+    VecBins v{bins, n};
+    uint32_t r = bin_intra_chroma_pred_mode(v, v);
+    if (used) *used = v.i;
+    return v.under ? -1 : int(r);
+}
+
+int heifgpu_bins_coeff_abs_level_remaining(const uint8_t *bins, int n, int c_rice, int *used) {
+    VecBins v{bins, n};
+    uint32_t r = bin_coeff_abs_level_remaining(v, c_rice);
+    if (used) *used = v.i;
+    return (v.under || r == 0xffffffffu) ? -1 : int(r);
+}
+
+int heifgpu_bins_exp_golomb(const uint8_t *bins, int n, int k, int *used) {
+    VecBins v{bins, n};
+    uint32_t r = bin_exp_golomb(v, k);
+    if (used) *used = v.i;
+    return (v.under || r == 0xffffffffu) ? -1 : int(r);
+}
+
+}  // extern "C"

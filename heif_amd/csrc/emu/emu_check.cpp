@@ -1,0 +1,138 @@
+// emu_check.cpp — TEST-ONLY driver: runs the decode kernels' own sources as
+// host C++ (HG_HOST_EMU, see kernels/wave.hpp) and diffs every plane against
+// the CPU oracle.  Never part of the product library.
+//   emu_check file.heic [stages=5]   stages: 1 parse .. 5 full (3 = before deblocking)
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../../oracle/oracle.h"
+#include "../host/batch.hpp"
+#include "../kernels/kernels.hpp"
+
+namespace hg {
+thread_local EmuCtx g_emu;
+}
+using namespace hg;
+
+int main(int argc, char **argv) {
+    if (argc < 2) return 2;
+    int stages = argc > 2 ? atoi(argv[2]) : 5;
+    FILE *f = fopen(argv[1], "rb");
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    std::vector<uint8_t> data(static_cast<size_t>(n), 0);
+    if (fread(data.data(), 1, size_t(n), f) != size_t(n)) return 2;
+    fclose(f);
+    ParsedImage im = parse_heic(data.data(), data.size());
+    const ParsedImage *ims[1] = {&im};
+    HostBatch hb = build_batch(ims, 1);
+    std::vector<TuRec> tus(hb.tu_n);
+    std::vector<Coef> coefs(hb.coef_n);
+    std::vector<uint32_t> rc(2 * hb.rows), status(hb.pics.size());
+    std::vector<uint8_t> recon(hb.recon_bytes), maps(hb.map_bytes);
+    std::vector<int16_t> resid(hb.resid_elems);
+    std::vector<SaoParams> sao(hb.sao_n);
+    const int W = int(im.out_width), H = int(im.out_height), bps = hb.bps;
+    const int CW = (W + 1) / 2, CH = (H + 1) / 2;
+    std::vector<uint8_t> oy(size_t(W) * H * bps), ocb(size_t(CW) * CH * bps), ocr(size_t(CW) * CH * bps);
+    OutImage out{};
+    out.plane[0] = uint64_t(oy.data());
+    out.plane[1] = uint64_t(ocb.data());
+    out.plane[2] = uint64_t(ocr.data());
+    out.pitch[0] = W * bps;
+    out.pitch[1] = out.pitch[2] = CW * bps;
+    out.width = W;
+    out.height = H;
+    BatchArgs a{};
+    a.bits = hb.bits.data();
+    a.pics = hb.pics.data();
+    a.subs = hb.subs.data();
+    a.seqs = hb.seqs.data();
+    a.sf = hb.sf.data();
+    a.outs = &out;
+    a.tus = tus.data();
+    a.coefs = coefs.data();
+    a.row_counts = rc.data();
+    a.recon = recon.data();
+    a.resid = resid.data();
+    a.maps = maps.data();
+    a.sao = sao.data();
+    a.status = status.data();
+    a.n_pics = int(hb.pics.size());
+    a.max_width = hb.max_w;
+    a.max_wctb = hb.max_wctb;
+    a.max_rows = hb.max_rows;
+    a.total_rows = int(hb.rows);
+    a.bytes_per_sample = bps;
+    emu_parse(a);
+    uint32_t st = 0;
+    for (uint32_t s : status) st |= s;
+    uint64_t ntu = 0, ncoef = 0;
+    for (uint32_t r = 0; r < hb.rows; ++r) {
+        ntu += rc[2 * r];
+        ncoef += rc[2 * r + 1];
+    }
+    printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);
+    if (stages >= 2) emu_transform(a);
+    if (stages >= 3) emu_intra(a);
+    if (stages >= 4) emu_deblock(a);
+    if (stages >= 5) {
+        emu_sao_out(a);
+    } else {
+        // copy the recon arena into the output planes (crop + grid placement, no SAO)
+        int dbk = stages >= 4 ? 0 : 1;
+        oracle_set_debug_flags(dbk | 2);
+        for (const PicDesc &pd : hb.pics) {
+            const SeqParams &sp = hb.seqs[pd.seq];
+            for (int c = 0; c < 3; ++c) {
+                int sub = c ? 1 : 0, PW = sp.width >> sub, PH = sp.height >> sub;
+                size_t off = c == 0 ? 0 : size_t(sp.width) * sp.height + size_t(c - 1) * PW * PH;
+                int vw = std::min(sp.out_w, W - pd.out_x) >> sub, vh = std::min(sp.out_h, H - pd.out_y) >> sub;
+                for (int y = 0; y < vh; ++y)
+                    for (int x = 0; x < vw; ++x) {
+                        size_t src = (off + size_t(y + (sp.conf_t >> sub)) * PW + x + (sp.conf_l >> sub)) * bps;
+                        uint8_t *dst = reinterpret_cast<uint8_t *>(out.plane[c]) +
+                                       size_t((pd.out_y >> sub) + y) * out.pitch[c] + size_t((pd.out_x >> sub) + x) * bps;
+                        memcpy(dst, recon.data() + pd.recon_off + src, size_t(bps));
+                    }
+            }
+        }
+    }
+    if (stages < 3) return st ? 1 : 0;
+    oracle_image ref;
+    if (oracle_decode_heic(data.data(), data.size(), &ref, nullptr, 0, nullptr)) {
+        printf("oracle failed: %s\n", oracle_last_error());
+        return 1;
+    }
+    long bad_total = 0;
+    const char *names[3] = {"Y", "Cb", "Cr"};
+    for (int c = 0; c < 3; ++c) {
+        const uint8_t *g = c == 0 ? oy.data() : (c == 1 ? ocb.data() : ocr.data());
+        int pw = int(ref.pw[c]), ph = int(ref.ph[c]);
+        long bad = 0;
+        int fx = -1, fy = -1;
+        for (int y = 0; y < ph; ++y)
+            for (int x = 0; x < pw; ++x) {
+                int gv = bps == 1 ? g[size_t(y) * pw + x] : reinterpret_cast<const uint16_t *>(g)[size_t(y) * pw + x];
+                if (gv != ref.plane[c][size_t(y) * pw + x]) {
+                    if (!bad) fx = x, fy = y;
+                    ++bad;
+                }
+            }
+        printf("%s: %ld mismatches", names[c], bad);
+        if (bad) {
+            int sub = c ? 2 : 1;
+            printf(" first at (%d,%d) tile (%d,%d) emu %d ref %d", fx, fy, fy * sub / int(im.tile_height),
+                   fx * sub / int(im.tile_width),
+                   bps == 1 ? g[size_t(fy) * pw + fx] : 0, ref.plane[c][size_t(fy) * pw + fx]);
+        }
+        printf("\n");
+        bad_total += bad;
+    }
+    oracle_image_free(&ref);
+    printf("%s\n", bad_total || st ? "EMU PARITY FAIL" : "EMU PARITY OK");
+    return bad_total || st ? 1 : 0;
+}

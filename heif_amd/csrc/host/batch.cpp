@@ -1,0 +1,149 @@
+// batch.cpp — see batch.hpp.
+#include "batch.hpp"
+
+#include <algorithm>
+
+namespace hg {
+
+namespace {
+
+SeqParams make_seq(const ParamSet &ps, uint32_t sf_off) {
+    const SequenceParameterSet &s = ps.sps;
+    const PictureParameterSet &p = ps.pps;
+    SeqParams q{};
+    q.width = s.pic_width_in_luma_samples;
+    q.height = s.pic_height_in_luma_samples;
+    q.log2_ctb = s.log2_ctb_size;
+    q.log2_min_cb = s.log2_min_luma_coding_block_size;
+    q.log2_min_tb = s.log2_min_tb_size;
+    q.log2_max_tb = s.log2_max_tb_size;
+    q.max_th_depth_intra = s.max_transform_hierarchy_depth_intra;
+    q.chroma_format = s.chroma_array_type();
+    q.bit_depth_y = 8 + s.bit_depth_luma_minus8;
+    q.bit_depth_c = 8 + s.bit_depth_chroma_minus8;
+    uint32_t f = 0;
+    if (s.scaling_list_enabled_flag) f |= SP_SCALING_LIST;
+    if (p.sign_data_hiding_enabled_flag) f |= SP_SIGN_HIDING;
+    if (p.transform_skip_enabled_flag) f |= SP_TRANSFORM_SKIP;
+    if (p.transquant_bypass_enabled_flag) f |= SP_TQ_BYPASS;
+    if (p.cu_qp_delta_enabled_flag) f |= SP_CU_QP_DELTA;
+    if (p.entropy_coding_sync_enabled_flag) f |= SP_WPP;
+    if (s.strong_intra_smoothing_enabled_flag) f |= SP_STRONG_INTRA;
+    if (s.pcm_enabled_flag) f |= SP_PCM;
+    if (s.pcm_loop_filter_disabled_flag) f |= SP_PCM_LOOP_FILTER_DISABLED;
+    if (s.sample_adaptive_offset_enabled_flag) f |= SP_SAO;
+    q.flags = f;
+    q.diff_cu_qp_delta_depth = p.diff_cu_qp_delta_depth;
+    q.cb_qp_offset = p.pps_cb_qp_offset;
+    q.cr_qp_offset = p.pps_cr_qp_offset;
+    q.log2_min_pcm = s.log2_min_pcm;
+    q.log2_max_pcm = s.log2_max_pcm;
+    q.pcm_bd_y = s.pcm_bit_depth_luma;
+    q.pcm_bd_c = s.pcm_bit_depth_chroma;
+    q.conf_l = s.conf_win_left;
+    q.conf_t = s.conf_win_top;
+    q.out_w = s.out_width();
+    q.out_h = s.out_height();
+    q.sf_off = sf_off;
+    return q;
+}
+
+void fill_scaling(const ParamSet &ps, uint8_t *blk) {
+    for (int sid = 0; sid < 4; ++sid) {
+        int n = 4 << sid;
+        for (int m = 0; m < 6; ++m) ps.pps.scaling.factors(sid, m, blk + sf_size_offset(sid) + uint32_t(m * n * n));
+    }
+}
+
+}  // namespace
+
+HostBatch build_batch(const ParsedImage *const *imgs, size_t n) {
+    HostBatch hb;
+    std::vector<std::vector<uint8_t>> seq_keys;
+    for (size_t i = 0; i < n; ++i) {
+        const ParsedImage &im = *imgs[i];
+        const SequenceParameterSet &s0 = im.params[0].sps;
+        int bps = s0.bit_depth_luma_minus8 > 0 ? 2 : 1;
+        if (hb.bps == 0) {
+            hb.bps = bps;
+            hb.chroma = s0.chroma_array_type();
+        } else if (hb.bps != bps || hb.chroma != s0.chroma_array_type()) {
+            throw UnsupportedError("a batch must share bit depth and chroma format");
+        }
+        for (size_t t = 0; t < im.tiles.size(); ++t) {
+            const TileJob &tj = im.tiles[t];
+            const ParamSet &ps = im.params[size_t(tj.param)];
+            uint32_t seq;
+            auto it = std::find(seq_keys.begin(), seq_keys.end(), ps.key);
+            if (it == seq_keys.end()) {
+                seq = uint32_t(seq_keys.size());
+                seq_keys.push_back(ps.key);
+                uint32_t off = uint32_t(hb.sf.size());
+                hb.sf.resize(hb.sf.size() + kSfBlockBytes);
+                fill_scaling(ps, hb.sf.data() + off);
+                hb.seqs.push_back(make_seq(ps, off));
+            } else {
+                seq = uint32_t(it - seq_keys.begin());
+            }
+            const SeqParams &sq = hb.seqs[seq];
+            const int ctb = 1 << sq.log2_ctb;
+            const int wctb = (sq.width + ctb - 1) / ctb, hctb = (sq.height + ctb - 1) / ctb;
+            const int w4 = (sq.width + 3) >> 2, h4 = (sq.height + 3) >> 2;
+            const uint64_t samples = uint64_t(sq.width) * sq.height * (sq.chroma_format ? 3 : 2) / 2;
+            PicDesc pd{};
+            pd.bits_off = hb.bits.size();
+            pd.bits_len = uint32_t(tj.payload.size());
+            hb.bits.insert(hb.bits.end(), tj.payload.begin(), tj.payload.end());
+            hb.bits.resize((hb.bits.size() + 63) & ~size_t(63));
+            pd.sub_first = uint32_t(hb.subs.size());
+            pd.n_sub = uint32_t(tj.sh.num_entry_point_offsets + 1);
+            uint32_t o = tj.sh.slice_data_raw_offset;
+            hb.subs.push_back(o);
+            for (uint32_t e : tj.sh.entry_point_offset) {
+                o += e;
+                hb.subs.push_back(o);
+            }
+            hb.subs.push_back(pd.bits_len);
+            if ((sq.flags & SP_WPP) && int(pd.n_sub) != hctb)
+                throw HeifError("WPP picture without one entry point per CTB row");
+            pd.seq = seq;
+            pd.slice_qp = 26 + ps.pps.init_qp_minus26 + tj.sh.slice_qp_delta;
+            pd.cb_qp_off = tj.sh.slice_cb_qp_offset;
+            pd.cr_qp_off = tj.sh.slice_cr_qp_offset;
+            pd.sao_luma = tj.sh.slice_sao_luma_flag;
+            pd.sao_chroma = tj.sh.slice_sao_chroma_flag;
+            pd.dbk_disabled = tj.sh.slice_deblocking_filter_disabled_flag;
+            pd.beta_off = tj.sh.slice_beta_offset_div2;
+            pd.tc_off = tj.sh.slice_tc_offset_div2;
+            pd.image = uint32_t(i);
+            pd.out_x = int32_t((t % im.cols) * im.tile_width);
+            pd.out_y = int32_t((t / im.cols) * im.tile_height);
+            pd.recon_off = hb.recon_bytes;
+            hb.recon_bytes += (samples * uint64_t(hb.bps) + 255) & ~uint64_t(255);
+            pd.resid_off = hb.resid_elems;
+            hb.resid_elems += (samples + 127) & ~uint64_t(127);
+            pd.map_off = hb.map_bytes;
+            hb.map_bytes += (uint64_t(2) * w4 * h4 + 255) & ~uint64_t(255);
+            pd.sao_off = hb.sao_n;
+            hb.sao_n += uint64_t(wctb) * hctb;
+            pd.row_off = hb.rows;
+            hb.rows += uint32_t(hctb);
+            // worst case per CTB row: every 8x8 CU split into four 4x4 luma TBs + 2 chroma TBs
+            pd.tu_cap_row = uint32_t(wctb * (ctb / 8) * (ctb / 8) * 6);
+            pd.coef_cap_row = uint32_t(wctb * ctb * ctb * 3 / 2);
+            pd.tu_off = hb.tu_n;
+            hb.tu_n += uint64_t(pd.tu_cap_row) * hctb;
+            pd.coef_off = hb.coef_n;
+            hb.coef_n += uint64_t(pd.coef_cap_row) * hctb;
+            hb.pics.push_back(pd);
+            hb.pic_image.push_back(uint32_t(i));
+            hb.max_w = std::max(hb.max_w, sq.width);
+            hb.max_wctb = std::max(hb.max_wctb, wctb);
+            hb.max_rows = std::max(hb.max_rows, hctb);
+        }
+    }
+    hb.bits.resize(hb.bits.size() + 128, 0);
+    return hb;
+}
+
+}  // namespace hg

@@ -1,0 +1,28 @@
+// batch.hpp — flattens parsed images into the device descriptor arrays of
+// common/desc.hpp (shared by the HIP path and the host-emulation test build).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../common/desc.hpp"
+#include "heic_image.hpp"
+
+namespace hg {
+
+struct HostBatch {
+    std::vector<uint8_t> bits;
+    std::vector<PicDesc> pics;
+    std::vector<uint32_t> subs;
+    std::vector<SeqParams> seqs;
+    std::vector<uint8_t> sf;
+    std::vector<uint32_t> pic_image;  // picture → image index
+    uint64_t recon_bytes = 0, resid_elems = 0, map_bytes = 0, sao_n = 0, tu_n = 0, coef_n = 0;
+    uint32_t rows = 0;
+    int max_w = 0, max_wctb = 0, max_rows = 0, bps = 0, chroma = -1;
+};
+
+// Throws HeifError / UnsupportedError.
+HostBatch build_batch(const ParsedImage *const *imgs, size_t n);
+
+}  // namespace hg

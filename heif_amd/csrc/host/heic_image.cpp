@@ -1,0 +1,138 @@
+// heic_image.cpp — see heic_image.hpp.
+#include "heic_image.hpp"
+
+#include <map>
+
+namespace hg {
+
+namespace {
+
+// read_hvcc_nal_unit (decoder.rs:135-143): 2-byte header + EP-stripped RBSP
+std::vector<uint8_t> nal_rbsp(const std::vector<uint8_t> &nal) {
+    if (nal.size() < 3) throw HeifError("nal unit is too short");
+    return RbspReader::remove_emulation_prevention(nal.data() + 2, nal.size() - 2);
+}
+
+void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p) {
+    if (s.chroma_format_idc == 2 || s.chroma_format_idc == 3) throw UnsupportedError("only 4:0:0 and 4:2:0 are supported");
+    if (s.separate_colour_plane_flag) throw UnsupportedError("separate_colour_plane_flag");
+    if (s.bit_depth_luma_minus8 != s.bit_depth_chroma_minus8) throw UnsupportedError("luma/chroma bit depth differ");
+    if (s.range_extension_tools || p.range_extension_tools) throw UnsupportedError("range-extension coding tools");
+    if (p.tiles_enabled_flag) throw UnsupportedError("HEVC tiles inside a picture");
+    if (s.pic_width_in_luma_samples > 8192 || s.pic_height_in_luma_samples > 8192)
+        throw UnsupportedError("picture larger than 8192");
+    if (s.pic_width_in_luma_samples % (1 << s.log2_min_luma_coding_block_size) ||
+        s.pic_height_in_luma_samples % (1 << s.log2_min_luma_coding_block_size))
+        throw HeifError("picture size not a multiple of MinCbSizeY");
+}
+
+}  // namespace
+
+ParsedImage parse_heic(const uint8_t *data, size_t len) {
+    HeifReader reader(data, len);
+    Heif heif = reader.read();
+    ParsedImage img;
+    img.primary_item_id = heif.primary_item_id;
+    const ItemInfo *pi = heif.item_info_by_item_id(heif.primary_item_id);
+    if (!pi) throw HeifError("primary item " + std::to_string(heif.primary_item_id) + " not found in item_info");
+    if (const Property *ispe = heif.item_property(*pi, fourcc('i', 's', 'p', 'e'))) {
+        if (ispe->length < 12) throw HeifError("ispe too short");
+        const uint8_t *q = data + ispe->offset + 4;
+        img.ispe_width = (uint32_t(q[0]) << 24) | (uint32_t(q[1]) << 16) | (uint32_t(q[2]) << 8) | q[3];
+        img.ispe_height = (uint32_t(q[4]) << 24) | (uint32_t(q[5]) << 16) | (uint32_t(q[6]) << 8) | q[7];
+    }
+    if (const Property *irot = heif.item_property(*pi, fourcc('i', 'r', 'o', 't')))
+        if (irot->length >= 1) img.rotation = data[irot->offset] & 3;
+    img.num_thumbnails = heif.num_thumbnails();
+
+    std::vector<uint32_t> tile_ids;
+    if (pi->type == fourcc('g', 'r', 'i', 'd')) {
+        ImageGrid g = heif.grid(*pi);
+        img.rows = g.rows;
+        img.cols = g.cols;
+        img.out_width = g.output_width;
+        img.out_height = g.output_height;
+        tile_ids = heif.references_from(fourcc('d', 'i', 'm', 'g'), pi->id);
+        if (tile_ids.empty()) throw HeifError("grid " + std::to_string(pi->id) + " has no tile references");
+        if (tile_ids.size() != size_t(g.rows) * g.cols) throw HeifError("grid tile count mismatch");
+    } else if (pi->type == fourcc('h', 'v', 'c', '1')) {
+        tile_ids.push_back(pi->id);
+    } else {
+        throw UnsupportedError("unsupported primary item type");
+    }
+
+    std::map<size_t, int> param_of_prop;  // hvcC property offset → params index
+    for (uint32_t id : tile_ids) {
+        const ItemInfo *it = heif.item_info_by_item_id(id);
+        if (!it) throw HeifError("tile item " + std::to_string(id) + " not found");
+        if (it->type != fourcc('h', 'v', 'c', '1')) throw UnsupportedError("grid tile is not hvc1");
+        const Property *hv = heif.item_property(*it, fourcc('h', 'v', 'c', 'C'));
+        if (!hv) throw HeifError("missing HEVC decoder configuration");
+        int param;
+        auto found = param_of_prop.find(hv->offset);
+        HevcConfig cfg = parse_hvcc(data + hv->offset, hv->length);
+        if (found == param_of_prop.end()) {
+            if (cfg.vps.empty()) throw HeifError("no VPS in hvcC");
+            if (cfg.sps.empty()) throw HeifError("no SPS in hvcC");
+            if (cfg.pps.empty()) throw HeifError("no PPS in hvcC");
+            ParamSet ps;
+            ps.key = cfg.sps[0];
+            ps.key.insert(ps.key.end(), cfg.pps[0].begin(), cfg.pps[0].end());
+            ps.vps = video_parameter_set_rbsp(nal_rbsp(cfg.vps[0]));
+            ps.sps = sequence_parameter_set_rbsp(nal_rbsp(cfg.sps[0]));
+            ps.pps = picture_parameter_set_rbsp(nal_rbsp(cfg.pps[0]), ps.sps);
+            check_supported(ps.sps, ps.pps);
+            param = int(img.params.size());
+            img.params.push_back(std::move(ps));
+            param_of_prop[hv->offset] = param;
+        } else {
+            param = found->second;
+        }
+        const ParamSet &ps = img.params[size_t(param)];
+        // read_item_nal_unit (decoder.rs:146-164), generalised: length-prefixed NAL units,
+        // exactly one VCL NAL (one slice segment per picture), non-VCL units skipped
+        std::vector<uint8_t> item = heif.item_data(*it);
+        img.coded_bytes += uint32_t(item.size());
+        int lsz = cfg.length_size_minus_one + 1;
+        size_t pos = 0;
+        bool have_vcl = false;
+        TileJob job;
+        job.param = param;
+        while (pos < item.size()) {
+            if (pos + size_t(lsz) > item.size()) throw HeifError("truncated NAL length prefix");
+            size_t nl = 0;
+            for (int k = 0; k < lsz; ++k) nl = (nl << 8) | item[pos + size_t(k)];
+            pos += size_t(lsz);
+            if (nl < 3 || pos + nl > item.size()) throw HeifError("NAL unit length out of range");
+            NalUnitHeader h{uint16_t((item[pos] << 8) | item[pos + 1])};
+            if (h.nal_unit_type() < 32) {
+                if (have_vcl) throw UnsupportedError("more than one slice segment per picture");
+                have_vcl = true;
+                job.nal = h;
+                job.payload.assign(item.begin() + long(pos) + 2, item.begin() + long(pos + nl));
+            }
+            pos += nl;
+        }
+        if (!have_vcl) throw HeifError("tile item holds no VCL NAL unit");
+        job.sh = slice_segment_header(job.payload.data(), job.payload.size(), job.nal, ps.sps, ps.pps);
+        img.tiles.push_back(std::move(job));
+    }
+    const SequenceParameterSet &s0 = img.params[0].sps;
+    img.tile_width = uint32_t(s0.out_width());
+    img.tile_height = uint32_t(s0.out_height());
+    for (auto &ps : img.params) {
+        if (ps.sps.out_width() != s0.out_width() || ps.sps.out_height() != s0.out_height())
+            throw UnsupportedError("grid tiles of different sizes");
+        if (ps.sps.bit_depth_luma_minus8 != s0.bit_depth_luma_minus8 || ps.sps.chroma_format_idc != s0.chroma_format_idc)
+            throw UnsupportedError("grid tiles with different formats");
+    }
+    if (pi->type != fourcc('g', 'r', 'i', 'd')) {
+        img.out_width = img.tile_width;
+        img.out_height = img.tile_height;
+    }
+    if (img.out_width > img.cols * img.tile_width || img.out_height > img.rows * img.tile_height)
+        throw HeifError("grid output larger than its tiles");
+    return img;
+}
+
+}  // namespace hg

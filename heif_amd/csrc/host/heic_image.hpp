@@ -1,0 +1,39 @@
+// heic_image.hpp — host half of HeicDecoder::decode (src/heic/decoder.rs:12-112).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "heif_reader.hpp"
+#include "hevc_ps.hpp"
+
+namespace hg {
+
+struct ParamSet {
+    std::vector<uint8_t> key;  // raw SPS ++ PPS NAL bytes (dedupe key)
+    VideoParameterSet vps;
+    SequenceParameterSet sps;
+    PictureParameterSet pps;
+};
+
+struct TileJob {
+    std::vector<uint8_t> payload;  // raw NAL payload after the 2-byte header (EP bytes kept)
+    NalUnitHeader nal;
+    SliceSegmentHeader sh;
+    int param = 0;
+};
+
+struct ParsedImage {
+    std::vector<ParamSet> params;
+    std::vector<TileJob> tiles;  // grid order (row-major)
+    uint32_t primary_item_id = 0, ispe_width = 0, ispe_height = 0, rotation = 0, num_thumbnails = 0;
+    uint32_t rows = 1, cols = 1, out_width = 0, out_height = 0;
+    uint32_t tile_width = 0, tile_height = 0, coded_bytes = 0;
+};
+
+// Throws HeifError (parse) or UnsupportedError (valid stream, tool outside this path).
+struct UnsupportedError : HeifError {
+    explicit UnsupportedError(const std::string &m) : HeifError(m) {}
+};
+ParsedImage parse_heic(const uint8_t *data, size_t len);
+
+}  // namespace hg

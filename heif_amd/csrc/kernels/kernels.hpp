@@ -1,0 +1,89 @@
+// kernels.hpp — launch interface of the gfx950 decode pipeline.
+//
+// Pipeline per batch (one HIP stream, 5 launches):
+//   1. k_parse      CABAC substreams → TU records + coefficients + QP/edge
+//                   maps + SAO parameters        (slice.rs:206-256 + todo!()s)
+//   2. k_transform  dequant (8.6.2-3) + inverse DST/DCT (8.6.4) → residuals
+//   3. k_intra      intra prediction (8.4.4.2) + reconstruction (8.6.7)
+//   4. k_deblock    vertical then horizontal edges (8.7.2), in place
+//   5. k_sao_out    SAO (8.7.3) + crop + grid placement into the caller's planes
+#pragma once
+#include "../common/desc.hpp"
+#include "wave.hpp"
+
+#if defined(HG_HOST_EMU)
+#include <atomic>
+#include <thread>
+#include <vector>
+#endif
+
+namespace hg {
+
+struct BatchArgs {
+    const uint8_t *bits;       // raw NAL payloads
+    const PicDesc *pics;
+    const uint32_t *subs;      // substream raw start offsets (n_sub + 1 per picture, last = len)
+    const SeqParams *seqs;
+    const uint8_t *sf;         // ScalingFactor blocks
+    const OutImage *outs;
+    TuRec *tus;
+    Coef *coefs;
+    uint32_t *row_counts;      // [row] = {ntu, ncoef}
+    uint8_t *recon;            // sample arena (uint8 or uint16 samples)
+    int16_t *resid;
+    uint8_t *maps;
+    SaoParams *sao;
+    uint32_t *status;          // per picture
+    int n_pics;
+    int max_width;             // luma samples, batch max
+    int max_wctb;
+    int max_rows;              // CTB rows, batch max
+    int total_rows;            // sum of CTB rows over pictures
+    int bytes_per_sample;      // 1 or 2
+};
+
+constexpr int kParseWaves = 16;
+size_t parse_lds_bytes(int max_width, int max_wctb);
+
+#if defined(HG_HOST_EMU)
+// Runs kernel(a) over a gx * gy grid, one block at a time, with `waves` host
+// threads per block (threadIdx.x = 64 * wave).  grid_stride kernels (which
+// loop t = blockIdx.x*blockDim.x+threadIdx.x .. total) get a 1x1 geometry in x.
+template <class K>
+void emu_launch(K kernel, int gx, int gy, int waves, const BatchArgs &a, bool grid_stride = false,
+                size_t dyn_lds = 0) {
+    for (int by = 0; by < gy; ++by)
+        for (int bx = 0; bx < (grid_stride ? 1 : gx); ++bx) {
+            std::atomic<int> cnt{0}, gen{0};
+            std::vector<std::thread> th;
+            unsigned char *lds = dyn_lds ? static_cast<unsigned char *>(std::malloc(dyn_lds)) : nullptr;
+            for (int w = 0; w < waves; ++w)
+                th.emplace_back([&, w] {
+                    g_emu.bidx = {unsigned(bx), unsigned(by), 0};
+                    g_emu.tidx = {unsigned(grid_stride ? 0 : 64 * w), 0, 0};
+                    g_emu.bdim = {unsigned(grid_stride ? 1 : 64 * waves), 1, 1};
+                    g_emu.gdim = {unsigned(grid_stride ? 1 : gx), unsigned(gy), 1};
+                    g_emu.bar_count = &cnt;
+                    g_emu.bar_gen = &gen;
+                    g_emu.bar_n = waves;
+                    g_emu.smem = lds;
+                    kernel(a);
+                });
+            for (auto &t : th) t.join();
+            std::free(lds);
+        }
+}
+void emu_parse(const BatchArgs &a);
+void emu_transform(const BatchArgs &a);
+void emu_intra(const BatchArgs &a);
+void emu_deblock(const BatchArgs &a);
+void emu_sao_out(const BatchArgs &a);
+#else
+hipError_t launch_parse(const BatchArgs &a, hipStream_t s);
+hipError_t launch_transform(const BatchArgs &a, hipStream_t s);
+hipError_t launch_intra(const BatchArgs &a, hipStream_t s);
+hipError_t launch_deblock(const BatchArgs &a, hipStream_t s);
+hipError_t launch_sao_out(const BatchArgs &a, hipStream_t s);
+#endif
+
+}  // namespace hg

@@ -1,0 +1,272 @@
+// loopfilter.hip — deblocking (stage 4) and SAO + output placement (stage 5).
+//
+// Deblocking, H.265 8.7.2: transform/prediction edges on the 8x8 grid, bS = 2
+// for intra, beta'/tC' tables 8-12, luma strong/normal decisions (dE, dEp,
+// dEq), chroma filtered only for bS = 2 on the 8x8 chroma grid with
+// QpC = table 8-10((QpQ + QpP + 1) >> 1 + cQpPicOffset); samples of
+// cu_transquant_bypass CUs are left untouched.  All vertical edges of a
+// picture are filtered before any horizontal edge, and the edges of one
+// direction never share a modified sample, so each direction is one launch
+// with one thread per 4-line edge segment (in place).
+//
+// SAO, H.265 8.7.3: band offset / edge offset per CTB on the deblocked
+// picture, EO neighbours outside the picture leave the sample unchanged.
+// The same pass crops the conformance window and writes the picture into
+// its grid position of the caller's output planes (coalesced along rows),
+// clipping to the grid's output size (ISO/IEC 23008-12 ImageGrid).  No
+// reference code exists for either stage (src/hevc/slice.rs:249-255).
+#include "kernels.hpp"
+
+namespace hg {
+
+namespace {
+
+__constant__ uint8_t c_beta[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
+                                   8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
+                                   34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
+__constant__ uint8_t c_tc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
+
+__device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__device__ __forceinline__ int chroma_qp_map(int qpi, int chroma) {
+    if (chroma != 1) return qpi < 51 ? qpi : 51;
+    if (qpi < 30) return qpi;
+    if (qpi > 43) return qpi - 6;
+    constexpr int t[14] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37};
+    return t[qpi - 30];
+}
+
+// one 4-line luma edge segment; q0 at `q`, step across the edge `sx`, along it `sk`
+template <typename Pel>
+__device__ void luma_segment(Pel *q, int sx, int sk, int qpP, int qpQ, bool nofp, bool nofq, int beta_off,
+                             int tc_off, int bd) {
+#define PS(i, k) q[(k) * sk - ((i) + 1) * sx]
+#define QS(i, k) q[(k) * sk + (i) * sx]
+    const int qpl = (qpQ + qpP + 1) >> 1;
+    const int beta = c_beta[clip3(0, 51, qpl + (beta_off << 1))] * (1 << (bd - 8));
+    const int tc = c_tc[clip3(0, 53, qpl + 2 + (tc_off << 1))] * (1 << (bd - 8));
+    const int dp0 = abs(PS(2, 0) - 2 * PS(1, 0) + PS(0, 0)), dp3 = abs(PS(2, 3) - 2 * PS(1, 3) + PS(0, 3));
+    const int dq0 = abs(QS(2, 0) - 2 * QS(1, 0) + QS(0, 0)), dq3 = abs(QS(2, 3) - 2 * QS(1, 3) + QS(0, 3));
+    const int dpq0 = dp0 + dq0, dpq3 = dp3 + dq3, dp = dp0 + dp3, dq = dq0 + dq3;
+    if (dpq0 + dpq3 >= beta) return;
+    auto dsam = [&](int k, int dpq) {
+        return dpq < (beta >> 2) && abs(PS(3, k) - PS(0, k)) + abs(QS(0, k) - QS(3, k)) < (beta >> 3) &&
+               abs(PS(0, k) - QS(0, k)) < ((5 * tc + 1) >> 1);
+    };
+    const bool strong = dsam(0, 2 * dpq0) && dsam(3, 2 * dpq3);
+    const bool dEp = dp < ((beta + (beta >> 1)) >> 3), dEq = dq < ((beta + (beta >> 1)) >> 3);
+    const int maxv = (1 << bd) - 1;
+    for (int k = 0; k < 4; ++k) {
+        const int p0 = PS(0, k), p1 = PS(1, k), p2 = PS(2, k), p3 = PS(3, k);
+        const int q0 = QS(0, k), q1 = QS(1, k), q2 = QS(2, k), q3 = QS(3, k);
+        if (strong) {
+            if (!nofp) {
+                PS(0, k) = (Pel)clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+                PS(1, k) = (Pel)clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2);
+                PS(2, k) = (Pel)clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+            }
+            if (!nofq) {
+                QS(0, k) = (Pel)clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+                QS(1, k) = (Pel)clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2);
+                QS(2, k) = (Pel)clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3);
+            }
+        } else {
+            int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
+            if (abs(delta) < tc * 10) {
+                delta = clip3(-tc, tc, delta);
+                if (!nofp) PS(0, k) = (Pel)clip3(0, maxv, p0 + delta);
+                if (!nofq) QS(0, k) = (Pel)clip3(0, maxv, q0 - delta);
+                if (dEp && !nofp)
+                    PS(1, k) = (Pel)clip3(0, maxv, p1 + clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1));
+                if (dEq && !nofq)
+                    QS(1, k) = (Pel)clip3(0, maxv, q1 + clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1));
+            }
+        }
+    }
+#undef PS
+#undef QS
+}
+
+}  // namespace
+
+// VERT: edges between columns (x-1 | x); otherwise between rows.
+template <typename Pel, bool VERT>
+__global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
+    const int pic = blockIdx.y;
+    const PicDesc pd = a.pics[pic];
+    if (pd.dbk_disabled) return;
+    const SeqParams sp = a.seqs[pd.seq];
+    const int W = sp.width, H = sp.height;
+    const int w4 = (W + 3) >> 2, h4 = (H + 3) >> 2;
+    const int8_t *qpy = reinterpret_cast<const int8_t *>(a.maps + pd.map_off);
+    const uint8_t *flg = a.maps + pd.map_off + (size_t)w4 * h4;
+    Pel *Y = reinterpret_cast<Pel *>(a.recon + pd.recon_off);
+    const int cw = sp.chroma_format ? W >> 1 : 0, ch = sp.chroma_format ? H >> 1 : 0;
+    // luma segments
+    const int ne_l = VERT ? (W - 1) >> 3 : (H - 1) >> 3;  // edges excluding the picture boundary
+    const int ns_l = VERT ? H >> 2 : W >> 2;               // 4-sample segments along each edge
+    const int nl = ne_l * ns_l;
+    const int ne_c = VERT ? (cw - 1) >> 3 : (ch - 1) >> 3;
+    const int ns_c = VERT ? ch >> 1 : cw >> 1;             // 2-sample chroma segments (= 4 luma)
+    const int nc = sp.chroma_format ? ne_c * ns_c : 0;
+    const int total = nl + 2 * nc;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        if (t < nl) {
+            int x, y;
+            if (VERT) {
+                x = 8 * (t % ne_l + 1);
+                y = 4 * (t / ne_l);
+            } else {
+                x = 4 * (t % ns_l);
+                y = 8 * (t / ns_l + 1);
+            }
+            const int fq = flg[(y >> 2) * w4 + (x >> 2)];
+            if (!(fq & (VERT ? MF_EDGE_V : MF_EDGE_H))) continue;
+            const int xp = VERT ? x - 1 : x, yp = VERT ? y : y - 1;
+            const int fp = flg[(yp >> 2) * w4 + (xp >> 2)];
+            luma_segment<Pel>(Y + (size_t)y * W + x, VERT ? 1 : W, VERT ? W : 1, qpy[(yp >> 2) * w4 + (xp >> 2)],
+                              qpy[(y >> 2) * w4 + (x >> 2)], fp & MF_NOFILT, fq & MF_NOFILT, pd.beta_off, pd.tc_off,
+                              sp.bit_depth_y);
+        } else {
+            const int u = t - nl;
+            const int cidx = 1 + u / nc, v = u % nc;
+            int xc, yc;
+            if (VERT) {
+                xc = 8 * (v % ne_c + 1);
+                yc = 2 * (v / ne_c);
+            } else {
+                xc = 2 * (v % ns_c);
+                yc = 8 * (v / ns_c + 1);
+            }
+            const int xl = xc << 1, yl = yc << 1;
+            const int fq = flg[(yl >> 2) * w4 + (xl >> 2)];
+            if (!(fq & (VERT ? MF_EDGE_V : MF_EDGE_H))) continue;
+            const int xlp = VERT ? xl - 1 : xl, ylp = VERT ? yl : yl - 1;
+            const int fp = flg[(ylp >> 2) * w4 + (xlp >> 2)];
+            const int qpP = qpy[(ylp >> 2) * w4 + (xlp >> 2)], qpQ = qpy[(yl >> 2) * w4 + (xl >> 2)];
+            const int off = cidx == 1 ? sp.cb_qp_offset : sp.cr_qp_offset;
+            const int qpc = chroma_qp_map(((qpQ + qpP + 1) >> 1) + off, sp.chroma_format);
+            const int bd = sp.bit_depth_c;
+            const int tc = c_tc[clip3(0, 53, qpc + 2 + (pd.tc_off << 1))] * (1 << (bd - 8));
+            const int maxv = (1 << bd) - 1;
+            Pel *C = Y + (size_t)W * H + (size_t)(cidx - 1) * cw * ch;
+            Pel *q = C + (size_t)yc * cw + xc;
+            const int sx = VERT ? 1 : cw, sk = VERT ? cw : 1;
+            for (int k = 0; k < 2; ++k) {
+                const int p0 = q[k * sk - sx], p1 = q[k * sk - 2 * sx], q0 = q[k * sk], q1 = q[k * sk + sx];
+                const int delta = clip3(-tc, tc, ((((q0 - p0) << 2) + p1 - q1 + 4) >> 3));
+                if (!(fp & MF_NOFILT)) q[k * sk - sx] = (Pel)clip3(0, maxv, p0 + delta);
+                if (!(fq & MF_NOFILT)) q[k * sk] = (Pel)clip3(0, maxv, q0 - delta);
+            }
+        }
+    }
+}
+
+// SAO + crop + grid placement: one thread per output sample
+template <typename Pel>
+__global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
+    const int pic = blockIdx.y;
+    const PicDesc pd = a.pics[pic];
+    const SeqParams sp = a.seqs[pd.seq];
+    const OutImage oi = a.outs[pd.image];
+    const int W = sp.width, H = sp.height, log2ctb = sp.log2_ctb;
+    const int wctb = (W + (1 << log2ctb) - 1) >> log2ctb;
+    const int w4 = (W + 3) >> 2, h4 = (H + 3) >> 2;
+    const uint8_t *flg = a.maps + pd.map_off + (size_t)w4 * h4;
+    const Pel *Y = reinterpret_cast<const Pel *>(a.recon + pd.recon_off);
+    const int cw = sp.chroma_format ? W >> 1 : 0, ch = sp.chroma_format ? H >> 1 : 0;
+    const SaoParams *sao = a.sao + pd.sao_off;
+    // visible region of this picture in the output image (luma)
+    const int vw = min(sp.out_w, oi.width - pd.out_x), vh = min(sp.out_h, oi.height - pd.out_y);
+    if (vw <= 0 || vh <= 0) return;
+    const int vcw = sp.chroma_format ? (vw + 1) >> 1 : 0, vch = sp.chroma_format ? (vh + 1) >> 1 : 0;
+    const int nl = vw * vh, nc = vcw * vch;
+    const int total = nl + 2 * nc;
+    const bool any_sao = pd.sao_luma || pd.sao_chroma;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+        int cidx, x, y, PW, PH, sub;
+        if (t < nl) {
+            cidx = 0;
+            x = t % vw;
+            y = t / vw;
+        } else {
+            const int u = t - nl;
+            cidx = 1 + u / nc;
+            x = (u % nc) % vcw;
+            y = (u % nc) / vcw;
+        }
+        sub = cidx ? 1 : 0;
+        PW = cidx ? cw : W;
+        PH = cidx ? ch : H;
+        const Pel *P = cidx == 0 ? Y : Y + (size_t)W * H + (size_t)(cidx - 1) * cw * ch;
+        const int xs = x + (sp.conf_l >> sub), ys = y + (sp.conf_t >> sub);  // picture coords
+        int v = P[(size_t)ys * PW + xs];
+        if (any_sao) {
+            const SaoParams &s = sao[(ys >> (log2ctb - sub)) * wctb + (xs >> (log2ctb - sub))];
+            const int type = s.type[cidx];
+            const bool nof = flg[((ys << sub) >> 2) * w4 + ((xs << sub) >> 2)] & MF_NOFILT;
+            if (type && !nof) {
+                const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
+                int o = 0;
+                if (type == 2) {
+                    const int cl = s.band_eo[cidx];
+                    const int hx = cl == 0 ? 1 : (cl == 1 ? 0 : (cl == 2 ? 1 : -1));
+                    const int vy = cl == 0 ? 0 : 1;
+                    const int ax = xs - hx, ay = ys - vy, bx = xs + hx, by = ys + vy;
+                    if (ax >= 0 && ay >= 0 && ax < PW && ay < PH && bx >= 0 && by >= 0 && bx < PW && by < PH) {
+                        const int na = P[(size_t)ay * PW + ax], nb = P[(size_t)by * PW + bx];
+                        int e = 2 + (v > na) - (v < na) + (v > nb) - (v < nb);
+                        if (e <= 2) e = e == 2 ? 0 : e + 1;
+                        o = e ? s.off[cidx][e - 1] : 0;
+                    }
+                } else {
+                    const int band = v >> (bd - 5);
+                    const int k = (band - s.band_eo[cidx]) & 31;
+                    o = k < 4 ? s.off[cidx][k] : 0;
+                }
+                v = clip3(0, (1 << bd) - 1, v + o);
+            }
+        }
+        const int ox = (pd.out_x >> sub) + x, oy = (pd.out_y >> sub) + y;
+        Pel *dst = reinterpret_cast<Pel *>(oi.plane[cidx] + (size_t)oy * oi.pitch[cidx]) + ox;
+        *dst = (Pel)v;
+    }
+}
+
+#if defined(HG_HOST_EMU)
+void emu_deblock(const BatchArgs &a) {
+    if (a.bytes_per_sample == 1) {
+        emu_launch(k_deblock<uint8_t, true>, 1, a.n_pics, 1, a, true);
+        emu_launch(k_deblock<uint8_t, false>, 1, a.n_pics, 1, a, true);
+    } else {
+        emu_launch(k_deblock<uint16_t, true>, 1, a.n_pics, 1, a, true);
+        emu_launch(k_deblock<uint16_t, false>, 1, a.n_pics, 1, a, true);
+    }
+}
+void emu_sao_out(const BatchArgs &a) {
+    if (a.bytes_per_sample == 1) emu_launch(k_sao_out<uint8_t>, 1, a.n_pics, 1, a, true);
+    else emu_launch(k_sao_out<uint16_t>, 1, a.n_pics, 1, a, true);
+}
+#else
+hipError_t launch_deblock(const BatchArgs &a, hipStream_t s) {
+    dim3 grid(64, a.n_pics), block(256);
+    if (a.bytes_per_sample == 1) {
+        hipLaunchKernelGGL((k_deblock<uint8_t, true>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((k_deblock<uint8_t, false>), grid, block, 0, s, a);
+    } else {
+        hipLaunchKernelGGL((k_deblock<uint16_t, true>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((k_deblock<uint16_t, false>), grid, block, 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_sao_out(const BatchArgs &a, hipStream_t s) {
+    dim3 grid(256, a.n_pics), block(256);
+    if (a.bytes_per_sample == 1) hipLaunchKernelGGL(k_sao_out<uint8_t>, grid, block, 0, s, a);
+    else hipLaunchKernelGGL(k_sao_out<uint16_t>, grid, block, 0, s, a);
+    return hipGetLastError();
+}
+#endif
+
+}  // namespace hg

@@ -1,0 +1,968 @@
+// parse.hip — CABAC slice-data parser for gfx950 (pipeline stage 1).
+//
+// Replaces SliceSegmentReader::read_data / read_coding_tree_unit and the
+// todo!() sao() / coding_quadtree() of src/hevc/slice.rs:206-256, with the
+// engine of src/cabac/arithmetic.rs and the binarizations of
+// src/cabac/decoder.rs, plus everything H.265 needs below them (7.3.8.3-14,
+// 9.3.4.2 ctxInc, 8.4.2 MPM, 8.6.1 QP).
+//
+// Mapping to MI355X: one workgroup per picture (HEIF grid tile), one wave per
+// WPP substream (= CTB row).  Row r may parse CTU c once row r-1 has finished
+// CTU c+1 (the WPP 2-CTU lag, which also covers the above-CTB split depth and
+// SAO merge-up data); the lag is enforced with per-wave progress counters in
+// LDS (workgroup-scope release/acquire, so no cross-CU protocol is needed).
+// All 64 lanes run the scalar syntax decode in lock-step; lanes fan out for
+// the byte-ring refill (coalesced 64-byte loads, EP bytes removed by ballot),
+// and for the map writes (QP, edges, modes, depths).
+#include "cabac.hpp"
+#include "kernels.hpp"
+#include "tables.hpp"
+
+namespace hg {
+
+__constant__ uint8_t c_lps[256] = {HG_LPS_TABLE};
+__constant__ uint8_t c_trans_lps[64] = {HG_TRANS_LPS};
+__constant__ uint8_t c_ctx_init[CTX_NUM] = {HG_CTX_INIT_VALUES};
+
+namespace {
+
+#define HG_INLINE __device__ __attribute__((always_inline)) inline
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return HG_UNI(v); }
+__device__ __forceinline__ int unis(int v) { return (int)HG_UNI((uint32_t)v); }
+
+struct alignas(16) WaveLds {
+    uint8_t ctx[CTX_PAD];
+    uint8_t ring[256];
+    uint8_t ipm[16][17];  // IntraPredModeY per 4x4 of the current CTB, column 0 = left CTB
+    uint8_t depth[8][9];  // CtDepth per 8x8, column 0 = left CTB
+    int8_t qpy[8][8];     // QpY per 8x8 of the current CTB
+    uint32_t cqt[24];     // coding_quadtree stack
+    uint64_t tt[24];      // transform_tree stack
+    SaoParams sao_left;
+    uint8_t pad_[2];
+};
+
+struct Parser {
+    // picture constants
+    int W, H, log2ctb, ctb, wctb, hctb, minCb, minTb, maxTb, maxDepthIntra, chroma, bdY, bdC, qpbdY, qpbdC;
+    int pcmMin, pcmMax;
+    uint32_t flags;
+    int log2qg, cbOff, crOff, sliceQp, saoL, saoC;
+    // engine (9.3.4.3) with a 16-bit-scaled value register
+    uint32_t range, value;
+    int bits_needed;
+    // byte ring
+    uint32_t rd, wr, src_pos, nal_end, prev1, prev2;
+    const uint8_t *src;
+    uint32_t status;
+    WaveLds *w;
+    int lane;
+    // CTB
+    int ctbx, ctby, rx, ry;
+    // quantization groups (8.6.1)
+    int qp_prev_last, qp_pred, cu_qp_delta_val, qpy_cur, qg_x, qg_y;
+    bool is_cu_qp_delta_coded, qg_new, first_qg_in_slice;
+    // coding unit
+    bool cu_bypass;
+    int cu_intra_split, cu_chroma_mode;
+    // outputs
+    TuRec *tu_out;
+    Coef *coef_out;
+    uint32_t ntu, tu_cap, ncoef, coef_cap;
+    int8_t *gqpy;
+    uint8_t *gflags;
+    int w4, h4;
+    const uint8_t *depth_above;  // LDS line of the CTB row above (8x8 units)
+};
+
+// ---------------------------------------------------------------- bytes
+#if defined(HG_HOST_EMU)
+HG_INLINE void ring_refill(Parser &p) {  // scalar equivalent of the 64-lane ballot refill
+    for (int lane = 0; lane < 64; ++lane) {
+        uint32_t pos = p.src_pos + lane;
+        if (pos >= p.nal_end) break;
+        uint32_t b = p.src[pos];
+        uint32_t nb = pos + 1 < p.nal_end ? p.src[pos + 1] : 0xffu;
+        bool ep = p.prev2 == 0 && p.prev1 == 0 && b == 3 && (pos + 1 >= p.nal_end || nb <= 3);
+        if (!ep) p.w->ring[p.wr++ & 255] = (uint8_t)b;
+        p.prev2 = p.prev1;
+        p.prev1 = b;
+    }
+    p.src_pos += 64;
+}
+#else
+HG_INLINE void ring_refill(Parser &p) {
+    const int lane = p.lane;
+    uint32_t pos = p.src_pos + lane;
+    bool valid = pos < p.nal_end;
+    uint32_t b = valid ? p.src[pos] : 0xffu;
+    uint32_t b64 = (p.src_pos + 64 < p.nal_end) ? p.src[p.src_pos + 64] : 0xffu;
+    uint32_t nb = __shfl(b, (lane + 1) & 63, 64);
+    if (lane == 63) nb = b64;
+    uint32_t bm1 = __shfl(b, (lane + 63) & 63, 64);
+    uint32_t bm2 = __shfl(b, (lane + 62) & 63, 64);
+    if (lane == 0) {
+        bm1 = p.prev1;
+        bm2 = p.prev2;
+    } else if (lane == 1) {
+        bm2 = p.prev1;
+    }
+    // rbsp_reader.rs:11-39: 00 00 03 followed by a byte <= 3 (or the end)
+    bool ep = valid && bm2 == 0 && bm1 == 0 && b == 3 && (pos + 1 >= p.nal_end || nb <= 3);
+    bool keep = valid && !ep;
+    uint64_t m = __ballot(keep);
+    uint32_t idx = __popcll(m & ((1ull << lane) - 1ull));
+    if (keep) p.w->ring[(p.wr + idx) & 255] = (uint8_t)b;
+    p.wr += __popcll(m);
+    p.prev2 = uni(__shfl(b, 62, 64));
+    p.prev1 = uni(__shfl(b, 63, 64));
+    p.src_pos += 64;
+}
+#endif
+
+__device__ __forceinline__ uint32_t next_byte(Parser &p) {
+    if (p.rd == p.wr) {
+        if (p.src_pos >= p.nal_end) {
+            p.status |= ST_OVERRUN;
+            return 0;
+        }
+        ring_refill(p);
+        if (p.rd == p.wr) {
+            p.status |= ST_OVERRUN;
+            return 0;
+        }
+    }
+    uint32_t v = uni(p.w->ring[p.rd & 255]);
+    ++p.rd;
+    return v;
+}
+
+// 9.3.2.5 initialization of the arithmetic decoding engine at a raw offset
+HG_INLINE void engine_init(Parser &p, uint32_t raw_start) {
+    p.src_pos = raw_start;
+    p.rd = p.wr = 0;
+    p.prev1 = raw_start >= 1 ? p.src[raw_start - 1] : 0xffu;
+    p.prev2 = raw_start >= 2 ? p.src[raw_start - 2] : 0xffu;
+    p.prev1 = uni(p.prev1);
+    p.prev2 = uni(p.prev2);
+    p.range = 510;
+    uint32_t b0 = next_byte(p);
+    uint32_t b1 = next_byte(p);
+    p.value = (b0 << 8) | b1;
+    p.bits_needed = -8;
+    if ((p.value >> 7) >= 510) p.status |= ST_CABAC_INIT;
+}
+
+// 9.3.2.2 context initialization
+HG_INLINE void ctx_init(Parser &p) {
+    for (int i = p.lane; i < CTX_NUM; i += kWave) p.w->ctx[i] = ctx_init_state(c_ctx_init[i], p.sliceQp);
+}
+
+// ---------------------------------------------------------------- engine
+// 9.3.4.3.2 DecodeDecision (arithmetic.rs:97-144)
+HG_INLINE int dec_bin(Parser &p, int ci) {
+    uint32_t s = uni(p.w->ctx[ci]);
+    uint32_t st = s >> 1, mps = s & 1;
+    uint32_t lps = c_lps[(st << 2) | ((p.range >> 6) & 3)];
+    p.range -= lps;
+    uint32_t scaled = p.range << 7;
+    int bin;
+    if (p.value < scaled) {
+        bin = (int)mps;
+        st = st < 62 ? st + 1 : st;
+        if (scaled < (256u << 7)) {
+            p.range = scaled >> 6;
+            p.value <<= 1;
+            if (++p.bits_needed == 0) {
+                p.bits_needed = -8;
+                p.value |= next_byte(p);
+            }
+        }
+    } else {
+        p.value -= scaled;
+        int nbits = __builtin_clz(lps) - 23;
+        p.value <<= nbits;
+        p.range = lps << nbits;
+        bin = (int)(mps ^ 1u);
+        if (st == 0) mps ^= 1u;
+        st = c_trans_lps[st];
+        p.bits_needed += nbits;
+        if (p.bits_needed >= 0) {
+            p.value |= next_byte(p) << p.bits_needed;
+            p.bits_needed -= 8;
+        }
+    }
+    p.w->ctx[ci] = (uint8_t)((st << 1) | mps);
+    return bin;
+}
+
+// 9.3.4.3.4 DecodeBypass (arithmetic.rs:146-157)
+__device__ __forceinline__ int dec_bypass(Parser &p) {
+    p.value <<= 1;
+    if (++p.bits_needed >= 0) {
+        p.bits_needed = -8;
+        p.value |= next_byte(p);
+    }
+    uint32_t scaled = p.range << 7;
+    if (p.value >= scaled) {
+        p.value -= scaled;
+        return 1;
+    }
+    return 0;
+}
+
+HG_INLINE uint32_t dec_bypass_bits(Parser &p, int n) {
+    uint32_t v = 0;
+    for (int i = 0; i < n; ++i) v = (v << 1) | (uint32_t)dec_bypass(p);
+    return v;
+}
+
+// 9.3.4.3.5 DecodeTerminate (arithmetic.rs:159-169)
+HG_INLINE int dec_term(Parser &p) {
+    p.range -= 2;
+    uint32_t scaled = p.range << 7;
+    if (p.value >= scaled) return 1;
+    if (scaled < (256u << 7)) {
+        p.range = scaled >> 6;
+        p.value <<= 1;
+        if (++p.bits_needed == 0) {
+            p.bits_needed = -8;
+            p.value |= next_byte(p);
+        }
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ int chroma_qp_map(int qpi, int chroma) {
+    if (chroma != 1) return qpi < 51 ? qpi : 51;
+    if (qpi < 30) return qpi;
+    if (qpi > 43) return qpi - 6;
+    constexpr int t[14] = {29, 30, 31, 32, 33, 33, 34, 34, 35, 35, 36, 36, 37, 37};
+    return t[qpi - 30];
+}
+
+__device__ __forceinline__ void update_qpy(Parser &p) {
+    p.qpy_cur = ((p.qp_pred + p.cu_qp_delta_val + 52 + 2 * p.qpbdY) % (52 + p.qpbdY)) - p.qpbdY;
+}
+
+// 8.6.1: qPY_PRED of the current quantization group
+HG_INLINE void derive_qp_pred(Parser &p) {
+    int prev;
+    bool first_in_ctb = p.qg_x == p.ctbx && p.qg_y == p.ctby;
+    if (p.first_qg_in_slice) {
+        prev = p.sliceQp;
+        p.first_qg_in_slice = false;
+    } else if ((p.flags & SP_WPP) && first_in_ctb && p.rx == 0) {
+        prev = p.sliceQp;
+    } else {
+        prev = p.qp_prev_last;
+    }
+    int mask = p.ctb - 1;
+    int qa = (p.qg_x & mask) ? unis(p.w->qpy[(p.qg_y - p.ctby) >> 3][((p.qg_x - p.ctbx) >> 3) - 1]) : prev;
+    int qb = (p.qg_y & mask) ? unis(p.w->qpy[((p.qg_y - p.ctby) >> 3) - 1][(p.qg_x - p.ctbx) >> 3]) : prev;
+    p.qp_pred = (qa + qb + 1) >> 1;
+}
+
+// ---------------------------------------------------------------- SAO syntax (7.3.8.3)
+HG_INLINE void parse_sao(Parser &p, SaoParams *sao_line_above, SaoParams *gsao) {
+    SaoParams s;
+    for (int c = 0; c < 3; ++c) {
+        s.type[c] = 0;
+        s.band_eo[c] = 0;
+        for (int i = 0; i < 4; ++i) s.off[c][i] = 0;
+    }
+    int ml = 0, mu = 0;
+    if (p.rx > 0) ml = dec_bin(p, CTX_SAO_MERGE);
+    if (p.ry > 0 && !ml) mu = dec_bin(p, CTX_SAO_MERGE);
+    if (ml) {
+        s = p.w->sao_left;
+    } else if (mu) {
+        s = sao_line_above[p.rx];
+    } else {
+        int ncomp = p.chroma ? 3 : 1;
+        for (int c = 0; c < ncomp; ++c) {
+            if (!((p.saoL && c == 0) || (p.saoC && c > 0))) continue;
+            if (c < 2) {
+                int t = 0;
+                if (dec_bin(p, CTX_SAO_TYPE)) t = dec_bypass(p) ? 2 : 1;
+                s.type[c] = (int8_t)t;
+            } else {
+                s.type[2] = s.type[1];
+            }
+            if (!s.type[c]) continue;
+            int bd = c ? p.bdC : p.bdY;
+            uint32_t cmax = (1u << ((bd < 10 ? bd : 10) - 5)) - 1;
+            int a[4];
+            for (int i = 0; i < 4; ++i) a[i] = (int)bin_truncated_rice([&]() { return dec_bypass(p); }, cmax, 0);
+            if (s.type[c] == 1) {
+                for (int i = 0; i < 4; ++i)
+                    if (a[i] && dec_bypass(p)) a[i] = -a[i];
+                s.band_eo[c] = (uint8_t)dec_bypass_bits(p, 5);
+                for (int i = 0; i < 4; ++i) s.off[c][i] = (int16_t)a[i];
+            } else {
+                if (c == 0) s.band_eo[0] = (uint8_t)dec_bypass_bits(p, 2);
+                if (c == 1) s.band_eo[1] = (uint8_t)dec_bypass_bits(p, 2);
+                if (c == 2) s.band_eo[2] = s.band_eo[1];
+                s.off[c][0] = (int16_t)a[0];
+                s.off[c][1] = (int16_t)a[1];
+                s.off[c][2] = (int16_t)-a[2];
+                s.off[c][3] = (int16_t)-a[3];
+            }
+        }
+    }
+    if (p.lane == 0) {
+        p.w->sao_left = s;
+        gsao[p.ry * p.wctb + p.rx] = s;
+    }
+}
+
+// ---------------------------------------------------------------- residual_coding (7.3.8.11)
+HG_INLINE void residual_coding(Parser &p, int log2n, int cidx, int mode, bool &ts, uint32_t &coef_first,
+                                uint32_t &ncoef) {
+    const int n = 1 << log2n;
+    ts = false;
+    if ((p.flags & SP_TRANSFORM_SKIP) && !p.cu_bypass && log2n == 2) ts = dec_bin(p, CTX_TS_FLAG + (cidx ? 1 : 0));
+    // last_sig_coeff_{x,y}_prefix (decoder.rs:109-130), suffixes (bypass)
+    int cmax = (log2n << 1) - 1;
+    int off, shift;
+    if (cidx == 0) {
+        off = 3 * (log2n - 2) + ((log2n - 1) >> 2);
+        shift = (log2n + 1) >> 2;
+    } else {
+        off = 15;
+        shift = log2n - 2;
+    }
+    int px = 0, py = 0;
+    while (px < cmax && dec_bin(p, CTX_LAST_X + off + (px >> shift))) ++px;
+    while (py < cmax && dec_bin(p, CTX_LAST_Y + off + (py >> shift))) ++py;
+    int lx = px, ly = py;
+    if (px > 3) {
+        int k = (px >> 1) - 1;
+        lx = (1 << k) * (2 + (px & 1)) + (int)dec_bypass_bits(p, k);
+    }
+    if (py > 3) {
+        int k = (py >> 1) - 1;
+        ly = (1 << k) * (2 + (py & 1)) + (int)dec_bypass_bits(p, k);
+    }
+    // 7.4.9.11 scanIdx
+    int scan = 0;
+    if (log2n == 2 || (log2n == 3 && cidx == 0)) {
+        if (mode >= 6 && mode <= 14) scan = 2;
+        else if (mode >= 22 && mode <= 30) scan = 1;
+    }
+    if (scan == 2) {
+        int t = lx;
+        lx = ly;
+        ly = t;
+    }
+    if (lx >= n || ly >= n) {
+        p.status |= ST_SYNTAX;
+        lx &= n - 1;
+        ly &= n - 1;
+    }
+    const int sbl = log2n - 2, sbw = 1 << sbl;
+    const int last_sub = kScanInv[sbl][scan][(ly >> 2) * sbw + (lx >> 2)];
+    const int last_pos = kScanInv[2][scan][(ly & 3) * 4 + (lx & 3)];
+    uint64_t csbf = 0;  // coded_sub_block_flag bitmap, bit yS*8+xS
+    int prev_c1 = 1;    // greater1Ctx state carried from the previous coded sub-block
+    bool any_sb = false;
+    coef_first = p.ncoef;
+    ncoef = 0;
+    for (int i = last_sub; i >= 0; --i) {
+        const int sp = kScanPos[sbl][scan][i];
+        const int xS = sp & 15, yS = sp >> 4;
+        bool coded;
+        bool infer_dc = false;
+        int prev_csbf = 0;
+        if (xS < sbw - 1) prev_csbf |= (int)((csbf >> (yS * 8 + xS + 1)) & 1);
+        if (yS < sbw - 1) prev_csbf |= (int)((csbf >> ((yS + 1) * 8 + xS)) & 1) << 1;
+        if (i < last_sub && i > 0) {
+            int ctx = ((prev_csbf & 1) | (prev_csbf >> 1)) + (cidx ? 2 : 0);
+            coded = dec_bin(p, CTX_CSBF + ctx);
+            infer_dc = true;
+        } else {
+            coded = true;
+        }
+        if (coded) csbf |= 1ull << (yS * 8 + xS);
+        uint32_t sig = 0;
+        if (coded) {
+            int nstart = 15;
+            if (i == last_sub) {
+                sig = 1u << last_pos;
+                nstart = last_pos - 1;
+            }
+            for (int nn = nstart; nn >= 0; --nn) {
+                const int pp = kScanPos[2][scan][nn];
+                const int xP = pp & 15, yP = pp >> 4;
+                if (nn > 0 || !infer_dc) {
+                    const int xC = (xS << 2) + xP, yC = (yS << 2) + yP;
+                    int sc;
+                    if (log2n == 2) {
+                        constexpr uint8_t map[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+                        sc = map[(yC << 2) + xC];
+                    } else if (xC + yC == 0) {
+                        sc = 0;
+                    } else {
+                        if (prev_csbf == 0) sc = (xP + yP == 0) ? 2 : (xP + yP < 3) ? 1 : 0;
+                        else if (prev_csbf == 1) sc = (yP == 0) ? 2 : (yP == 1) ? 1 : 0;
+                        else if (prev_csbf == 2) sc = (xP == 0) ? 2 : (xP == 1) ? 1 : 0;
+                        else sc = 2;
+                        if (cidx == 0) {
+                            if (xS > 0 || yS > 0) sc += 3;
+                            sc += (log2n == 3) ? (scan == 0 ? 9 : 15) : 21;
+                        } else {
+                            sc += (log2n == 3) ? 9 : 12;
+                        }
+                    }
+                    if (dec_bin(p, CTX_SIG + (cidx ? 27 + sc : sc))) {
+                        sig |= 1u << nn;
+                        infer_dc = false;
+                    }
+                } else {
+                    sig |= 1u;  // inferred DC of a coded sub-block
+                }
+            }
+        }
+        if (!sig) continue;
+        // greater1 / greater2 (9.3.4.2.6-7)
+        int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
+        if (any_sb && prev_c1 == 0) ++ctx_set;
+        any_sb = true;
+        int c1 = 1;
+        uint32_t g1 = 0, g2 = 0;
+        int first_sig = 31 - __builtin_clz(sig & -sig);  // lowest set bit
+        int last_sig = 31 - __builtin_clz(sig);
+        int num_g1 = 0, last_g1 = -1;
+        for (uint32_t m = sig; m; ) {
+            int nn = 31 - __builtin_clz(m);
+            m &= ~(1u << nn);
+            if (num_g1 >= 8) break;
+            int ci = ctx_set * 4 + (c1 < 3 ? c1 : 3) + (cidx ? 16 : 0);
+            int f = dec_bin(p, CTX_GT1 + ci);
+            ++num_g1;
+            if (f) {
+                g1 |= 1u << nn;
+                if (last_g1 < 0) last_g1 = nn;
+            }
+            if (c1 > 0) c1 = f ? 0 : c1 + 1;
+        }
+        prev_c1 = c1;
+        bool sign_hidden = !p.cu_bypass && (last_sig - first_sig > 3);
+        if (last_g1 >= 0 && dec_bin(p, CTX_GT2 + ctx_set + (cidx ? 4 : 0))) g2 = 1u << last_g1;
+        bool hide = (p.flags & SP_SIGN_HIDING) && sign_hidden;
+        int nsign = __builtin_popcount(sig) - (hide ? 1 : 0);
+        uint32_t signs = dec_bypass_bits(p, nsign);
+        signs = nsign ? signs << (32 - nsign) : 0u;  // first decoded sign in bit 31
+        int num_sig = 0, sum_abs = 0;
+        int c_last_abs = 0, c_last_rice = 0;
+        bool first_rem = true;
+        for (uint32_t m = sig; m; ) {
+            int nn = 31 - __builtin_clz(m);
+            m &= ~(1u << nn);
+            int base = 1 + (int)((g1 >> nn) & 1) + (int)((g2 >> nn) & 1);
+            int rem = 0;
+            if (base == ((num_sig < 8) ? ((nn == last_g1) ? 3 : 2) : 1)) {
+                int k;
+                if (first_rem) {
+                    k = 0;
+                    first_rem = false;
+                } else {
+                    k = c_last_rice + (c_last_abs > 3 * (1 << c_last_rice) ? 1 : 0);
+                    k = k < 4 ? k : 4;
+                }
+                uint32_t r = bin_coeff_abs_level_remaining([&]() { return dec_bypass(p); }, k);
+                if (r == 0xffffffffu) {
+                    p.status |= ST_SYNTAX;
+                    r = 0;
+                }
+                rem = (int)r;
+                c_last_abs = base + rem;
+                c_last_rice = k;
+            }
+            int v = base + rem;
+            bool neg;
+            if (hide && nn == first_sig) {
+                sum_abs += v;
+                neg = (sum_abs & 1) != 0;
+            } else {
+                neg = (signs >> 31) != 0;
+                signs <<= 1;
+                if (hide) sum_abs += v;
+            }
+            if (neg) v = -v;
+            const int pp = kScanPos[2][scan][nn];
+            const int xC = (xS << 2) + (pp & 15), yC = (yS << 2) + (pp >> 4);
+            if (v > 32767) v = 32767;
+            if (v < -32768) v = -32768;
+            if (p.ncoef < p.coef_cap) {
+                if (p.lane == 0)
+                    p.coef_out[p.ncoef] = ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC);
+                ++p.ncoef;
+                ++ncoef;
+            } else {
+                p.status |= ST_CAPACITY;
+            }
+            ++num_sig;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- TB emission
+HG_INLINE void emit_tb(Parser &p, int cidx, int x, int y, int log2n, int mode, bool cbf) {
+    bool ts = false;
+    uint32_t first = p.ncoef, nc = 0;
+    if (cbf) residual_coding(p, log2n, cidx, mode, ts, first, nc);
+    int qp;
+    if (cidx == 0) {
+        qp = p.qpy_cur + p.qpbdY;
+    } else {
+        int off = cidx == 1 ? p.cbOff : p.crOff;
+        int qpi = p.qpy_cur + off;
+        qpi = qpi < -p.qpbdC ? -p.qpbdC : (qpi > 57 ? 57 : qpi);
+        qp = chroma_qp_map(qpi, p.chroma) + p.qpbdC;
+    }
+    uint8_t fl = (uint8_t)cidx;
+    if (cbf) fl |= TU_CBF;
+    if (ts) fl |= TU_TSKIP;
+    if (p.cu_bypass) fl |= TU_BYPASS;
+    if (cidx == 0 && log2n == 2) fl |= TU_DST;
+    if (p.ntu < p.tu_cap) {
+        if (p.lane == 0) {
+            TuRec r;
+            r.x = (uint16_t)x;
+            r.y = (uint16_t)y;
+            r.log2 = (uint8_t)log2n;
+            r.flags = fl;
+            r.mode = (uint8_t)mode;
+            r.qp = (uint8_t)qp;
+            r.coef = first;
+            r.ncoef = (uint16_t)nc;
+            r.ctu = (uint16_t)p.rx;
+            p.tu_out[p.ntu] = r;
+        }
+        ++p.ntu;
+    } else {
+        p.status |= ST_CAPACITY;
+    }
+}
+
+// 7.3.8.10 transform_unit
+HG_INLINE void transform_unit(Parser &p, int x0, int y0, int xb, int yb, int log2n, int blk, bool cbf_l, bool cbf_cb,
+                               bool cbf_cr, bool pcb, bool pcr) {
+    const bool chroma4 = p.chroma == 1 && log2n == 2;
+    const bool cbf_c = p.chroma == 0 ? false : (chroma4 ? (pcb || pcr) : (cbf_cb || cbf_cr));
+    if ((cbf_l || cbf_c) && (p.flags & SP_CU_QP_DELTA) && !p.is_cu_qp_delta_coded) {
+        int v = 0;
+        while (v < 5 && dec_bin(p, CTX_CU_QP_DELTA + (v == 0 ? 0 : 1))) ++v;
+        if (v == 5) {
+            uint32_t s = bin_exp_golomb([&]() { return dec_bypass(p); }, 0);
+            if (s == 0xffffffffu) {
+                p.status |= ST_SYNTAX;
+                s = 0;
+            }
+            v += (int)s;
+        }
+        if (v && dec_bypass(p)) v = -v;
+        p.is_cu_qp_delta_coded = true;
+        p.cu_qp_delta_val = v;
+        update_qpy(p);
+    }
+    // edge / no-filter flags of every 4x4 luma block of this TB (MF_*)
+    {
+        const int nb = 1 << (log2n - 2);
+        for (int k = p.lane; k < nb * nb; k += kWave) {
+            int bx = k % nb, by = k / nb;
+            int gx = (x0 >> 2) + bx, gy = (y0 >> 2) + by;
+            if (gx < p.w4 && gy < p.h4)
+                p.gflags[gy * p.w4 + gx] =
+                    (uint8_t)((bx == 0 ? MF_EDGE_V : 0) | (by == 0 ? MF_EDGE_H : 0) | (p.cu_bypass ? MF_NOFILT : 0));
+        }
+    }
+    const int lmode = unis(p.w->ipm[(y0 - p.ctby) >> 2][((x0 - p.ctbx) >> 2) + 1]);
+    // luma TB, then (4:2:0) the Cb and Cr TBs — one emit_tb call site so it inlines once
+    int ntb = 1;
+    if (p.chroma != 0 && (!chroma4 || blk == 3)) ntb = 3;
+    for (int t = 0; t < ntb; ++t) {
+        int x, y, l, m;
+        bool cbf;
+        if (t == 0) {
+            x = x0, y = y0, l = log2n, m = lmode, cbf = cbf_l;
+        } else if (!chroma4) {
+            x = x0 >> 1, y = y0 >> 1, l = log2n - 1, m = p.cu_chroma_mode, cbf = t == 1 ? cbf_cb : cbf_cr;
+        } else {
+            x = xb >> 1, y = yb >> 1, l = 2, m = p.cu_chroma_mode, cbf = t == 1 ? pcb : pcr;
+        }
+        emit_tb(p, t, x, y, l, m, cbf);
+    }
+}
+
+// 7.3.8.8 transform_tree, iterative (pre-order, children 0..3)
+HG_INLINE void transform_tree(Parser &p, int x0, int y0, int log2cb) {
+    auto pack = [](int x, int y, int xb, int yb, int l, int d, int blk, int pcb, int pcr) -> uint64_t {
+        return (uint64_t)x | ((uint64_t)y << 13) | ((uint64_t)xb << 26) | ((uint64_t)yb << 39) |
+               ((uint64_t)l << 52) | ((uint64_t)d << 55) | ((uint64_t)blk << 58) | ((uint64_t)pcb << 60) |
+               ((uint64_t)pcr << 61);
+    };
+    uint64_t *st = p.w->tt;
+    int sp = 0;
+    if (p.lane == 0) st[0] = pack(x0, y0, x0, y0, log2cb, 0, 0, 0, 0);
+    sp = 1;
+    const int max_depth = p.maxDepthIntra + p.cu_intra_split;
+    while (sp > 0) {
+        --sp;
+        uint64_t e = st[sp];
+        uint32_t lo = uni((uint32_t)e), hi = uni((uint32_t)(e >> 32));
+        e = ((uint64_t)hi << 32) | lo;
+        int x = (int)(e & 8191), y = (int)((e >> 13) & 8191), xb = (int)((e >> 26) & 8191), yb = (int)((e >> 39) & 8191);
+        int l = (int)((e >> 52) & 7), d = (int)((e >> 55) & 7), blk = (int)((e >> 58) & 3);
+        bool pcb = (e >> 60) & 1, pcr = (e >> 61) & 1;
+        bool split;
+        if (l <= p.maxTb && l > p.minTb && d < max_depth && !(p.cu_intra_split && d == 0))
+            split = dec_bin(p, CTX_SPLIT_TF + 5 - l);
+        else
+            split = l > p.maxTb || (p.cu_intra_split && d == 0);
+        bool cbf_cb = false, cbf_cr = false;
+        if (l > 2 && p.chroma != 0) {
+            if (d == 0 || pcb) cbf_cb = dec_bin(p, CTX_CBF_CHROMA + d);
+            if (d == 0 || pcr) cbf_cr = dec_bin(p, CTX_CBF_CHROMA + d);
+        }
+        if (split) {
+            int h = 1 << (l - 1);
+            if (p.lane == 0) {
+                st[sp + 0] = pack(x + h, y + h, x, y, l - 1, d + 1, 3, cbf_cb, cbf_cr);
+                st[sp + 1] = pack(x, y + h, x, y, l - 1, d + 1, 2, cbf_cb, cbf_cr);
+                st[sp + 2] = pack(x + h, y, x, y, l - 1, d + 1, 1, cbf_cb, cbf_cr);
+                st[sp + 3] = pack(x, y, x, y, l - 1, d + 1, 0, cbf_cb, cbf_cr);
+            }
+            sp += 4;
+            continue;
+        }
+        bool cbf_l = dec_bin(p, CTX_CBF_LUMA + (d == 0 ? 1 : 0));
+        transform_unit(p, x, y, xb, yb, l, blk, cbf_l, cbf_cb, cbf_cr, pcb, pcr);
+    }
+}
+
+// 8.4.2 luma intra prediction mode
+HG_INLINE int derive_luma_mode(Parser &p, int xPb, int yPb, int prev, int mpm_idx, int rem) {
+    int ca, cb;
+    if (xPb <= 0) ca = 1;
+    else ca = unis(p.w->ipm[(yPb - p.ctby) >> 2][((xPb - 1 - p.ctbx) >> 2) + 1]);
+    if (yPb - 1 < p.ctby) cb = 1;  // above CTB (or picture edge) → DC
+    else cb = unis(p.w->ipm[((yPb - 1 - p.ctby) >> 2)][((xPb - p.ctbx) >> 2) + 1]);
+    int l0, l1, l2;
+    if (ca == cb) {
+        if (ca < 2) {
+            l0 = 0;
+            l1 = 1;
+            l2 = 26;
+        } else {
+            l0 = ca;
+            l1 = 2 + ((ca + 29) % 32);
+            l2 = 2 + ((ca - 2 + 1) % 32);
+        }
+    } else {
+        l0 = ca;
+        l1 = cb;
+        if (ca != 0 && cb != 0) l2 = 0;
+        else if (ca != 1 && cb != 1) l2 = 1;
+        else l2 = 26;
+    }
+    if (prev) return mpm_idx == 0 ? l0 : (mpm_idx == 1 ? l1 : l2);
+    int t;
+    if (l0 > l1) { t = l0; l0 = l1; l1 = t; }
+    if (l0 > l2) { t = l0; l0 = l2; l2 = t; }
+    if (l1 > l2) { t = l1; l1 = l2; l2 = t; }
+    int m = rem;
+    if (m >= l0) ++m;
+    if (m >= l1) ++m;
+    if (m >= l2) ++m;
+    return m;
+}
+
+// 7.3.8.5 coding_unit (intra)
+HG_INLINE void coding_unit(Parser &p, int x0, int y0, int log2cb, int depth) {
+    const int n = 1 << log2cb;
+    if (p.qg_new) {
+        derive_qp_pred(p);
+        p.qg_new = false;
+    }
+    update_qpy(p);
+    p.cu_bypass = (p.flags & SP_TQ_BYPASS) ? dec_bin(p, CTX_TQ_BYPASS) : 0;
+    int nxn = 0;
+    if (log2cb == p.minCb) nxn = !dec_bin(p, CTX_PART_MODE);
+    if (!nxn && (p.flags & SP_PCM) && log2cb >= p.pcmMin && log2cb <= p.pcmMax && dec_term(p)) {
+        // pcm_flag = 1: not supported on the GPU path (halfmoonbay has pcm_enabled_flag = 0)
+        p.status |= ST_UNSUPPORTED;
+        return;
+    }
+    // CtDepth of the CU
+    {
+        const int nd = n >> 3;
+        const int dx = (x0 - p.ctbx) >> 3, dy = (y0 - p.ctby) >> 3;
+        for (int k = p.lane; k < nd * nd; k += kWave) p.w->depth[dy + k / nd][dx + k % nd + 1] = (uint8_t)depth;
+    }
+    const int np = nxn ? 4 : 1, pb = nxn ? n >> 1 : n;
+    int prev[4] = {0, 0, 0, 0};
+    for (int i = 0; i < np; ++i) prev[i] = dec_bin(p, CTX_PREV_INTRA);
+    for (int i = 0; i < np; ++i) {
+        int mpm = 0, rem = 0;
+        if (prev[i]) mpm = dec_bypass(p) ? (dec_bypass(p) ? 2 : 1) : 0;
+        else rem = (int)dec_bypass_bits(p, 5);
+        const int xPb = x0 + (i & 1) * pb, yPb = y0 + (i >> 1) * pb;
+        const int m = derive_luma_mode(p, xPb, yPb, prev[i], mpm, rem);
+        const int nb = pb >> 2;
+        const int bx = (xPb - p.ctbx) >> 2, by = (yPb - p.ctby) >> 2;
+        for (int k = p.lane; k < nb * nb; k += kWave) p.w->ipm[by + k / nb][bx + k % nb + 1] = (uint8_t)m;
+    }
+    if (p.chroma != 0) {
+        int icpm = dec_bin(p, CTX_CHROMA_MODE) ? (int)dec_bypass_bits(p, 2) : 4;
+        int lm = unis(p.w->ipm[(y0 - p.ctby) >> 2][((x0 - p.ctbx) >> 2) + 1]);
+        int cm;
+        if (icpm == 4) {
+            cm = lm;
+        } else {
+            cm = icpm == 0 ? 0 : (icpm == 1 ? 26 : (icpm == 2 ? 10 : 1));
+            if (cm == lm) cm = 34;
+        }
+        p.cu_chroma_mode = cm;
+    }
+    p.cu_intra_split = nxn;
+    transform_tree(p, x0, y0, log2cb);
+    // QpY of the CU: local 8x8 map (for qPY_A/B) and global 4x4 map (deblocking)
+    {
+        const int nd = n >> 3;
+        const int dx = (x0 - p.ctbx) >> 3, dy = (y0 - p.ctby) >> 3;
+        for (int k = p.lane; k < nd * nd; k += kWave) p.w->qpy[dy + k / nd][dx + k % nd] = (int8_t)p.qpy_cur;
+        const int nb = n >> 2;
+        for (int k = p.lane; k < nb * nb; k += kWave) {
+            int gx = (x0 >> 2) + k % nb, gy = (y0 >> 2) + k / nb;
+            if (gx < p.w4 && gy < p.h4) p.gqpy[gy * p.w4 + gx] = (int8_t)p.qpy_cur;
+        }
+    }
+    p.qp_prev_last = p.qpy_cur;
+}
+
+// 7.3.8.4 coding_quadtree, iterative
+HG_INLINE void coding_quadtree(Parser &p) {
+    uint32_t *st = p.w->cqt;
+    if (p.lane == 0) st[0] = (uint32_t)p.ctbx | ((uint32_t)p.ctby << 13) | ((uint32_t)p.log2ctb << 26);
+    int sp = 1;
+    while (sp > 0 && !(p.status & ST_UNSUPPORTED)) {
+        --sp;
+        uint32_t e = uni(st[sp]);
+        int x = (int)(e & 8191), y = (int)((e >> 13) & 8191), l = (int)((e >> 26) & 7), d = (int)(e >> 29);
+        const int n = 1 << l;
+        bool split;
+        if (x + n <= p.W && y + n <= p.H && l > p.minCb) {
+            int cond = 0;
+            const int dx = (x - p.ctbx) >> 3, dy = (y - p.ctby) >> 3;
+            if (x > 0 && unis(p.w->depth[dy][dx]) > d) ++cond;  // column dx is x-8 (shifted by 1)
+            if (y > 0) {
+                int ad = (y - 1 < p.ctby) ? unis(p.depth_above[x >> 3]) : unis(p.w->depth[dy - 1][dx + 1]);
+                if (ad > d) ++cond;
+            }
+            split = dec_bin(p, CTX_SPLIT_CU + cond);
+        } else {
+            split = l > p.minCb;
+        }
+        if (l >= p.log2qg) {
+            p.is_cu_qp_delta_coded = false;
+            p.cu_qp_delta_val = 0;
+            p.qg_new = true;
+            p.qg_x = x;
+            p.qg_y = y;
+        }
+        if (split) {
+            const int h = n >> 1;
+            auto pk = [&](int cx, int cy) {
+                return (uint32_t)cx | ((uint32_t)cy << 13) | ((uint32_t)(l - 1) << 26) | ((uint32_t)(d + 1) << 29);
+            };
+            // push in reverse so child 0 is processed first
+            if (x + h < p.W && y + h < p.H) {
+                if (p.lane == 0) st[sp] = pk(x + h, y + h);
+                ++sp;
+            }
+            if (y + h < p.H) {
+                if (p.lane == 0) st[sp] = pk(x, y + h);
+                ++sp;
+            }
+            if (x + h < p.W) {
+                if (p.lane == 0) st[sp] = pk(x + h, y);
+                ++sp;
+            }
+            if (p.lane == 0) st[sp] = pk(x, y);
+            ++sp;
+            continue;
+        }
+        coding_unit(p, x, y, l, d);
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- kernel
+__global__ void __launch_bounds__(kParseWaves * 64) k_parse(BatchArgs a) {
+#if defined(HG_HOST_EMU)
+    unsigned char *smem = g_emu.smem;
+#else
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#endif
+    const int pic = blockIdx.x;
+    const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const PicDesc pd = a.pics[pic];
+    const SeqParams sp = a.seqs[pd.seq];
+
+    WaveLds *wl = reinterpret_cast<WaveLds *>(smem) + wave;
+    uint32_t *progress = reinterpret_cast<uint32_t *>(smem + sizeof(WaveLds) * kParseWaves);
+    uint8_t *wpp_slot = reinterpret_cast<uint8_t *>(progress + kParseWaves);  // [2][CTX_PAD]
+    const int dl_stride = ((a.max_width >> 3) + 15) & ~15;
+    uint8_t *depth_line = wpp_slot + 2 * CTX_PAD;                              // [2][dl_stride]
+    SaoParams *sao_line = reinterpret_cast<SaoParams *>(depth_line + 2 * dl_stride);  // [2][max_wctb]
+
+    Parser p;
+    p.W = sp.width;
+    p.H = sp.height;
+    p.log2ctb = sp.log2_ctb;
+    p.ctb = 1 << sp.log2_ctb;
+    p.wctb = (p.W + p.ctb - 1) >> p.log2ctb;
+    p.hctb = (p.H + p.ctb - 1) >> p.log2ctb;
+    p.minCb = sp.log2_min_cb;
+    p.minTb = sp.log2_min_tb;
+    p.maxTb = sp.log2_max_tb;
+    p.maxDepthIntra = sp.max_th_depth_intra;
+    p.chroma = sp.chroma_format;
+    p.bdY = sp.bit_depth_y;
+    p.bdC = sp.bit_depth_c;
+    p.qpbdY = 6 * (p.bdY - 8);
+    p.qpbdC = 6 * (p.bdC - 8);
+    p.flags = sp.flags;
+    p.pcmMin = sp.log2_min_pcm;
+    p.pcmMax = sp.log2_max_pcm;
+    p.log2qg = p.log2ctb - sp.diff_cu_qp_delta_depth;
+    p.cbOff = sp.cb_qp_offset + pd.cb_qp_off;
+    p.crOff = sp.cr_qp_offset + pd.cr_qp_off;
+    p.sliceQp = pd.slice_qp;
+    p.saoL = pd.sao_luma;
+    p.saoC = pd.sao_chroma;
+    p.src = a.bits + pd.bits_off;
+    p.nal_end = pd.bits_len;
+    p.status = 0;
+    p.w = wl;
+    p.lane = lane;
+    p.w4 = (p.W + 3) >> 2;
+    p.h4 = (p.H + 3) >> 2;
+    p.gqpy = reinterpret_cast<int8_t *>(a.maps + pd.map_off);
+    p.gflags = a.maps + pd.map_off + (size_t)p.w4 * p.h4;
+    SaoParams *gsao = a.sao + pd.sao_off;
+    const uint32_t *subs = a.subs + pd.sub_first;
+    const bool wpp = (p.flags & SP_WPP) != 0;
+
+    if (lane == 0) progress[wave] = 0;
+    __syncthreads();
+
+    // rows: WPP → one substream per CTB row, wave w takes rows w, w+16, ...;
+    // otherwise the picture is one substream and wave 0 walks every row.
+    const int row_step = wpp ? kParseWaves : 1;
+    const int first_row = wpp ? wave : (wave == 0 ? 0 : p.hctb);
+    const uint32_t stride = (uint32_t)p.wctb + 1;
+    const int prev_wave = (wave + kParseWaves - 1) % kParseWaves;
+    bool stop = false;
+    for (int r = first_row; r < p.hctb && !stop; r += row_step) {
+        p.ry = r;
+        p.tu_out = a.tus + pd.tu_off + (uint64_t)r * pd.tu_cap_row;
+        p.coef_out = a.coefs + pd.coef_off + (uint64_t)r * pd.coef_cap_row;
+        p.ntu = p.ncoef = 0;
+        p.tu_cap = pd.tu_cap_row;
+        p.coef_cap = pd.coef_cap_row;
+        p.depth_above = depth_line + ((r + 1) & 1) * dl_stride;
+        uint8_t *depth_cur_line = depth_line + (r & 1) * dl_stride;
+        SaoParams *sao_above = sao_line + ((r + 1) & 1) * a.max_wctb;
+        SaoParams *sao_cur_line = sao_line + (r & 1) * a.max_wctb;
+        for (int c = 0; c < p.wctb; ++c) {
+            p.rx = c;
+            p.ctbx = c << p.log2ctb;
+            p.ctby = r << p.log2ctb;
+            if (wpp && r > 0) {
+                // WPP lag: row r-1 must have finished CTU min(c+1, wctb-1)
+                const uint32_t need = (uint32_t)(r - 1) * stride + (uint32_t)((c + 2) < p.wctb ? (c + 2) : p.wctb);
+                for (uint32_t spin = 0; hg_atomic_load(&progress[prev_wave]) < need; ++spin) {
+                    if (spin > (1u << 24)) {  // bounded: never hang the device
+                        p.status |= ST_SUBSTREAM_END;
+                        break;
+                    }
+                    HG_SLEEP();
+                }
+                HG_FENCE_ACQ();
+            }
+            if (c == 0 && (wpp || r == 0)) {
+                // substream start: contexts (init or WPP sync, 9.3.1) + engine (9.3.2.5)
+                if (r == 0 || p.wctb < 2) ctx_init(p);
+                else
+                    for (int i = lane; i < CTX_PAD; i += kWave) wl->ctx[i] = wpp_slot[((r + 1) & 1) * CTX_PAD + i];
+                engine_init(p, subs[wpp ? r : 0]);
+                if (r == 0) p.first_qg_in_slice = true;
+            }
+            // left-CTB columns of the per-wave maps
+            if (c > 0) {
+                const int nb4 = p.ctb >> 2, nb8 = p.ctb >> 3;
+                for (int k = lane; k < nb4; k += kWave) wl->ipm[k][0] = wl->ipm[k][nb4];
+                for (int k = lane; k < nb8; k += kWave) wl->depth[k][0] = wl->depth[k][nb8];
+            }
+            if (p.saoL || p.saoC) parse_sao(p, sao_above, gsao);
+            coding_quadtree(p);
+            if (p.status & ST_UNSUPPORTED) {
+                stop = true;
+            }
+            if (wpp && c == 1)
+                for (int i = lane; i < CTX_PAD; i += kWave) wpp_slot[(r & 1) * CTX_PAD + i] = wl->ctx[i];
+            // bottom row of this CTB for the row below: depths, SAO parameters
+            {
+                const int nb8 = p.ctb >> 3;
+                for (int k = lane; k < nb8; k += kWave) depth_cur_line[(p.ctbx >> 3) + k] = wl->depth[nb8 - 1][k + 1];
+                if (lane == 0) sao_cur_line[c] = wl->sao_left;
+            }
+            // end_of_slice_segment_flag / end_of_subset_one_bit (slice.rs:214-227)
+            const bool last_in_pic = (r == p.hctb - 1) && (c == p.wctb - 1);
+            int eos = dec_term(p);
+            if (eos != (last_in_pic ? 1 : 0)) p.status |= ST_SUBSTREAM_END;
+            if (!last_in_pic && wpp && c == p.wctb - 1) {
+                if (!dec_term(p)) p.status |= ST_SUBSTREAM_END;
+            }
+            // publish progress (release: LDS lines, WPP slot, global maps)
+            HG_FENCE_REL();
+            if (lane == 0) hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)(c + 1));
+            if (stop) break;
+        }
+        if (lane == 0) {
+            a.row_counts[2 * (pd.row_off + r)] = p.ntu;
+            a.row_counts[2 * (pd.row_off + r) + 1] = p.ncoef;
+        }
+    }
+    if (stop && wpp) {
+        // let rows waiting on this wave drain
+        if (lane == 0) hg_atomic_store(&progress[wave], 0x7fffffffu);
+    }
+    if (p.status && lane == 0) atomicOr(&a.status[pic], p.status);
+}
+
+size_t parse_lds_bytes(int max_width, int max_wctb) {
+    size_t dl_stride = (size_t)(((max_width >> 3) + 15) & ~15);
+    return sizeof(WaveLds) * kParseWaves + sizeof(uint32_t) * kParseWaves + 2 * CTX_PAD + 2 * dl_stride +
+           2 * (size_t)max_wctb * sizeof(SaoParams);
+}
+
+#if defined(HG_HOST_EMU)
+void emu_parse(const BatchArgs &a) {
+    emu_launch(k_parse, a.n_pics, 1, kParseWaves, a, false, parse_lds_bytes(a.max_width, a.max_wctb));
+}
+#else
+hipError_t launch_parse(const BatchArgs &a, hipStream_t s) {
+    size_t lds = parse_lds_bytes(a.max_width, a.max_wctb);
+    hipLaunchKernelGGL(k_parse, dim3(a.n_pics), dim3(kParseWaves * 64), lds, s, a);
+    return hipGetLastError();
+}
+#endif
+
+}  // namespace hg

@@ -1,0 +1,168 @@
+// transform.hip — scaling + inverse transform (pipeline stage 2).
+//
+// H.265 8.6.2 (residual derivation), 8.6.3 (scaling with ScalingFactor m and
+// levelScale, 64-bit products, clip to 16 bits), 8.6.4.2 (two-stage inverse
+// DST-VII 4x4 / DCT 4..32, first-stage (e + 64) >> 7 clipped to 16 bits,
+// second stage + (20 - bitDepth) shift).  No reference code exists for this
+// (slice.rs:253-255 is todo!()).
+//
+// Mapping: every coded TB is independent, so this stage runs at full chip
+// parallelism: one 256-thread workgroup per CTB row of a picture, each wave
+// taking every 4th TB of the row's TU list.  Coefficients arrive sparse
+// (value, raster position) and are scattered into a per-wave LDS tile; the
+// row pass only spans rows up to the last nonzero coefficient row.  Integer
+// butterflies on VALU — no MFMA (the products are exact int32, and TBs are
+// at most 32x32).
+#include "kernels.hpp"
+
+namespace hg {
+
+namespace {
+
+constexpr int kWaves = 4;
+
+// transMatrix of 8.6.4.2 (32x32 DCT; smaller sizes use rows k * 32/n)
+struct TransMatrix {
+    int8_t m[32][32];
+};
+constexpr TransMatrix make_matrix() {
+    TransMatrix t{};
+    constexpr int odd[16] = {90, 90, 88, 85, 82, 78, 73, 67, 61, 54, 46, 38, 31, 22, 13, 4};
+    constexpr int e2[8] = {90, 87, 80, 70, 57, 43, 25, 9};
+    constexpr int e4[4] = {89, 75, 50, 18};
+    int cv[33] = {};
+    cv[0] = 64;
+    cv[8] = 83;
+    cv[16] = 64;
+    cv[24] = 36;
+    cv[32] = 0;
+    for (int i = 0; i < 16; ++i) cv[2 * i + 1] = odd[i];
+    for (int i = 0; i < 8; ++i) cv[2 * (2 * i + 1)] = e2[i];
+    for (int i = 0; i < 4; ++i) cv[4 * (2 * i + 1)] = e4[i];
+    for (int k = 0; k < 32; ++k)
+        for (int n = 0; n < 32; ++n) {
+            int j = ((2 * n + 1) * k) % 128;
+            int v = j <= 32 ? cv[j] : j <= 64 ? -cv[64 - j] : j <= 96 ? -cv[j - 64] : cv[128 - j];
+            t.m[k][n] = (int8_t)v;
+        }
+    return t;
+}
+__constant__ TransMatrix c_tm = make_matrix();
+__constant__ int8_t c_dst[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
+__constant__ int16_t c_level_scale[6] = {40, 45, 51, 57, 64, 72};
+
+#define wave_sync() HG_WAVE_SYNC()
+
+__device__ __forceinline__ int clip16(int64_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : (int)v); }
+
+}  // namespace
+
+__global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
+    HG_BLOCK_SHARED int32_t tile[kWaves][2][32 * 32];
+    HG_BLOCK_SHARED int32_t maxrow[kWaves];
+    const int pic = blockIdx.y, row = blockIdx.x;
+    const PicDesc pd = a.pics[pic];
+    const SeqParams sp = a.seqs[pd.seq];
+    const int hctb = (sp.height + (1 << sp.log2_ctb) - 1) >> sp.log2_ctb;
+    if (row >= hctb) return;
+    const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t ntu = a.row_counts[2 * (pd.row_off + row)];
+    const TuRec *tus = a.tus + pd.tu_off + (uint64_t)row * pd.tu_cap_row;
+    const Coef *coefs = a.coefs + pd.coef_off + (uint64_t)row * pd.coef_cap_row;
+    const int W = sp.width, H = sp.height;
+    const int cw = sp.chroma_format ? W >> 1 : 0, ch = sp.chroma_format ? H >> 1 : 0;
+    int16_t *res_plane[3] = {a.resid + pd.resid_off, a.resid + pd.resid_off + (size_t)W * H,
+                             a.resid + pd.resid_off + (size_t)W * H + (size_t)cw * ch};
+    const int pitch[3] = {W, cw, cw};
+    const bool scaling = (sp.flags & SP_SCALING_LIST) != 0;
+    int32_t *d = tile[wave][0];
+    int32_t *g = tile[wave][1];
+
+    for (uint32_t t = wave; t < ntu; t += kWaves) {
+        const TuRec tu = tus[t];
+        if (!(tu.flags & TU_CBF)) continue;
+        const int cidx = tu.flags & TU_CIDX_MASK;
+        const int log2n = tu.log2, n = 1 << log2n;
+        if (log2n < 2 || log2n > 5 || cidx > 2 || tu.x + n > pitch[cidx] || tu.y + n > (cidx ? ch : H)) continue;
+        const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
+        const bool bypass = (tu.flags & TU_BYPASS) != 0, ts = (tu.flags & TU_TSKIP) != 0;
+        // 1. zero the tile, scatter d[y][x] (scaled unless bypass)
+        for (int i = lane; i < n * n; i += kWave) d[i] = 0;
+        if (lane == 0) maxrow[wave] = 0;
+        wave_sync();
+        const int qp = tu.qp;
+        const int bd_shift = bd + log2n - 5;
+        const int64_t rnd = (int64_t)1 << (bd_shift - 1);
+        const int ls = c_level_scale[qp % 6] << (qp / 6);
+        const bool use_m = scaling && !(ts && n > 4);
+        const uint8_t *mtab = a.sf + sp.sf_off + sf_size_offset(log2n - 2) + (uint32_t)cidx * (uint32_t)(n * n);
+        int my_max = 0;
+        for (int k = lane; k < tu.ncoef; k += kWave) {
+            const Coef c = coefs[tu.coef + k];
+            const int pos = (int)(c & 0xffffu) & (n * n - 1);
+            const int v = (int)(int16_t)(c >> 16);
+            int dv;
+            if (bypass) {
+                dv = v;
+            } else {
+                const int m = use_m ? mtab[pos] : 16;
+                dv = clip16(((int64_t)v * m * ls + rnd) >> bd_shift);
+            }
+            d[pos] = dv;
+            my_max = max(my_max, pos >> log2n);
+        }
+        if (my_max) atomicMax(&maxrow[wave], my_max);
+        wave_sync();
+        const int rows = maxrow[wave] + 1;  // rows of d beyond this are zero
+        const int bd2 = 20 - bd;
+        int16_t *dst = res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x;
+        if (bypass || ts) {
+            // bypass: r = TransCoeffLevel; transform skip: r = (d << tsShift) then >> bdShift
+            const int ts_shift = 5 + log2n;
+            for (int i = lane; i < n * n; i += kWave) {
+                int r = d[i];
+                if (!bypass) r = ((r << ts_shift) + (1 << (bd2 - 1))) >> bd2;
+                dst[(i >> log2n) * pitch[cidx] + (i & (n - 1))] = (int16_t)clip16(r);
+            }
+            wave_sync();
+            continue;
+        }
+        const bool dst_tr = (tu.flags & TU_DST) != 0;
+        const int kstep = 32 >> log2n;
+        // 2. vertical (column) pass: e[y][x] = sum_j M[j][y] d[j][x]; g = clip16((e + 64) >> 7)
+        for (int o = lane; o < n * n; o += kWave) {
+            const int y = o >> log2n, x = o & (n - 1);
+            int32_t s = 0;
+            if (dst_tr) {
+                for (int j = 0; j < rows; ++j) s += (int32_t)c_dst[j][y] * d[j * n + x];
+            } else {
+                for (int j = 0; j < rows; ++j) s += (int32_t)c_tm.m[j * kstep][y] * d[j * n + x];
+            }
+            g[o] = clip16(((int64_t)s + 64) >> 7);
+        }
+        wave_sync();
+        // 3. horizontal (row) pass: r[y][x] = sum_j M[j][x] g[y][j]; (r + rnd) >> (20 - bitDepth)
+        for (int o = lane; o < n * n; o += kWave) {
+            const int y = o >> log2n, x = o & (n - 1);
+            int64_t s = 0;
+            if (dst_tr) {
+                for (int j = 0; j < n; ++j) s += (int32_t)c_dst[j][x] * g[y * n + j];
+            } else {
+                for (int j = 0; j < n; ++j) s += (int32_t)c_tm.m[j * kstep][x] * g[y * n + j];
+            }
+            dst[y * pitch[cidx] + x] = (int16_t)clip16((s + (1 << (bd2 - 1))) >> bd2);
+        }
+        wave_sync();
+    }
+}
+
+#if defined(HG_HOST_EMU)
+void emu_transform(const BatchArgs &a) { emu_launch(k_transform, a.max_rows, a.n_pics, kWaves, a); }
+#else
+hipError_t launch_transform(const BatchArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(k_transform, dim3(a.max_rows, a.n_pics), dim3(kWaves * 64), 0, s, a);
+    return hipGetLastError();
+}
+#endif
+
+}  // namespace hg

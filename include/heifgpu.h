@@ -1,0 +1,128 @@
+/*
+ * heifgpu.h — C ABI of the MI355X-native HEIC (HEVC intra still) decode path.
+ *
+ * Drop-in boundary for friendlymatthew/heif:
+ *   - heifgpu_image_parse / heifgpu_image_info replace the host half of
+ *     HeicDecoder::decode (src/heic/decoder.rs:12-112: HeifReader::read,
+ *     hvcC → VPS/SPS/PPS, primary item → grid tiles → slice headers);
+ *   - heifgpu_decode_batch replaces the serial per-tile loop
+ *     (src/heic/decoder.rs:114-119: SliceSegmentReader::try_new +
+ *     read_data, src/hevc/slice.rs:19-42, :206-256) and, unlike the
+ *     reference (which returns Result<()> and panics at slice.rs:250), writes
+ *     the reconstructed Y/Cb/Cr planes.
+ * The test hooks at the end expose the host pieces the reference unit-tests
+ * (src/hevc/rbsp_reader.rs:139-303, src/cabac/decoder.rs:286-373,
+ * tests/libheif_comparison.rs:173-276).
+ *
+ * Conventions: functions return 0 on success and a negative HEIFGPU_E_*
+ * code on failure (the reference's anyhow::Result / ensure! / bail!);
+ * heifgpu_last_error() returns the message of the last failure on the
+ * calling thread.  All pointers are plain host or device pointers; no
+ * framework types cross the boundary.  A context is bound to one device and
+ * must not be used from two threads at once; distinct contexts may run
+ * concurrently (one per GPU).
+ */
+#ifndef HEIFGPU_H
+#define HEIFGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HEIFGPU_ABI_VERSION 1
+
+enum {
+    HEIFGPU_OK = 0,
+    HEIFGPU_E_INVALID = -1,     /* bad argument */
+    HEIFGPU_E_PARSE = -2,       /* container / parameter-set / slice-header error */
+    HEIFGPU_E_UNSUPPORTED = -3, /* valid stream using a tool outside this path */
+    HEIFGPU_E_DEVICE = -4,      /* HIP runtime error */
+    HEIFGPU_E_DECODE = -5       /* a picture's bitstream failed the kernel checks */
+};
+
+/* per-image status bits reported by heifgpu_batch_status */
+enum {
+    HEIFGPU_ST_CABAC_INIT = 1 << 0,
+    HEIFGPU_ST_SUBSTREAM_END = 1 << 1,
+    HEIFGPU_ST_OVERRUN = 1 << 2,
+    HEIFGPU_ST_SYNTAX = 1 << 3,
+    HEIFGPU_ST_UNSUPPORTED = 1 << 4,
+    HEIFGPU_ST_CAPACITY = 1 << 5
+};
+
+typedef struct heifgpu_image heifgpu_image; /* host-parsed HEIC image */
+typedef struct heifgpu_ctx heifgpu_ctx;     /* per-device decoder context */
+typedef struct heifgpu_batch heifgpu_batch; /* device-resident batch */
+
+typedef struct {
+    uint32_t width, height;       /* output (grid-cropped) size, coded orientation */
+    uint32_t chroma_format_idc;   /* 0 = 4:0:0, 1 = 4:2:0 */
+    uint32_t bit_depth;           /* luma bit depth (chroma equal) */
+    uint32_t bytes_per_sample;    /* 1 for 8-bit, 2 otherwise */
+    uint32_t grid_rows, grid_cols;/* 1x1 for a single coded item */
+    uint32_t tile_width, tile_height;
+    uint32_t num_tiles;
+    uint32_t rotation;            /* irot angle, anticlockwise in 90-degree units */
+    uint32_t ispe_width, ispe_height;
+    uint32_t coded_bytes;         /* sum of tile item bytes */
+    uint32_t primary_item_id;
+    uint32_t num_thumbnails;
+    uint32_t matrix_coeffs, full_range;
+} heifgpu_image_info;
+
+typedef struct {
+    void *plane[3];               /* device pointers, caller-owned (Y, Cb, Cr) */
+    int32_t pitch[3];             /* bytes per row */
+} heifgpu_planes;
+
+/* ---- host: demux + parameter sets + slice headers ------------------- */
+/* data is copied; the returned image owns its bytes. */
+int heifgpu_image_parse(const uint8_t *data, size_t len, heifgpu_image **out);
+int heifgpu_image_get_info(const heifgpu_image *img, heifgpu_image_info *info);
+void heifgpu_image_free(heifgpu_image *img);
+
+/* ---- device context --------------------------------------------------- */
+int heifgpu_create(int device, heifgpu_ctx **out);
+void heifgpu_destroy(heifgpu_ctx *ctx);
+const char *heifgpu_last_error(void);
+
+/* ---- batched decode ----------------------------------------------------
+ * heifgpu_batch_prepare flattens n images (all must share bit depth and
+ * chroma format) into device descriptors, uploads their bitstreams
+ * (synchronously) and allocates the work arenas.  heifgpu_batch_decode
+ * then enqueues the five decode stages on `stream` (a hipStream_t, NULL =
+ * the context's default stream) and returns immediately; out[i] receives
+ * image i.  It may be called repeatedly on the same batch (the bench times
+ * exactly this call).  heifgpu_batch_status synchronises the stream and
+ * returns the per-image status words (0 = ok). */
+int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, heifgpu_batch **out);
+int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *batch, const heifgpu_planes *out, void *stream);
+int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *batch, uint32_t *status, void *stream);
+void heifgpu_batch_free(heifgpu_batch *batch);
+/* per-launch stage timing of the last decode (ms, from HIP events when
+ * enabled with heifgpu_set_timing(ctx, 1)): parse, transform, intra,
+ * deblock, sao/output */
+int heifgpu_set_timing(heifgpu_ctx *ctx, int enable);
+int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[5]);
+/* convenience: prepare + decode + status + free */
+int heifgpu_decode_batch(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, const heifgpu_planes *out,
+                         void *stream, uint32_t *status);
+
+/* ---- host test hooks (reference unit-test surface) -------------------- */
+size_t heifgpu_remove_emulation_prevention(const uint8_t *in, size_t n, uint8_t *out); /* rbsp_reader.rs:11-39 */
+int heifgpu_read_ue(const uint8_t *buf, size_t n, uint32_t *val);                      /* rbsp_reader.rs:87-99 */
+int heifgpu_read_se(const uint8_t *buf, size_t n, int32_t *val);                       /* rbsp_reader.rs:101-113 */
+/* the kernels' binarizations (cabac/decoder.rs:152-261) over explicit bins;
+ * return the value (or -1 on underrun), *used = bins consumed */
+int heifgpu_bins_truncated_rice(const uint8_t *bins, int n, int c_max, int c_rice, int *used);
+int heifgpu_bins_chroma_pred_mode(const uint8_t *bins, int n, int *used);
+int heifgpu_bins_coeff_abs_level_remaining(const uint8_t *bins, int n, int c_rice, int *used);
+int heifgpu_bins_exp_golomb(const uint8_t *bins, int n, int k, int *used);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -28,6 +28,8 @@
 #include <string.h>
 
 static __thread char g_err[256];
+static __thread int g_debug_flags; /* bit0: skip deblocking, bit1: skip SAO (bring-up only) */
+void oracle_set_debug_flags(int flags) { g_debug_flags = flags; }
 int oracle_fail(const char *msg) {
     snprintf(g_err, sizeof(g_err), "%s", msg);
     return -1;
@@ -988,14 +990,14 @@ static void residual_from_coeffs(pic_t *p, int cIdx, int log2n, const int *coef,
     const uint8_t *m = p->sf[log2n - 2][log2n == 5 ? (cIdx ? cIdx : 0) : cIdx];
     for (int i = 0; i < n * n; i++) {
         int mm = (!p->sps->scaling_list_enabled || (ts && n > 4)) ? 16 : m[i];
-        int64_t v = ((int64_t)coef[i] * mm * ls[qp % 6]) << (qp / 6);
+        int64_t v = (int64_t)coef[i] * mm * ls[qp % 6] * ((int64_t)1 << (qp / 6));
         v = (v + ((int64_t)1 << (bdShift - 1))) >> bdShift;
         d[i] = (int)CLIP3(-32768, 32767, v);
     }
     int r[32 * 32];
     if (ts) {
         int tsShift = 5 + log2n;
-        for (int i = 0; i < n * n; i++) r[i] = d[i] << tsShift;
+        for (int i = 0; i < n * n; i++) r[i] = d[i] * (1 << tsShift);
     } else {
         int col[32], out[32], g[32 * 32];
         for (int x = 0; x < n; x++) { /* vertical: each column */
@@ -1474,9 +1476,9 @@ static void dbk_luma_seg(pic_t *p, int x, int y, int vertical) {
     int qpl = (qQ + qP + 1) >> 1;
     int bS = 2;
     int bd = p->bdY;
-    int Q = CLIP3(0, 51, qpl + (p->beta_off << 1));
+    int Q = CLIP3(0, 51, qpl + p->beta_off * 2);
     int beta = k_beta[Q] * (1 << (bd - 8));
-    Q = CLIP3(0, 53, qpl + 2 * (bS - 1) + (p->tc_off << 1));
+    Q = CLIP3(0, 53, qpl + 2 * (bS - 1) + p->tc_off * 2);
     int tc = k_tc[Q] * (1 << (bd - 8));
     /* sample accessor: P(i,k) = p_i at line k, Qs(i,k) = q_i */
     int stepx = vertical ? 1 : ps, stepk = vertical ? ps : 1;
@@ -1545,7 +1547,7 @@ static void dbk_chroma_seg(pic_t *p, int cIdx, int xc, int yc, int vertical, int
     int off = cIdx == 1 ? p->pps->cb_qp_offset : p->pps->cr_qp_offset;
     int qpi = ((qQ + qP + 1) >> 1) + off;
     int qpc = chroma_qp_map(qpi, p->chroma);
-    int Q = CLIP3(0, 53, qpc + 2 + (p->tc_off << 1));
+    int Q = CLIP3(0, 53, qpc + 2 + p->tc_off * 2);
     int tc = k_tc[Q] * (1 << (p->bdC - 8));
     int maxv = (1 << p->bdC) - 1;
     int stepx = vertical ? 1 : ps, stepk = vertical ? ps : 1;
@@ -1553,7 +1555,7 @@ static void dbk_chroma_seg(pic_t *p, int cIdx, int xc, int yc, int vertical, int
     for (int k = 0; k < lines; k++) {
         int p0 = q0p[k * stepk - stepx], p1 = q0p[k * stepk - 2 * stepx];
         int q0 = q0p[k * stepk], q1 = q0p[k * stepk + stepx];
-        int delta = CLIP3(-tc, tc, ((((q0 - p0) << 2) + p1 - q1 + 4) >> 3));
+        int delta = CLIP3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
         if (!(fp & F_NOFILT)) q0p[k * stepk - stepx] = (uint16_t)CLIP3(0, maxv, p0 + delta);
         if (!(fq & F_NOFILT)) q0p[k * stepk] = (uint16_t)CLIP3(0, maxv, q0 - delta);
     }
@@ -1883,7 +1885,7 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
             if (ctbAddr >= nctb) { oracle_fail("missing end_of_slice_segment_flag"); goto out; }
         }
     }
-    deblock_picture(p);
+    if (!(g_debug_flags & 1)) deblock_picture(p);
     {
         /* SAO into full-size temp, then crop into caller planes */
         uint16_t *full[3] = {0, 0, 0};
@@ -1891,7 +1893,7 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
         int nc = p->chroma ? 3 : 1;
         for (int ci = 0; ci < nc; ci++)
             full[ci] = (uint16_t *)malloc(sizeof(uint16_t) * (size_t)(ci ? p->cw * p->chh : p->W * p->H));
-        if (p->sao_luma || p->sao_chroma) sao_picture(p, full, fps);
+        if ((p->sao_luma || p->sao_chroma) && !(g_debug_flags & 2)) sao_picture(p, full, fps);
         else
             for (int ci = 0; ci < nc; ci++)
                 memcpy(full[ci], p->pl[ci], sizeof(uint16_t) * (size_t)(ci ? p->cw * p->chh : p->W * p->H));

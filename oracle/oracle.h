@@ -108,6 +108,8 @@ int oracle_list_tiles(const uint8_t *data, size_t len, uint32_t *off, uint32_t *
                       int max, uint32_t *hvcc_off, uint32_t *hvcc_len);
 
 const char *oracle_last_error(void);
+/* bring-up: bit0 skips deblocking, bit1 skips SAO (thread-local) */
+void oracle_set_debug_flags(int flags);
 
 #ifdef __cplusplus
 }
