@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py — Mpixels/s of bit-exact HEIC decode on MI355X (BASELINE.json metric).
+
+Workload (one shard per GPU, weak scaling): every
+rank decodes a batch of `--batch` synthetic 4032x3024 8-bit 4:2:0 intra HEIC
+stills; image i is halfmoonbay.heic with its 48 grid tiles permuted by
+mt19937_64(seed=i) (heif_amd/synthetic.py).  A "step" is one decode of the
+whole batch: bitstreams, parameter sets and slice headers are resident in HBM
+before timing (host demux + upload happen once, outside the timed region);
+the step runs the five gfx950 kernels and writes every image's cropped
+Y/Cb/Cr planes to HBM.  `value` = all ranks' output luma pixels / max-over-
+ranks wall time of K steps.
+
+roofline: the dominant kernel (k_parse) measured with HIP events on the
+decode stream; algorithmic bytes per image = compressed tile bytes +
+reconstructed planes (1,704,187 + 18,874,368 B).
+
+cpu_baseline: the CPU oracle (oracle/, spec restatement; the reference Rust
+path cannot decode pixels) decoding tiles on a thread pool for ~10 s.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+SAMPLE = ROOT / "tests" / "golden" / "halfmoonbay.heic"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return rank, world, local
+
+
+def shard_seeds(batch_per_rank: int, rank: int) -> list:
+    """Image seeds of this rank: a contiguous block of the global batch."""
+    return list(range(rank * batch_per_rank, (rank + 1) * batch_per_rank))
+
+
+def cpu_baseline(data: bytes, seconds: float, threads: int) -> dict:
+    from oracle import oracle
+
+    tiles, (ho, hl) = oracle.list_tiles(data)
+    hvcc = data[ho:ho + hl]
+    items = [data[o:o + n] for o, n in tiles]
+    meta = oracle.read_meta(data)
+    tw, th = meta["tile_width"], meta["tile_height"]
+    out_px_per_tile = meta["out_width"] * meta["out_height"] / len(items)
+    count = 0
+    deadline = time.perf_counter() + seconds
+
+    def worker(k):
+        n = 0
+        i = k
+        while time.perf_counter() < deadline:
+            oracle.decode_tile(hvcc, items[i % len(items)], tw, th)
+            n += 1
+            i += threads
+        return n
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        count = sum(ex.map(worker, range(threads)))
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(count * out_px_per_tile / dt / 1e6, 2),
+        "unit": "Mpixels/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{count} halfmoonbay 512x512 tiles decoded by the C oracle in {dt:.1f} s "
+                  f"({threads} threads, output-pixel-equivalent of {count / len(items):.1f} 4032x3024 images)",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=128, help="images per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", type=int, default=2, help="images checked bit-exact against the oracle (rank 0)")
+    args = ap.parse_args()
+
+    import torch
+
+    rank, world, local = dist_env()
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local)
+
+    import heif_amd as H
+    from heif_amd.synthetic import permuted_heic
+
+    src = SAMPLE.read_bytes()
+    seeds = shard_seeds(args.batch, rank)
+    t0 = time.perf_counter()
+    files = [permuted_heic(src, s) for s in seeds]
+    images = [H.HeifImage.parse(f) for f in files]
+    host_parse_ms = (time.perf_counter() - t0) * 1e3 / len(files)
+    info = images[0].info
+    ctx = H.DecodeContext(local)
+    outs = ctx.alloc_outputs(images)
+    t0 = time.perf_counter()
+    batch = ctx.prepare(images)
+    upload_s = time.perf_counter() - t0
+    stream = torch.cuda.Stream(device=local)
+    ctx.set_timing(True)
+
+    def step():
+        batch.decode_async(outs, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    st = batch.status(stream.cuda_stream)
+    if any(st):
+        raise SystemExit(f"rank {rank}: decode status {st}")
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    stage_ms = [0.0] * 5
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        ms = ctx.stage_times()  # HIP events on the decode stream (syncs on the last one)
+        stage_ms = [a + b for a, b in zip(stage_ms, ms)]
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=f"cuda:{local}")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = batch.status(stream.cuda_stream)
+    if any(st):
+        raise SystemExit(f"rank {rank}: decode status {st}")
+
+    if rank == 0:
+        verified = 0
+        if args.verify:
+            import numpy as np
+            from oracle import oracle
+
+            for i in range(min(args.verify, len(files))):
+                ref = oracle.decode_heic(files[i], with_checks=False)
+                for g, r in ((outs[i].y, ref.y), (outs[i].cb, ref.cb), (outs[i].cr, ref.cr)):
+                    if not np.array_equal(g.cpu().numpy().astype(np.uint16), r):
+                        raise SystemExit(f"image {i}: GPU planes differ from the oracle")
+                verified += 1
+        px = info.width * info.height
+        total_images = args.batch * world
+        value = total_images * px / elapsed / 1e6
+        per_step = [m / args.steps for m in stage_ms]
+        parse_ms = per_step[0]
+        coded_px = info.grid_cols * info.tile_width * info.grid_rows * info.tile_height
+        algo_per_image = info.coded_bytes + coded_px * 3 // 2  # compressed + coded planes
+        achieved = args.batch * algo_per_image / (parse_ms / 1e3) / 1e9
+        traffic = None
+        tfile = ROOT / "profiles" / "pmc_traffic.json"
+        if tfile.exists():
+            try:
+                tj = json.loads(tfile.read_text())
+                if tj.get("batch") == args.batch:
+                    traffic = tj.get("k_parse_hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "Mpixels/s decoded (bit-exact) on 4032x3024 HEIC batch",
+            "value": round(value, 2),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: halfmoonbay.heic tiles permuted per image (mt19937_64 Fisher-Yates)",
+            "config": {
+                "workload": f"config4 shard: {args.batch} x 4032x3024 8-bit 4:2:0 intra HEIC grid stills per GPU "
+                            f"(48 tiles of 512x512, WPP)",
+                "images_per_gpu": args.batch,
+                "global_batch": total_images,
+                "parallelism": f"images sharded over {world} GPU(s), no collective on the data path",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6),
+                "traffic": traffic,
+                "kernel": "k_parse (CABAC)",
+                "kernel_ms_per_launch": round(parse_ms, 3),
+                "algorithmic_bytes_per_launch": args.batch * algo_per_image,
+            },
+            "stage_ms_per_step": {k: round(v, 3) for k, v in zip(
+                ["parse", "transform", "intra", "deblock", "sao_out"], per_step)},
+            "pipeline_hbm_gbs": round(args.batch * algo_per_image / (elapsed / args.steps) / 1e9, 2),
+            "host_parse_ms_per_image": round(host_parse_ms, 3),
+            "upload_s": round(upload_s, 3),
+            "verified_images": verified,
+        }
+        if not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(src, args.cpu_seconds, threads)
+        print(json.dumps(line), flush=True)
+    batch.free()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
