@@ -10,7 +10,9 @@ import os
 import pathlib
 
 _HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = _HERE / "libheifgpu.so"
+# HEIFGPU_LIBRARY selects another in-tree build of the same ABI (e.g. the
+# counter-instrumented heif_amd/libheifgpu_prof.so from `make prof`)
+LIB_PATH = pathlib.Path(os.environ.get("HEIFGPU_LIBRARY", _HERE / "libheifgpu.so"))
 
 HEIFGPU_OK = 0
 HEIFGPU_E_INVALID = -1
@@ -52,7 +54,7 @@ EXPORTS = (
     "heifgpu_batch_status", "heifgpu_batch_free", "heifgpu_set_timing", "heifgpu_stage_times",
     "heifgpu_decode_batch", "heifgpu_remove_emulation_prevention", "heifgpu_read_ue",
     "heifgpu_read_se", "heifgpu_bins_truncated_rice", "heifgpu_bins_chroma_pred_mode",
-    "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb",
+    "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb", "heifgpu_debug_counters",
 )
 
 
@@ -96,6 +98,7 @@ def _load() -> ctypes.CDLL:
         "heifgpu_bins_chroma_pred_mode": (I32, [u8p, I32, P(I32)]),
         "heifgpu_bins_coeff_abs_level_remaining": (I32, [u8p, I32, I32, P(I32)]),
         "heifgpu_bins_exp_golomb": (I32, [u8p, I32, I32, P(I32)]),
+        "heifgpu_debug_counters": (I32, [P(ctypes.c_uint64), I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

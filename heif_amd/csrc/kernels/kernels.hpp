@@ -10,6 +10,7 @@
 #pragma once
 #include "../common/desc.hpp"
 #include "wave.hpp"
+#include <cstdlib>
 
 #if defined(HG_HOST_EMU)
 #include <atomic>
@@ -40,10 +41,30 @@ struct BatchArgs {
     int max_rows;              // CTB rows, batch max
     int total_rows;            // sum of CTB rows over pictures
     int bytes_per_sample;      // 1 or 2
+    int parse_group;           // k_parse waves per picture (set by launch_parse)
 };
 
-constexpr int kParseWaves = 16;
-size_t parse_lds_bytes(int max_width, int max_wctb);
+constexpr int kParseWaves = 16;              // k_parse block size limit (waves)
+constexpr int kParseSerialMinPics = 1024;    // from this many pictures on: one wave per picture
+constexpr int kParseSerialPicsPerBlock = 4;  // pictures (waves) per block in that mode
+struct ParseShape {
+    int group, pics_per_block, blocks, threads;
+    size_t lds;
+};
+ParseShape parse_shape(const BatchArgs &a);
+// LDS of one picture group: progress[G] (padded to 4), WPP context slots
+// [2][64] words, CtDepth lines [2][dl_stride], SAO lines [2][max_wctb]
+#if defined(HG_HOST_EMU)
+inline
+#else
+__host__ __device__ inline
+#endif
+size_t parse_group_bytes(int max_width, int max_wctb, int group) {
+    const size_t dl_stride = (size_t)(((max_width >> 3) + 15) & ~15);
+    const size_t b = sizeof(uint32_t) * ((group + 3) & ~3) + 2 * 64 * sizeof(uint32_t) + 2 * dl_stride +
+                     2 * (size_t)max_wctb * sizeof(SaoParams);
+    return (b + 15) & ~(size_t)15;
+}
 
 #if defined(HG_HOST_EMU)
 // Runs kernel(a) over a gx * gy grid, one block at a time, with `waves` host

@@ -23,16 +23,32 @@ namespace hg {
 __constant__ uint8_t c_lps[256] = {HG_LPS_TABLE};
 __constant__ uint8_t c_trans_lps[64] = {HG_TRANS_LPS};
 __constant__ uint8_t c_ctx_init[CTX_NUM] = {HG_CTX_INIT_VALUES};
+#if defined(HG_PARSE_PROF) && !defined(HG_HOST_EMU)
+__device__ uint64_t g_prof[16];
+#endif
 
 namespace {
 
 #define HG_INLINE __device__ __attribute__((always_inline)) inline
+// lane-parallel loop with a wave-uniform trip count; only the body is predicated
+#define HG_LANE_LOOP(k, lane_, n)                                       \
+    for (int k##_0 = 0, k = (lane_); k##_0 < (n); k##_0 += kWave, k = k##_0 + (lane_)) \
+        if (k < (n))
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return HG_UNI(v); }
 __device__ __forceinline__ int unis(int v) { return (int)HG_UNI((uint32_t)v); }
 
+// Optional cycle/bin counters (build with -DHG_PARSE_PROF; read back with
+// heifgpu_debug_counters).  Compiled out of the product library.
+#if defined(HG_PARSE_PROF) && !defined(HG_HOST_EMU)
+#define HG_PROF(x) x
+__device__ __forceinline__ uint64_t prof_clock() { return __builtin_amdgcn_s_memtime(); }
+#else
+#define HG_PROF(x)
+#endif
+enum { PF_WAVE, PF_SPIN, PF_BINS, PF_BYPASS, PF_REFILL, PF_CQT, PF_RESID, PF_SAO, PF_N };
+
 struct alignas(16) WaveLds {
-    uint8_t ctx[CTX_PAD];
     uint8_t ring[256];
     uint8_t ipm[16][17];  // IntraPredModeY per 4x4 of the current CTB, column 0 = left CTB
     uint8_t depth[8][9];  // CtDepth per 8x8, column 0 = left CTB
@@ -42,6 +58,73 @@ struct alignas(16) WaveLds {
     SaoParams sao_left;
     uint8_t pad_[2];
 };
+
+
+// ---------------------------------------------------------------- context registers
+// The 137 context variables live in ONE VGPR of the wave: context i is byte
+// (i >> 6) of lane (i & 63).  A bin reads its context with v_readlane (SGPR
+// lane select) and writes it back with v_writelane, so the serial bin chain
+// never waits on LDS.  rangeTabLps (Table 9-52) rides in a second VGPR (lane
+// = pStateIdx, 4 bytes = qRangeIdx) and transIdxLps (Table 9-53) in a third.
+// In the host emulation (kWave = 1) the same interface is plain arrays.
+#if defined(HG_HOST_EMU)
+struct CtxRegs {
+    uint8_t b[256];
+    uint8_t lps[64][4];
+    uint8_t trans[64];
+    void load_tables(int) {
+        for (int st = 0; st < 64; ++st) {
+            for (int q = 0; q < 4; ++q) lps[st][q] = c_lps[(st << 2) | q];
+            trans[st] = c_trans_lps[st];
+        }
+    }
+    uint32_t word(int ci) const { return b[ci]; }
+    static uint32_t state(uint32_t w, int) { return w; }
+    void put(int ci, uint32_t, uint32_t s) { b[ci] = (uint8_t)s; }
+    uint32_t lps_of(uint32_t st, uint32_t q) const { return lps[st][q]; }
+    uint32_t trans_of(uint32_t st) const { return trans[st]; }
+    void init(int, int qp) {
+        for (int i = 0; i < 256; ++i) b[i] = i < CTX_NUM ? ctx_init_state(c_ctx_init[i], qp) : 0;
+    }
+    void save(uint32_t *slot, int) const { std::memcpy(slot, b, 256); }
+    void restore(const uint32_t *slot, int) { std::memcpy(b, slot, 256); }
+};
+#else
+struct CtxRegs {
+    uint32_t v;      // contexts
+    uint32_t lpsv;   // rangeTabLps row of state = lane
+    uint32_t transv; // transIdxLps of state = lane
+    __device__ void load_tables(int lane) {
+        lpsv = (uint32_t)c_lps[lane << 2] | ((uint32_t)c_lps[(lane << 2) | 1] << 8) |
+               ((uint32_t)c_lps[(lane << 2) | 2] << 16) | ((uint32_t)c_lps[(lane << 2) | 3] << 24);
+        transv = c_trans_lps[lane];
+    }
+    __device__ uint32_t word(int ci) const { return (uint32_t)__builtin_amdgcn_readlane((int)v, ci & 63); }
+    static __device__ uint32_t state(uint32_t w, int ci) { return (w >> ((ci >> 6) << 3)) & 0xffu; }
+    __device__ void put(int ci, uint32_t w, uint32_t s) {
+        const int sh = (ci >> 6) << 3;
+        w = (w & ~(0xffu << sh)) | (s << sh);
+        v = __lane_id() == (ci & 63) ? w : v;  // v_writelane equivalent (v_cmp + v_cndmask)
+    }
+    __device__ uint32_t lps_of(uint32_t st, uint32_t q) const {
+        return ((uint32_t)__builtin_amdgcn_readlane((int)lpsv, (int)st) >> (q << 3)) & 0xffu;
+    }
+    __device__ uint32_t trans_of(uint32_t st) const {
+        return (uint32_t)__builtin_amdgcn_readlane((int)transv, (int)st);
+    }
+    __device__ void init(int lane, int qp) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int i = lane + 64 * k;
+            if (i < CTX_NUM) w |= (uint32_t)ctx_init_state(c_ctx_init[i], qp) << (8 * k);
+        }
+        v = w;
+    }
+    __device__ void save(uint32_t *slot, int lane) const { slot[lane] = v; }
+    __device__ void restore(const uint32_t *slot, int lane) { v = slot[lane]; }
+};
+#endif
 
 struct Parser {
     // picture constants
@@ -54,10 +137,16 @@ struct Parser {
     int bits_needed;
     // byte ring
     uint32_t rd, wr, src_pos, nal_end, prev1, prev2;
+#if !defined(HG_HOST_EMU)
+    uint32_t ringv;  // the ring, 4 bytes per lane
+    uint32_t scanv;  // 8x8 diagonal scan: byte 0 = x | (y << 3) of sPos = lane, byte 1 = sPos of raster lane
+#endif
     const uint8_t *src;
     uint32_t status;
     WaveLds *w;
+    CtxRegs cx;
     int lane;
+    HG_PROF(uint64_t prof[PF_N];)
     // CTB
     int ctbx, ctby, rx, ry;
     // quantization groups (8.6.1)
@@ -77,6 +166,17 @@ struct Parser {
 };
 
 // ---------------------------------------------------------------- bytes
+// The RBSP bytes of the substream flow through a 256-byte ring per wave.
+// ring_refill converts the next 64 raw bytes (one per lane, emulation-
+// prevention bytes dropped via ballot compaction) and appends them.  Refills
+// happen only at a few syntax points (ensure_bytes): CTU start/end, every
+// coding-quadtree and transform-tree node and every residual sub-block, each
+// of which consumes at most ~175 bytes of a conforming stream (a 4x4
+// sub-block: 42 context bins of <= 6 bits + 16 coeff_abs_level_remaining of
+// <= 72 bypass bins).  next_byte is therefore branch-free.  On the GPU the
+// ring also lives in a VGPR (byte rd of lane (rd >> 2) & 63), so the byte
+// fetch of the bin loop is a v_readlane rather than an LDS round trip.
+constexpr uint32_t kRingLowWater = 192;  // ring - 64: a refill never overwrites unread bytes
 #if defined(HG_HOST_EMU)
 HG_INLINE void ring_refill(Parser &p) {  // scalar equivalent of the 64-lane ballot refill
     for (int lane = 0; lane < 64; ++lane) {
@@ -91,6 +191,7 @@ HG_INLINE void ring_refill(Parser &p) {  // scalar equivalent of the 64-lane bal
     }
     p.src_pos += 64;
 }
+HG_INLINE uint32_t next_byte(Parser &p) { return p.w->ring[p.rd++ & 255]; }
 #else
 HG_INLINE void ring_refill(Parser &p) {
     const int lane = p.lane;
@@ -102,12 +203,8 @@ HG_INLINE void ring_refill(Parser &p) {
     if (lane == 63) nb = b64;
     uint32_t bm1 = __shfl(b, (lane + 63) & 63, 64);
     uint32_t bm2 = __shfl(b, (lane + 62) & 63, 64);
-    if (lane == 0) {
-        bm1 = p.prev1;
-        bm2 = p.prev2;
-    } else if (lane == 1) {
-        bm2 = p.prev1;
-    }
+    bm1 = lane == 0 ? p.prev1 : bm1;
+    bm2 = lane == 0 ? p.prev2 : (lane == 1 ? p.prev1 : bm2);
     // rbsp_reader.rs:11-39: 00 00 03 followed by a byte <= 3 (or the end)
     bool ep = valid && bm2 == 0 && bm1 == 0 && b == 3 && (pos + 1 >= p.nal_end || nb <= 3);
     bool keep = valid && !ep;
@@ -118,24 +215,31 @@ HG_INLINE void ring_refill(Parser &p) {
     p.prev2 = uni(__shfl(b, 62, 64));
     p.prev1 = uni(__shfl(b, 63, 64));
     p.src_pos += 64;
+    p.ringv = reinterpret_cast<const uint32_t *>(p.w->ring)[lane];  // same wave: LDS is in order
+}
+HG_INLINE uint32_t next_byte(Parser &p) {
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)p.ringv, (int)((p.rd >> 2) & 63));
+    const uint32_t v = (d >> ((p.rd & 3) << 3)) & 0xffu;
+    ++p.rd;
+    return v;
 }
 #endif
 
-__device__ __forceinline__ uint32_t next_byte(Parser &p) {
-    if (p.rd == p.wr) {
-        if (p.src_pos >= p.nal_end) {
-            p.status |= ST_OVERRUN;
-            return 0;
-        }
+
+// top up the ring to the low-water mark (or the end of the NAL unit)
+HG_INLINE void ensure_bytes(Parser &p) {
+    while (p.wr - p.rd < kRingLowWater && p.src_pos < p.nal_end) {
         ring_refill(p);
-        if (p.rd == p.wr) {
-            p.status |= ST_OVERRUN;
-            return 0;
-        }
+        // rd is untouched by the refill, but without this the uniformity
+        // analysis loses track of it here and the whole bin loop goes to VGPRs
+        p.rd = uni(p.rd);
+        HG_PROF(++p.prof[PF_REFILL]);
     }
-    uint32_t v = uni(p.w->ring[p.rd & 255]);
-    ++p.rd;
-    return v;
+}
+
+// a conforming substream never reads past the bytes it was given
+HG_INLINE void check_overrun(Parser &p) {
+    if ((int32_t)(p.wr - p.rd) < 0) p.status |= ST_OVERRUN;
 }
 
 // 9.3.2.5 initialization of the arithmetic decoding engine at a raw offset
@@ -147,6 +251,7 @@ HG_INLINE void engine_init(Parser &p, uint32_t raw_start) {
     p.prev1 = uni(p.prev1);
     p.prev2 = uni(p.prev2);
     p.range = 510;
+    ensure_bytes(p);
     uint32_t b0 = next_byte(p);
     uint32_t b1 = next_byte(p);
     p.value = (b0 << 8) | b1;
@@ -156,15 +261,17 @@ HG_INLINE void engine_init(Parser &p, uint32_t raw_start) {
 
 // 9.3.2.2 context initialization
 HG_INLINE void ctx_init(Parser &p) {
-    for (int i = p.lane; i < CTX_NUM; i += kWave) p.w->ctx[i] = ctx_init_state(c_ctx_init[i], p.sliceQp);
+    p.cx.init(p.lane, p.sliceQp);
 }
 
 // ---------------------------------------------------------------- engine
 // 9.3.4.3.2 DecodeDecision (arithmetic.rs:97-144)
 HG_INLINE int dec_bin(Parser &p, int ci) {
-    uint32_t s = uni(p.w->ctx[ci]);
+    HG_PROF(++p.prof[PF_BINS]);
+    const uint32_t w = p.cx.word(ci);
+    const uint32_t s = CtxRegs::state(w, ci);
     uint32_t st = s >> 1, mps = s & 1;
-    uint32_t lps = c_lps[(st << 2) | ((p.range >> 6) & 3)];
+    const uint32_t lps = p.cx.lps_of(st, (p.range >> 6) & 3);
     p.range -= lps;
     uint32_t scaled = p.range << 7;
     int bin;
@@ -186,19 +293,20 @@ HG_INLINE int dec_bin(Parser &p, int ci) {
         p.range = lps << nbits;
         bin = (int)(mps ^ 1u);
         if (st == 0) mps ^= 1u;
-        st = c_trans_lps[st];
+        st = p.cx.trans_of(st);
         p.bits_needed += nbits;
         if (p.bits_needed >= 0) {
             p.value |= next_byte(p) << p.bits_needed;
             p.bits_needed -= 8;
         }
     }
-    p.w->ctx[ci] = (uint8_t)((st << 1) | mps);
+    p.cx.put(ci, w, (st << 1) | mps);
     return bin;
 }
 
 // 9.3.4.3.4 DecodeBypass (arithmetic.rs:146-157)
 __device__ __forceinline__ int dec_bypass(Parser &p) {
+    HG_PROF(++p.prof[PF_BYPASS]);
     p.value <<= 1;
     if (++p.bits_needed >= 0) {
         p.bits_needed = -8;
@@ -267,6 +375,7 @@ HG_INLINE void derive_qp_pred(Parser &p) {
 
 // ---------------------------------------------------------------- SAO syntax (7.3.8.3)
 HG_INLINE void parse_sao(Parser &p, SaoParams *sao_line_above, SaoParams *gsao) {
+    ensure_bytes(p);
     SaoParams s;
     for (int c = 0; c < 3; ++c) {
         s.type[c] = 0;
@@ -281,8 +390,12 @@ HG_INLINE void parse_sao(Parser &p, SaoParams *sao_line_above, SaoParams *gsao) 
     } else if (mu) {
         s = sao_line_above[p.rx];
     } else {
-        int ncomp = p.chroma ? 3 : 1;
-        for (int c = 0; c < ncomp; ++c) {
+        // component loop fully unrolled: a runtime index into the private
+        // SaoParams would keep it in scratch (and scratch loads are divergent)
+        const int ncomp = p.chroma ? 3 : 1;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (c >= ncomp) break;
             if (!((p.saoL && c == 0) || (p.saoC && c > 0))) continue;
             if (c < 2) {
                 int t = 0;
@@ -295,16 +408,18 @@ HG_INLINE void parse_sao(Parser &p, SaoParams *sao_line_above, SaoParams *gsao) 
             int bd = c ? p.bdC : p.bdY;
             uint32_t cmax = (1u << ((bd < 10 ? bd : 10) - 5)) - 1;
             int a[4];
+#pragma unroll
             for (int i = 0; i < 4; ++i) a[i] = (int)bin_truncated_rice([&]() { return dec_bypass(p); }, cmax, 0);
             if (s.type[c] == 1) {
+#pragma unroll
                 for (int i = 0; i < 4; ++i)
                     if (a[i] && dec_bypass(p)) a[i] = -a[i];
                 s.band_eo[c] = (uint8_t)dec_bypass_bits(p, 5);
+#pragma unroll
                 for (int i = 0; i < 4; ++i) s.off[c][i] = (int16_t)a[i];
             } else {
-                if (c == 0) s.band_eo[0] = (uint8_t)dec_bypass_bits(p, 2);
-                if (c == 1) s.band_eo[1] = (uint8_t)dec_bypass_bits(p, 2);
-                if (c == 2) s.band_eo[2] = s.band_eo[1];
+                if (c < 2) s.band_eo[c] = (uint8_t)dec_bypass_bits(p, 2);
+                else s.band_eo[2] = s.band_eo[1];
                 s.off[c][0] = (int16_t)a[0];
                 s.off[c][1] = (int16_t)a[1];
                 s.off[c][2] = (int16_t)-a[2];
@@ -312,10 +427,40 @@ HG_INLINE void parse_sao(Parser &p, SaoParams *sao_line_above, SaoParams *gsao) 
             }
         }
     }
-    if (p.lane == 0) {
-        p.w->sao_left = s;
-        gsao[p.ry * p.wctb + p.rx] = s;
+    p.w->sao_left = s;  // every lane stores the same value: no divergent branch
+    gsao[p.ry * p.wctb + p.rx] = s;
+}
+
+// ---------------------------------------------------------------- scans (6.5.3-6.5.5)
+// Per-coefficient lookups must not touch memory: 2x2 and 4x4 scans are packed
+// 64-bit immediates, the 8x8 diagonal scan (32x32 TBs' sub-block order) sits
+// in a VGPR read with v_readlane.  Results use kScanPos's x | (y << 4) form.
+HG_INLINE int scan_pos(const Parser &p, int l, int scan, int i) {
+#if defined(HG_HOST_EMU)
+    return kScanPos[l][scan][i];
+#else
+    if (l == 3) {
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readlane((int)p.scanv, i) & 0xffu;
+        return (int)((e & 7) | ((e >> 3) << 4));
     }
+    if (l == 0) return 0;
+    const uint64_t t = l == 2 ? (scan == 0 ? kScan4Pos[0] : scan == 1 ? kScan4Pos[1] : kScan4Pos[2])
+                              : (scan == 0 ? kScan2Pos[0] : scan == 1 ? kScan2Pos[1] : kScan2Pos[2]);
+    const uint32_t e = (uint32_t)(t >> (4 * i)) & 15u;
+    return (int)((e & 3) | ((e >> 2) << 4));
+#endif
+}
+
+HG_INLINE int scan_inv(const Parser &p, int l, int scan, int raster) {
+#if defined(HG_HOST_EMU)
+    return kScanInv[l][scan][raster];
+#else
+    if (l == 3) return (int)(((uint32_t)__builtin_amdgcn_readlane((int)p.scanv, raster) >> 8) & 0xffu);
+    if (l == 0) return 0;
+    const uint64_t t = l == 2 ? (scan == 0 ? kScan4Inv[0] : scan == 1 ? kScan4Inv[1] : kScan4Inv[2])
+                              : (scan == 0 ? kScan2Inv[0] : scan == 1 ? kScan2Inv[1] : kScan2Inv[2]);
+    return (int)((uint32_t)(t >> (4 * raster)) & 15u);
+#endif
 }
 
 // ---------------------------------------------------------------- residual_coding (7.3.8.11)
@@ -363,15 +508,16 @@ HG_INLINE void residual_coding(Parser &p, int log2n, int cidx, int mode, bool &t
         ly &= n - 1;
     }
     const int sbl = log2n - 2, sbw = 1 << sbl;
-    const int last_sub = kScanInv[sbl][scan][(ly >> 2) * sbw + (lx >> 2)];
-    const int last_pos = kScanInv[2][scan][(ly & 3) * 4 + (lx & 3)];
+    const int last_sub = scan_inv(p, sbl, scan, (ly >> 2) * sbw + (lx >> 2));
+    const int last_pos = scan_inv(p, 2, scan, (ly & 3) * 4 + (lx & 3));
     uint64_t csbf = 0;  // coded_sub_block_flag bitmap, bit yS*8+xS
     int prev_c1 = 1;    // greater1Ctx state carried from the previous coded sub-block
     bool any_sb = false;
     coef_first = p.ncoef;
     ncoef = 0;
     for (int i = last_sub; i >= 0; --i) {
-        const int sp = kScanPos[sbl][scan][i];
+        ensure_bytes(p);
+        const int sp = scan_pos(p, sbl, scan, i);
         const int xS = sp & 15, yS = sp >> 4;
         bool coded;
         bool infer_dc = false;
@@ -394,14 +540,13 @@ HG_INLINE void residual_coding(Parser &p, int log2n, int cidx, int mode, bool &t
                 nstart = last_pos - 1;
             }
             for (int nn = nstart; nn >= 0; --nn) {
-                const int pp = kScanPos[2][scan][nn];
+                const int pp = scan_pos(p, 2, scan, nn);
                 const int xP = pp & 15, yP = pp >> 4;
                 if (nn > 0 || !infer_dc) {
                     const int xC = (xS << 2) + xP, yC = (yS << 2) + yP;
                     int sc;
                     if (log2n == 2) {
-                        constexpr uint8_t map[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
-                        sc = map[(yC << 2) + xC];
+                        sc = (int)((kSigCtxMap4 >> (4 * ((yC << 2) + xC))) & 15u);  // Table 9-50
                     } else if (xC + yC == 0) {
                         sc = 0;
                     } else {
@@ -492,13 +637,12 @@ HG_INLINE void residual_coding(Parser &p, int log2n, int cidx, int mode, bool &t
                 if (hide) sum_abs += v;
             }
             if (neg) v = -v;
-            const int pp = kScanPos[2][scan][nn];
+            const int pp = scan_pos(p, 2, scan, nn);
             const int xC = (xS << 2) + (pp & 15), yC = (yS << 2) + (pp >> 4);
             if (v > 32767) v = 32767;
             if (v < -32768) v = -32768;
             if (p.ncoef < p.coef_cap) {
-                if (p.lane == 0)
-                    p.coef_out[p.ncoef] = ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC);
+                p.coef_out[p.ncoef] = ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC);
                 ++p.ncoef;
                 ++ncoef;
             } else {
@@ -513,7 +657,9 @@ HG_INLINE void residual_coding(Parser &p, int log2n, int cidx, int mode, bool &t
 HG_INLINE void emit_tb(Parser &p, int cidx, int x, int y, int log2n, int mode, bool cbf) {
     bool ts = false;
     uint32_t first = p.ncoef, nc = 0;
+    HG_PROF(uint64_t t_rc = prof_clock());
     if (cbf) residual_coding(p, log2n, cidx, mode, ts, first, nc);
+    HG_PROF(p.prof[PF_RESID] += prof_clock() - t_rc);
     int qp;
     if (cidx == 0) {
         qp = p.qpy_cur + p.qpbdY;
@@ -529,7 +675,7 @@ HG_INLINE void emit_tb(Parser &p, int cidx, int x, int y, int log2n, int mode, b
     if (p.cu_bypass) fl |= TU_BYPASS;
     if (cidx == 0 && log2n == 2) fl |= TU_DST;
     if (p.ntu < p.tu_cap) {
-        if (p.lane == 0) {
+        {
             TuRec r;
             r.x = (uint16_t)x;
             r.y = (uint16_t)y;
@@ -572,7 +718,7 @@ HG_INLINE void transform_unit(Parser &p, int x0, int y0, int xb, int yb, int log
     // edge / no-filter flags of every 4x4 luma block of this TB (MF_*)
     {
         const int nb = 1 << (log2n - 2);
-        for (int k = p.lane; k < nb * nb; k += kWave) {
+        HG_LANE_LOOP(k, p.lane, nb * nb) {
             int bx = k % nb, by = k / nb;
             int gx = (x0 >> 2) + bx, gy = (y0 >> 2) + by;
             if (gx < p.w4 && gy < p.h4)
@@ -607,10 +753,11 @@ HG_INLINE void transform_tree(Parser &p, int x0, int y0, int log2cb) {
     };
     uint64_t *st = p.w->tt;
     int sp = 0;
-    if (p.lane == 0) st[0] = pack(x0, y0, x0, y0, log2cb, 0, 0, 0, 0);
+    st[0] = pack(x0, y0, x0, y0, log2cb, 0, 0, 0, 0);
     sp = 1;
     const int max_depth = p.maxDepthIntra + p.cu_intra_split;
     while (sp > 0) {
+        ensure_bytes(p);
         --sp;
         uint64_t e = st[sp];
         uint32_t lo = uni((uint32_t)e), hi = uni((uint32_t)(e >> 32));
@@ -630,12 +777,10 @@ HG_INLINE void transform_tree(Parser &p, int x0, int y0, int log2cb) {
         }
         if (split) {
             int h = 1 << (l - 1);
-            if (p.lane == 0) {
-                st[sp + 0] = pack(x + h, y + h, x, y, l - 1, d + 1, 3, cbf_cb, cbf_cr);
-                st[sp + 1] = pack(x, y + h, x, y, l - 1, d + 1, 2, cbf_cb, cbf_cr);
-                st[sp + 2] = pack(x + h, y, x, y, l - 1, d + 1, 1, cbf_cb, cbf_cr);
-                st[sp + 3] = pack(x, y, x, y, l - 1, d + 1, 0, cbf_cb, cbf_cr);
-            }
+            st[sp + 0] = pack(x + h, y + h, x, y, l - 1, d + 1, 3, cbf_cb, cbf_cr);
+            st[sp + 1] = pack(x, y + h, x, y, l - 1, d + 1, 2, cbf_cb, cbf_cr);
+            st[sp + 2] = pack(x + h, y, x, y, l - 1, d + 1, 1, cbf_cb, cbf_cr);
+            st[sp + 3] = pack(x, y, x, y, l - 1, d + 1, 0, cbf_cb, cbf_cr);
             sp += 4;
             continue;
         }
@@ -701,7 +846,7 @@ HG_INLINE void coding_unit(Parser &p, int x0, int y0, int log2cb, int depth) {
     {
         const int nd = n >> 3;
         const int dx = (x0 - p.ctbx) >> 3, dy = (y0 - p.ctby) >> 3;
-        for (int k = p.lane; k < nd * nd; k += kWave) p.w->depth[dy + k / nd][dx + k % nd + 1] = (uint8_t)depth;
+        HG_LANE_LOOP(k, p.lane, nd * nd) p.w->depth[dy + k / nd][dx + k % nd + 1] = (uint8_t)depth;
     }
     const int np = nxn ? 4 : 1, pb = nxn ? n >> 1 : n;
     int prev[4] = {0, 0, 0, 0};
@@ -714,7 +859,7 @@ HG_INLINE void coding_unit(Parser &p, int x0, int y0, int log2cb, int depth) {
         const int m = derive_luma_mode(p, xPb, yPb, prev[i], mpm, rem);
         const int nb = pb >> 2;
         const int bx = (xPb - p.ctbx) >> 2, by = (yPb - p.ctby) >> 2;
-        for (int k = p.lane; k < nb * nb; k += kWave) p.w->ipm[by + k / nb][bx + k % nb + 1] = (uint8_t)m;
+        HG_LANE_LOOP(k, p.lane, nb * nb) p.w->ipm[by + k / nb][bx + k % nb + 1] = (uint8_t)m;
     }
     if (p.chroma != 0) {
         int icpm = dec_bin(p, CTX_CHROMA_MODE) ? (int)dec_bypass_bits(p, 2) : 4;
@@ -734,9 +879,9 @@ HG_INLINE void coding_unit(Parser &p, int x0, int y0, int log2cb, int depth) {
     {
         const int nd = n >> 3;
         const int dx = (x0 - p.ctbx) >> 3, dy = (y0 - p.ctby) >> 3;
-        for (int k = p.lane; k < nd * nd; k += kWave) p.w->qpy[dy + k / nd][dx + k % nd] = (int8_t)p.qpy_cur;
+        HG_LANE_LOOP(k, p.lane, nd * nd) p.w->qpy[dy + k / nd][dx + k % nd] = (int8_t)p.qpy_cur;
         const int nb = n >> 2;
-        for (int k = p.lane; k < nb * nb; k += kWave) {
+        HG_LANE_LOOP(k, p.lane, nb * nb) {
             int gx = (x0 >> 2) + k % nb, gy = (y0 >> 2) + k / nb;
             if (gx < p.w4 && gy < p.h4) p.gqpy[gy * p.w4 + gx] = (int8_t)p.qpy_cur;
         }
@@ -747,9 +892,10 @@ HG_INLINE void coding_unit(Parser &p, int x0, int y0, int log2cb, int depth) {
 // 7.3.8.4 coding_quadtree, iterative
 HG_INLINE void coding_quadtree(Parser &p) {
     uint32_t *st = p.w->cqt;
-    if (p.lane == 0) st[0] = (uint32_t)p.ctbx | ((uint32_t)p.ctby << 13) | ((uint32_t)p.log2ctb << 26);
+    st[0] = (uint32_t)p.ctbx | ((uint32_t)p.ctby << 13) | ((uint32_t)p.log2ctb << 26);
     int sp = 1;
     while (sp > 0 && !(p.status & ST_UNSUPPORTED)) {
+        ensure_bytes(p);
         --sp;
         uint32_t e = uni(st[sp]);
         int x = (int)(e & 8191), y = (int)((e >> 13) & 8191), l = (int)((e >> 26) & 7), d = (int)(e >> 29);
@@ -781,18 +927,18 @@ HG_INLINE void coding_quadtree(Parser &p) {
             };
             // push in reverse so child 0 is processed first
             if (x + h < p.W && y + h < p.H) {
-                if (p.lane == 0) st[sp] = pk(x + h, y + h);
+                st[sp] = pk(x + h, y + h);
                 ++sp;
             }
             if (y + h < p.H) {
-                if (p.lane == 0) st[sp] = pk(x, y + h);
+                st[sp] = pk(x, y + h);
                 ++sp;
             }
             if (x + h < p.W) {
-                if (p.lane == 0) st[sp] = pk(x + h, y);
+                st[sp] = pk(x + h, y);
                 ++sp;
             }
-            if (p.lane == 0) st[sp] = pk(x, y);
+            st[sp] = pk(x, y);
             ++sp;
             continue;
         }
@@ -803,22 +949,43 @@ HG_INLINE void coding_quadtree(Parser &p) {
 }  // namespace
 
 // ---------------------------------------------------------------- kernel
-__global__ void __launch_bounds__(kParseWaves * 64) k_parse(BatchArgs a) {
+// Occupancy: 6 waves/SIMD (<= 80 VGPRs) so most pictures of a large batch are
+// resident at once; the bin loop is latency-bound per wave, so more waves
+// per SIMD is worth the few spills this costs.  HG_PARSE_WPE=0 disables.
+#ifndef HG_PARSE_WPE
+#define HG_PARSE_WPE 6
+#endif
+#if HG_PARSE_WPE > 0 && !defined(HG_HOST_EMU)
+#define HG_PARSE_ATTR __attribute__((amdgpu_waves_per_eu(HG_PARSE_WPE, HG_PARSE_WPE)))
+#else
+#define HG_PARSE_ATTR
+#endif
+__global__ void __launch_bounds__(kParseWaves * 64) HG_PARSE_ATTR k_parse(BatchArgs a) {
 #if defined(HG_HOST_EMU)
     unsigned char *smem = g_emu.smem;
 #else
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #endif
-    const int pic = blockIdx.x;
+    // block = P pictures x G waves; wave (g, w) parses rows w, w+G, ... of picture
+    // blockIdx.x * P + g.  G = 1 (the batch default) walks every WPP row of its
+    // picture itself; G > 1 runs the rows of one picture concurrently.
+    const int nwb = (int)HG_UNI(blockDim.x >> 6);
+    const int G = a.parse_group;
+    const int P = nwb / G;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int gi = wave / G, wrow = wave - gi * G;
+    const int pic_raw = blockIdx.x * P + gi;
+    const bool active = pic_raw < a.n_pics;
+    const int pic = active ? pic_raw : 0;
     const PicDesc pd = a.pics[pic];
     const SeqParams sp = a.seqs[pd.seq];
 
     WaveLds *wl = reinterpret_cast<WaveLds *>(smem) + wave;
-    uint32_t *progress = reinterpret_cast<uint32_t *>(smem + sizeof(WaveLds) * kParseWaves);
-    uint8_t *wpp_slot = reinterpret_cast<uint8_t *>(progress + kParseWaves);  // [2][CTX_PAD]
     const int dl_stride = ((a.max_width >> 3) + 15) & ~15;
-    uint8_t *depth_line = wpp_slot + 2 * CTX_PAD;                              // [2][dl_stride]
+    uint8_t *grp = smem + sizeof(WaveLds) * nwb + (size_t)gi * parse_group_bytes(a.max_width, a.max_wctb, G);
+    uint32_t *progress = reinterpret_cast<uint32_t *>(grp);                      // [G]
+    uint32_t *wpp_slot = progress + ((G + 3) & ~3);                              // [2][64] context words
+    uint8_t *depth_line = reinterpret_cast<uint8_t *>(wpp_slot + 2 * 64);         // [2][dl_stride]
     SaoParams *sao_line = reinterpret_cast<SaoParams *>(depth_line + 2 * dl_stride);  // [2][max_wctb]
 
     Parser p;
@@ -851,6 +1018,14 @@ __global__ void __launch_bounds__(kParseWaves * 64) k_parse(BatchArgs a) {
     p.status = 0;
     p.w = wl;
     p.lane = lane;
+    p.cx.load_tables(lane);
+#if !defined(HG_HOST_EMU)
+    {
+        const uint32_t e = kScanPos[3][0][lane];
+        p.scanv = ((e & 7) | ((e >> 4) << 3)) | ((uint32_t)kScanInv[3][0][lane] << 8);
+    }
+#endif
+    HG_PROF(for (int k = 0; k < PF_N; ++k) p.prof[k] = 0; const uint64_t t_start = prof_clock();)
     p.w4 = (p.W + 3) >> 2;
     p.h4 = (p.H + 3) >> 2;
     p.gqpy = reinterpret_cast<int8_t *>(a.maps + pd.map_off);
@@ -859,15 +1034,15 @@ __global__ void __launch_bounds__(kParseWaves * 64) k_parse(BatchArgs a) {
     const uint32_t *subs = a.subs + pd.sub_first;
     const bool wpp = (p.flags & SP_WPP) != 0;
 
-    if (lane == 0) progress[wave] = 0;
+    progress[wrow] = 0;
     __syncthreads();
 
     // rows: WPP → one substream per CTB row, wave w takes rows w, w+16, ...;
     // otherwise the picture is one substream and wave 0 walks every row.
-    const int row_step = wpp ? kParseWaves : 1;
-    const int first_row = wpp ? wave : (wave == 0 ? 0 : p.hctb);
+    const int row_step = wpp ? G : 1;
+    const int first_row = !active ? p.hctb : (wpp ? wrow : (wrow == 0 ? 0 : p.hctb));
     const uint32_t stride = (uint32_t)p.wctb + 1;
-    const int prev_wave = (wave + kParseWaves - 1) % kParseWaves;
+    const int prev_wave = (wrow + G - 1) % G;
     bool stop = false;
     for (int r = first_row; r < p.hctb && !stop; r += row_step) {
         p.ry = r;
@@ -886,8 +1061,9 @@ __global__ void __launch_bounds__(kParseWaves * 64) k_parse(BatchArgs a) {
             p.ctby = r << p.log2ctb;
             if (wpp && r > 0) {
                 // WPP lag: row r-1 must have finished CTU min(c+1, wctb-1)
+                HG_PROF(uint64_t t_w = prof_clock());
                 const uint32_t need = (uint32_t)(r - 1) * stride + (uint32_t)((c + 2) < p.wctb ? (c + 2) : p.wctb);
-                for (uint32_t spin = 0; hg_atomic_load(&progress[prev_wave]) < need; ++spin) {
+                for (uint32_t spin = 0; uni(hg_atomic_load(&progress[prev_wave])) < need; ++spin) {
                     if (spin > (1u << 24)) {  // bounded: never hang the device
                         p.status |= ST_SUBSTREAM_END;
                         break;
@@ -895,74 +1071,117 @@ __global__ void __launch_bounds__(kParseWaves * 64) k_parse(BatchArgs a) {
                     HG_SLEEP();
                 }
                 HG_FENCE_ACQ();
+                HG_PROF(p.prof[PF_SPIN] += prof_clock() - t_w);
             }
             if (c == 0 && (wpp || r == 0)) {
                 // substream start: contexts (init or WPP sync, 9.3.1) + engine (9.3.2.5)
                 if (r == 0 || p.wctb < 2) ctx_init(p);
                 else
-                    for (int i = lane; i < CTX_PAD; i += kWave) wl->ctx[i] = wpp_slot[((r + 1) & 1) * CTX_PAD + i];
+                    p.cx.restore(wpp_slot + ((r + 1) & 1) * 64, lane);
                 engine_init(p, subs[wpp ? r : 0]);
                 if (r == 0) p.first_qg_in_slice = true;
             }
             // left-CTB columns of the per-wave maps
             if (c > 0) {
                 const int nb4 = p.ctb >> 2, nb8 = p.ctb >> 3;
-                for (int k = lane; k < nb4; k += kWave) wl->ipm[k][0] = wl->ipm[k][nb4];
-                for (int k = lane; k < nb8; k += kWave) wl->depth[k][0] = wl->depth[k][nb8];
+                HG_LANE_LOOP(k, lane, nb4) wl->ipm[k][0] = wl->ipm[k][nb4];
+                HG_LANE_LOOP(k, lane, nb8) wl->depth[k][0] = wl->depth[k][nb8];
             }
+            HG_PROF(uint64_t t_s = prof_clock());
             if (p.saoL || p.saoC) parse_sao(p, sao_above, gsao);
+            HG_PROF(uint64_t t_q = prof_clock());
             coding_quadtree(p);
+            HG_PROF(p.prof[PF_SAO] += t_q - t_s; p.prof[PF_CQT] += prof_clock() - t_q);
             if (p.status & ST_UNSUPPORTED) {
                 stop = true;
             }
             if (wpp && c == 1)
-                for (int i = lane; i < CTX_PAD; i += kWave) wpp_slot[(r & 1) * CTX_PAD + i] = wl->ctx[i];
+                p.cx.save(wpp_slot + (r & 1) * 64, lane);
             // bottom row of this CTB for the row below: depths, SAO parameters
             {
                 const int nb8 = p.ctb >> 3;
-                for (int k = lane; k < nb8; k += kWave) depth_cur_line[(p.ctbx >> 3) + k] = wl->depth[nb8 - 1][k + 1];
-                if (lane == 0) sao_cur_line[c] = wl->sao_left;
+                HG_LANE_LOOP(k, lane, nb8) depth_cur_line[(p.ctbx >> 3) + k] = wl->depth[nb8 - 1][k + 1];
+                sao_cur_line[c] = wl->sao_left;
             }
             // end_of_slice_segment_flag / end_of_subset_one_bit (slice.rs:214-227)
             const bool last_in_pic = (r == p.hctb - 1) && (c == p.wctb - 1);
+            ensure_bytes(p);
             int eos = dec_term(p);
             if (eos != (last_in_pic ? 1 : 0)) p.status |= ST_SUBSTREAM_END;
             if (!last_in_pic && wpp && c == p.wctb - 1) {
                 if (!dec_term(p)) p.status |= ST_SUBSTREAM_END;
             }
+            check_overrun(p);
             // publish progress (release: LDS lines, WPP slot, global maps)
             HG_FENCE_REL();
-            if (lane == 0) hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)(c + 1));
+            hg_atomic_store(&progress[wrow], (uint32_t)r * stride + (uint32_t)(c + 1));
             if (stop) break;
         }
-        if (lane == 0) {
-            a.row_counts[2 * (pd.row_off + r)] = p.ntu;
-            a.row_counts[2 * (pd.row_off + r) + 1] = p.ncoef;
-        }
+        a.row_counts[2 * (pd.row_off + r)] = p.ntu;
+        a.row_counts[2 * (pd.row_off + r) + 1] = p.ncoef;
     }
     if (stop && wpp) {
         // let rows waiting on this wave drain
-        if (lane == 0) hg_atomic_store(&progress[wave], 0x7fffffffu);
+        hg_atomic_store(&progress[wrow], 0x7fffffffu);
     }
-    if (p.status && lane == 0) atomicOr(&a.status[pic], p.status);
+    if (p.status) atomicOr(&a.status[pic], p.status);  // uniform branch; idempotent OR
+    HG_PROF(p.prof[PF_WAVE] = prof_clock() - t_start;
+            if (lane == 0) for (int k = 0; k < PF_N; ++k) atomicAdd((unsigned long long *)&g_prof[k], (unsigned long long)p.prof[k]);)
 }
 
-size_t parse_lds_bytes(int max_width, int max_wctb) {
-    size_t dl_stride = (size_t)(((max_width >> 3) + 15) & ~15);
-    return sizeof(WaveLds) * kParseWaves + sizeof(uint32_t) * kParseWaves + 2 * CTX_PAD + 2 * dl_stride +
-           2 * (size_t)max_wctb * sizeof(SaoParams);
+ParseShape parse_shape(const BatchArgs &a) {
+    // Many pictures: one wave per picture (no WPP wait, every wave busy);
+    // few: the rows of a picture on G waves.  HEIFGPU_PARSE_GROUP overrides.
+    static const int forced = [] {
+        const char *e = std::getenv("HEIFGPU_PARSE_GROUP");
+        return e ? std::atoi(e) : 0;
+    }();
+    const int rows = a.max_rows < 1 ? 1 : (a.max_rows > kParseWaves ? kParseWaves : a.max_rows);
+    ParseShape sh;
+    sh.group = forced > 0 ? (forced < rows ? forced : rows) : (a.n_pics >= kParseSerialMinPics ? 1 : rows);
+    sh.pics_per_block = sh.group == 1 ? kParseSerialPicsPerBlock : 1;
+    sh.blocks = (a.n_pics + sh.pics_per_block - 1) / sh.pics_per_block;
+    const int nwb = sh.group * sh.pics_per_block;
+    sh.threads = 64 * nwb;
+    sh.lds = sizeof(WaveLds) * nwb + sh.pics_per_block * parse_group_bytes(a.max_width, a.max_wctb, sh.group);
+    return sh;
 }
 
 #if defined(HG_HOST_EMU)
-void emu_parse(const BatchArgs &a) {
-    emu_launch(k_parse, a.n_pics, 1, kParseWaves, a, false, parse_lds_bytes(a.max_width, a.max_wctb));
+void emu_parse(const BatchArgs &a0) {
+    BatchArgs a = a0;
+    const ParseShape sh = parse_shape(a);
+    a.parse_group = sh.group;
+    emu_launch(k_parse, sh.blocks, 1, sh.threads / 64, a, false, sh.lds);
 }
 #else
-hipError_t launch_parse(const BatchArgs &a, hipStream_t s) {
-    size_t lds = parse_lds_bytes(a.max_width, a.max_wctb);
-    hipLaunchKernelGGL(k_parse, dim3(a.n_pics), dim3(kParseWaves * 64), lds, s, a);
+hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
+    BatchArgs a = a0;
+    const ParseShape sh = parse_shape(a);
+    a.parse_group = sh.group;
+    hipLaunchKernelGGL(k_parse, dim3(sh.blocks), dim3(sh.threads), sh.lds, s, a);
     return hipGetLastError();
 }
 #endif
 
 }  // namespace hg
+
+#if !defined(HG_HOST_EMU)
+// Debug hook (include/heifgpu.h): copies the k_parse counters out and zeroes
+// them.  Returns the number of counters, or 0 when the library was built
+// without -DHG_PARSE_PROF (the product build).
+extern "C" int heifgpu_debug_counters(uint64_t *out, int n) {
+#if defined(HG_PARSE_PROF)
+    uint64_t tmp[16] = {};
+    if (hipMemcpyFromSymbol(tmp, HIP_SYMBOL(hg::g_prof), sizeof(tmp)) != hipSuccess) return -1;
+    uint64_t zero[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_prof), zero, sizeof(zero)) != hipSuccess) return -1;
+    for (int k = 0; k < n && k < hg::PF_N; ++k) out[k] = tmp[k];
+    return hg::PF_N;
+#else
+    (void)out;
+    (void)n;
+    return 0;
+#endif
+}
+#endif

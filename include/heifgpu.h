@@ -122,6 +122,14 @@ int heifgpu_bins_chroma_pred_mode(const uint8_t *bins, int n, int *used);
 int heifgpu_bins_coeff_abs_level_remaining(const uint8_t *bins, int n, int c_rice, int *used);
 int heifgpu_bins_exp_golomb(const uint8_t *bins, int n, int k, int *used);
 
+/* ---- tuning hook ------------------------------------------------------ */
+/* k_parse cycle/bin counters (wave cycles, WPP wait cycles, context bins,
+ * bypass bins, ring refills, coding_quadtree / residual_coding / SAO cycles),
+ * summed over waves since the last call, then reset.  Returns the number of
+ * counters written, or 0 for the product build (counters compiled out; the
+ * `make prof` library has them). */
+int heifgpu_debug_counters(uint64_t *out, int n);
+
 #ifdef __cplusplus
 }
 #endif

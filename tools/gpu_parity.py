@@ -43,8 +43,12 @@ def main():
             scale = 1 if name == "Y" else 2
             print("  first mismatch at", (y, x), "tile", (y * scale // 512, x * scale // 512), "gpu", g[y, x], "ref", r[y, x])
     # throughput on a repeated decode
-    for _ in range(3):
+    for k in range(3):
         batch.decode_async(outs)
+        st2 = batch.status()
+        if any(st2):
+            print("repeat decode", k, "status", st2)
+            ok = False
     torch.cuda.synchronize()
     t0 = time.time()
     n = 10
