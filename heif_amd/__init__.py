@@ -69,9 +69,17 @@ class HeifImage:
         _lib.check(lib.heifgpu_image_get_info(self._h, ctypes.byref(info)))
         return info
 
+    def tile_params(self, tile: int) -> dict:
+        """Parsed SPS/PPS/slice-header fields of grid tile `tile` (row-major)."""
+        tp = _lib.TileParams()
+        _lib.check(lib.heifgpu_image_tile_params(self._h, tile, ctypes.byref(tp)))
+        d = {n: getattr(tp, n) for n, _ in tp._fields_ if n != "entry_point_offset"}
+        d["entry_point_offset"] = list(tp.entry_point_offset[: min(tp.num_entry_point_offsets, 64)])
+        return d
+
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value:
+        if h is not None and h.value and lib is not None:  # lib is None during interpreter teardown
             lib.heifgpu_image_free(h)
             self._h = None
 

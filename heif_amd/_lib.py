@@ -43,6 +43,67 @@ class ImageInfo(ctypes.Structure):
     ]
 
 
+class TileParams(ctypes.Structure):
+    """heifgpu_tile_params (parsed SPS/PPS/slice header of one tile)."""
+    _fields_ = [(name, ctypes.c_int32) for name in (
+            "nal_unit_type",
+            "slice_type",
+            "first_slice_segment_in_pic",
+            "general_profile_idc",
+            "general_level_idc",
+            "pic_width",
+            "pic_height",
+            "chroma_format_idc",
+            "bit_depth_luma",
+            "bit_depth_chroma",
+            "log2_max_poc_lsb",
+            "log2_min_cb",
+            "log2_ctb",
+            "log2_min_tb",
+            "log2_max_tb",
+            "max_th_depth_inter",
+            "max_th_depth_intra",
+            "scaling_list_enabled",
+            "amp",
+            "sao",
+            "pcm",
+            "num_short_term_ref_pic_sets",
+            "long_term_refs",
+            "temporal_mvp",
+            "strong_intra_smoothing",
+            "video_full_range",
+            "colour_primaries",
+            "transfer_characteristics",
+            "matrix_coeffs",
+            "init_qp",
+            "sign_data_hiding",
+            "cabac_init_present",
+            "constrained_intra_pred",
+            "transform_skip",
+            "cu_qp_delta_enabled",
+            "diff_cu_qp_delta_depth",
+            "cb_qp_offset",
+            "cr_qp_offset",
+            "slice_chroma_qp_offsets_present",
+            "transquant_bypass",
+            "tiles_enabled",
+            "entropy_coding_sync",
+            "loop_filter_across_slices",
+            "deblocking_control_present",
+            "deblocking_override_enabled",
+            "deblocking_disabled",
+            "beta_offset_div2",
+            "tc_offset_div2",
+            "log2_parallel_merge_level",
+            "slice_sao_luma",
+            "slice_sao_chroma",
+            "slice_qp_y",
+            "num_entry_point_offsets",
+            "slice_data_raw_offset",
+            "payload_bytes",
+    )] + [("entry_point_offset", ctypes.c_uint32 * 64)]
+
+
 class Planes(ctypes.Structure):
     _fields_ = [("plane", ctypes.c_void_p * 3), ("pitch", ctypes.c_int32 * 3)]
 
@@ -54,7 +115,7 @@ EXPORTS = (
     "heifgpu_batch_status", "heifgpu_batch_free", "heifgpu_set_timing", "heifgpu_stage_times",
     "heifgpu_decode_batch", "heifgpu_remove_emulation_prevention", "heifgpu_read_ue",
     "heifgpu_read_se", "heifgpu_bins_truncated_rice", "heifgpu_bins_chroma_pred_mode",
-    "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb", "heifgpu_debug_counters",
+    "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb", "heifgpu_image_tile_params", "heifgpu_debug_counters",
 )
 
 
@@ -68,7 +129,21 @@ class UnsupportedError(HeifGpuError):
     pass
 
 
+def _bind_hip_runtime() -> None:
+    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64;
+    if libheifgpu.so were loaded first it would pull /opt/rocm's copy and the
+    two runtimes cannot share the device (whichever initialises second sees
+    no GPU).  Importing torch first makes the dynamic linker bind
+    libheifgpu.so's libamdhip64.so.7 dependency to torch's already-loaded
+    copy.  Without torch (e.g. a C/Rust host) nothing changes."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load() -> ctypes.CDLL:
+    _bind_hip_runtime()
     if not LIB_PATH.exists():
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
@@ -98,6 +173,7 @@ def _load() -> ctypes.CDLL:
         "heifgpu_bins_chroma_pred_mode": (I32, [u8p, I32, P(I32)]),
         "heifgpu_bins_coeff_abs_level_remaining": (I32, [u8p, I32, I32, P(I32)]),
         "heifgpu_bins_exp_golomb": (I32, [u8p, I32, I32, P(I32)]),
+        "heifgpu_image_tile_params": (I32, [VP, U32, P(TileParams)]),
         "heifgpu_debug_counters": (I32, [P(ctypes.c_uint64), I32]),
     }
     for name, (res, args) in sig.items():

@@ -24,7 +24,6 @@ struct heifgpu_image {
 
 struct heifgpu_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
     bool timing = false;
     hipEvent_t ev[6] = {};
     float stage_ms[5] = {};
@@ -138,7 +137,6 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     HIP_TRY(hipSetDevice(device));
     auto c = std::make_unique<heifgpu_ctx>();
     c->device = device;
-    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
     *out = c.release();
     return HEIFGPU_OK;
@@ -149,7 +147,6 @@ void heifgpu_destroy(heifgpu_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     for (auto &e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
@@ -251,7 +248,7 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
 int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_planes *out, void *stream) {
     if (!ctx || !b || !out) return fail(HEIFGPU_E_INVALID, "invalid argument");
     if (b->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream, as in HIP
     HIP_TRY(hipSetDevice(ctx->device));
     bool changed = false;
     for (size_t i = 0; i < b->n_images; ++i) {
@@ -300,7 +297,7 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
 
 int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *b, uint32_t *status, void *stream) {
     if (!ctx || !b) return fail(HEIFGPU_E_INVALID, "invalid argument");
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream, as in HIP
     HIP_TRY(hipSetDevice(ctx->device));
     std::vector<uint32_t> st(size_t(b->n_pics));
     HIP_TRY(hipMemcpyAsync(st.data(), b->status.p, st.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -400,6 +397,74 @@ int heifgpu_bins_exp_golomb(const uint8_t *bins, int n, int k, int *used) {
     uint32_t r = bin_exp_golomb(v, k);
     if (used) *used = v.i;
     return (v.under || r == 0xffffffffu) ? -1 : int(r);
+}
+
+int heifgpu_image_tile_params(const heifgpu_image *img, uint32_t tile, heifgpu_tile_params *o) {
+    if (!img || !o) return fail(HEIFGPU_E_INVALID, "invalid argument");
+    const ParsedImage &pi = img->img;
+    if (tile >= pi.tiles.size()) return fail(HEIFGPU_E_INVALID, "tile index out of range");
+    const TileJob &t = pi.tiles[tile];
+    const SequenceParameterSet &sps = pi.params[t.param].sps;
+    const PictureParameterSet &pps = pi.params[t.param].pps;
+    const SliceSegmentHeader &sh = t.sh;
+    std::memset(o, 0, sizeof(*o));
+    o->nal_unit_type = t.nal.nal_unit_type();
+    o->slice_type = sh.slice_type;
+    o->first_slice_segment_in_pic = sh.first_slice_segment_in_pic_flag;
+    o->general_profile_idc = sps.general_profile_idc;
+    o->general_level_idc = sps.general_level_idc;
+    o->pic_width = sps.pic_width_in_luma_samples;
+    o->pic_height = sps.pic_height_in_luma_samples;
+    o->chroma_format_idc = sps.chroma_format_idc;
+    o->bit_depth_luma = 8 + sps.bit_depth_luma_minus8;
+    o->bit_depth_chroma = 8 + sps.bit_depth_chroma_minus8;
+    o->log2_max_poc_lsb = sps.log2_max_pic_order_cnt_lsb;
+    o->log2_min_cb = sps.log2_min_luma_coding_block_size;
+    o->log2_ctb = sps.log2_ctb_size;
+    o->log2_min_tb = sps.log2_min_tb_size;
+    o->log2_max_tb = sps.log2_max_tb_size;
+    o->max_th_depth_inter = sps.max_transform_hierarchy_depth_inter;
+    o->max_th_depth_intra = sps.max_transform_hierarchy_depth_intra;
+    o->scaling_list_enabled = sps.scaling_list_enabled_flag;
+    o->amp = sps.amp_enabled_flag;
+    o->sao = sps.sample_adaptive_offset_enabled_flag;
+    o->pcm = sps.pcm_enabled_flag;
+    o->num_short_term_ref_pic_sets = sps.num_short_term_ref_pic_sets;
+    o->long_term_refs = sps.long_term_ref_pics_present_flag;
+    o->temporal_mvp = sps.sps_temporal_mvp_enabled_flag;
+    o->strong_intra_smoothing = sps.strong_intra_smoothing_enabled_flag;
+    o->video_full_range = sps.video_full_range_flag;
+    o->colour_primaries = sps.colour_primaries;
+    o->transfer_characteristics = sps.transfer_characteristics;
+    o->matrix_coeffs = sps.matrix_coeffs;
+    o->init_qp = 26 + pps.init_qp_minus26;
+    o->sign_data_hiding = pps.sign_data_hiding_enabled_flag;
+    o->cabac_init_present = pps.cabac_init_present_flag;
+    o->constrained_intra_pred = pps.constrained_intra_pred_flag;
+    o->transform_skip = pps.transform_skip_enabled_flag;
+    o->cu_qp_delta_enabled = pps.cu_qp_delta_enabled_flag;
+    o->diff_cu_qp_delta_depth = pps.diff_cu_qp_delta_depth;
+    o->cb_qp_offset = pps.pps_cb_qp_offset;
+    o->cr_qp_offset = pps.pps_cr_qp_offset;
+    o->slice_chroma_qp_offsets_present = pps.pps_slice_chroma_qp_offsets_present_flag;
+    o->transquant_bypass = pps.transquant_bypass_enabled_flag;
+    o->tiles_enabled = pps.tiles_enabled_flag;
+    o->entropy_coding_sync = pps.entropy_coding_sync_enabled_flag;
+    o->loop_filter_across_slices = pps.pps_loop_filter_across_slices_enabled_flag;
+    o->deblocking_control_present = pps.deblocking_filter_control_present_flag;
+    o->deblocking_override_enabled = pps.deblocking_filter_override_enabled_flag;
+    o->deblocking_disabled = sh.slice_deblocking_filter_disabled_flag;
+    o->beta_offset_div2 = sh.slice_beta_offset_div2;
+    o->tc_offset_div2 = sh.slice_tc_offset_div2;
+    o->log2_parallel_merge_level = pps.log2_parallel_merge_level;
+    o->slice_sao_luma = sh.slice_sao_luma_flag;
+    o->slice_sao_chroma = sh.slice_sao_chroma_flag;
+    o->slice_qp_y = 26 + pps.init_qp_minus26 + sh.slice_qp_delta;
+    o->num_entry_point_offsets = sh.num_entry_point_offsets;
+    o->slice_data_raw_offset = int32_t(sh.slice_data_raw_offset);
+    o->payload_bytes = int32_t(t.payload.size());
+    for (size_t i = 0; i < sh.entry_point_offset.size() && i < 64; ++i) o->entry_point_offset[i] = sh.entry_point_offset[i];
+    return HEIFGPU_OK;
 }
 
 }  // extern "C"

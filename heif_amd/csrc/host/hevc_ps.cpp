@@ -379,7 +379,8 @@ PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp,
         p.loop_filter_across_tiles_enabled_flag = r.read_flag();
     }
     p.pps_loop_filter_across_slices_enabled_flag = r.read_flag();
-    if (r.read_flag()) {
+    p.deblocking_filter_control_present_flag = r.read_flag();
+    if (p.deblocking_filter_control_present_flag) {
         p.deblocking_filter_override_enabled_flag = r.read_flag();
         p.pps_deblocking_filter_disabled_flag = r.read_flag();
         if (!p.pps_deblocking_filter_disabled_flag) {

@@ -85,6 +85,7 @@ struct PictureParameterSet {
     std::vector<int> column_widths, row_heights;  // kept (reference drops them, :393-400)
     bool uniform_spacing_flag = true, loop_filter_across_tiles_enabled_flag = false;
     bool pps_loop_filter_across_slices_enabled_flag = false;
+    bool deblocking_filter_control_present_flag = false;
     bool deblocking_filter_override_enabled_flag = false, pps_deblocking_filter_disabled_flag = false;
     int pps_beta_offset_div2 = 0, pps_tc_offset_div2 = 0;
     bool pps_scaling_list_data_present_flag = false;

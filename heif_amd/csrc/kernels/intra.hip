@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_intra(BatchArgs a) {
                 cur = c;
                 if (r > 0) {
                     const uint32_t need = (uint32_t)(r - 1) * stride + (uint32_t)min(c + 2, wctb);
-                    for (uint32_t spin = 0; HG_UNI(hg_atomic_load(&progress[prev_wave])) < need; ++spin) {
+                    for (uint32_t spin = 0; (uint32_t)HG_UNI(hg_atomic_load(&progress[prev_wave])) < need; ++spin) {
                         if (spin > (1u << 24)) {  // bounded: never hang the device
                             if (lane == 0) atomicOr(&a.status[pic], ST_SUBSTREAM_END);
                             break;

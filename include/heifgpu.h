@@ -93,8 +93,8 @@ const char *heifgpu_last_error(void);
  * heifgpu_batch_prepare flattens n images (all must share bit depth and
  * chroma format) into device descriptors, uploads their bitstreams
  * (synchronously) and allocates the work arenas.  heifgpu_batch_decode
- * then enqueues the five decode stages on `stream` (a hipStream_t, NULL =
- * the context's default stream) and returns immediately; out[i] receives
+ * then enqueues the five decode stages on `stream` (a hipStream_t; NULL =
+ * the device's null stream, as everywhere in HIP) and returns immediately; out[i] receives
  * image i.  It may be called repeatedly on the same batch (the bench times
  * exactly this call).  heifgpu_batch_status synchronises the stream and
  * returns the per-image status words (0 = ok). */
@@ -121,6 +121,28 @@ int heifgpu_bins_truncated_rice(const uint8_t *bins, int n, int c_max, int c_ric
 int heifgpu_bins_chroma_pred_mode(const uint8_t *bins, int n, int *used);
 int heifgpu_bins_coeff_abs_level_remaining(const uint8_t *bins, int n, int c_rice, int *used);
 int heifgpu_bins_exp_golomb(const uint8_t *bins, int n, int k, int *used);
+
+/* parsed parameter sets + slice header of one tile (grammar.rs:224-572;
+ * the values SURVEY Appendix A lists for halfmoonbay) */
+typedef struct {
+    int32_t nal_unit_type, slice_type, first_slice_segment_in_pic;
+    int32_t general_profile_idc, general_level_idc;
+    int32_t pic_width, pic_height, chroma_format_idc, bit_depth_luma, bit_depth_chroma;
+    int32_t log2_max_poc_lsb, log2_min_cb, log2_ctb, log2_min_tb, log2_max_tb;
+    int32_t max_th_depth_inter, max_th_depth_intra;
+    int32_t scaling_list_enabled, amp, sao, pcm, num_short_term_ref_pic_sets, long_term_refs;
+    int32_t temporal_mvp, strong_intra_smoothing;
+    int32_t video_full_range, colour_primaries, transfer_characteristics, matrix_coeffs;
+    int32_t init_qp, sign_data_hiding, cabac_init_present, constrained_intra_pred, transform_skip;
+    int32_t cu_qp_delta_enabled, diff_cu_qp_delta_depth, cb_qp_offset, cr_qp_offset;
+    int32_t slice_chroma_qp_offsets_present, transquant_bypass, tiles_enabled, entropy_coding_sync;
+    int32_t loop_filter_across_slices, deblocking_control_present, deblocking_override_enabled;
+    int32_t deblocking_disabled, beta_offset_div2, tc_offset_div2, log2_parallel_merge_level;
+    int32_t slice_sao_luma, slice_sao_chroma, slice_qp_y, num_entry_point_offsets;
+    int32_t slice_data_raw_offset, payload_bytes;
+    uint32_t entry_point_offset[64]; /* offset_minus1 + 1 (raw bytes), first 64 */
+} heifgpu_tile_params;
+int heifgpu_image_tile_params(const heifgpu_image *img, uint32_t tile, heifgpu_tile_params *out);
 
 /* ---- tuning hook ------------------------------------------------------ */
 /* k_parse cycle/bin counters (wave cycles, WPP wait cycles, context bins,

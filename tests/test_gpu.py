@@ -1,0 +1,167 @@
+"""GPU parity through the C ABI (run with -m gpu on an MI355X).
+
+Bar: bit-exact planes against the CPU oracle on the same input.  At the
+bench's batch sizes the check is size-independent: a permuted image is the
+oracle's 48 independently decoded tiles re-placed by the permutation, so
+every image of a large batch (which also switches k_parse to one wave per
+picture) is checked without re-running the oracle per image.
+"""
+import ctypes
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def H():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import heif_amd
+
+    return heif_amd
+
+
+@pytest.fixture(scope="module")
+def ctx(H):
+    c = H.DecodeContext(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def oracle_tiles(oracle_mod, halfmoonbay):
+    tiles, (ho, hl) = oracle_mod.list_tiles(halfmoonbay)
+    hvcc = halfmoonbay[ho:ho + hl]
+    return [oracle_mod.decode_tile(hvcc, halfmoonbay[o:o + n], 512, 512) for o, n in tiles]
+
+
+def assemble(tiles, perm, rows=6, cols=8, w=4032, h=3024):
+    y = np.zeros((h, w), np.uint16)
+    cb = np.zeros((h // 2, w // 2), np.uint16)
+    cr = np.zeros_like(cb)
+    for k in range(rows * cols):
+        r, c = divmod(k, cols)
+        ty, tcb, tcr = tiles[perm[k]]
+        hh, ww = min(512, h - 512 * r), min(512, w - 512 * c)
+        y[512 * r:512 * r + hh, 512 * c:512 * c + ww] = ty[:hh, :ww]
+        cb[256 * r:256 * r + hh // 2, 256 * c:256 * c + ww // 2] = tcb[:hh // 2, :ww // 2]
+        cr[256 * r:256 * r + hh // 2, 256 * c:256 * c + ww // 2] = tcr[:hh // 2, :ww // 2]
+    return y, cb, cr
+
+
+def planes_np(o):
+    return [t.cpu().numpy().astype(np.uint16) for t in (o.y, o.cb, o.cr)]
+
+
+def test_halfmoonbay_bit_exact(H, oracle_halfmoonbay, halfmoonbay):
+    out = H.HeicDecoder.decode(halfmoonbay)
+    y, cb, cr = planes_np(out)
+    assert np.array_equal(y, oracle_halfmoonbay.y)
+    assert np.array_equal(cb, oracle_halfmoonbay.cb)
+    assert np.array_equal(cr, oracle_halfmoonbay.cr)
+    g = json.loads((GOLDEN / "halfmoonbay_planes.json").read_text())
+    assert hashlib.sha256(out.y.cpu().numpy().tobytes()).hexdigest() == g["planes"]["y"]
+
+
+def test_permuted_batch_row_parallel(H, ctx, oracle_tiles, halfmoonbay):
+    from heif_amd.synthetic import permutation, permuted_heic
+
+    seeds = [1, 2, 3]
+    imgs = [H.HeifImage.parse(permuted_heic(halfmoonbay, s)) for s in seeds]
+    outs = ctx.alloc_outputs(imgs)
+    b = ctx.prepare(imgs)
+    b.decode_async(outs)
+    assert b.status() == [0, 0, 0]
+    for s, o in zip(seeds, outs):
+        want = assemble(oracle_tiles, permutation(48, s))
+        for got, w in zip(planes_np(o), want):
+            assert np.array_equal(got, w), s
+    b.free()
+
+
+def test_large_batch_one_wave_per_picture(H, ctx, oracle_tiles, halfmoonbay):
+    """22 images = 1056 pictures >= kParseSerialMinPics: the serial-row parse mode."""
+    from heif_amd.synthetic import permutation, permuted_heic
+
+    seeds = list(range(100, 122))
+    imgs = [H.HeifImage.parse(permuted_heic(halfmoonbay, s)) for s in seeds]
+    outs = ctx.alloc_outputs(imgs)
+    b = ctx.prepare(imgs)
+    b.decode_async(outs)
+    assert not any(b.status())
+    for s, o in zip(seeds, outs):
+        want = assemble(oracle_tiles, permutation(48, s))
+        for got, w in zip(planes_np(o), want):
+            assert np.array_equal(got, w), s
+    b.free()
+
+
+def test_repeat_decode_is_deterministic(H, ctx, halfmoonbay):
+    imgs = [H.HeifImage.parse(halfmoonbay)]
+    outs = ctx.alloc_outputs(imgs)
+    b = ctx.prepare(imgs)
+    b.decode_async(outs)
+    first = [t.clone() for t in (outs[0].y, outs[0].cb, outs[0].cr)]
+    for _ in range(3):
+        for t in (outs[0].y, outs[0].cb, outs[0].cr):
+            t.fill_(0)
+        b.decode_async(outs)
+        assert b.status() == [0]
+        for a, t in zip(first, (outs[0].y, outs[0].cb, outs[0].cr)):
+            assert torch.equal(a, t)
+    b.free()
+
+
+def test_pitched_outputs(H, ctx, oracle_halfmoonbay, halfmoonbay):
+    """Caller-owned planes with a row pitch larger than the width."""
+    from heif_amd import _lib
+
+    img = H.HeifImage.parse(halfmoonbay)
+    y = torch.zeros((3024, 4096), dtype=torch.uint8, device="cuda")
+    cb = torch.zeros((1512, 2048), dtype=torch.uint8, device="cuda")
+    cr = torch.zeros((1512, 2048), dtype=torch.uint8, device="cuda")
+    planes = (_lib.Planes * 1)()
+    for c, t in enumerate((y, cb, cr)):
+        planes[0].plane[c] = t.data_ptr()
+        planes[0].pitch[c] = t.stride(0)
+    st = (ctypes.c_uint32 * 1)()
+    arr = (ctypes.c_void_p * 1)(img._h.value)
+    s = torch.cuda.current_stream().cuda_stream
+    assert _lib.lib.heifgpu_decode_batch(ctx._h, arr, 1, planes, ctypes.c_void_p(s), st) == 0
+    assert st[0] == 0
+    assert np.array_equal(y[:, :4032].cpu().numpy(), oracle_halfmoonbay.y)
+    assert np.array_equal(cr[:, :2016].cpu().numpy(), oracle_halfmoonbay.cr)
+    assert int(y[:, 4032:].abs().sum()) == 0  # nothing written past the width
+
+
+@pytest.mark.parametrize("mode", ["random", "zeroed"])
+def test_corrupt_stream_sets_status_not_fault(H, ctx, halfmoonbay, mode):
+    from test_emulation import _corrupt
+
+    imgs = [H.HeifImage.parse(_corrupt(halfmoonbay, mode)), H.HeifImage.parse(halfmoonbay)]
+    outs = ctx.alloc_outputs(imgs)
+    b = ctx.prepare(imgs)
+    b.decode_async(outs)
+    st = b.status()
+    assert st[0] != 0 and st[1] == 0
+    b.free()
+
+
+def test_empty_batch_rejected(H, ctx):
+    with pytest.raises(H.HeifGpuError):
+        ctx.prepare([])
+
+
+def test_native_library_is_loaded(H):
+    import pathlib
+
+    maps = pathlib.Path("/proc/self/maps").read_text()
+    assert "libheifgpu" in maps
