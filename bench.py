@@ -166,7 +166,7 @@ def main():
                 verified += 1
         px = info.width * info.height
         total_images = args.batch * world
-        value = total_images * px / elapsed / 1e6
+        value = total_images * px * args.steps / elapsed / 1e6  # every step decodes the whole batch
         per_step = [m / args.steps for m in stage_ms]
         parse_ms = per_step[0]
         coded_px = info.grid_cols * info.tile_width * info.grid_rows * info.tile_height
@@ -221,7 +221,11 @@ def main():
         }
         if not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(src, args.cpu_seconds, threads)
+            cb = cpu_baseline(src, args.cpu_seconds, threads)
+            one = cpu_baseline(src, min(args.cpu_seconds, 4.0), 1)
+            cb["value_1core"] = one["value"]
+            cb["host_cpus"] = os.cpu_count()
+            line["cpu_baseline"] = cb
         print(json.dumps(line), flush=True)
     batch.free()
     if world > 1:
