@@ -38,7 +38,6 @@ const char *oracle_last_error(void) { return g_err; }
 
 #define CLIP3(lo, hi, v) ((v) < (lo) ? (lo) : ((v) > (hi) ? (hi) : (v)))
 static int imin(int a, int b) { return a < b ? a : b; }
-static int imax(int a, int b) { return a > b ? a : b; }
 static int iabs(int a) { return a < 0 ? -a : a; }
 
 /* ===================================================================== */
@@ -789,6 +788,7 @@ static void intra_predict(pic_t *p, int cIdx, int xTb, int yTb, int log2n, int m
     int PW = cIdx ? p->cw : p->W, PH = cIdx ? p->chh : p->H;
     /* ref arrays: left[0] = p[-1][-1], left[1+y] = p[-1][y]; top[1+x] = p[x][-1] */
     int left[129], top[129], av_l[129], av_t[129];
+    left[0] = top[0] = 0;
     int xc = xTb * sw, yc = yTb * sh;
     int any = 0;
     for (int i = -1; i < 2 * n; i++) {
@@ -1942,8 +1942,8 @@ int oracle_decode_tile(const uint8_t *hvcc, size_t hvcc_len, const uint8_t *item
                        int ypitch, uint16_t *cb, int cbpitch, uint16_t *cr, int crpitch) {
     hevc_ps ps;
     if (hevc_parse_hvcc(hvcc, hvcc_len, &ps)) return -1;
-    const uint8_t *nal;
-    size_t nl;
+    const uint8_t *nal = NULL;
+    size_t nl = 0;
     if (tile_nal(item, item_len, &nal, &nl)) return -1;
     uint16_t *o[3] = {y, cb, cr};
     int op[3] = {ypitch, cbpitch, crpitch};
@@ -2023,8 +2023,8 @@ int oracle_decode_heic(const uint8_t *data, size_t len, oracle_image *out, oracl
         size_t il;
         uint8_t *item = heif_item_data(f, it, &il);
         if (!item) goto free_grid;
-        const uint8_t *nal;
-        size_t nl;
+        const uint8_t *nal = NULL;
+        size_t nl = 0;
         if (tile_nal(item, il, &nal, &nl)) { free(item); goto free_grid; }
         int r = t / cols, c = t % cols;
         uint16_t *o[3] = {0, 0, 0};
