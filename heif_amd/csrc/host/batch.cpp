@@ -129,8 +129,8 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n) {
             pd.row_off = hb.rows;
             hb.rows += uint32_t(hctb);
             // worst case per CTB row: every 8x8 CU split into four 4x4 luma TBs + 2 chroma TBs
-            pd.tu_cap_row = uint32_t(wctb * (ctb / 8) * (ctb / 8) * 6);
-            pd.coef_cap_row = uint32_t(wctb * ctb * ctb * 3 / 2);
+            pd.tu_cap_row = uint32_t(wctb * (ctb / 8) * (ctb / 8) * 6 + 64);  // + staging trash slot / slack
+            pd.coef_cap_row = uint32_t(wctb * ctb * ctb * 3 / 2 + 64);  // + staging trash slot / slack
             pd.tu_off = hb.tu_n;
             hb.tu_n += uint64_t(pd.tu_cap_row) * hctb;
             pd.coef_off = hb.coef_n;

@@ -48,8 +48,24 @@ __device__ __forceinline__ uint64_t prof_clock() { return __builtin_amdgcn_s_mem
 #endif
 enum { PF_WAVE, PF_SPIN, PF_BINS, PF_BYPASS, PF_REFILL, PF_CQT, PF_RESID, PF_SAO, PF_N };
 
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HG_GLOBAL __attribute__((address_space(1)))  // keeps LDS-held pointers global (not flat)
+#else
+#define HG_GLOBAL
+#endif
+struct PicConst {
+    int W, H, wctb, hctb, minCb, minTb, maxTb, maxDepthIntra, chroma, bdY, bdC, qpbdY, qpbdC;
+    int pcmMin, pcmMax, log2qg, cbOff, crOff, sliceQp, saoL, saoC, w4, h4;
+    uint32_t tu_cap, coef_cap;
+    HG_GLOBAL int8_t *gqpy;
+    HG_GLOBAL uint8_t *gflags;
+    HG_GLOBAL TuRec *tu_out;
+    HG_GLOBAL Coef *coef_out;
+};
+
 struct alignas(16) WaveLds {
-    uint8_t ring[256];
+    PicConst pc;
+    uint8_t ring[256 + 16];  // + trash byte for dropped lanes (ring_refill)
     uint8_t ipm[16][17];  // IntraPredModeY per 4x4 of the current CTB, column 0 = left CTB
     uint8_t depth[8][9];  // CtDepth per 8x8, column 0 = left CTB
     int8_t qpy[8][8];     // QpY per 8x8 of the current CTB
@@ -127,21 +143,25 @@ struct CtxRegs {
 #endif
 
 struct Parser {
-    // picture constants
-    int W, H, log2ctb, ctb, wctb, hctb, minCb, minTb, maxTb, maxDepthIntra, chroma, bdY, bdC, qpbdY, qpbdC;
-    int pcmMin, pcmMax;
+    // Cold per-picture constants and output pointers live in the wave's LDS
+    // block (WaveLds::pc, read through PCV/PCP at their few use sites): the
+    // register file is kept for the CABAC engine and the per-CU state, so the
+    // bin loops do not spill SGPRs into VGPR lanes.
+    int log2ctb, ctb;
     uint32_t flags;
-    int log2qg, cbOff, crOff, sliceQp, saoL, saoC;
     // engine (9.3.4.3) with a 16-bit-scaled value register
     uint32_t range, value;
     int bits_needed;
     // byte ring
     uint32_t rd, wr, src_pos, nal_end, prev1, prev2;
+    const uint8_t *src;
+    const uint8_t *depth_above;  // LDS line of the CTB row above (8x8 units)
 #if !defined(HG_HOST_EMU)
+    uint32_t cstage, cstage_n;  // coefficient staging (coef_put)
+    uint32_t tstage[4], tstage_n;  // TU record staging (tu_put)
     uint32_t ringv;  // the ring, 4 bytes per lane
     uint32_t scanv;  // 8x8 diagonal scan: byte 0 = x | (y << 3) of sPos = lane, byte 1 = sPos of raster lane
 #endif
-    const uint8_t *src;
     uint32_t status;
     WaveLds *w;
     CtxRegs cx;
@@ -156,14 +176,10 @@ struct Parser {
     bool cu_bypass;
     int cu_intra_split, cu_chroma_mode;
     // outputs
-    TuRec *tu_out;
-    Coef *coef_out;
-    uint32_t ntu, tu_cap, ncoef, coef_cap;
-    int8_t *gqpy;
-    uint8_t *gflags;
-    int w4, h4;
-    const uint8_t *depth_above;  // LDS line of the CTB row above (8x8 units)
+    uint32_t ntu, ncoef;
 };
+#define PCV(f) unis(p.w->pc.f)
+#define PCP(f) (p.w->pc.f)
 
 // ---------------------------------------------------------------- bytes
 // The RBSP bytes of the substream flow through a 256-byte ring per wave.
@@ -210,7 +226,9 @@ HG_INLINE void ring_refill(Parser &p) {
     bool keep = valid && !ep;
     uint64_t m = __ballot(keep);
     uint32_t idx = __popcll(m & ((1ull << lane) - 1ull));
-    if (keep) p.w->ring[(p.wr + idx) & 255] = (uint8_t)b;
+    // no divergent branch around the store (it would make the compiler treat the
+    // ring state, and so the whole engine, as divergent): dropped bytes go to ring[256]
+    p.w->ring[keep ? (p.wr + idx) & 255 : 256] = (uint8_t)b;
     p.wr += __popcll(m);
     p.prev2 = uni(__shfl(b, 62, 64));
     p.prev1 = uni(__shfl(b, 63, 64));
@@ -230,9 +248,6 @@ HG_INLINE uint32_t next_byte(Parser &p) {
 HG_INLINE void ensure_bytes(Parser &p) {
     while (p.wr - p.rd < kRingLowWater && p.src_pos < p.nal_end) {
         ring_refill(p);
-        // rd is untouched by the refill, but without this the uniformity
-        // analysis loses track of it here and the whole bin loop goes to VGPRs
-        p.rd = uni(p.rd);
         HG_PROF(++p.prof[PF_REFILL]);
     }
 }
@@ -261,7 +276,7 @@ HG_INLINE void engine_init(Parser &p, uint32_t raw_start) {
 
 // 9.3.2.2 context initialization
 HG_INLINE void ctx_init(Parser &p) {
-    p.cx.init(p.lane, p.sliceQp);
+    p.cx.init(p.lane, PCV(sliceQp));
 }
 
 // ---------------------------------------------------------------- engine
@@ -352,7 +367,7 @@ __device__ __forceinline__ int chroma_qp_map(int qpi, int chroma) {
 }
 
 __device__ __forceinline__ void update_qpy(Parser &p) {
-    p.qpy_cur = ((p.qp_pred + p.cu_qp_delta_val + 52 + 2 * p.qpbdY) % (52 + p.qpbdY)) - p.qpbdY;
+    p.qpy_cur = ((p.qp_pred + p.cu_qp_delta_val + 52 + 2 * PCV(qpbdY)) % (52 + PCV(qpbdY))) - PCV(qpbdY);
 }
 
 // 8.6.1: qPY_PRED of the current quantization group
@@ -360,10 +375,10 @@ HG_INLINE void derive_qp_pred(Parser &p) {
     int prev;
     bool first_in_ctb = p.qg_x == p.ctbx && p.qg_y == p.ctby;
     if (p.first_qg_in_slice) {
-        prev = p.sliceQp;
+        prev = PCV(sliceQp);
         p.first_qg_in_slice = false;
     } else if ((p.flags & SP_WPP) && first_in_ctb && p.rx == 0) {
-        prev = p.sliceQp;
+        prev = PCV(sliceQp);
     } else {
         prev = p.qp_prev_last;
     }
@@ -392,11 +407,11 @@ HG_INLINE void parse_sao(Parser &p, SaoParams *sao_line_above, SaoParams *gsao) 
     } else {
         // component loop fully unrolled: a runtime index into the private
         // SaoParams would keep it in scratch (and scratch loads are divergent)
-        const int ncomp = p.chroma ? 3 : 1;
+        const int ncomp = PCV(chroma) ? 3 : 1;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             if (c >= ncomp) break;
-            if (!((p.saoL && c == 0) || (p.saoC && c > 0))) continue;
+            if (!((PCV(saoL) && c == 0) || (PCV(saoC) && c > 0))) continue;
             if (c < 2) {
                 int t = 0;
                 if (dec_bin(p, CTX_SAO_TYPE)) t = dec_bypass(p) ? 2 : 1;
@@ -405,7 +420,7 @@ HG_INLINE void parse_sao(Parser &p, SaoParams *sao_line_above, SaoParams *gsao) 
                 s.type[2] = s.type[1];
             }
             if (!s.type[c]) continue;
-            int bd = c ? p.bdC : p.bdY;
+            int bd = c ? PCV(bdC) : PCV(bdY);
             uint32_t cmax = (1u << ((bd < 10 ? bd : 10) - 5)) - 1;
             int a[4];
 #pragma unroll
@@ -428,7 +443,7 @@ HG_INLINE void parse_sao(Parser &p, SaoParams *sao_line_above, SaoParams *gsao) 
         }
     }
     p.w->sao_left = s;  // every lane stores the same value: no divergent branch
-    gsao[p.ry * p.wctb + p.rx] = s;
+    gsao[p.ry * PCV(wctb) + p.rx] = s;
 }
 
 // ---------------------------------------------------------------- scans (6.5.3-6.5.5)
@@ -460,6 +475,64 @@ HG_INLINE int scan_inv(const Parser &p, int l, int scan, int raster) {
     const uint64_t t = l == 2 ? (scan == 0 ? kScan4Inv[0] : scan == 1 ? kScan4Inv[1] : kScan4Inv[2])
                               : (scan == 0 ? kScan2Inv[0] : scan == 1 ? kScan2Inv[1] : kScan2Inv[2]);
     return (int)((uint32_t)(t >> (4 * raster)) & 15u);
+#endif
+}
+
+// sig_coeff_flag ctxInc patterns (9.3.4.2.5) per prevCsbf, byte per raster
+// position e = x | (y << 2); and Table 9-50's ctxIdxMap for 4x4 TBs
+constexpr uint64_t sig_pat_word(int pc, int half) {
+    uint64_t w = 0;
+    for (int k = 0; k < 8; ++k) {
+        const int e = half * 8 + k, x = e & 3, y = e >> 2;
+        const int v = pc == 0 ? (x + y == 0 ? 2 : (x + y < 3 ? 1 : 0))
+                    : pc == 1 ? (y == 0 ? 2 : (y == 1 ? 1 : 0))
+                    : pc == 2 ? (x == 0 ? 2 : (x == 1 ? 1 : 0)) : 2;
+        w |= (uint64_t)v << (8 * k);
+    }
+    return w;
+}
+constexpr uint64_t sig_map4_word(int half) {
+    uint64_t w = 0;
+    for (int k = 0; k < 8; ++k) w |= ((kSigCtxMap4 >> (4 * (half * 8 + k))) & 15u) << (8 * k);
+    return w;
+}
+constexpr uint64_t kSigPat[4][2] = {{sig_pat_word(0, 0), sig_pat_word(0, 1)}, {sig_pat_word(1, 0), sig_pat_word(1, 1)},
+                                    {sig_pat_word(2, 0), sig_pat_word(2, 1)}, {sig_pat_word(3, 0), sig_pat_word(3, 1)}};
+constexpr uint64_t kSigMap4Lo = sig_map4_word(0), kSigMap4Hi = sig_map4_word(1);
+
+HG_INLINE uint64_t scan4_word(int scan) {
+    return scan == 0 ? kScan4Pos[0] : (scan == 1 ? kScan4Pos[1] : kScan4Pos[2]);
+}
+
+// Coefficients leave k_parse 64 at a time: coefficient k of the pending group
+// sits in lane k of a staging VGPR and one coalesced store writes the group.
+// (A per-coefficient global store would make the next overwrite of its data
+// VGPR wait for the store to complete: an s_waitcnt vmcnt(0) per coefficient.)
+HG_INLINE void coef_flush(Parser &p) {
+#if !defined(HG_HOST_EMU)
+    if (p.cstage_n) {
+        const uint32_t n = p.cstage_n;
+        const uint32_t cap = PCV(coef_cap) - 1;  // the row's last slot is the trash slot
+        if (p.ncoef + n <= cap) {
+            // every lane stores (no divergent branch): lanes past n hit the trash slot
+            const uint32_t idx = (uint32_t)p.lane < n ? p.ncoef + p.lane : cap;
+            PCP(coef_out)[idx] = p.cstage;
+            p.ncoef += n;
+        } else {
+            p.status |= ST_CAPACITY;
+        }
+        p.cstage_n = 0;
+    }
+#endif
+}
+
+HG_INLINE void coef_put(Parser &p, uint32_t packed) {
+#if defined(HG_HOST_EMU)
+    if (p.ncoef < PCV(coef_cap)) PCP(coef_out)[p.ncoef++] = packed;
+    else p.status |= ST_CAPACITY;
+#else
+    p.cstage = __lane_id() == p.cstage_n ? packed : p.cstage;
+    if (++p.cstage_n == 64) coef_flush(p);
 #endif
 }
 
@@ -539,29 +612,30 @@ HG_INLINE void residual_coding(Parser &p, int log2n, int cidx, int mode, bool &t
                 sig = 1u << last_pos;
                 nstart = last_pos - 1;
             }
+            // ctxInc of sig_coeff_flag (9.3.4.2.5) for every raster position e = xP | (yP << 2)
+            // of this sub-block, one byte each in two words: the bin loop does one shift
+            uint64_t t0, t1;
+            if (log2n == 2) {
+                t0 = kSigMap4Lo;
+                t1 = kSigMap4Hi;
+            } else {
+                const int off = cidx == 0 ? ((xS | yS) ? 3 : 0) + (log2n == 3 ? (scan == 0 ? 9 : 15) : 21)
+                                          : (log2n == 3 ? 9 : 12);
+                const uint64_t rep = 0x0101010101010101ull * (uint64_t)off;
+                t0 = (prev_csbf == 0 ? kSigPat[0][0] : prev_csbf == 1 ? kSigPat[1][0]
+                      : prev_csbf == 2 ? kSigPat[2][0] : kSigPat[3][0]) + rep;
+                t1 = (prev_csbf == 0 ? kSigPat[0][1] : prev_csbf == 1 ? kSigPat[1][1]
+                      : prev_csbf == 2 ? kSigPat[2][1] : kSigPat[3][1]) + rep;
+                if ((xS | yS) == 0) t0 &= ~0xffull;  // DC of the TB: sigCtx 0
+            }
+            const int cbase = CTX_SIG + (cidx ? 27 : 0);
+            const uint64_t sw = scan4_word(scan);
             for (int nn = nstart; nn >= 0; --nn) {
-                const int pp = scan_pos(p, 2, scan, nn);
-                const int xP = pp & 15, yP = pp >> 4;
                 if (nn > 0 || !infer_dc) {
-                    const int xC = (xS << 2) + xP, yC = (yS << 2) + yP;
-                    int sc;
-                    if (log2n == 2) {
-                        sc = (int)((kSigCtxMap4 >> (4 * ((yC << 2) + xC))) & 15u);  // Table 9-50
-                    } else if (xC + yC == 0) {
-                        sc = 0;
-                    } else {
-                        if (prev_csbf == 0) sc = (xP + yP == 0) ? 2 : (xP + yP < 3) ? 1 : 0;
-                        else if (prev_csbf == 1) sc = (yP == 0) ? 2 : (yP == 1) ? 1 : 0;
-                        else if (prev_csbf == 2) sc = (xP == 0) ? 2 : (xP == 1) ? 1 : 0;
-                        else sc = 2;
-                        if (cidx == 0) {
-                            if (xS > 0 || yS > 0) sc += 3;
-                            sc += (log2n == 3) ? (scan == 0 ? 9 : 15) : 21;
-                        } else {
-                            sc += (log2n == 3) ? 9 : 12;
-                        }
-                    }
-                    if (dec_bin(p, CTX_SIG + (cidx ? 27 + sc : sc))) {
+                    const int e = (int)((sw >> (4 * nn)) & 15u);
+                    const uint64_t t = (e & 8) ? t1 : t0;
+                    const int sc = (int)((t >> ((e & 7) * 8)) & 0xffu);
+                    if (dec_bin(p, cbase + sc)) {
                         sig |= 1u << nn;
                         infer_dc = false;
                     }
@@ -641,16 +715,53 @@ HG_INLINE void residual_coding(Parser &p, int log2n, int cidx, int mode, bool &t
             const int xC = (xS << 2) + (pp & 15), yC = (yS << 2) + (pp >> 4);
             if (v > 32767) v = 32767;
             if (v < -32768) v = -32768;
-            if (p.ncoef < p.coef_cap) {
-                p.coef_out[p.ncoef] = ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC);
-                ++p.ncoef;
-                ++ncoef;
-            } else {
-                p.status |= ST_CAPACITY;
-            }
+            coef_put(p, ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC));
             ++num_sig;
         }
     }
+    coef_flush(p);
+    ncoef = p.ncoef - coef_first;  // what was actually stored (capacity overflow drops a group)
+}
+
+// TU records are staged like coefficients: record k of the pending group in
+// lane k of four staging VGPRs, one 16-byte store per lane at flush time.
+HG_INLINE void tu_flush(Parser &p) {
+#if !defined(HG_HOST_EMU)
+    if (p.tstage_n) {
+        const uint32_t n = p.tstage_n;
+        const uint32_t cap = PCV(tu_cap) - 1;  // last slot = trash slot
+        if (p.ntu + n <= cap) {
+            const uint32_t idx = (uint32_t)p.lane < n ? p.ntu + p.lane : cap;
+            HG_GLOBAL uint4 *d = (HG_GLOBAL uint4 *)(PCP(tu_out) + idx);
+            *d = make_uint4(p.tstage[0], p.tstage[1], p.tstage[2], p.tstage[3]);
+            p.ntu += n;
+        } else {
+            p.status |= ST_CAPACITY;
+        }
+        p.tstage_n = 0;
+    }
+#endif
+}
+
+HG_INLINE void tu_put(Parser &p, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+#if defined(HG_HOST_EMU)
+    if (p.ntu < PCV(tu_cap)) {
+        uint32_t *d = reinterpret_cast<uint32_t *>(PCP(tu_out) + p.ntu++);
+        d[0] = w0;
+        d[1] = w1;
+        d[2] = w2;
+        d[3] = w3;
+    } else {
+        p.status |= ST_CAPACITY;
+    }
+#else
+    const bool mine = __lane_id() == p.tstage_n;
+    p.tstage[0] = mine ? w0 : p.tstage[0];
+    p.tstage[1] = mine ? w1 : p.tstage[1];
+    p.tstage[2] = mine ? w2 : p.tstage[2];
+    p.tstage[3] = mine ? w3 : p.tstage[3];
+    if (++p.tstage_n == 64) tu_flush(p);
+#endif
 }
 
 // ---------------------------------------------------------------- TB emission
@@ -662,43 +773,29 @@ HG_INLINE void emit_tb(Parser &p, int cidx, int x, int y, int log2n, int mode, b
     HG_PROF(p.prof[PF_RESID] += prof_clock() - t_rc);
     int qp;
     if (cidx == 0) {
-        qp = p.qpy_cur + p.qpbdY;
+        qp = p.qpy_cur + PCV(qpbdY);
     } else {
-        int off = cidx == 1 ? p.cbOff : p.crOff;
+        int off = cidx == 1 ? PCV(cbOff) : PCV(crOff);
         int qpi = p.qpy_cur + off;
-        qpi = qpi < -p.qpbdC ? -p.qpbdC : (qpi > 57 ? 57 : qpi);
-        qp = chroma_qp_map(qpi, p.chroma) + p.qpbdC;
+        qpi = qpi < -PCV(qpbdC) ? -PCV(qpbdC) : (qpi > 57 ? 57 : qpi);
+        qp = chroma_qp_map(qpi, PCV(chroma)) + PCV(qpbdC);
     }
     uint8_t fl = (uint8_t)cidx;
     if (cbf) fl |= TU_CBF;
     if (ts) fl |= TU_TSKIP;
     if (p.cu_bypass) fl |= TU_BYPASS;
     if (cidx == 0 && log2n == 2) fl |= TU_DST;
-    if (p.ntu < p.tu_cap) {
-        {
-            TuRec r;
-            r.x = (uint16_t)x;
-            r.y = (uint16_t)y;
-            r.log2 = (uint8_t)log2n;
-            r.flags = fl;
-            r.mode = (uint8_t)mode;
-            r.qp = (uint8_t)qp;
-            r.coef = first;
-            r.ncoef = (uint16_t)nc;
-            r.ctu = (uint16_t)p.rx;
-            p.tu_out[p.ntu] = r;
-        }
-        ++p.ntu;
-    } else {
-        p.status |= ST_CAPACITY;
-    }
+    const uint32_t lo = (uint32_t)x | ((uint32_t)y << 16);
+    const uint32_t mid = (uint32_t)log2n | ((uint32_t)fl << 8) | ((uint32_t)mode << 16) | ((uint32_t)(uint8_t)qp << 24);
+    const uint32_t hi = (uint32_t)nc | ((uint32_t)p.rx << 16);
+    tu_put(p, lo, mid, first, hi);
 }
 
 // 7.3.8.10 transform_unit
 HG_INLINE void transform_unit(Parser &p, int x0, int y0, int xb, int yb, int log2n, int blk, bool cbf_l, bool cbf_cb,
                                bool cbf_cr, bool pcb, bool pcr) {
-    const bool chroma4 = p.chroma == 1 && log2n == 2;
-    const bool cbf_c = p.chroma == 0 ? false : (chroma4 ? (pcb || pcr) : (cbf_cb || cbf_cr));
+    const bool chroma4 = PCV(chroma) == 1 && log2n == 2;
+    const bool cbf_c = PCV(chroma) == 0 ? false : (chroma4 ? (pcb || pcr) : (cbf_cb || cbf_cr));
     if ((cbf_l || cbf_c) && (p.flags & SP_CU_QP_DELTA) && !p.is_cu_qp_delta_coded) {
         int v = 0;
         while (v < 5 && dec_bin(p, CTX_CU_QP_DELTA + (v == 0 ? 0 : 1))) ++v;
@@ -721,15 +818,15 @@ HG_INLINE void transform_unit(Parser &p, int x0, int y0, int xb, int yb, int log
         HG_LANE_LOOP(k, p.lane, nb * nb) {
             int bx = k % nb, by = k / nb;
             int gx = (x0 >> 2) + bx, gy = (y0 >> 2) + by;
-            if (gx < p.w4 && gy < p.h4)
-                p.gflags[gy * p.w4 + gx] =
+            if (gx < PCV(w4) && gy < PCV(h4))
+                PCP(gflags)[gy * PCV(w4) + gx] =
                     (uint8_t)((bx == 0 ? MF_EDGE_V : 0) | (by == 0 ? MF_EDGE_H : 0) | (p.cu_bypass ? MF_NOFILT : 0));
         }
     }
     const int lmode = unis(p.w->ipm[(y0 - p.ctby) >> 2][((x0 - p.ctbx) >> 2) + 1]);
     // luma TB, then (4:2:0) the Cb and Cr TBs — one emit_tb call site so it inlines once
     int ntb = 1;
-    if (p.chroma != 0 && (!chroma4 || blk == 3)) ntb = 3;
+    if (PCV(chroma) != 0 && (!chroma4 || blk == 3)) ntb = 3;
     for (int t = 0; t < ntb; ++t) {
         int x, y, l, m;
         bool cbf;
@@ -755,7 +852,7 @@ HG_INLINE void transform_tree(Parser &p, int x0, int y0, int log2cb) {
     int sp = 0;
     st[0] = pack(x0, y0, x0, y0, log2cb, 0, 0, 0, 0);
     sp = 1;
-    const int max_depth = p.maxDepthIntra + p.cu_intra_split;
+    const int max_depth = PCV(maxDepthIntra) + p.cu_intra_split;
     while (sp > 0) {
         ensure_bytes(p);
         --sp;
@@ -766,12 +863,12 @@ HG_INLINE void transform_tree(Parser &p, int x0, int y0, int log2cb) {
         int l = (int)((e >> 52) & 7), d = (int)((e >> 55) & 7), blk = (int)((e >> 58) & 3);
         bool pcb = (e >> 60) & 1, pcr = (e >> 61) & 1;
         bool split;
-        if (l <= p.maxTb && l > p.minTb && d < max_depth && !(p.cu_intra_split && d == 0))
+        if (l <= PCV(maxTb) && l > PCV(minTb) && d < max_depth && !(p.cu_intra_split && d == 0))
             split = dec_bin(p, CTX_SPLIT_TF + 5 - l);
         else
-            split = l > p.maxTb || (p.cu_intra_split && d == 0);
+            split = l > PCV(maxTb) || (p.cu_intra_split && d == 0);
         bool cbf_cb = false, cbf_cr = false;
-        if (l > 2 && p.chroma != 0) {
+        if (l > 2 && PCV(chroma) != 0) {
             if (d == 0 || pcb) cbf_cb = dec_bin(p, CTX_CBF_CHROMA + d);
             if (d == 0 || pcr) cbf_cr = dec_bin(p, CTX_CBF_CHROMA + d);
         }
@@ -836,8 +933,8 @@ HG_INLINE void coding_unit(Parser &p, int x0, int y0, int log2cb, int depth) {
     update_qpy(p);
     p.cu_bypass = (p.flags & SP_TQ_BYPASS) ? dec_bin(p, CTX_TQ_BYPASS) : 0;
     int nxn = 0;
-    if (log2cb == p.minCb) nxn = !dec_bin(p, CTX_PART_MODE);
-    if (!nxn && (p.flags & SP_PCM) && log2cb >= p.pcmMin && log2cb <= p.pcmMax && dec_term(p)) {
+    if (log2cb == PCV(minCb)) nxn = !dec_bin(p, CTX_PART_MODE);
+    if (!nxn && (p.flags & SP_PCM) && log2cb >= PCV(pcmMin) && log2cb <= PCV(pcmMax) && dec_term(p)) {
         // pcm_flag = 1: not supported on the GPU path (halfmoonbay has pcm_enabled_flag = 0)
         p.status |= ST_UNSUPPORTED;
         return;
@@ -861,7 +958,7 @@ HG_INLINE void coding_unit(Parser &p, int x0, int y0, int log2cb, int depth) {
         const int bx = (xPb - p.ctbx) >> 2, by = (yPb - p.ctby) >> 2;
         HG_LANE_LOOP(k, p.lane, nb * nb) p.w->ipm[by + k / nb][bx + k % nb + 1] = (uint8_t)m;
     }
-    if (p.chroma != 0) {
+    if (PCV(chroma) != 0) {
         int icpm = dec_bin(p, CTX_CHROMA_MODE) ? (int)dec_bypass_bits(p, 2) : 4;
         int lm = unis(p.w->ipm[(y0 - p.ctby) >> 2][((x0 - p.ctbx) >> 2) + 1]);
         int cm;
@@ -883,7 +980,7 @@ HG_INLINE void coding_unit(Parser &p, int x0, int y0, int log2cb, int depth) {
         const int nb = n >> 2;
         HG_LANE_LOOP(k, p.lane, nb * nb) {
             int gx = (x0 >> 2) + k % nb, gy = (y0 >> 2) + k / nb;
-            if (gx < p.w4 && gy < p.h4) p.gqpy[gy * p.w4 + gx] = (int8_t)p.qpy_cur;
+            if (gx < PCV(w4) && gy < PCV(h4)) PCP(gqpy)[gy * PCV(w4) + gx] = (int8_t)p.qpy_cur;
         }
     }
     p.qp_prev_last = p.qpy_cur;
@@ -901,7 +998,7 @@ HG_INLINE void coding_quadtree(Parser &p) {
         int x = (int)(e & 8191), y = (int)((e >> 13) & 8191), l = (int)((e >> 26) & 7), d = (int)(e >> 29);
         const int n = 1 << l;
         bool split;
-        if (x + n <= p.W && y + n <= p.H && l > p.minCb) {
+        if (x + n <= PCV(W) && y + n <= PCV(H) && l > PCV(minCb)) {
             int cond = 0;
             const int dx = (x - p.ctbx) >> 3, dy = (y - p.ctby) >> 3;
             if (x > 0 && unis(p.w->depth[dy][dx]) > d) ++cond;  // column dx is x-8 (shifted by 1)
@@ -911,9 +1008,9 @@ HG_INLINE void coding_quadtree(Parser &p) {
             }
             split = dec_bin(p, CTX_SPLIT_CU + cond);
         } else {
-            split = l > p.minCb;
+            split = l > PCV(minCb);
         }
-        if (l >= p.log2qg) {
+        if (l >= PCV(log2qg)) {
             p.is_cu_qp_delta_coded = false;
             p.cu_qp_delta_val = 0;
             p.qg_new = true;
@@ -926,15 +1023,15 @@ HG_INLINE void coding_quadtree(Parser &p) {
                 return (uint32_t)cx | ((uint32_t)cy << 13) | ((uint32_t)(l - 1) << 26) | ((uint32_t)(d + 1) << 29);
             };
             // push in reverse so child 0 is processed first
-            if (x + h < p.W && y + h < p.H) {
+            if (x + h < PCV(W) && y + h < PCV(H)) {
                 st[sp] = pk(x + h, y + h);
                 ++sp;
             }
-            if (y + h < p.H) {
+            if (y + h < PCV(H)) {
                 st[sp] = pk(x, y + h);
                 ++sp;
             }
-            if (x + h < p.W) {
+            if (x + h < PCV(W)) {
                 st[sp] = pk(x + h, y);
                 ++sp;
             }
@@ -989,47 +1086,51 @@ __global__ void __launch_bounds__(kParseWaves * 64) HG_PARSE_ATTR k_parse(BatchA
     SaoParams *sao_line = reinterpret_cast<SaoParams *>(depth_line + 2 * dl_stride);  // [2][max_wctb]
 
     Parser p;
-    p.W = sp.width;
-    p.H = sp.height;
+    p.w = wl;
+    p.w->pc.W = sp.width;
+    p.w->pc.H = sp.height;
     p.log2ctb = sp.log2_ctb;
     p.ctb = 1 << sp.log2_ctb;
-    p.wctb = (p.W + p.ctb - 1) >> p.log2ctb;
-    p.hctb = (p.H + p.ctb - 1) >> p.log2ctb;
-    p.minCb = sp.log2_min_cb;
-    p.minTb = sp.log2_min_tb;
-    p.maxTb = sp.log2_max_tb;
-    p.maxDepthIntra = sp.max_th_depth_intra;
-    p.chroma = sp.chroma_format;
-    p.bdY = sp.bit_depth_y;
-    p.bdC = sp.bit_depth_c;
-    p.qpbdY = 6 * (p.bdY - 8);
-    p.qpbdC = 6 * (p.bdC - 8);
+    p.w->pc.wctb = (PCV(W) + p.ctb - 1) >> p.log2ctb;
+    p.w->pc.hctb = (PCV(H) + p.ctb - 1) >> p.log2ctb;
+    p.w->pc.minCb = sp.log2_min_cb;
+    p.w->pc.minTb = sp.log2_min_tb;
+    p.w->pc.maxTb = sp.log2_max_tb;
+    p.w->pc.maxDepthIntra = sp.max_th_depth_intra;
+    p.w->pc.chroma = sp.chroma_format;
+    p.w->pc.bdY = sp.bit_depth_y;
+    p.w->pc.bdC = sp.bit_depth_c;
+    p.w->pc.qpbdY = 6 * (PCV(bdY) - 8);
+    p.w->pc.qpbdC = 6 * (PCV(bdC) - 8);
     p.flags = sp.flags;
-    p.pcmMin = sp.log2_min_pcm;
-    p.pcmMax = sp.log2_max_pcm;
-    p.log2qg = p.log2ctb - sp.diff_cu_qp_delta_depth;
-    p.cbOff = sp.cb_qp_offset + pd.cb_qp_off;
-    p.crOff = sp.cr_qp_offset + pd.cr_qp_off;
-    p.sliceQp = pd.slice_qp;
-    p.saoL = pd.sao_luma;
-    p.saoC = pd.sao_chroma;
+    p.w->pc.pcmMin = sp.log2_min_pcm;
+    p.w->pc.pcmMax = sp.log2_max_pcm;
+    p.w->pc.log2qg = p.log2ctb - sp.diff_cu_qp_delta_depth;
+    p.w->pc.cbOff = sp.cb_qp_offset + pd.cb_qp_off;
+    p.w->pc.crOff = sp.cr_qp_offset + pd.cr_qp_off;
+    p.w->pc.sliceQp = pd.slice_qp;
+    p.w->pc.saoL = pd.sao_luma;
+    p.w->pc.saoC = pd.sao_chroma;
     p.src = a.bits + pd.bits_off;
     p.nal_end = pd.bits_len;
     p.status = 0;
-    p.w = wl;
     p.lane = lane;
     p.cx.load_tables(lane);
 #if !defined(HG_HOST_EMU)
+    p.cstage = 0;
+    p.cstage_n = 0;
+    p.tstage[0] = p.tstage[1] = p.tstage[2] = p.tstage[3] = 0;
+    p.tstage_n = 0;
     {
         const uint32_t e = kScanPos[3][0][lane];
         p.scanv = ((e & 7) | ((e >> 4) << 3)) | ((uint32_t)kScanInv[3][0][lane] << 8);
     }
 #endif
     HG_PROF(for (int k = 0; k < PF_N; ++k) p.prof[k] = 0; const uint64_t t_start = prof_clock();)
-    p.w4 = (p.W + 3) >> 2;
-    p.h4 = (p.H + 3) >> 2;
-    p.gqpy = reinterpret_cast<int8_t *>(a.maps + pd.map_off);
-    p.gflags = a.maps + pd.map_off + (size_t)p.w4 * p.h4;
+    p.w->pc.w4 = (PCV(W) + 3) >> 2;
+    p.w->pc.h4 = (PCV(H) + 3) >> 2;
+    p.w->pc.gqpy = (HG_GLOBAL int8_t *)(a.maps + pd.map_off);
+    p.w->pc.gflags = (HG_GLOBAL uint8_t *)(a.maps + pd.map_off + (size_t)PCV(w4) * PCV(h4));
     SaoParams *gsao = a.sao + pd.sao_off;
     const uint32_t *subs = a.subs + pd.sub_first;
     const bool wpp = (p.flags & SP_WPP) != 0;
@@ -1040,29 +1141,29 @@ __global__ void __launch_bounds__(kParseWaves * 64) HG_PARSE_ATTR k_parse(BatchA
     // rows: WPP → one substream per CTB row, wave w takes rows w, w+16, ...;
     // otherwise the picture is one substream and wave 0 walks every row.
     const int row_step = wpp ? G : 1;
-    const int first_row = !active ? p.hctb : (wpp ? wrow : (wrow == 0 ? 0 : p.hctb));
-    const uint32_t stride = (uint32_t)p.wctb + 1;
+    const int first_row = !active ? PCV(hctb) : (wpp ? wrow : (wrow == 0 ? 0 : PCV(hctb)));
+    const uint32_t stride = (uint32_t)PCV(wctb) + 1;
     const int prev_wave = (wrow + G - 1) % G;
     bool stop = false;
-    for (int r = first_row; r < p.hctb && !stop; r += row_step) {
+    for (int r = first_row; r < PCV(hctb) && !stop; r += row_step) {
         p.ry = r;
-        p.tu_out = a.tus + pd.tu_off + (uint64_t)r * pd.tu_cap_row;
-        p.coef_out = a.coefs + pd.coef_off + (uint64_t)r * pd.coef_cap_row;
+        p.w->pc.tu_out = (HG_GLOBAL TuRec *)(a.tus + pd.tu_off + (uint64_t)r * pd.tu_cap_row);
+        p.w->pc.coef_out = (HG_GLOBAL Coef *)(a.coefs + pd.coef_off + (uint64_t)r * pd.coef_cap_row);
         p.ntu = p.ncoef = 0;
-        p.tu_cap = pd.tu_cap_row;
-        p.coef_cap = pd.coef_cap_row;
+        p.w->pc.tu_cap = pd.tu_cap_row;
+        p.w->pc.coef_cap = pd.coef_cap_row;
         p.depth_above = depth_line + ((r + 1) & 1) * dl_stride;
         uint8_t *depth_cur_line = depth_line + (r & 1) * dl_stride;
         SaoParams *sao_above = sao_line + ((r + 1) & 1) * a.max_wctb;
         SaoParams *sao_cur_line = sao_line + (r & 1) * a.max_wctb;
-        for (int c = 0; c < p.wctb; ++c) {
+        for (int c = 0; c < PCV(wctb); ++c) {
             p.rx = c;
             p.ctbx = c << p.log2ctb;
             p.ctby = r << p.log2ctb;
             if (wpp && r > 0) {
                 // WPP lag: row r-1 must have finished CTU min(c+1, wctb-1)
                 HG_PROF(uint64_t t_w = prof_clock());
-                const uint32_t need = (uint32_t)(r - 1) * stride + (uint32_t)((c + 2) < p.wctb ? (c + 2) : p.wctb);
+                const uint32_t need = (uint32_t)(r - 1) * stride + (uint32_t)((c + 2) < PCV(wctb) ? (c + 2) : PCV(wctb));
                 for (uint32_t spin = 0; uni(hg_atomic_load(&progress[prev_wave])) < need; ++spin) {
                     if (spin > (1u << 24)) {  // bounded: never hang the device
                         p.status |= ST_SUBSTREAM_END;
@@ -1075,7 +1176,7 @@ __global__ void __launch_bounds__(kParseWaves * 64) HG_PARSE_ATTR k_parse(BatchA
             }
             if (c == 0 && (wpp || r == 0)) {
                 // substream start: contexts (init or WPP sync, 9.3.1) + engine (9.3.2.5)
-                if (r == 0 || p.wctb < 2) ctx_init(p);
+                if (r == 0 || PCV(wctb) < 2) ctx_init(p);
                 else
                     p.cx.restore(wpp_slot + ((r + 1) & 1) * 64, lane);
                 engine_init(p, subs[wpp ? r : 0]);
@@ -1088,7 +1189,7 @@ __global__ void __launch_bounds__(kParseWaves * 64) HG_PARSE_ATTR k_parse(BatchA
                 HG_LANE_LOOP(k, lane, nb8) wl->depth[k][0] = wl->depth[k][nb8];
             }
             HG_PROF(uint64_t t_s = prof_clock());
-            if (p.saoL || p.saoC) parse_sao(p, sao_above, gsao);
+            if (PCV(saoL) || PCV(saoC)) parse_sao(p, sao_above, gsao);
             HG_PROF(uint64_t t_q = prof_clock());
             coding_quadtree(p);
             HG_PROF(p.prof[PF_SAO] += t_q - t_s; p.prof[PF_CQT] += prof_clock() - t_q);
@@ -1104,11 +1205,11 @@ __global__ void __launch_bounds__(kParseWaves * 64) HG_PARSE_ATTR k_parse(BatchA
                 sao_cur_line[c] = wl->sao_left;
             }
             // end_of_slice_segment_flag / end_of_subset_one_bit (slice.rs:214-227)
-            const bool last_in_pic = (r == p.hctb - 1) && (c == p.wctb - 1);
+            const bool last_in_pic = (r == PCV(hctb) - 1) && (c == PCV(wctb) - 1);
             ensure_bytes(p);
             int eos = dec_term(p);
             if (eos != (last_in_pic ? 1 : 0)) p.status |= ST_SUBSTREAM_END;
-            if (!last_in_pic && wpp && c == p.wctb - 1) {
+            if (!last_in_pic && wpp && c == PCV(wctb) - 1) {
                 if (!dec_term(p)) p.status |= ST_SUBSTREAM_END;
             }
             check_overrun(p);
@@ -1117,6 +1218,7 @@ __global__ void __launch_bounds__(kParseWaves * 64) HG_PARSE_ATTR k_parse(BatchA
             hg_atomic_store(&progress[wrow], (uint32_t)r * stride + (uint32_t)(c + 1));
             if (stop) break;
         }
+        tu_flush(p);
         a.row_counts[2 * (pd.row_off + r)] = p.ntu;
         a.row_counts[2 * (pd.row_off + r) + 1] = p.ncoef;
     }
