@@ -18,6 +18,11 @@
 #include "kernels.hpp"
 #include "tables.hpp"
 
+#if !defined(HG_HOST_EMU)
+// v_writelane_b32 (this clang exposes no builtin for it): lane `lane` of `old` := src
+extern "C" __device__ int hg_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+#endif
+
 namespace hg {
 
 __constant__ uint8_t c_lps[256] = {HG_LPS_TABLE};
@@ -36,6 +41,7 @@ namespace {
         if (k < (n))
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return HG_UNI(v); }
+
 __device__ __forceinline__ int unis(int v) { return (int)HG_UNI((uint32_t)v); }
 
 // Optional cycle/bin counters (build with -DHG_PARSE_PROF; read back with
@@ -120,7 +126,7 @@ struct CtxRegs {
     __device__ void put(int ci, uint32_t w, uint32_t s) {
         const int sh = (ci >> 6) << 3;
         w = (w & ~(0xffu << sh)) | (s << sh);
-        v = __lane_id() == (ci & 63) ? w : v;  // v_writelane equivalent (v_cmp + v_cndmask)
+        v = (uint32_t)hg_writelane((int)w, ci & 63, (int)v);
     }
     __device__ uint32_t lps_of(uint32_t st, uint32_t q) const {
         return ((uint32_t)__builtin_amdgcn_readlane((int)lpsv, (int)st) >> (q << 3)) & 0xffu;
@@ -151,7 +157,7 @@ struct Parser {
     uint32_t flags;
     // engine (9.3.4.3) with a 16-bit-scaled value register
     uint32_t range, value;
-    int bits_needed;
+    uint32_t bits;  // bits consumed from the low byte of `value` (libde265's bits_needed + 8), 0..7
     // byte ring
     uint32_t rd, wr, src_pos, nal_end, prev1, prev2;
     const uint8_t *src;
@@ -270,7 +276,7 @@ HG_INLINE void engine_init(Parser &p, uint32_t raw_start) {
     uint32_t b0 = next_byte(p);
     uint32_t b1 = next_byte(p);
     p.value = (b0 << 8) | b1;
-    p.bits_needed = -8;
+    p.bits = 0;
     if ((p.value >> 7) >= 510) p.status |= ST_CABAC_INIT;
 }
 
@@ -283,48 +289,44 @@ HG_INLINE void ctx_init(Parser &p) {
 // 9.3.4.3.2 DecodeDecision (arithmetic.rs:97-144)
 HG_INLINE int dec_bin(Parser &p, int ci) {
     HG_PROF(++p.prof[PF_BINS]);
+    // Both outcomes are computed and selected (s_cselect), so the only branch
+    // is the byte refill; rangeTabLps and transIdxLps reads are independent.
     const uint32_t w = p.cx.word(ci);
     const uint32_t s = CtxRegs::state(w, ci);
-    uint32_t st = s >> 1, mps = s & 1;
+    const uint32_t st = s >> 1, mps = s & 1;
     const uint32_t lps = p.cx.lps_of(st, (p.range >> 6) & 3);
-    p.range -= lps;
-    uint32_t scaled = p.range << 7;
-    int bin;
-    if (p.value < scaled) {
-        bin = (int)mps;
-        st = st < 62 ? st + 1 : st;
-        if (scaled < (256u << 7)) {
-            p.range = scaled >> 6;
-            p.value <<= 1;
-            if (++p.bits_needed == 0) {
-                p.bits_needed = -8;
-                p.value |= next_byte(p);
-            }
-        }
-    } else {
-        p.value -= scaled;
-        int nbits = __builtin_clz(lps) - 23;
-        p.value <<= nbits;
-        p.range = lps << nbits;
-        bin = (int)(mps ^ 1u);
-        if (st == 0) mps ^= 1u;
-        st = p.cx.trans_of(st);
-        p.bits_needed += nbits;
-        if (p.bits_needed >= 0) {
-            p.value |= next_byte(p) << p.bits_needed;
-            p.bits_needed -= 8;
-        }
+    const uint32_t tr = p.cx.trans_of(st);
+    const uint32_t rm = p.range - lps;
+    const uint32_t scaled = rm << 7;
+    // all-ones when the LPS path is taken (value >= scaled; both < 2^17).  Pure
+    // integer masks, no bool: an i1 held across instructions becomes a lane
+    // mask and the compiler converts it back and forth through the VALU.
+    const uint32_t m = (uint32_t)((int32_t)(scaled - 1u - p.value) >> 31);
+    const uint32_t v = p.value - (scaled & m);
+    const uint32_t r = (lps & m) | (rm & ~m);
+    const uint32_t inc = st + (((st - 62u) >> 31) & 1u);           // min(st + 1, 62)
+    const uint32_t nst = (tr & m) | (inc & ~m);
+    const uint32_t nmps = mps ^ (m & ((st - 1u) >> 31));          // flip on LPS at st == 0
+    const uint32_t bin = mps ^ (m & 1u);
+    // 9.3.4.3.3 renormalisation: r in [6, 510]; shift it back to >= 256
+    const uint32_t sh = (uint32_t)__builtin_clz(r) - 23u;
+    p.range = r << sh;
+    p.value = v << sh;
+    p.bits += sh;  // <= 7 + 6
+    if (p.bits & 8u) {
+        p.bits &= 7u;
+        p.value |= next_byte(p) << p.bits;
     }
-    p.cx.put(ci, w, (st << 1) | mps);
-    return bin;
+    p.cx.put(ci, w, (nst << 1) | nmps);
+    return (int)bin;
 }
 
 // 9.3.4.3.4 DecodeBypass (arithmetic.rs:146-157)
 __device__ __forceinline__ int dec_bypass(Parser &p) {
     HG_PROF(++p.prof[PF_BYPASS]);
     p.value <<= 1;
-    if (++p.bits_needed >= 0) {
-        p.bits_needed = -8;
+    if (++p.bits & 8u) {
+        p.bits = 0;
         p.value |= next_byte(p);
     }
     uint32_t scaled = p.range << 7;
@@ -349,8 +351,8 @@ HG_INLINE int dec_term(Parser &p) {
     if (scaled < (256u << 7)) {
         p.range = scaled >> 6;
         p.value <<= 1;
-        if (++p.bits_needed == 0) {
-            p.bits_needed = -8;
+        if (++p.bits & 8u) {
+            p.bits = 0;
             p.value |= next_byte(p);
         }
     }
@@ -531,7 +533,7 @@ HG_INLINE void coef_put(Parser &p, uint32_t packed) {
     if (p.ncoef < PCV(coef_cap)) PCP(coef_out)[p.ncoef++] = packed;
     else p.status |= ST_CAPACITY;
 #else
-    p.cstage = __lane_id() == p.cstage_n ? packed : p.cstage;
+    p.cstage = (uint32_t)hg_writelane((int)packed, (int)p.cstage_n, (int)p.cstage);
     if (++p.cstage_n == 64) coef_flush(p);
 #endif
 }
@@ -755,11 +757,10 @@ HG_INLINE void tu_put(Parser &p, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t
         p.status |= ST_CAPACITY;
     }
 #else
-    const bool mine = __lane_id() == p.tstage_n;
-    p.tstage[0] = mine ? w0 : p.tstage[0];
-    p.tstage[1] = mine ? w1 : p.tstage[1];
-    p.tstage[2] = mine ? w2 : p.tstage[2];
-    p.tstage[3] = mine ? w3 : p.tstage[3];
+    p.tstage[0] = (uint32_t)hg_writelane((int)w0, (int)p.tstage_n, (int)p.tstage[0]);
+    p.tstage[1] = (uint32_t)hg_writelane((int)w1, (int)p.tstage_n, (int)p.tstage[1]);
+    p.tstage[2] = (uint32_t)hg_writelane((int)w2, (int)p.tstage_n, (int)p.tstage[2]);
+    p.tstage[3] = (uint32_t)hg_writelane((int)w3, (int)p.tstage_n, (int)p.tstage[3]);
     if (++p.tstage_n == 64) tu_flush(p);
 #endif
 }
