@@ -157,7 +157,7 @@ struct Parser {
     uint32_t flags;
     // engine (9.3.4.3) with a 16-bit-scaled value register
     uint32_t range, value;
-    uint32_t bits;  // bits consumed from the low byte of `value` (libde265's bits_needed + 8), 0..7
+    int bits_needed;
     // byte ring
     uint32_t rd, wr, src_pos, nal_end, prev1, prev2;
     const uint8_t *src;
@@ -276,7 +276,7 @@ HG_INLINE void engine_init(Parser &p, uint32_t raw_start) {
     uint32_t b0 = next_byte(p);
     uint32_t b1 = next_byte(p);
     p.value = (b0 << 8) | b1;
-    p.bits = 0;
+    p.bits_needed = -8;
     if ((p.value >> 7) >= 510) p.status |= ST_CABAC_INIT;
 }
 
@@ -289,47 +289,55 @@ HG_INLINE void ctx_init(Parser &p) {
 // 9.3.4.3.2 DecodeDecision (arithmetic.rs:97-144)
 HG_INLINE int dec_bin(Parser &p, int ci) {
     HG_PROF(++p.prof[PF_BINS]);
-    // Both outcomes are computed and selected (s_cselect), so the only branch
-    // is the byte refill; rangeTabLps and transIdxLps reads are independent.
+    // Branchy on purpose: at 6 waves/SIMD k_parse is issue-bound, and the MPS
+    // path (the common one) is the shortest instruction sequence.  (Measured:
+    // a branch-free select version, and a bit counter tested with `& 8`, both
+    // cost +30 % on the bench.)
     const uint32_t w = p.cx.word(ci);
     const uint32_t s = CtxRegs::state(w, ci);
-    const uint32_t st = s >> 1, mps = s & 1;
+    uint32_t st = s >> 1, mps = s & 1;
     const uint32_t lps = p.cx.lps_of(st, (p.range >> 6) & 3);
-    const uint32_t tr = p.cx.trans_of(st);
-    const uint32_t rm = p.range - lps;
-    const uint32_t scaled = rm << 7;
-    // all-ones when the LPS path is taken (value >= scaled; both < 2^17).  Pure
-    // integer masks, no bool: an i1 held across instructions becomes a lane
-    // mask and the compiler converts it back and forth through the VALU.
-    const uint32_t m = (uint32_t)((int32_t)(scaled - 1u - p.value) >> 31);
-    const uint32_t v = p.value - (scaled & m);
-    const uint32_t r = (lps & m) | (rm & ~m);
-    const uint32_t inc = st + (((st - 62u) >> 31) & 1u);           // min(st + 1, 62)
-    const uint32_t nst = (tr & m) | (inc & ~m);
-    const uint32_t nmps = mps ^ (m & ((st - 1u) >> 31));          // flip on LPS at st == 0
-    const uint32_t bin = mps ^ (m & 1u);
-    // 9.3.4.3.3 renormalisation: r in [6, 510]; shift it back to >= 256
-    const uint32_t sh = (uint32_t)__builtin_clz(r) - 23u;
-    p.range = r << sh;
-    p.value = v << sh;
-    p.bits += sh;  // <= 7 + 6
-    if (p.bits & 8u) {
-        p.bits &= 7u;
-        p.value |= next_byte(p) << p.bits;
+    p.range -= lps;
+    const uint32_t scaled = p.range << 7;
+    int bin;
+    if (p.value < scaled) {
+        bin = (int)mps;
+        st = st < 62 ? st + 1 : st;
+        if (scaled < (256u << 7)) {
+            p.range = scaled >> 6;
+            p.value <<= 1;
+            if (++p.bits_needed == 0) {
+                p.bits_needed = -8;
+                p.value |= next_byte(p);
+            }
+        }
+    } else {
+        p.value -= scaled;
+        const uint32_t nbits = (uint32_t)__builtin_clz(lps) - 23u;
+        p.value <<= nbits;
+        p.range = lps << nbits;
+        bin = (int)(mps ^ 1u);
+        if (st == 0) mps ^= 1u;
+        st = p.cx.trans_of(st);
+        p.bits_needed += (int)nbits;
+        if (p.bits_needed >= 0) {
+            p.value |= next_byte(p) << p.bits_needed;
+            p.bits_needed -= 8;
+        }
     }
-    p.cx.put(ci, w, (nst << 1) | nmps);
-    return (int)bin;
+    p.cx.put(ci, w, (st << 1) | mps);
+    return bin;
 }
 
 // 9.3.4.3.4 DecodeBypass (arithmetic.rs:146-157)
 __device__ __forceinline__ int dec_bypass(Parser &p) {
     HG_PROF(++p.prof[PF_BYPASS]);
     p.value <<= 1;
-    if (++p.bits & 8u) {
-        p.bits = 0;
+    if (++p.bits_needed >= 0) {
+        p.bits_needed = -8;
         p.value |= next_byte(p);
     }
-    uint32_t scaled = p.range << 7;
+    const uint32_t scaled = p.range << 7;
     if (p.value >= scaled) {
         p.value -= scaled;
         return 1;
@@ -351,8 +359,8 @@ HG_INLINE int dec_term(Parser &p) {
     if (scaled < (256u << 7)) {
         p.range = scaled >> 6;
         p.value <<= 1;
-        if (++p.bits & 8u) {
-            p.bits = 0;
+        if (++p.bits_needed == 0) {
+            p.bits_needed = -8;
             p.value |= next_byte(p);
         }
     }

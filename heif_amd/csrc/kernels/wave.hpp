@@ -87,11 +87,15 @@ constexpr int kWave = 64;
 #define HG_UNI(v) __builtin_amdgcn_readfirstlane(v)
 #define HG_FENCE_ACQ() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup")
 #define HG_FENCE_REL() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup")
+// Orders one wave's own LDS traffic across lanes (write by lane i, read by
+// lane j).  A wave's LDS instructions execute in order, so wavefront scope is
+// enough; workgroup scope would also drain the wave's outstanding global
+// stores (s_waitcnt vmcnt(0)) at every call.
 #define HG_WAVE_SYNC()                                       \
     do {                                                     \
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
         __builtin_amdgcn_wave_barrier();                     \
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
     } while (0)
 #define HG_SLEEP() __builtin_amdgcn_s_sleep(2)
 template <class T>
