@@ -238,6 +238,7 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
     a.max_width = max_w;
     a.max_wctb = max_wctb;
     a.max_rows = max_rows;
+    a.max_log2ctb = hb.max_log2ctb;
     a.total_rows = int(rows);
     a.bytes_per_sample = bps;
     b->out_host.assign(n, OutImage{});

@@ -65,6 +65,7 @@ int main(int argc, char **argv) {
     a.max_width = hb.max_w;
     a.max_wctb = hb.max_wctb;
     a.max_rows = hb.max_rows;
+    a.max_log2ctb = hb.max_log2ctb;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = bps;
     emu_parse(a);

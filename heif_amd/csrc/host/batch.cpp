@@ -140,6 +140,7 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n) {
             hb.max_w = std::max(hb.max_w, sq.width);
             hb.max_wctb = std::max(hb.max_wctb, wctb);
             hb.max_rows = std::max(hb.max_rows, hctb);
+            hb.max_log2ctb = std::max(hb.max_log2ctb, int(sq.log2_ctb));
         }
     }
     hb.bits.resize(hb.bits.size() + 128, 0);

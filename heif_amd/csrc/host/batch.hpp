@@ -19,7 +19,7 @@ struct HostBatch {
     std::vector<uint32_t> pic_image;  // picture → image index
     uint64_t recon_bytes = 0, resid_elems = 0, map_bytes = 0, sao_n = 0, tu_n = 0, coef_n = 0;
     uint32_t rows = 0;
-    int max_w = 0, max_wctb = 0, max_rows = 0, bps = 0, chroma = -1;
+    int max_w = 0, max_wctb = 0, max_rows = 0, max_log2ctb = 4, bps = 0, chroma = -1;
 };
 
 // Throws HeifError / UnsupportedError.

@@ -8,28 +8,34 @@
 //
 // Mapping: the serial part of HEVC intra decoding is the TB-to-TB
 // dependency inside a CTU row.  One workgroup per picture, one wave per CTB
-// row; row r starts CTU c once row r-1 has finished CTU c+1 (every above-right
-// neighbour lies in CTU c+1 at most), signalled through per-wave progress
-// counters in LDS with workgroup-scope release/acquire — all waves of a
-// picture share one CU, so the reconstructed samples they exchange through
-// global memory stay coherent in that CU's L1.  Inside a TB all 64 lanes
-// work: reference samples are gathered one per lane, the substitution
-// process (8.4.4.2.2) becomes three 64-bit ballots + a nearest-available
-// lookup, and prediction/residual-add run one sample per lane.
+// row; row r starts CTU c once row r-1 has finished CTU c+1 (every
+// above-right neighbour lies in CTU c+1 at most), signalled through per-wave
+// progress counters in LDS with workgroup-scope release/acquire.
+//
+// Each wave reconstructs its current CTU in an LDS window: the CTU's samples,
+// the column left of it (kept from the previous CTU), the row above it
+// (2*ctb+1 samples incl. the corner and above-right, loaded once per CTU from
+// the picture after the progress wait) and the CTU's residuals (one coalesced
+// load per CTU).  Every TB then works on LDS only — neighbour gather,
+// substitution (three 64-bit ballots + a nearest-available lookup),
+// filtering, prediction and residual add run one sample per lane — and the
+// finished CTU is written to the picture once.
 #include "kernels.hpp"
 
 namespace hg {
 
 namespace {
 
-constexpr int kWaves = 16;
+constexpr int kMaxWaves = 16;
+constexpr int kResidentIntraWaves = 4096;  // ~16 per CU: enough pictures in flight to hide TB latency
+constexpr size_t kIntraLdsBudget = 128 * 1024;
 
 __constant__ int8_t c_angle[35] = {0, 0, 32, 26, 21, 17, 13, 9, 5, 2, 0, -2, -5, -9, -13, -17, -21, -26,
                                    -32, -26, -21, -17, -13, -9, -5, -2, 0, 2, 5, 9, 13, 17, 21, 26, 32};
 __constant__ int16_t c_inv_angle[35] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -4096, -1638, -910, -630, -482, -390, -315,
                                         -256, -315, -390, -482, -630, -910, -1638, -4096, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
-struct alignas(16) IntraLds {
+struct alignas(16) IntraScratch {
     int16_t left[132];  // [0] = p[-1][-1], [1+y] = p[-1][y]
     int16_t top[132];   // [0] = p[-1][-1], [1+x] = p[x][-1]
     int16_t fl[132];
@@ -37,6 +43,47 @@ struct alignas(16) IntraLds {
     int16_t ref[200];   // angular reference, index + 64
     int32_t dc;
 };
+
+// Per-wave LDS block: scratch, then per component the CTU window.
+struct WinLayout {
+    int cs[3];                                   // component CTB size
+    uint32_t cur[3], left[3], above[3], res[3];  // byte offsets in the block
+    uint32_t bytes;                              // block size (16-aligned)
+};
+
+#if defined(HG_HOST_EMU)
+inline
+#else
+__host__ __device__ inline
+#endif
+WinLayout win_layout(int log2ctb, int chroma, int bps) {
+    WinLayout L{};
+    uint32_t o = (uint32_t)((sizeof(IntraScratch) + 15) & ~size_t(15));
+    const int ncomp = chroma ? 3 : 1;
+    for (int k = 0; k < 3; ++k) {
+        const int cs = k == 0 ? (1 << log2ctb) : (chroma ? (1 << log2ctb) >> 1 : 0);
+        L.cs[k] = cs;
+        if (k >= ncomp) continue;
+        L.cur[k] = o;
+        o += (uint32_t)(cs * cs * bps + 15) & ~15u;
+        L.left[k] = o;
+        o += (uint32_t)(cs * bps + 15) & ~15u;
+        L.above[k] = o;
+        o += (uint32_t)((2 * cs + 1) * bps + 15) & ~15u;
+        L.res[k] = o;
+        o += (uint32_t)(cs * cs * 2 + 15) & ~15u;
+    }
+    L.bytes = o;
+    return L;
+}
+
+int intra_waves(int log2ctb, int chroma, int bps, int max_rows) {
+    const WinLayout L = win_layout(log2ctb, chroma, bps);
+    int nw = (int)((kIntraLdsBudget - 64) / L.bytes);
+    nw = nw < kMaxWaves ? nw : kMaxWaves;
+    nw = nw < max_rows ? nw : max_rows;
+    return nw < 1 ? 1 : nw;
+}
 
 #define wave_sync() HG_WAVE_SYNC()
 
@@ -48,10 +95,27 @@ __device__ __forceinline__ int zscan(int xl, int yl, int log2ctb, int min_tb, in
     return v;
 }
 
+// One component's CTU window in LDS.
 template <typename Pel>
-__device__ __attribute__((always_inline)) inline void predict_tb(IntraLds *L, const TuRec &tu, Pel *plane, int pitch, int PW, int PH, int cidx,
-                           const int16_t *res, int res_pitch, int bd, bool strong, int log2ctb, int min_tb,
-                           int wctb, int lane) {
+struct Win {
+    Pel *cur, *left, *above;
+    int16_t *res;
+    int cs, cx0, cy0;  // CTB size and origin in component samples
+    // a decoded neighbour (xn, yn) in picture coordinates; only called for
+    // available samples, which lie in the row above, the column to the left
+    // or the current CTU
+    __device__ __forceinline__ int fetch(int xn, int yn) const {
+        const int lx = xn - cx0, ly = yn - cy0;
+        if (ly < 0) return above[lx + 1];
+        if (lx < 0) return left[ly];
+        return cur[ly * cs + lx];
+    }
+};
+
+template <typename Pel>
+__device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L, const TuRec &tu, const Win<Pel> &w,
+                                                                 int PW, int PH, int cidx, int bd, bool strong,
+                                                                 int log2ctb, int min_tb, int wctb, int lane) {
     const int log2n = tu.log2, n = 1 << log2n, mode = tu.mode;
     const int x0 = tu.x, y0 = tu.y;
     const int sub = cidx ? 1 : 0;  // 4:2:0 chroma → luma = 2x
@@ -78,7 +142,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraLds *L, co
             }
             sa[s] = xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
                     zscan(xn << sub, yn << sub, log2ctb, min_tb, wctb) <= zcur;
-            sv[s] = sa[s] ? (int)plane[(size_t)yn * pitch + xn] : 0;
+            sv[s] = sa[s] ? w.fetch(xn, yn) : 0;
             any_av |= sa[s];
         }
         int first = -1;
@@ -113,7 +177,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraLds *L, co
         }
         bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
                   zscan(xn << sub, yn << sub, log2ctb, min_tb, wctb) <= zcur;
-        val[k] = av ? (int)plane[(size_t)yn * pitch + xn] : 0;
+        val[k] = av ? w.fetch(xn, yn) : 0;
         msk[k] = __ballot(av);
     }
     // 2. substitution: nearest available predecessor in search order, else the first available
@@ -220,6 +284,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraLds *L, co
         wave_sync();
     }
     const int dc = mode == 1 ? L->dc : 0;
+    const int lx0 = x0 - w.cx0, ly0 = y0 - w.cy0;
     for (int o = lane; o < n * n; o += kWave) {
         const int x = o & (n - 1), y = o >> log2n;
         int pv;
@@ -244,9 +309,10 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraLds *L, co
                 if (mode == 10 && y == 0) pv = min(max(lf[1] + ((tp[1 + x] - tp[0]) >> 1), 0), maxv);
             }
         }
-        if (tu.flags & TU_CBF) pv += res[(size_t)(y0 + y) * res_pitch + x0 + x];
+        const int li = (ly0 + y) * w.cs + lx0 + x;
+        if (tu.flags & TU_CBF) pv += w.res[li];
         pv = min(max(pv, 0), maxv);
-        plane[(size_t)(y0 + y) * pitch + x0 + x] = (Pel)pv;
+        w.cur[li] = (Pel)pv;
     }
     wave_sync();
 }
@@ -254,40 +320,74 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraLds *L, co
 }  // namespace
 
 template <typename Pel>
-__global__ void __launch_bounds__(kWaves * 64) k_intra(BatchArgs a) {
-    HG_BLOCK_SHARED IntraLds lds[kWaves];
-    HG_BLOCK_SHARED uint32_t progress[kWaves];
+__global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
+#if defined(HG_HOST_EMU)
+    unsigned char *smem = g_emu.smem;
+#else
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#endif
+    const int nw = (int)HG_UNI(blockDim.x >> 6);
     const int pic = blockIdx.x;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const PicDesc pd = a.pics[pic];
     const SeqParams sp = a.seqs[pd.seq];
     const int W = sp.width, H = sp.height, log2ctb = sp.log2_ctb;
     const int wctb = (W + (1 << log2ctb) - 1) >> log2ctb, hctb = (H + (1 << log2ctb) - 1) >> log2ctb;
-    const int cw = sp.chroma_format ? W >> 1 : 0, ch = sp.chroma_format ? H >> 1 : 0;
+    const int chroma = sp.chroma_format;
+    const int cw = chroma ? W >> 1 : 0, ch = chroma ? H >> 1 : 0;
+    const int ncomp = chroma ? 3 : 1;
     Pel *planes[3];
     planes[0] = reinterpret_cast<Pel *>(a.recon + pd.recon_off);
     planes[1] = planes[0] + (size_t)W * H;
     planes[2] = planes[1] + (size_t)cw * ch;
-    const int16_t *res[3] = {a.resid + pd.resid_off, a.resid + pd.resid_off + (size_t)W * H,
-                             a.resid + pd.resid_off + (size_t)W * H + (size_t)cw * ch};
+    const int16_t *resp[3] = {a.resid + pd.resid_off, a.resid + pd.resid_off + (size_t)W * H,
+                              a.resid + pd.resid_off + (size_t)W * H + (size_t)cw * ch};
     const bool strong = (sp.flags & SP_STRONG_INTRA) != 0;
-    if (lane == 0) progress[wave] = 0;
+    const WinLayout lay = win_layout(log2ctb, chroma, (int)sizeof(Pel));
+    uint32_t *progress = reinterpret_cast<uint32_t *>(smem);  // [nw], 64 B reserved
+    unsigned char *blk = smem + 64 + (size_t)wave * lay.bytes;
+    IntraScratch *S = reinterpret_cast<IntraScratch *>(blk);
+    Win<Pel> win[3];
+    for (int k = 0; k < 3; ++k) {
+        win[k].cur = reinterpret_cast<Pel *>(blk + lay.cur[k]);
+        win[k].left = reinterpret_cast<Pel *>(blk + lay.left[k]);
+        win[k].above = reinterpret_cast<Pel *>(blk + lay.above[k]);
+        win[k].res = reinterpret_cast<int16_t *>(blk + lay.res[k]);
+        win[k].cs = lay.cs[k];
+    }
+    progress[wave] = 0;  // every lane writes the same value
     __syncthreads();
     const uint32_t stride = (uint32_t)wctb + 1;
-    const int prev_wave = (wave + kWaves - 1) % kWaves;
-    IntraLds *L = &lds[wave];
-    for (int r = wave; r < hctb; r += kWaves) {
+    const int prev_wave = (wave + nw - 1) % nw;
+    for (int r = wave; r < hctb; r += nw) {
         const uint32_t ntu = a.row_counts[2 * (pd.row_off + r)];
         const TuRec *tus = a.tus + pd.tu_off + (uint64_t)r * pd.tu_cap_row;
         int cur = -1;
-        for (uint32_t t = 0; t < ntu; ++t) {
-            const TuRec tu = tus[t];
-            const int c = (int)HG_UNI((uint32_t)tu.ctu);
+        for (uint32_t t = 0; t <= ntu; ++t) {
+            TuRec tu{};
+            int c = wctb;  // sentinel after the last TB: finish the open CTU
+            if (t < ntu) {
+                tu = tus[t];
+                c = (int)HG_UNI((uint32_t)tu.ctu);
+            }
             if (c != cur) {
                 if (cur >= 0) {
+                    // finish CTU `cur`: write the window back, keep its last column as `left`
+                    for (int k = 0; k < ncomp; ++k) {
+                        const Win<Pel> &w = win[k];
+                        const int PW = k ? cw : W, PH = k ? ch : H;
+                        const int vw = min(w.cs, PW - w.cx0), vh = min(w.cs, PH - w.cy0);
+                        for (int o = lane; o < vw * vh; o += kWave) {
+                            const int x = o % vw, y = o / vw;
+                            planes[k][(size_t)(w.cy0 + y) * PW + w.cx0 + x] = w.cur[y * w.cs + x];
+                        }
+                        for (int y = lane; y < w.cs; y += kWave) w.left[y] = w.cur[y * w.cs + w.cs - 1];
+                    }
+                    wave_sync();
                     HG_FENCE_REL();
-                    if (lane == 0) hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)c);
+                    hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)cur + 1u);
                 }
+                if (c >= wctb) break;
                 cur = c;
                 if (r > 0) {
                     const uint32_t need = (uint32_t)(r - 1) * stride + (uint32_t)min(c + 2, wctb);
@@ -300,30 +400,77 @@ __global__ void __launch_bounds__(kWaves * 64) k_intra(BatchArgs a) {
                     }
                     HG_FENCE_ACQ();
                 }
+                // start CTU c: the row above (corner .. above-right) and the residuals
+                for (int k = 0; k < ncomp; ++k) {
+                    Win<Pel> &w = win[k];
+                    const int PW = k ? cw : W, PH = k ? ch : H;
+                    w.cx0 = c * w.cs;
+                    w.cy0 = r * w.cs;
+                    const int yg = w.cy0 - 1;
+                    for (int i = lane; i <= 2 * w.cs; i += kWave) {
+                        const int xg = w.cx0 - 1 + i;
+                        w.above[i] = (yg >= 0 && xg >= 0 && xg < PW) ? planes[k][(size_t)yg * PW + xg] : (Pel)0;
+                    }
+                    const int vw = min(w.cs, PW - w.cx0), vh = min(w.cs, PH - w.cy0);
+                    for (int o = lane; o < vw * vh; o += kWave) {
+                        const int x = o % vw, y = o / vw;
+                        w.res[y * w.cs + x] = resp[k][(size_t)(w.cy0 + y) * PW + w.cx0 + x];
+                    }
+                }
+                wave_sync();
             }
             const int cidx = tu.flags & TU_CIDX_MASK;
+            if (cidx >= ncomp) continue;
+            const Win<Pel> &w = win[cidx];
             const int PW = cidx ? cw : W, PH = cidx ? ch : H;
-            if (tu.log2 < 2 || tu.log2 > 5 || cidx > 2 || tu.x + (1 << tu.log2) > PW || tu.y + (1 << tu.log2) > PH)
+            // a TB must lie inside the picture and inside its CTU window
+            if (tu.log2 < 2 || tu.log2 > 5 || tu.x + (1 << tu.log2) > PW || tu.y + (1 << tu.log2) > PH ||
+                tu.x < w.cx0 || tu.y < w.cy0 || tu.x + (1 << tu.log2) > w.cx0 + w.cs ||
+                tu.y + (1 << tu.log2) > w.cy0 + w.cs)
                 continue;
-            predict_tb<Pel>(L, tu, planes[cidx], PW, PW, PH, cidx, res[cidx], PW,
-                            cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, log2ctb, sp.log2_min_tb, wctb, lane);
+            predict_tb<Pel>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, log2ctb,
+                            sp.log2_min_tb, wctb, lane);
         }
         HG_FENCE_REL();
-        if (lane == 0) hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
+        hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
     }
+}
+
+static int intra_launch_waves(const BatchArgs &a) {
+    // all pictures of a batch share bit depth and chroma format; the CTB size
+    // may differ, so size for the largest one.  HEIFGPU_INTRA_WAVES caps the
+    // waves per picture (tuning: fewer waves = more pictures per CU).
+    // Measured (128 x 48 tiles): 16 waves/picture 142 ms, 8: 71, 4: 48, 1: 61 —
+    // many pictures per CU beat deep per-picture row parallelism, so waves per
+    // picture shrink as the batch grows (floor 4).
+    static const int forced = [] {
+        const char *e = std::getenv("HEIFGPU_INTRA_WAVES");
+        return e ? std::atoi(e) : 0;
+    }();
+    int cap = forced > 0 ? forced : kResidentIntraWaves / (a.n_pics > 0 ? a.n_pics : 1);
+    if (forced <= 0) cap = cap < 4 ? 4 : cap;
+    const int nw = intra_waves(a.max_log2ctb, 1, a.bytes_per_sample, a.max_rows);
+    return cap < nw ? cap : nw;
+}
+
+static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
+    return 64 + (size_t)nw * win_layout(a.max_log2ctb, 1, a.bytes_per_sample).bytes;
 }
 
 #if defined(HG_HOST_EMU)
 void emu_intra(const BatchArgs &a) {
-    if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t>, a.n_pics, 1, kWaves, a);
-    else emu_launch(k_intra<uint16_t>, a.n_pics, 1, kWaves, a);
+    const int nw = intra_launch_waves(a);
+    if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
+    else emu_launch(k_intra<uint16_t>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
 }
 #else
 hipError_t launch_intra(const BatchArgs &a, hipStream_t s) {
+    const int nw = intra_launch_waves(a);
+    const size_t lds = intra_lds_bytes(a, nw);
     if (a.bytes_per_sample == 1)
-        hipLaunchKernelGGL(k_intra<uint8_t>, dim3(a.n_pics), dim3(kWaves * 64), 0, s, a);
+        hipLaunchKernelGGL(k_intra<uint8_t>, dim3(a.n_pics), dim3(nw * 64), lds, s, a);
     else
-        hipLaunchKernelGGL(k_intra<uint16_t>, dim3(a.n_pics), dim3(kWaves * 64), 0, s, a);
+        hipLaunchKernelGGL(k_intra<uint16_t>, dim3(a.n_pics), dim3(nw * 64), lds, s, a);
     return hipGetLastError();
 }
 #endif

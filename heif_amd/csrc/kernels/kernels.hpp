@@ -42,6 +42,7 @@ struct BatchArgs {
     int total_rows;            // sum of CTB rows over pictures
     int bytes_per_sample;      // 1 or 2
     int parse_group;           // k_parse waves per picture (set by launch_parse)
+    int max_log2ctb;           // largest CTB size in the batch (sizes k_intra's LDS)
 };
 
 constexpr int kParseWaves = 16;              // k_parse block size limit (waves)
