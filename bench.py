@@ -168,7 +168,8 @@ def main():
         total_images = args.batch * world
         value = total_images * px * args.steps / elapsed / 1e6  # every step decodes the whole batch
         per_step = [m / args.steps for m in stage_ms]
-        parse_ms = per_step[0]
+        parse_ms = per_step[0]  # k_parse time per step, summed over the step's chunk launches
+        chunks = max(1, ctx.last_chunks())
         coded_px = info.grid_cols * info.tile_width * info.grid_rows * info.tile_height
         algo_per_image = info.coded_bytes + coded_px * 3 // 2  # compressed + coded planes
         achieved = args.batch * algo_per_image / (parse_ms / 1e3) / 1e9
@@ -177,7 +178,7 @@ def main():
         if tfile.exists():
             try:
                 tj = json.loads(tfile.read_text())
-                if tj.get("batch") == args.batch:
+                if tj.get("batch") == args.batch and tj.get("chunks", 1) == chunks:
                     traffic = tj.get("k_parse_hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -209,8 +210,9 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": traffic,
                 "kernel": "k_parse (CABAC)",
-                "kernel_ms_per_launch": round(parse_ms, 3),
-                "algorithmic_bytes_per_launch": args.batch * algo_per_image,
+                "kernel_ms_per_launch": round(parse_ms / chunks, 3),
+                "algorithmic_bytes_per_launch": args.batch * algo_per_image // chunks,
+                "launches_per_step": chunks,
             },
             "stage_ms_per_step": {k: round(v, 3) for k, v in zip(
                 ["parse", "transform", "intra", "deblock", "sao_out"], per_step)},

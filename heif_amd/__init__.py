@@ -150,6 +150,10 @@ class DecodeContext:
     def set_timing(self, enable: bool):
         _lib.check(lib.heifgpu_set_timing(self._h, 1 if enable else 0))
 
+    def last_chunks(self) -> int:
+        """Picture chunks the last decode was pipelined in (parse ∥ reconstruction)."""
+        return int(lib.heifgpu_last_chunks(self._h))
+
     def stage_times(self) -> List[float]:
         ms = (ctypes.c_float * 5)()
         _lib.check(lib.heifgpu_stage_times(self._h, ms))

@@ -112,7 +112,7 @@ class Planes(ctypes.Structure):
 EXPORTS = (
     "heifgpu_image_parse", "heifgpu_image_get_info", "heifgpu_image_free", "heifgpu_create",
     "heifgpu_destroy", "heifgpu_last_error", "heifgpu_batch_prepare", "heifgpu_batch_decode",
-    "heifgpu_batch_status", "heifgpu_batch_free", "heifgpu_set_timing", "heifgpu_stage_times",
+    "heifgpu_batch_status", "heifgpu_batch_free", "heifgpu_set_timing", "heifgpu_stage_times", "heifgpu_last_chunks",
     "heifgpu_decode_batch", "heifgpu_remove_emulation_prevention", "heifgpu_read_ue",
     "heifgpu_read_se", "heifgpu_bins_truncated_rice", "heifgpu_bins_chroma_pred_mode",
     "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb", "heifgpu_image_tile_params", "heifgpu_debug_counters",
@@ -165,6 +165,7 @@ def _load() -> ctypes.CDLL:
         "heifgpu_batch_free": (None, [VP]),
         "heifgpu_set_timing": (I32, [VP, I32]),
         "heifgpu_stage_times": (I32, [VP, P(ctypes.c_float)]),
+        "heifgpu_last_chunks": (I32, [VP]),
         "heifgpu_decode_batch": (I32, [VP, P(VP), SZ, P(Planes), VP, P(U32)]),
         "heifgpu_remove_emulation_prevention": (SZ, [u8p, SZ, u8p]),
         "heifgpu_read_ue": (I32, [u8p, SZ, P(U32)]),

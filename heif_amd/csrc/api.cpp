@@ -22,11 +22,21 @@ struct heifgpu_image {
     ParsedImage img;
 };
 
+// Pipelined decode: the pictures of a batch are cut into chunks; chunk i's
+// k_parse (scalar-issue-bound) runs on the caller's stream while chunk i-1's
+// reconstruction kernels (vector/memory-bound) run on a second stream.
+constexpr int kMaxChunks = 16;
+constexpr int kChunkMinPics = 6144;  // pictures that keep k_parse at ~6 waves/SIMD on 256 CUs
+
 struct heifgpu_ctx {
     int device = 0;
     bool timing = false;
-    hipEvent_t ev[6] = {};
-    float stage_ms[5] = {};
+    hipStream_t recon = nullptr;                     // second stream (reconstruction)
+    hipEvent_t fork = nullptr, join = nullptr;       // caller stream <-> recon stream
+    hipEvent_t parsed[kMaxChunks] = {};              // chunk i parsed
+    hipEvent_t tev[kMaxChunks][7] = {};              // timing: parse start/end, recon start, 4 stage ends
+    int timed_chunks = 0;
+    int last_chunks = 0;
 };
 
 namespace {
@@ -137,7 +147,12 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     HIP_TRY(hipSetDevice(device));
     auto c = std::make_unique<heifgpu_ctx>();
     c->device = device;
-    for (auto &e : c->ev) HIP_TRY(hipEventCreate(&e));
+    HIP_TRY(hipStreamCreateWithFlags(&c->recon, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
+    for (auto &e : c->parsed) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto &row : c->tev)
+        for (auto &e : row) HIP_TRY(hipEventCreate(&e));
     *out = c.release();
     return HEIFGPU_OK;
 }
@@ -145,8 +160,14 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
 void heifgpu_destroy(heifgpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    for (auto &e : ctx->ev)
+    for (auto &row : ctx->tev)
+        for (auto &e : row)
+            if (e) (void)hipEventDestroy(e);
+    for (auto &e : ctx->parsed)
         if (e) (void)hipEventDestroy(e);
+    if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+    if (ctx->join) (void)hipEventDestroy(ctx->join);
+    if (ctx->recon) (void)hipStreamDestroy(ctx->recon);
     delete ctx;
 }
 
@@ -156,11 +177,23 @@ int heifgpu_set_timing(heifgpu_ctx *ctx, int enable) {
     return HEIFGPU_OK;
 }
 
+int heifgpu_last_chunks(const heifgpu_ctx *ctx) { return ctx ? ctx->last_chunks : 0; }
+
 int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[5]) {
     if (!ctx || !ms) return fail(HEIFGPU_E_INVALID, "null argument");
     if (!ctx->timing) return fail(HEIFGPU_E_INVALID, "timing disabled");
-    HIP_TRY(hipEventSynchronize(ctx->ev[5]));
-    for (int i = 0; i < 5; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], ctx->ev[i], ctx->ev[i + 1]));
+    // per stage: summed over chunks (stages of different chunks overlap in time)
+    for (int i = 0; i < 5; ++i) ms[i] = 0.f;
+    for (int k = 0; k < ctx->timed_chunks; ++k) {
+        HIP_TRY(hipEventSynchronize(ctx->tev[k][6]));
+        float t;
+        HIP_TRY(hipEventElapsedTime(&t, ctx->tev[k][0], ctx->tev[k][1]));
+        ms[0] += t;
+        for (int i = 1; i < 5; ++i) {
+            HIP_TRY(hipEventElapsedTime(&t, ctx->tev[k][i + 1], ctx->tev[k][i + 2]));
+            ms[i] += t;
+        }
+    }
     return HEIFGPU_OK;
 }
 
@@ -282,17 +315,42 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         for (int i = 0; i < max_stages; ++i) HIP_TRY(fns[i](a, s));
         return HEIFGPU_OK;
     }
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[0], s));
-    HIP_TRY(launch_parse(a, s));
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[1], s));
-    HIP_TRY(launch_transform(a, s));
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[2], s));
-    HIP_TRY(launch_intra(a, s));
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[3], s));
-    HIP_TRY(launch_deblock(a, s));
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[4], s));
-    HIP_TRY(launch_sao_out(a, s));
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->ev[5], s));
+    // chunks: HEIFGPU_CHUNKS overrides.  k_parse needs ~6 waves per SIMD (6144
+    // pictures) in flight to be efficient — measured on 6144 pictures: 1 chunk
+    // 287 ms of parse, 2 chunks 402, 4 chunks 705 — so a batch is only cut
+    // when every chunk still fills the GPU.
+    static const int forced_chunks = [] {
+        const char *e = std::getenv("HEIFGPU_CHUNKS");
+        return e ? std::atoi(e) : 0;
+    }();
+    int nchunks = forced_chunks > 0 ? forced_chunks : std::max(1, a.n_pics / kChunkMinPics);
+    nchunks = std::min(std::max(nchunks, 1), std::min(kMaxChunks, a.n_pics));
+    HIP_TRY(hipEventRecord(ctx->fork, s));
+    HIP_TRY(hipStreamWaitEvent(ctx->recon, ctx->fork, 0));
+    for (int k = 0; k < nchunks; ++k) {
+        BatchArgs c = a;
+        c.pic0 = int((int64_t)a.n_pics * k / nchunks);
+        c.n_pics = int((int64_t)a.n_pics * (k + 1) / nchunks) - c.pic0;
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][0], s));
+        HIP_TRY(launch_parse(c, s));
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][1], s));
+        HIP_TRY(hipEventRecord(ctx->parsed[k], s));
+        HIP_TRY(hipStreamWaitEvent(ctx->recon, ctx->parsed[k], 0));
+        hipStream_t r = ctx->recon;
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][2], r));
+        HIP_TRY(launch_transform(c, r));
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][3], r));
+        HIP_TRY(launch_intra(c, r));
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][4], r));
+        HIP_TRY(launch_deblock(c, r));
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][5], r));
+        HIP_TRY(launch_sao_out(c, r));
+        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][6], r));
+    }
+    ctx->timed_chunks = ctx->timing ? nchunks : 0;
+    ctx->last_chunks = nchunks;
+    HIP_TRY(hipEventRecord(ctx->join, ctx->recon));
+    HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
     return HEIFGPU_OK;
 }
 

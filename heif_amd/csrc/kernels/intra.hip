@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #endif
     const int nw = (int)HG_UNI(blockDim.x >> 6);
-    const int pic = blockIdx.x;
+    const int pic = a.pic0 + blockIdx.x;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const PicDesc pd = a.pics[pic];
     const SeqParams sp = a.seqs[pd.seq];

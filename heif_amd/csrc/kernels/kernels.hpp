@@ -35,7 +35,8 @@ struct BatchArgs {
     uint8_t *maps;
     SaoParams *sao;
     uint32_t *status;          // per picture
-    int n_pics;
+    int n_pics;                // pictures of this launch: [pic0, pic0 + n_pics)
+    int pic0;
     int max_width;             // luma samples, batch max
     int max_wctb;
     int max_rows;              // CTB rows, batch max

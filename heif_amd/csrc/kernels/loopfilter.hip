@@ -93,7 +93,7 @@ __device__ void luma_segment(Pel *q, int sx, int sk, int qpP, int qpQ, bool nofp
 // VERT: edges between columns (x-1 | x); otherwise between rows.
 template <typename Pel, bool VERT>
 __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
-    const int pic = blockIdx.y;
+    const int pic = a.pic0 + blockIdx.y;
     const PicDesc pd = a.pics[pic];
     if (pd.dbk_disabled) return;
     const SeqParams sp = a.seqs[pd.seq];
@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
 // SAO + crop + grid placement: one thread per output sample
 template <typename Pel>
 __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
-    const int pic = blockIdx.y;
+    const int pic = a.pic0 + blockIdx.y;
     const PicDesc pd = a.pics[pic];
     const SeqParams sp = a.seqs[pd.seq];
     const OutImage oi = a.outs[pd.image];

@@ -1080,9 +1080,9 @@ __global__ void __launch_bounds__(kParseWaves * 64) HG_PARSE_ATTR k_parse(BatchA
     const int P = nwb / G;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int gi = wave / G, wrow = wave - gi * G;
-    const int pic_raw = blockIdx.x * P + gi;
-    const bool active = pic_raw < a.n_pics;
-    const int pic = active ? pic_raw : 0;
+    const int pic_raw = a.pic0 + blockIdx.x * P + gi;
+    const bool active = pic_raw < a.pic0 + a.n_pics;
+    const int pic = active ? pic_raw : a.pic0;
     const PicDesc pd = a.pics[pic];
     const SeqParams sp = a.seqs[pd.seq];
 

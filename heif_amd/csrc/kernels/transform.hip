@@ -60,7 +60,7 @@ __device__ __forceinline__ int clip16(int64_t v) { return v < -32768 ? -32768 : 
 __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     HG_BLOCK_SHARED int32_t tile[kWaves][2][32 * 32];
     HG_BLOCK_SHARED int32_t maxrow[kWaves];
-    const int pic = blockIdx.y, row = blockIdx.x;
+    const int pic = a.pic0 + blockIdx.y, row = blockIdx.x;
     const PicDesc pd = a.pics[pic];
     const SeqParams sp = a.seqs[pd.seq];
     const int hctb = (sp.height + (1 << sp.log2_ctb) - 1) >> sp.log2_ctb;
