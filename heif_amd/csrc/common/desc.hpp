@@ -63,7 +63,7 @@ struct PicDesc {
     // work-arena offsets
     uint64_t recon_off;   // bytes: Y (width*height samples), then Cb, Cr
     uint64_t resid_off;   // int16 elements: same layout as recon
-    uint64_t map_off;     // bytes: qpy[w4*h4] then flags[w4*h4]
+    uint64_t map_off;     // bytes: qpy[w4*h4], flags[w4*h4], then bottom CtDepth per CTB row [hctb][w8]
     uint64_t sao_off;     // SaoParams index of CTB 0
     uint64_t tu_off;      // TuRec index of row 0 (row r at tu_off + r*tu_cap_row)
     uint64_t coef_off;    // Coef index of row 0
@@ -105,12 +105,13 @@ static_assert(sizeof(TuRec) == 16, "TuRec layout");
 typedef uint32_t Coef;
 
 // SAO parameters of one CTB (7.3.8.3 semantics, SaoOffsetVal already signed).
-struct SaoParams {
+struct alignas(4) SaoParams {
     int8_t type[3];       // SaoTypeIdx
     uint8_t band_eo[3];   // sao_band_position or SaoEoClass
     int16_t off[3][4];    // SaoOffsetVal[1..4]
+    int16_t pad;          // 32 bytes: word-aligned for k_parse_lanes' L1-bypassing reads
 };
-static_assert(sizeof(SaoParams) == 30, "SaoParams layout");
+static_assert(sizeof(SaoParams) == 32, "SaoParams layout");
 
 // Per-picture status word bits (kernels OR these in).
 enum : uint32_t {

@@ -123,7 +123,8 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n) {
             pd.resid_off = hb.resid_elems;
             hb.resid_elems += (samples + 127) & ~uint64_t(127);
             pd.map_off = hb.map_bytes;
-            hb.map_bytes += (uint64_t(2) * w4 * h4 + 255) & ~uint64_t(255);
+            const int w8 = (sq.width + 7) >> 3;
+            hb.map_bytes += (uint64_t(2) * w4 * h4 + uint64_t(hctb) * w8 + 255) & ~uint64_t(255);
             pd.sao_off = hb.sao_n;
             hb.sao_n += uint64_t(wctb) * hctb;
             pd.row_off = hb.rows;
