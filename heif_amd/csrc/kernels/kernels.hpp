@@ -68,6 +68,10 @@ size_t parse_group_bytes(int max_width, int max_wctb, int group) {
     return (b + 15) & ~(size_t)15;
 }
 
+// k_parse_lanes (parse_lanes.hip): one substream per lane; HEIFGPU_PARSE=lanes selects it
+bool parse_lanes_supported(const BatchArgs &a);
+bool parse_lanes_selected(const BatchArgs &a);
+
 #if defined(HG_HOST_EMU)
 // Runs kernel(a) over a gx * gy grid, one block at a time, with `waves` host
 // threads per block (threadIdx.x = 64 * wave).  grid_stride kernels (which
@@ -97,12 +101,15 @@ void emu_launch(K kernel, int gx, int gy, int waves, const BatchArgs &a, bool gr
         }
 }
 void emu_parse(const BatchArgs &a);
+void emu_parse_lanes(const BatchArgs &a);
 void emu_transform(const BatchArgs &a);
 void emu_intra(const BatchArgs &a);
 void emu_deblock(const BatchArgs &a);
 void emu_sao_out(const BatchArgs &a);
 #else
 hipError_t launch_parse(const BatchArgs &a, hipStream_t s);
+hipError_t launch_parse_lanes(const BatchArgs &a, hipStream_t s);
+int parse_lanes_counters(uint64_t *out8);
 hipError_t launch_transform(const BatchArgs &a, hipStream_t s);
 hipError_t launch_intra(const BatchArgs &a, hipStream_t s);
 hipError_t launch_deblock(const BatchArgs &a, hipStream_t s);

@@ -1260,6 +1260,7 @@ ParseShape parse_shape(const BatchArgs &a) {
 
 #if defined(HG_HOST_EMU)
 void emu_parse(const BatchArgs &a0) {
+    if (parse_lanes_selected(a0)) return emu_parse_lanes(a0);
     BatchArgs a = a0;
     const ParseShape sh = parse_shape(a);
     a.parse_group = sh.group;
@@ -1267,6 +1268,7 @@ void emu_parse(const BatchArgs &a0) {
 }
 #else
 hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
+    if (parse_lanes_selected(a0)) return launch_parse_lanes(a0, s);
     BatchArgs a = a0;
     const ParseShape sh = parse_shape(a);
     a.parse_group = sh.group;
@@ -1287,8 +1289,9 @@ extern "C" int heifgpu_debug_counters(uint64_t *out, int n) {
     if (hipMemcpyFromSymbol(tmp, HIP_SYMBOL(hg::g_prof), sizeof(tmp)) != hipSuccess) return -1;
     uint64_t zero[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_prof), zero, sizeof(zero)) != hipSuccess) return -1;
-    for (int k = 0; k < n && k < hg::PF_N; ++k) out[k] = tmp[k];
-    return hg::PF_N;
+    if (hg::parse_lanes_counters(tmp + 8) < 0) return -1;  // k_parse_lanes: slots 8..15
+    for (int k = 0; k < n && k < 16; ++k) out[k] = tmp[k];
+    return 16;
 #else
     (void)out;
     (void)n;

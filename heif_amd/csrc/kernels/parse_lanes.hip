@@ -1,0 +1,1287 @@
+// parse_lanes.hip — CABAC slice-data parser with one substream per LANE
+// (pipeline stage 1; alternative to parse.hip's one-substream-per-wave k_parse).
+//
+// Same syntax and the same outputs as k_parse (TU records, coefficients, the
+// QP / edge maps, SAO parameters, per-row counts; see parse.hip for the
+// per-clause references into H.265 and the reference's
+// src/hevc/slice.rs:206-256 / src/cabac), but every lane of a wave runs its
+// own WPP substream: lane = one CTB row of one picture, and a picture's rows
+// sit in consecutive lanes.  Each lane walks its substream as a sequence of
+// syntax units (CTU start + SAO, coding-quadtree descent, coding-unit header,
+// transform-tree descent + transform_unit, residual header, one 4x4
+// sub-block, CTU end); one pass of the kernel loop runs one unit on every
+// live lane, the lanes in the same kind of unit sharing its instructions, and
+// the arithmetic decoder (context bytes in the lane's LDS block) runs inline
+// inside the units.  So up to 64 substreams share each engine instruction,
+// where k_parse spends a whole wave on one.
+//
+// WPP (9.3.1) inside the wave: lane r+1 starts CTU c once lane r has finished
+// CTU c+1 (per-lane progress words in LDS); lane r writes its contexts after
+// CTU 1 straight into lane r+1's context block.  The CtDepth of a CTB's bottom
+// 8x8 row and its SAO parameters reach the row below through global memory
+// (maps arena / SAO array), read with L1-bypassing loads.
+//
+// Left / above neighbour state (IntraPredModeY, CtDepth, QpY) needs no CTB
+// map: in z-order the last block written in a 4x4 (8x8) row of the CTB row is
+// always the left neighbour of the next block in that row, and likewise for
+// columns within a CTB, so a "last written" value per row and per column is
+// enough (ipmL/ipmA, dL/dA, qL/qA).
+#include "cabac.hpp"
+#include "kernels.hpp"
+#include "tables.hpp"
+
+#if defined(HG_HOST_EMU)
+#include <cstdio>
+#endif
+
+namespace hg {
+
+__constant__ uint8_t c_lps_l[256] = {HG_LPS_TABLE};
+__constant__ uint8_t c_trans_l[64] = {HG_TRANS_LPS};
+__constant__ uint8_t c_ctx_init_l[CTX_NUM] = {HG_CTX_INIT_VALUES};
+#if defined(HG_PARSE_PROF) && !defined(HG_HOST_EMU)
+// s_memtime cycles per wave: [0] kernel, [1] passes, [2..7] unit kinds CTU, tree (CQT+CU+TT), TB, SB,
+// CTU_END, refill (tuning build only; heifgpu_debug_counters slots 8..15)
+__device__ uint64_t g_prof_lanes[8];
+#endif
+
+namespace {
+
+constexpr uint32_t kProgDone = 0x7fffffffu;
+
+// per-lane LDS block
+struct alignas(16) LaneLds {
+    uint8_t ring[128];           // RBSP bytes of the substream (emulation prevention removed)
+    uint8_t ctx[CTX_PAD];
+    SaoParams sao;               // SAO parameters of the last CTB (= the left CTB for merge_left)
+    uint8_t ipmL[16], ipmA[16];  // IntraPredModeY (4x4 units): last written per row / per column
+    uint8_t dL[8], dA[8];        // CtDepth (8x8 units)
+    int8_t qL[8], qA[8];         // QpY (8x8 units)
+};
+
+// picture constants and output pointers (LDS, one per picture of the wave)
+struct LanePic {
+    int W, H, log2ctb, wctb, hctb, minCb, minTb, maxTb, maxDepthIntra, chroma;
+    int log2qg, bdY, bdC, qpbdY, qpbdC, pcmMin, pcmMax, cbOff, crOff, sliceQp;
+    int w4, h4, w8, saoL, saoC;
+    uint32_t flags, bits_off, bits_end, sub_first, row_off, tu_cap, coef_cap, pic;
+    int8_t *gqpy;
+    uint8_t *gflags, *gdepth;
+    SaoParams *gsao;
+    TuRec *tu_base;
+    Coef *coef_base;
+};
+
+// syntax units (Lane.st)
+enum Unit : int {
+    U_DONE = 0,
+    U_CTU,      // WPP wait, substream start, sao()                      7.3.8.2-3
+    U_CQT,      // coding_quadtree descent from the current node         7.3.8.4
+    U_CU,       // coding_unit up to transform_tree                      7.3.8.5
+    U_TT,       // transform_tree descent + transform_unit               7.3.8.8-10
+    U_TB,       // next TB of the TU: record, or residual_coding header  7.3.8.11
+    U_SB,       // one 4x4 sub-block of residual_coding                  7.3.8.11
+    U_CTU_END,  // end_of_slice_segment_flag / end_of_subset_one_bit     7.3.8.1
+};
+
+// Lane.fl bits
+enum : uint32_t {
+    F_WPP = 1u << 0,
+    F_FIRST_QG = 1u << 1,
+    F_QG_NEW = 1u << 2,
+    F_DQP_CODED = 1u << 3,
+    F_BYPASS = 1u << 4,   // cu_transquant_bypass_flag
+    F_NXN = 1u << 5,      // PART_NxN
+    F_CBF_L = 1u << 6,
+    F_CBF_CB = 1u << 7,
+    F_CBF_CR = 1u << 8,
+    F_TS = 1u << 9,       // transform_skip_flag of the current TB
+    F_TB_CBF = 1u << 10,
+    F_ANY_SB = 1u << 11,  // a sub-block of the TB had significant coefficients
+    F_STOP = 1u << 12,
+};
+
+struct Lane {
+    // arithmetic decoder (9.3.4.3, 16-bit-scaled value) and raw byte position
+    uint32_t range, value;
+    int bits_needed;
+    uint32_t rd, wr;             // ring read / write counts
+    uint32_t src, prev1, prev2;  // next raw byte (absolute offset into BatchArgs::bits); EP history
+    uint32_t status;
+    int st;
+    uint32_t fl;
+    int row, c, ctbx, ctby;
+    // coding quadtree / transform tree node
+    int qx, qy, ql, qd;
+    int tx, ty, tl, td;
+    uint32_t tcbf;  // cbf_cb | cbf_cr << 1 of the transform tree node at depth d, at bit 2d
+    // quantization (8.6.1)
+    int qp_prev_last, qp_pred, cu_qp_delta_val, qpy_cur, qg_x, qg_y;
+    // coding unit: IntraPredModeY of PB k in byte k, IntraPredModeC
+    int cu_modes, cu_chroma;
+    // transform block
+    int tb_t, tb_n, tb_cidx, tb_x, tb_y, tb_log2, tb_mode;
+    uint32_t tb_coef0;
+    // residual_coding state carried across sub-blocks
+    int rc_scan, rc_last_sub, rc_last_pos, rc_i, rc_prev_c1;
+    uint64_t rc_csbf;  // coded_sub_block_flag, bit yS * 8 + xS
+    uint32_t ntu, ncoef;
+    uint32_t tu_row, coef_row;  // TuRec / Coef index of the current row's outputs
+};
+
+// engine context of one lane
+struct Eng {
+    uint8_t *ctx, *ring;
+    const uint8_t *lps, *trans, *bits;
+    uint32_t end;
+};
+
+// ------------------------------------------------------------------ memory helpers
+#if defined(HG_HOST_EMU)
+inline uint32_t prog_load(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+inline void prog_store(uint32_t *p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+inline uint32_t load_word_coherent(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+inline void release_fence() { std::atomic_thread_fence(std::memory_order_release); }
+inline void store_tu(TuRec *d, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+    uint32_t *p = reinterpret_cast<uint32_t *>(d);
+    p[0] = x;
+    p[1] = y;
+    p[2] = z;
+    p[3] = w;
+}
+#else
+__device__ __forceinline__ uint32_t prog_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+__device__ __forceinline__ void prog_store(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+// 4-byte load that bypasses the L1: the word was written by another lane of
+// this wave (same CU, so the L2 of this XCD has it)
+__device__ __forceinline__ uint32_t load_word_coherent(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// drain this wave's global stores (SAO parameters, depth line) before the
+// progress word that lets the lane below read them
+__device__ __forceinline__ void release_fence() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+__device__ __forceinline__ void store_tu(TuRec *d, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+    *reinterpret_cast<uint4 *>(d) = make_uint4(x, y, z, w);
+}
+#endif
+
+HG_HD inline uint8_t load_byte_coherent(const uint8_t *p) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t w = load_word_coherent(reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3)));
+    return (uint8_t)(w >> ((a & 3) * 8));
+}
+
+// ------------------------------------------------------------------ bytes
+// The RBSP bytes of each lane's substream flow through a 128-byte LDS ring.
+// The kernel loop tops the ring up before a lane runs a unit (refill), so
+// next_byte inside the units is a single LDS read.  Every unit consumes less
+// than the low-water mark of a conforming stream (SAO of 10-bit video, the
+// largest, < 50 bytes; a 4x4 sub-block < 26 bytes before its
+// coeff_abs_level_remaining values, each of which (<= 72 bypass bins) tops
+// the ring up again when it is below kRingCoefWater).  An overrun of a
+// corrupt stream shows as rd > wr at the CTU end (ST_OVERRUN), as in k_parse.
+constexpr uint32_t kRingSize = 128, kRingLowWater = 96, kRingCoefWater = 24;
+
+HG_HD inline uint32_t next_byte(Lane &L, const Eng &G) { return G.ring[L.rd++ & (kRingSize - 1)]; }
+
+#if !defined(HG_HOST_EMU)
+__device__ __forceinline__ uint4 load16(const uint8_t *bits, uint32_t off) {
+    return *reinterpret_cast<const uint4 *>(bits + off);
+}
+#endif
+
+// raw → RBSP bytes (rbsp_reader.rs:11-39: 00 00 03 followed by a byte <= 3, or
+// by the end of the NAL unit, loses the 03) until the ring holds the low-water
+// mark or the NAL unit ends.  Raw bytes are read 16 at a time.
+HG_HD inline void refill(Lane &L, const Eng &G) {
+    while (L.wr - L.rd < kRingLowWater && L.src < G.end) {
+        const uint32_t base = L.src & ~15u;
+#if defined(HG_HOST_EMU)
+        uint64_t lo = 0, hi = 0;
+        for (int k = 0; k < 8; ++k) {
+            lo |= (uint64_t)G.bits[base + k] << (8 * k);
+            hi |= (uint64_t)G.bits[base + 8 + k] << (8 * k);
+        }
+#else
+        const uint4 q = load16(G.bits, base);
+        const uint64_t lo = (uint64_t)q.x | ((uint64_t)q.y << 32), hi = (uint64_t)q.z | ((uint64_t)q.w << 32);
+#endif
+        const uint32_t stop = base + 16 < G.end ? base + 16 : G.end;
+        for (uint32_t o = L.src; o < stop; ++o) {
+            const uint32_t k = o & 15u;
+            const uint32_t b = (uint32_t)(((k & 8u) ? hi : lo) >> ((k & 7u) << 3)) & 0xffu;
+            bool ep = false;
+            if (b == 3 && L.prev2 == 0 && L.prev1 == 0) {
+                const uint32_t nb = o + 1 >= G.end ? 0u : (k < 15 ? (uint32_t)((((k + 1) & 8u) ? hi : lo) >> (((k + 1) & 7u) << 3)) & 0xffu
+                                                                    : (uint32_t)G.bits[o + 1]);
+                ep = o + 1 >= G.end || nb <= 3;
+            }
+            if (!ep) G.ring[L.wr++ & (kRingSize - 1)] = (uint8_t)b;
+            L.prev2 = L.prev1;
+            L.prev1 = b;
+        }
+        L.src = stop;
+    }
+}
+
+// 9.3.2.5: engine initialisation at raw offset `start` (absolute)
+HG_HD inline void engine_init(Lane &L, const Eng &G, uint32_t start) {
+    L.src = start;
+    L.rd = L.wr = 0;
+    L.prev1 = G.bits[start - 1];  // the 2-byte NAL header precedes every payload
+    L.prev2 = G.bits[start - 2];
+    refill(L, G);
+    L.range = 510;
+    const uint32_t b0 = next_byte(L, G);
+    const uint32_t b1 = next_byte(L, G);
+    L.value = (b0 << 8) | b1;
+    L.bits_needed = -8;
+    if ((L.value >> 7) >= 510) L.status |= ST_CABAC_INIT;
+}
+
+// ------------------------------------------------------------------ engine (9.3.4.3)
+// DecodeDecision (arithmetic.rs:97-144)
+HG_HD inline int dec(Lane &L, const Eng &G, int ci) {
+    const uint32_t s = G.ctx[ci];
+    uint32_t st = s >> 1, mps = s & 1;
+    const uint32_t lps = G.lps[(st << 2) | ((L.range >> 6) & 3)];
+    L.range -= lps;
+    const uint32_t scaled = L.range << 7;
+    int bin;
+    if (L.value < scaled) {
+        bin = (int)mps;
+        st = st < 62 ? st + 1 : st;
+        if (scaled < (256u << 7)) {
+            L.range = scaled >> 6;
+            L.value <<= 1;
+            if (++L.bits_needed == 0) {
+                L.bits_needed = -8;
+                L.value |= next_byte(L, G);
+            }
+        }
+    } else {
+        L.value -= scaled;
+        const int nb = __builtin_clz(lps) - 23;
+        L.value <<= nb;
+        L.range = lps << nb;
+        bin = (int)(mps ^ 1u);
+        if (st == 0) mps ^= 1u;
+        st = G.trans[st];
+        L.bits_needed += nb;
+        if (L.bits_needed >= 0) {
+            L.value |= next_byte(L, G) << L.bits_needed;
+            L.bits_needed -= 8;
+        }
+    }
+    G.ctx[ci] = (uint8_t)((st << 1) | mps);
+    return bin;
+}
+
+// DecodeBypass (arithmetic.rs:146-157)
+HG_HD inline int byp(Lane &L, const Eng &G) {
+    L.value <<= 1;
+    if (++L.bits_needed >= 0) {
+        L.bits_needed = -8;
+        L.value |= next_byte(L, G);
+    }
+    const uint32_t scaled = L.range << 7;
+    if (L.value >= scaled) {
+        L.value -= scaled;
+        return 1;
+    }
+    return 0;
+}
+
+HG_HD inline uint32_t byp_bits(Lane &L, const Eng &G, int n) {
+    uint32_t v = 0;
+    for (int i = 0; i < n; ++i) v = (v << 1) | (uint32_t)byp(L, G);
+    return v;
+}
+
+// DecodeTerminate (arithmetic.rs:159-169)
+HG_HD inline int term(Lane &L, const Eng &G) {
+    L.range -= 2;
+    const uint32_t scaled = L.range << 7;
+    if (L.value >= scaled) return 1;
+    if (scaled < (256u << 7)) {
+        L.range = scaled >> 6;
+        L.value <<= 1;
+        if (++L.bits_needed == 0) {
+            L.bits_needed = -8;
+            L.value |= next_byte(L, G);
+        }
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ derivations
+HG_HD inline int chroma_qp_map(int qpi, int chroma) {
+    if (chroma != 1) return qpi < 51 ? qpi : 51;
+    if (qpi < 30) return qpi;
+    if (qpi > 43) return qpi - 6;
+    // Table 8-10 for qPi 30..43 (29 30 31 32 33 33 34 34 35 35 36 36 37 37), without a private array
+    return qpi < 34 ? qpi - 1 : 33 + ((qpi - 34) >> 1);
+}
+
+HG_HD inline void update_qpy(Lane &L, const LanePic &P) {
+    L.qpy_cur = ((L.qp_pred + L.cu_qp_delta_val + 52 + 2 * P.qpbdY) % (52 + P.qpbdY)) - P.qpbdY;
+}
+
+// 8.6.1 qPY_PRED of the current quantization group
+HG_HD inline void derive_qp_pred(Lane &L, const LaneLds &ld, const LanePic &P) {
+    int prev;
+    const bool first_in_ctb = L.qg_x == L.ctbx && L.qg_y == L.ctby;
+    if (L.fl & F_FIRST_QG) {
+        prev = P.sliceQp;
+        L.fl &= ~F_FIRST_QG;
+    } else if ((L.fl & F_WPP) && first_in_ctb && L.c == 0) {
+        prev = P.sliceQp;
+    } else {
+        prev = L.qp_prev_last;
+    }
+    const int mask = (1 << P.log2ctb) - 1;
+    const int qa = (L.qg_x & mask) ? ld.qL[(L.qg_y - L.ctby) >> 3] : prev;
+    const int qb = (L.qg_y & mask) ? ld.qA[(L.qg_x - L.ctbx) >> 3] : prev;
+    L.qp_pred = (qa + qb + 1) >> 1;
+}
+
+// 8.4.2 luma intra prediction mode of the PB at (xPb, yPb)
+HG_HD inline int derive_luma_mode(const Lane &L, const LaneLds &ld, int xPb, int yPb, int prev, int mpm_idx,
+                                  int rem) {
+    const int ca = xPb <= 0 ? 1 : ld.ipmL[(yPb - L.ctby) >> 2];
+    const int cb = (yPb - 1 < L.ctby) ? 1 : ld.ipmA[(xPb - L.ctbx) >> 2];  // above CTB (or picture edge) → DC
+    int l0, l1, l2;
+    if (ca == cb) {
+        if (ca < 2) {
+            l0 = 0;
+            l1 = 1;
+            l2 = 26;
+        } else {
+            l0 = ca;
+            l1 = 2 + ((ca + 29) % 32);
+            l2 = 2 + ((ca - 2 + 1) % 32);
+        }
+    } else {
+        l0 = ca;
+        l1 = cb;
+        if (ca != 0 && cb != 0) l2 = 0;
+        else if (ca != 1 && cb != 1) l2 = 1;
+        else l2 = 26;
+    }
+    if (prev) return mpm_idx == 0 ? l0 : (mpm_idx == 1 ? l1 : l2);
+    int t;
+    if (l0 > l1) { t = l0; l0 = l1; l1 = t; }
+    if (l0 > l2) { t = l0; l0 = l2; l2 = t; }
+    if (l1 > l2) { t = l1; l1 = l2; l2 = t; }
+    int m = rem;
+    if (m >= l0) ++m;
+    if (m >= l1) ++m;
+    if (m >= l2) ++m;
+    return m;
+}
+
+// 6.5.3-6.5.5 scans.  Packed 4-bit 2x2 / 4x4 scans (entry x | (y << 2)) are
+// selected, not indexed, so they stay immediates; the 8x8 sub-block scan of
+// 32x32 TBs comes from the table.  scan_pos returns x | (y << 4).
+HG_HD inline uint64_t scan4_word(int scan) { return scan == 0 ? kScan4Pos[0] : (scan == 1 ? kScan4Pos[1] : kScan4Pos[2]); }
+HG_HD inline int scan_pos(int l, int scan, int i) {
+    if (l == 3) return kScanPos[3][scan][i];
+    if (l == 0) return 0;
+    const uint64_t t = l == 2 ? scan4_word(scan) : (scan == 0 ? kScan2Pos[0] : (scan == 1 ? kScan2Pos[1] : kScan2Pos[2]));
+    const uint32_t e = (uint32_t)(t >> (4 * i)) & 15u;
+    return (int)((e & 3) | ((e >> 2) << 4));
+}
+HG_HD inline int scan_inv(int l, int scan, int raster) {
+    if (l == 3) return kScanInv[3][scan][raster];
+    if (l == 0) return 0;
+    const uint64_t t = l == 2 ? (scan == 0 ? kScan4Inv[0] : (scan == 1 ? kScan4Inv[1] : kScan4Inv[2]))
+                              : (scan == 0 ? kScan2Inv[0] : (scan == 1 ? kScan2Inv[1] : kScan2Inv[2]));
+    return (int)((uint32_t)(t >> (4 * raster)) & 15u);
+}
+
+// sig_coeff_flag ctxInc patterns (9.3.4.2.5) per prevCsbf, byte per raster e = x | (y << 2)
+constexpr uint64_t sig_pat_word_l(int pc, int half) {
+    uint64_t w = 0;
+    for (int k = 0; k < 8; ++k) {
+        const int e = half * 8 + k, x = e & 3, y = e >> 2;
+        const int v = pc == 0 ? (x + y == 0 ? 2 : (x + y < 3 ? 1 : 0))
+                    : pc == 1 ? (y == 0 ? 2 : (y == 1 ? 1 : 0))
+                    : pc == 2 ? (x == 0 ? 2 : (x == 1 ? 1 : 0)) : 2;
+        w |= (uint64_t)v << (8 * k);
+    }
+    return w;
+}
+constexpr uint64_t sig_map4_word_l(int half) {
+    uint64_t w = 0;
+    for (int k = 0; k < 8; ++k) w |= ((kSigCtxMap4 >> (4 * (half * 8 + k))) & 15u) << (8 * k);
+    return w;
+}
+HG_HD inline uint64_t sig_pat(int pcs, int half) {
+    return half == 0 ? (pcs == 0 ? sig_pat_word_l(0, 0) : pcs == 1 ? sig_pat_word_l(1, 0)
+                        : pcs == 2 ? sig_pat_word_l(2, 0) : sig_pat_word_l(3, 0))
+                     : (pcs == 0 ? sig_pat_word_l(0, 1) : pcs == 1 ? sig_pat_word_l(1, 1)
+                        : pcs == 2 ? sig_pat_word_l(2, 1) : sig_pat_word_l(3, 1));
+}
+
+HG_HD inline int msb32(uint32_t m) { return 31 - __builtin_clz(m); }
+
+struct Env {
+    const BatchArgs *a;
+    LaneLds *lds;    // the wave's 64 lane blocks
+    uint32_t *prog;  // [64] CTUs finished in the lane's current row
+    int lane;
+};
+
+HG_HD inline void row_outputs(Lane &L, const LanePic &P) {
+    L.tu_row = (uint32_t)L.row * P.tu_cap;
+    L.coef_row = (uint32_t)L.row * P.coef_cap;
+    L.ntu = L.ncoef = 0;
+}
+
+// ------------------------------------------------------------------ units
+// U_CTU: CTU start (7.3.8.2) and sao() (7.3.8.3).  Returns without a state
+// change while the row above is less than two CTUs ahead (WPP).
+HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const Eng &G) {
+    if ((L.fl & F_WPP) && L.row > 0) {
+        const uint32_t need = (uint32_t)(L.c + 2 < P.wctb ? L.c + 2 : P.wctb);
+        if (prog_load(&E.prog[E.lane - 1]) < need) return;
+    }
+    L.ctbx = L.c << P.log2ctb;
+    L.ctby = L.row << P.log2ctb;
+    if (L.c == 0 && ((L.fl & F_WPP) || L.row == 0)) {
+        // substream start: contexts (init, or the WPP copy already in ld.ctx) + engine
+        if (L.row == 0 || P.wctb < 2 || !(L.fl & F_WPP))
+#pragma nounroll
+            for (int i = 0; i < CTX_NUM; ++i) ld.ctx[i] = ctx_init_state(c_ctx_init_l[i], P.sliceQp);
+        const uint32_t *subs = E.a->subs + P.sub_first;
+        engine_init(L, G, P.bits_off + subs[(L.fl & F_WPP) ? L.row : 0]);
+        if (L.row == 0) L.fl |= F_FIRST_QG;
+    }
+    if (P.saoL || P.saoC) {
+        int ml = 0, mu = 0;
+        if (L.c > 0) ml = dec(L, G, CTX_SAO_MERGE);
+        if (L.row > 0 && !ml) mu = dec(L, G, CTX_SAO_MERGE);
+        uint32_t *w = reinterpret_cast<uint32_t *>(&ld.sao);
+        if (ml) {
+            // ld.sao still holds the left CTB's parameters
+        } else if (mu) {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(P.gsao + (size_t)(L.row - 1) * P.wctb + L.c);
+            for (int k = 0; k < 8; ++k) w[k] = load_word_coherent(src + k);
+        } else {
+            for (int k = 0; k < 8; ++k) w[k] = 0;
+            SaoParams &s = ld.sao;
+            const int ncomp = P.chroma ? 3 : 1;
+            for (int cc = 0; cc < ncomp; ++cc) {
+                if (!((P.saoL && cc == 0) || (P.saoC && cc > 0))) continue;
+                if (cc < 2) s.type[cc] = (int8_t)(dec(L, G, CTX_SAO_TYPE) ? (byp(L, G) ? 2 : 1) : 0);
+                else s.type[2] = s.type[1];
+                if (!s.type[cc]) continue;
+                const int bd = cc ? P.bdC : P.bdY;
+                const int cmax = (1 << ((bd < 10 ? bd : 10) - 5)) - 1;
+                // SaoOffsetVal straight into LDS, loops kept rolled (an unrolled
+                // local array here costs ~200 VGPRs in the kernel)
+#pragma nounroll
+                for (int i = 0; i < 4; ++i) {  // TR(cMax), bypass
+                    int v = 0;
+                    while (v < cmax && byp(L, G)) ++v;
+                    s.off[cc][i] = (int16_t)v;
+                }
+                if (s.type[cc] == 1) {
+#pragma nounroll
+                    for (int i = 0; i < 4; ++i)
+                        if (s.off[cc][i] && byp(L, G)) s.off[cc][i] = (int16_t)-s.off[cc][i];
+                    s.band_eo[cc] = (uint8_t)byp_bits(L, G, 5);
+                } else {
+                    if (cc < 2) s.band_eo[cc] = (uint8_t)byp_bits(L, G, 2);
+                    else s.band_eo[2] = s.band_eo[1];
+                    s.off[cc][2] = (int16_t)-s.off[cc][2];
+                    s.off[cc][3] = (int16_t)-s.off[cc][3];
+                }
+            }
+        }
+        uint32_t *dst = reinterpret_cast<uint32_t *>(P.gsao + (size_t)L.row * P.wctb + L.c);
+        for (int k = 0; k < 8; ++k) dst[k] = w[k];
+    }
+    L.qx = L.ctbx, L.qy = L.ctby, L.ql = P.log2ctb, L.qd = 0;
+    L.st = U_CQT;
+}
+
+// U_CQT: split_cu_flag descent (7.3.8.4) from the current node to a CU
+HG_HD inline void unit_cqt(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+    for (;;) {
+        const int n = 1 << L.ql;
+        bool split;
+        if (L.qx + n <= P.W && L.qy + n <= P.H && L.ql > P.minCb) {
+            int cond = 0;  // 9.3.4.2.2 ctxInc of split_cu_flag
+            if (L.qx > 0 && ld.dL[(L.qy - L.ctby) >> 3] > L.qd) ++cond;
+            if (L.qy > 0) {
+                const int ad = (L.qy - 1 < L.ctby)
+                                   ? load_byte_coherent(P.gdepth + (size_t)(L.row - 1) * P.w8 + (L.qx >> 3))
+                                   : ld.dA[(L.qx - L.ctbx) >> 3];
+                if (ad > L.qd) ++cond;
+            }
+            split = dec(L, G, CTX_SPLIT_CU + cond) != 0;
+        } else {
+            split = L.ql > P.minCb;
+        }
+        if (L.ql >= P.log2qg) {
+            L.fl = (L.fl & ~F_DQP_CODED) | F_QG_NEW;
+            L.cu_qp_delta_val = 0;
+            L.qg_x = L.qx;
+            L.qg_y = L.qy;
+        }
+        if (!split) break;
+        --L.ql;  // child 0 (always inside the picture)
+        ++L.qd;
+    }
+    L.st = U_CU;
+}
+
+// U_CU: coding_unit (7.3.8.5) up to its transform_tree
+HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+    if (L.fl & F_QG_NEW) {
+        derive_qp_pred(L, ld, P);
+        L.fl &= ~F_QG_NEW;
+    }
+    update_qpy(L, P);
+    L.fl &= ~(F_BYPASS | F_NXN);
+    if ((P.flags & SP_TQ_BYPASS) && dec(L, G, CTX_TQ_BYPASS)) L.fl |= F_BYPASS;
+    if (L.ql == P.minCb && !dec(L, G, CTX_PART_MODE)) L.fl |= F_NXN;
+    const bool nxn = (L.fl & F_NXN) != 0;
+    if (!nxn && (P.flags & SP_PCM) && L.ql >= P.pcmMin && L.ql <= P.pcmMax && term(L, G)) {
+        // pcm_flag = 1: not supported on the GPU path
+        L.status |= ST_UNSUPPORTED;
+        L.fl |= F_STOP;
+        L.st = U_CTU_END;
+        return;
+    }
+    {  // CtDepth of the CU
+        const int nd = 1 << (L.ql - 3);
+        const int dy = (L.qy - L.ctby) >> 3, dx = (L.qx - L.ctbx) >> 3;
+        for (int k = 0; k < nd; ++k) {
+            ld.dL[dy + k] = (uint8_t)L.qd;
+            ld.dA[dx + k] = (uint8_t)L.qd;
+        }
+    }
+    const int np = nxn ? 4 : 1;
+    const int pb = nxn ? 1 << (L.ql - 1) : 1 << L.ql;
+    int prev = 0;
+    for (int i = 0; i < np; ++i) prev |= dec(L, G, CTX_PREV_INTRA) << i;
+    int modes = 0;
+    for (int i = 0; i < np; ++i) {
+        const int p = (prev >> i) & 1;
+        int mpm = 0, rem = 0;
+        if (p) mpm = byp(L, G) ? (byp(L, G) ? 2 : 1) : 0;
+        else rem = (int)byp_bits(L, G, 5);
+        const int xPb = L.qx + (i & 1) * pb, yPb = L.qy + (i >> 1) * pb;
+        const int m = derive_luma_mode(L, ld, xPb, yPb, p, mpm, rem);
+        modes |= m << (8 * i);
+        const int nb = pb >> 2, by = (yPb - L.ctby) >> 2, bx = (xPb - L.ctbx) >> 2;
+        for (int k = 0; k < nb; ++k) {
+            ld.ipmL[by + k] = (uint8_t)m;
+            ld.ipmA[bx + k] = (uint8_t)m;
+        }
+    }
+    L.cu_modes = modes;
+    if (P.chroma) {
+        const int icpm = dec(L, G, CTX_CHROMA_MODE) ? (int)byp_bits(L, G, 2) : 4;
+        const int lm = modes & 0xff;
+        int cm;
+        if (icpm == 4) {
+            cm = lm;
+        } else {
+            cm = icpm == 0 ? 0 : (icpm == 1 ? 26 : (icpm == 2 ? 10 : 1));
+            if (cm == lm) cm = 34;
+        }
+        L.cu_chroma = cm;
+    }
+    L.tx = L.qx, L.ty = L.qy, L.tl = L.ql, L.td = 0, L.tcbf = 0;
+    L.st = U_TT;
+}
+
+// U_TT: transform_tree descent (7.3.8.8) from the current node to a leaf,
+// then transform_unit (7.3.8.10) up to its first TB
+HG_HD inline void unit_tt(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+    const bool nxn = (L.fl & F_NXN) != 0;
+    const int max_depth = P.maxDepthIntra + (nxn ? 1 : 0);
+    for (;;) {
+        bool split;
+        if (L.tl <= P.maxTb && L.tl > P.minTb && L.td < max_depth && !(nxn && L.td == 0))
+            split = dec(L, G, CTX_SPLIT_TF + 5 - L.tl) != 0;
+        else
+            split = L.tl > P.maxTb || (nxn && L.td == 0);
+        uint32_t cbf = 0;  // cbf_cb | cbf_cr << 1
+        if (L.tl > 2 && P.chroma) {
+            const uint32_t pc = L.td == 0 ? 3u : (L.tcbf >> (2 * (L.td - 1))) & 3u;
+            if (pc & 1) cbf |= (uint32_t)dec(L, G, CTX_CBF_CHROMA + L.td);
+            if (pc & 2) cbf |= (uint32_t)dec(L, G, CTX_CBF_CHROMA + L.td) << 1;
+        }
+        L.tcbf = (L.tcbf & ~(3u << (2 * L.td))) | (cbf << (2 * L.td));
+        if (!split) break;
+        --L.tl;  // child 0
+        ++L.td;
+    }
+    const uint32_t cbf = (L.tcbf >> (2 * L.td)) & 3u;
+    L.fl = (L.fl & ~(F_CBF_L | F_CBF_CB | F_CBF_CR)) | ((cbf & 1) ? F_CBF_CB : 0u) | ((cbf & 2) ? F_CBF_CR : 0u);
+    if (dec(L, G, CTX_CBF_LUMA + (L.td == 0 ? 1 : 0))) L.fl |= F_CBF_L;
+    // transform_unit
+    const bool chroma4 = P.chroma == 1 && L.tl == 2;
+    const uint32_t pc = L.td > 0 ? (L.tcbf >> (2 * (L.td - 1))) & 3u : 0u;  // parent's cbf_cb/cbf_cr
+    const bool cbf_c = P.chroma == 0 ? false : (chroma4 ? pc != 0 : cbf != 0);
+    if (((L.fl & F_CBF_L) || cbf_c) && (P.flags & SP_CU_QP_DELTA) && !(L.fl & F_DQP_CODED)) {
+        int v = 0;  // cu_qp_delta_abs: TR prefix (cMax 5), EG0 suffix
+        while (v < 5 && dec(L, G, CTX_CU_QP_DELTA + (v == 0 ? 0 : 1))) ++v;
+        if (v == 5) {
+            int ones = 0;
+            bool bad = false;
+            while (byp(L, G)) {
+                if (++ones > 31) {
+                    bad = true;
+                    break;
+                }
+            }
+            if (bad) L.status |= ST_SYNTAX;
+            else v += (int)(((1u << ones) - 1u) + byp_bits(L, G, ones));
+        }
+        if (v && byp(L, G)) v = -v;
+        L.fl |= F_DQP_CODED;
+        L.cu_qp_delta_val = v;
+        update_qpy(L, P);
+    }
+    {  // edge / no-filter flags of every 4x4 luma block of the TB (MF_*)
+        const int nb = 1 << (L.tl - 2), gx0 = L.tx >> 2, gy0 = L.ty >> 2;
+        const int wx = gx0 + nb <= P.w4 ? nb : P.w4 - gx0, hy = gy0 + nb <= P.h4 ? nb : P.h4 - gy0;
+        const uint8_t nf = (L.fl & F_BYPASS) ? MF_NOFILT : 0;
+        for (int y = 0; y < hy; ++y) {
+            uint8_t *row = P.gflags + (size_t)(gy0 + y) * P.w4 + gx0;
+            const uint8_t h = (uint8_t)((y == 0 ? MF_EDGE_H : 0) | nf);
+            for (int x = 0; x < wx; ++x) row[x] = (uint8_t)(h | (x == 0 ? MF_EDGE_V : 0));
+        }
+    }
+    const int blk = L.td == 0 ? 0 : (((L.tx >> L.tl) & 1) | (((L.ty >> L.tl) & 1) << 1));
+    L.tb_n = (P.chroma != 0 && (!chroma4 || blk == 3)) ? 3 : 1;
+    L.tb_t = 0;
+    L.st = U_TB;
+}
+
+// record of the current TB (TuRec, desc.hpp)
+HG_HD inline void tu_emit(Lane &L, const LanePic &P) {
+    int qp;
+    if (L.tb_cidx == 0) {
+        qp = L.qpy_cur + P.qpbdY;
+    } else {
+        const int off = L.tb_cidx == 1 ? P.cbOff : P.crOff;
+        int qpi = L.qpy_cur + off;
+        qpi = qpi < -P.qpbdC ? -P.qpbdC : (qpi > 57 ? 57 : qpi);
+        qp = chroma_qp_map(qpi, P.chroma) + P.qpbdC;
+    }
+    uint32_t f = (uint32_t)L.tb_cidx;
+    if (L.fl & F_TB_CBF) f |= TU_CBF;
+    if (L.fl & F_TS) f |= TU_TSKIP;
+    if (L.fl & F_BYPASS) f |= TU_BYPASS;
+    if (L.tb_cidx == 0 && L.tb_log2 == 2) f |= TU_DST;
+    if (L.ntu < P.tu_cap) {
+        store_tu(P.tu_base + L.tu_row + L.ntu, (uint32_t)L.tb_x | ((uint32_t)L.tb_y << 16),
+                 (uint32_t)L.tb_log2 | (f << 8) | ((uint32_t)L.tb_mode << 16) | ((uint32_t)(uint8_t)qp << 24),
+                 L.tb_coef0, (L.ncoef - L.tb_coef0) | ((uint32_t)L.c << 16));
+        ++L.ntu;
+    } else {
+        L.status |= ST_CAPACITY;
+    }
+}
+
+// After a TB: its record, then the next TB of the TU, the next transform-tree
+// node, or (tree done) the CU's QpY and the next coding-quadtree node / CTU end.
+HG_HD inline void tb_done(Lane &L, LaneLds &ld, LanePic &P) {
+    tu_emit(L, P);
+    if (++L.tb_t < L.tb_n) {
+        L.st = U_TB;
+        return;
+    }
+    // next transform-tree node in z-order (nodes are aligned to their size)
+    while (L.td > 0) {
+        const int s = 1 << L.tl;
+        const int b = ((L.tx >> L.tl) & 1) | (((L.ty >> L.tl) & 1) << 1);
+        if (b < 3) {
+            const int px = L.tx & ~(2 * s - 1), py = L.ty & ~(2 * s - 1);
+            L.tx = px + ((b + 1) & 1) * s;
+            L.ty = py + ((b + 1) >> 1) * s;
+            L.st = U_TT;
+            return;
+        }
+        L.tx &= ~(2 * s - 1);
+        L.ty &= ~(2 * s - 1);
+        ++L.tl;
+        --L.td;
+    }
+    {  // end of the CU: QpY for qPY_A/B and the 4x4 map (deblocking)
+        const int n = 1 << L.ql, nd = n >> 3;
+        const int dy = (L.qy - L.ctby) >> 3, dx = (L.qx - L.ctbx) >> 3;
+        for (int k = 0; k < nd; ++k) {
+            ld.qL[dy + k] = (int8_t)L.qpy_cur;
+            ld.qA[dx + k] = (int8_t)L.qpy_cur;
+        }
+        const int nb = n >> 2, gx0 = L.qx >> 2, gy0 = L.qy >> 2;
+        const int wx = gx0 + nb <= P.w4 ? nb : P.w4 - gx0, hy = gy0 + nb <= P.h4 ? nb : P.h4 - gy0;
+        for (int y = 0; y < hy; ++y) {
+            int8_t *row = P.gqpy + (size_t)(gy0 + y) * P.w4 + gx0;
+            for (int x = 0; x < wx; ++x) row[x] = (int8_t)L.qpy_cur;
+        }
+        L.qp_prev_last = L.qpy_cur;
+    }
+    // next coding-quadtree node in z-order, skipping children outside the picture
+    while (L.qd > 0) {
+        const int s = 1 << L.ql;
+        const int px = L.qx & ~(2 * s - 1), py = L.qy & ~(2 * s - 1);
+        for (int b = (((L.qx >> L.ql) & 1) | (((L.qy >> L.ql) & 1) << 1)) + 1; b < 4; ++b) {
+            const int cx = px + (b & 1) * s, cy = py + (b >> 1) * s;
+            if (cx < P.W && cy < P.H) {
+                L.qx = cx;
+                L.qy = cy;
+                L.st = U_CQT;
+                return;
+            }
+        }
+        L.qx = px;
+        L.qy = py;
+        ++L.ql;
+        --L.qd;
+    }
+    L.st = U_CTU_END;
+}
+
+// U_TB: TB tb_t of the TU; without coefficients it is done here, otherwise
+// residual_coding's header (transform_skip_flag, last position) is parsed
+HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+    const int t = L.tb_t;
+    const bool chroma4 = P.chroma == 1 && L.tl == 2;
+    bool cbf;
+    L.tb_cidx = t;
+    if (t == 0) {
+        L.tb_x = L.tx;
+        L.tb_y = L.ty;
+        L.tb_log2 = L.tl;
+        int k = 0;  // IntraPredModeY of the PB the TB lies in
+        if (L.fl & F_NXN) {
+            const int half = 1 << (L.ql - 1);
+            k = ((L.ty - L.qy) >= half ? 2 : 0) + ((L.tx - L.qx) >= half ? 1 : 0);
+        }
+        L.tb_mode = (L.cu_modes >> (8 * k)) & 0xff;
+        cbf = (L.fl & F_CBF_L) != 0;
+    } else if (!chroma4) {
+        L.tb_x = L.tx >> 1;
+        L.tb_y = L.ty >> 1;
+        L.tb_log2 = L.tl - 1;
+        L.tb_mode = L.cu_chroma;
+        cbf = (L.fl & (t == 1 ? F_CBF_CB : F_CBF_CR)) != 0;
+    } else {  // 4:2:0, 4x4 luma TBs: the chroma TBs of the 8x8 parent, after its 4th luma TB
+        const int s = 1 << (L.tl + 1);
+        L.tb_x = (L.tx & ~(s - 1)) >> 1;
+        L.tb_y = (L.ty & ~(s - 1)) >> 1;
+        L.tb_log2 = 2;
+        L.tb_mode = L.cu_chroma;
+        const uint32_t pc = (L.tcbf >> (2 * (L.td - 1))) & 3u;
+        cbf = ((pc >> (t - 1)) & 1u) != 0;
+    }
+    L.fl = (L.fl & ~(F_TS | F_TB_CBF)) | (cbf ? F_TB_CBF : 0u);
+    L.tb_coef0 = L.ncoef;
+    if (!cbf) {
+        tb_done(L, ld, P);
+        return;
+    }
+    // residual_coding header (7.3.8.11)
+    const int l2 = L.tb_log2, n = 1 << l2, cidx = t;
+    if ((P.flags & SP_TRANSFORM_SKIP) && !(L.fl & F_BYPASS) && l2 == 2 && dec(L, G, CTX_TS_FLAG + (cidx ? 1 : 0)))
+        L.fl |= F_TS;
+    // last_sig_coeff_{x,y}_prefix (decoder.rs:109-130), suffixes
+    const int cmax = (l2 << 1) - 1;
+    const int off = cidx == 0 ? 3 * (l2 - 2) + ((l2 - 1) >> 2) : 15;
+    const int shift = cidx == 0 ? (l2 + 1) >> 2 : l2 - 2;
+    int px = 0, py = 0;
+    while (px < cmax && dec(L, G, CTX_LAST_X + off + (px >> shift))) ++px;
+    while (py < cmax && dec(L, G, CTX_LAST_Y + off + (py >> shift))) ++py;
+    int lx = px, ly = py;
+    if (px > 3) {
+        const int k = (px >> 1) - 1;
+        lx = (1 << k) * (2 + (px & 1)) + (int)byp_bits(L, G, k);
+    }
+    if (py > 3) {
+        const int k = (py >> 1) - 1;
+        ly = (1 << k) * (2 + (py & 1)) + (int)byp_bits(L, G, k);
+    }
+    int scan = 0;  // 7.4.9.11 scanIdx
+    if (l2 == 2 || (l2 == 3 && cidx == 0)) {
+        if (L.tb_mode >= 6 && L.tb_mode <= 14) scan = 2;
+        else if (L.tb_mode >= 22 && L.tb_mode <= 30) scan = 1;
+    }
+    if (scan == 2) {
+        const int tt = lx;
+        lx = ly;
+        ly = tt;
+    }
+    if (lx >= n || ly >= n) {
+        L.status |= ST_SYNTAX;
+        lx &= n - 1;
+        ly &= n - 1;
+    }
+    const int sbl = l2 - 2, sbw = 1 << sbl;
+    L.rc_scan = scan;
+    L.rc_last_sub = scan_inv(sbl, scan, (ly >> 2) * sbw + (lx >> 2));
+    L.rc_last_pos = scan_inv(2, scan, (ly & 3) * 4 + (lx & 3));
+    L.rc_csbf = 0;
+    L.rc_prev_c1 = 1;
+    L.fl &= ~F_ANY_SB;
+    L.rc_i = L.rc_last_sub;
+    L.st = U_SB;
+}
+
+// U_SB: sub-block rc_i of residual_coding (7.3.8.11, 9.3.4.2.5-7)
+HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+    const int l2 = L.tb_log2, cidx = L.tb_cidx, i = L.rc_i;
+    const int sbl = l2 - 2, sbw = 1 << sbl;
+    const int sp = scan_pos(sbl, L.rc_scan, i);
+    const int xS = sp & 15, yS = sp >> 4;
+    int pcs = 0;  // prevCsbf
+    if (xS < sbw - 1) pcs |= (int)((L.rc_csbf >> (yS * 8 + xS + 1)) & 1);
+    if (yS < sbw - 1) pcs |= (int)((L.rc_csbf >> ((yS + 1) * 8 + xS)) & 1) << 1;
+    bool coded = true, infer_dc = false;
+    if (i < L.rc_last_sub && i > 0) {
+        coded = dec(L, G, CTX_CSBF + ((pcs & 1) | (pcs >> 1)) + (cidx ? 2 : 0)) != 0;
+        infer_dc = true;
+    }
+    uint32_t sig = 0;
+    if (coded) {
+        L.rc_csbf |= 1ull << (yS * 8 + xS);
+        int nstart = 15;
+        if (i == L.rc_last_sub) {
+            sig = 1u << L.rc_last_pos;
+            nstart = L.rc_last_pos - 1;
+        }
+        // ctxInc of sig_coeff_flag per raster position e of the sub-block, one byte each
+        uint64_t t0, t1;
+        if (l2 == 2) {
+            t0 = sig_map4_word_l(0);
+            t1 = sig_map4_word_l(1);
+        } else {
+            const int off = cidx == 0 ? ((xS | yS) ? 3 : 0) + (l2 == 3 ? (L.rc_scan == 0 ? 9 : 15) : 21)
+                                      : (l2 == 3 ? 9 : 12);
+            const uint64_t rep = 0x0101010101010101ull * (uint64_t)off;
+            t0 = sig_pat(pcs, 0) + rep;
+            t1 = sig_pat(pcs, 1) + rep;
+            if ((xS | yS) == 0) t0 &= ~0xffull;  // DC of the TB: sigCtx 0
+        }
+        const int cbase = CTX_SIG + (cidx ? 27 : 0);
+        const uint64_t sw = scan4_word(L.rc_scan);
+        for (int nn = nstart; nn >= 0; --nn) {
+            if (nn > 0 || !infer_dc) {
+                const int e = (int)((sw >> (4 * nn)) & 15u);
+                const uint64_t t = (e & 8) ? t1 : t0;
+                if (dec(L, G, cbase + (int)((t >> ((e & 7) * 8)) & 0xffu))) {
+                    sig |= 1u << nn;
+                    infer_dc = false;
+                }
+            } else {
+                sig |= 1u;  // inferred DC of a coded sub-block
+            }
+        }
+    }
+    if (sig) {
+        // greater1 / greater2 (9.3.4.2.6-7)
+        int ctx_set = (i == 0 || cidx > 0) ? 0 : 2;
+        if ((L.fl & F_ANY_SB) && L.rc_prev_c1 == 0) ++ctx_set;
+        L.fl |= F_ANY_SB;
+        int c1 = 1;
+        uint32_t g1 = 0, g2 = 0;
+        const int first_sig = 31 - __builtin_clz(sig & (0u - sig));
+        const int last_sig = msb32(sig);
+        int num_g1 = 0, last_g1 = -1;
+        for (uint32_t m = sig; m && num_g1 < 8;) {
+            const int nn = msb32(m);
+            m &= ~(1u << nn);
+            const int f = dec(L, G, CTX_GT1 + ctx_set * 4 + (c1 < 3 ? c1 : 3) + (cidx ? 16 : 0));
+            ++num_g1;
+            if (f) {
+                g1 |= 1u << nn;
+                if (last_g1 < 0) last_g1 = nn;
+            }
+            if (c1 > 0) c1 = f ? 0 : c1 + 1;
+        }
+        L.rc_prev_c1 = c1;
+        if (last_g1 >= 0 && dec(L, G, CTX_GT2 + ctx_set + (cidx ? 4 : 0))) g2 = 1u << last_g1;
+        const bool sign_hidden = !(L.fl & F_BYPASS) && (last_sig - first_sig > 3);
+        const bool hide = (P.flags & SP_SIGN_HIDING) && sign_hidden;
+        const int nsign = __builtin_popcount(sig) - (hide ? 1 : 0);
+        uint32_t signs = byp_bits(L, G, nsign);
+        signs = nsign ? signs << (32 - nsign) : 0u;  // first decoded sign in bit 31
+        int num_sig = 0, sum_abs = 0, last_abs = 0, last_rice = 0;
+        bool first_rem = true;
+        const int n = 1 << l2;
+        for (uint32_t m = sig; m;) {
+            const int nn = msb32(m);
+            m &= ~(1u << nn);
+            const int base = 1 + (int)((g1 >> nn) & 1) + (int)((g2 >> nn) & 1);
+            int rem = 0;
+            if (base == ((num_sig < 8) ? ((nn == last_g1) ? 3 : 2) : 1)) {
+                int k;
+                if (first_rem) {
+                    k = 0;
+                    first_rem = false;
+                } else {
+                    k = last_rice + (last_abs > 3 * (1 << last_rice) ? 1 : 0);
+                    k = k < 4 ? k : 4;
+                }
+                // coeff_abs_level_remaining (decoder.rs:230-261): TR(4 << k, k) prefix, EG(k + 1) escape
+                if (L.wr - L.rd < kRingCoefWater) refill(L, G);
+                int p = 0;
+                while (p < 4 && byp(L, G)) ++p;
+                if (p < 4) {
+                    rem = (p << k) + (int)byp_bits(L, G, k);
+                } else {
+                    int ones = 0;
+                    bool bad = false;
+                    while (byp(L, G)) {
+                        if (++ones > 31 - (k + 1)) {
+                            bad = true;
+                            break;
+                        }
+                    }
+                    if (bad) {
+                        L.status |= ST_SYNTAX;
+                        rem = 0;
+                    } else {
+                        rem = (int)((4u << k) + (((1u << ones) - 1u) << (k + 1)) + byp_bits(L, G, ones + k + 1));
+                    }
+                }
+                last_abs = base + rem;
+                last_rice = k;
+            }
+            int v = base + rem;
+            bool neg;
+            if (hide && nn == first_sig) {
+                sum_abs += v;
+                neg = (sum_abs & 1) != 0;
+            } else {
+                neg = (signs >> 31) != 0;
+                signs <<= 1;
+                if (hide) sum_abs += v;
+            }
+            if (neg) v = -v;
+            const uint32_t pp = (uint32_t)(scan4_word(L.rc_scan) >> (4 * nn)) & 15u;
+            const int xC = (xS << 2) + (int)(pp & 3), yC = (yS << 2) + (int)(pp >> 2);
+            if (v > 32767) v = 32767;
+            if (v < -32768) v = -32768;
+            if (L.ncoef < P.coef_cap)
+                P.coef_base[L.coef_row + L.ncoef++] = ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC);
+            else
+                L.status |= ST_CAPACITY;
+            ++num_sig;
+        }
+    }
+    if (--L.rc_i < 0) tb_done(L, ld, P);
+}
+
+// U_CTU_END: WPP context storage, the depth line, end_of_slice_segment_flag /
+// end_of_subset_one_bit (slice.rs:214-227), progress, next CTU / row
+HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const Eng &G) {
+    if ((L.fl & F_WPP) && L.c == 1 && L.row + 1 < P.hctb) {
+        // 9.3.2.4 storage for the next row's substream: straight into its lane's block
+        uint32_t *dst = reinterpret_cast<uint32_t *>(E.lds[E.lane + 1].ctx);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(ld.ctx);
+#pragma nounroll
+        for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = src[k];
+    }
+    {  // bottom CtDepth of this CTB for the row below
+        const int nb8 = 1 << (P.log2ctb - 3), col0 = L.ctbx >> 3;
+        uint8_t *line = P.gdepth + (size_t)L.row * P.w8;
+        for (int k = 0; k < nb8 && col0 + k < P.w8; ++k) line[col0 + k] = ld.dA[k];
+    }
+    const bool last_in_pic = L.row == P.hctb - 1 && L.c == P.wctb - 1;
+    if (term(L, G) != (last_in_pic ? 1 : 0)) L.status |= ST_SUBSTREAM_END;
+    if (!last_in_pic && (L.fl & F_WPP) && L.c == P.wctb - 1 && !term(L, G)) L.status |= ST_SUBSTREAM_END;
+    if ((int32_t)(L.wr - L.rd) < 0) L.status |= ST_OVERRUN;  // read past the NAL unit
+    release_fence();
+    ++L.c;
+    prog_store(&E.prog[E.lane], (L.fl & F_STOP) ? kProgDone : (uint32_t)L.c);
+    if (!(L.fl & F_STOP) && L.c < P.wctb) {
+        L.st = U_CTU;
+        return;
+    }
+    uint32_t *rc = E.a->row_counts + 2 * (size_t)(P.row_off + L.row);
+    rc[0] = L.ntu;
+    rc[1] = L.ncoef;
+    if (!(L.fl & (F_STOP | F_WPP)) && L.row + 1 < P.hctb) {  // one substream: walk on to the next row
+        ++L.row;
+        L.c = 0;
+        row_outputs(L, P);
+        L.st = U_CTU;
+        return;
+    }
+    if (L.status) atomicOr(&E.a->status[P.pic], L.status);
+    L.st = U_DONE;
+}
+
+// Runs unit `kind` on this lane (the caller passes a wave-uniform kind and
+// only lanes in that unit).  One unit kind per pass keeps the dispatch a
+// uniform branch: a divergent switch over the units would linearise them, and
+// every L field a unit updates would then need a register per unit.
+HG_HD inline void run_unit(int kind, Lane &L, LaneLds &ld, LanePic &P, const Env &E, const Eng &G) {
+    switch (kind) {
+    case U_SB: unit_sb(L, ld, P, G); break;
+    case U_TB: unit_tb(L, ld, P, G); break;
+    case U_TT: unit_tt(L, ld, P, G); break;
+    case U_CU: unit_cu(L, ld, P, G); break;
+    case U_CQT: unit_cqt(L, ld, P, G); break;
+    case U_CTU: unit_ctu(L, ld, P, E, G); break;
+    case U_CTU_END: unit_ctu_end(L, ld, P, E, G); break;
+    default: break;
+    }
+}
+
+// a lane in U_CTU can start its CTU (WPP: the row above is two CTUs ahead)
+HG_HD inline bool ctu_ready(const Lane &L, const LanePic &P, const Env &E) {
+    if (!(L.fl & F_WPP) || L.row == 0) return true;
+    const uint32_t need = (uint32_t)(L.c + 2 < P.wctb ? L.c + 2 : P.wctb);
+    return prog_load(&E.prog[E.lane - 1]) >= need;
+}
+
+// lane setup: picture constants, outputs, first state.  Returns false for an idle lane.
+HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a, int pic, int row) {
+    const PicDesc &pd = a.pics[pic];
+    const SeqParams &sp = a.seqs[pd.seq];
+    const int log2ctb = sp.log2_ctb, ctb = 1 << log2ctb;
+    const int hctb = (sp.height + ctb - 1) >> log2ctb;
+    const bool wpp = (sp.flags & SP_WPP) != 0;
+    if (wpp ? row >= hctb : row != 0) return false;
+    P.W = sp.width;
+    P.H = sp.height;
+    P.log2ctb = log2ctb;
+    P.wctb = (sp.width + ctb - 1) >> log2ctb;
+    P.hctb = hctb;
+    P.minCb = sp.log2_min_cb;
+    P.minTb = sp.log2_min_tb;
+    P.maxTb = sp.log2_max_tb;
+    P.maxDepthIntra = sp.max_th_depth_intra;
+    P.chroma = sp.chroma_format;
+    P.log2qg = log2ctb - sp.diff_cu_qp_delta_depth;
+    P.bdY = sp.bit_depth_y;
+    P.bdC = sp.bit_depth_c;
+    P.qpbdY = 6 * (sp.bit_depth_y - 8);
+    P.qpbdC = 6 * (sp.bit_depth_c - 8);
+    P.pcmMin = sp.log2_min_pcm;
+    P.pcmMax = sp.log2_max_pcm;
+    P.cbOff = sp.cb_qp_offset + pd.cb_qp_off;
+    P.crOff = sp.cr_qp_offset + pd.cr_qp_off;
+    P.sliceQp = pd.slice_qp;
+    P.w4 = (sp.width + 3) >> 2;
+    P.h4 = (sp.height + 3) >> 2;
+    P.w8 = (sp.width + 7) >> 3;
+    P.saoL = pd.sao_luma;
+    P.saoC = pd.sao_chroma;
+    P.flags = sp.flags;
+    P.bits_off = (uint32_t)pd.bits_off;
+    P.bits_end = (uint32_t)pd.bits_off + pd.bits_len;
+    P.sub_first = pd.sub_first;
+    P.row_off = pd.row_off;
+    P.tu_cap = pd.tu_cap_row;
+    P.coef_cap = pd.coef_cap_row;
+    P.pic = (uint32_t)pic;
+    P.gqpy = reinterpret_cast<int8_t *>(a.maps + pd.map_off);
+    P.gflags = a.maps + pd.map_off + (size_t)P.w4 * P.h4;
+    P.gdepth = a.maps + pd.map_off + 2 * (size_t)P.w4 * P.h4;
+    P.gsao = a.sao + pd.sao_off;
+    P.tu_base = a.tus + pd.tu_off;
+    P.coef_base = a.coefs + pd.coef_off;
+    L.status = 0;
+    L.rd = L.wr = 0;
+    L.src = P.bits_end;  // nothing to refill before the substream's engine_init
+    L.fl = wpp ? F_WPP : 0u;
+    L.row = row;
+    L.c = 0;
+    L.qp_prev_last = pd.slice_qp;
+    row_outputs(L, P);
+    for (int k = 0; k < 8; ++k) reinterpret_cast<uint32_t *>(&ld.sao)[k] = 0;
+    L.st = U_CTU;
+    return true;
+}
+
+// pictures per wave: a picture's CTB rows occupy consecutive lanes.
+// HEIFGPU_LANES_PPW lowers it (more, emptier waves) for tuning.
+inline int lanes_pics_per_wave(int max_rows) {
+    static const int forced = [] {
+        const char *e = std::getenv("HEIFGPU_LANES_PPW");
+        return e ? std::atoi(e) : 0;
+    }();
+    const int full = 64 / (max_rows < 1 ? 1 : max_rows);
+    return forced > 0 && forced < full ? forced : full;
+}
+
+}  // namespace
+
+bool parse_lanes_supported(const BatchArgs &a) { return a.max_rows >= 1 && a.max_rows <= 64; }
+
+bool parse_lanes_selected(const BatchArgs &a) {
+    static const int mode = [] {
+        const char *e = std::getenv("HEIFGPU_PARSE");
+        return (e && e[0] == 'l') ? 1 : 0;  // "lanes" | "scalar"
+    }();
+    return mode == 1 && parse_lanes_supported(a);
+}
+
+#if defined(HG_HOST_EMU)
+// one wave at a time, one unit per live lane per pass, lanes in order
+void emu_parse_lanes(const BatchArgs &a) {
+    const int ppw = lanes_pics_per_wave(a.max_rows);
+    const int waves = (a.n_pics + ppw - 1) / ppw;
+    uint8_t lps[256], trans[64];
+    for (int i = 0; i < 256; ++i) lps[i] = c_lps_l[i];
+    for (int i = 0; i < 64; ++i) trans[i] = c_trans_l[i];
+    std::vector<LaneLds> lds(64);
+    std::vector<LanePic> pics(64);
+    std::vector<Lane> lanes(64);
+    uint32_t prog[64];
+    static const bool stats = std::getenv("HEIFGPU_LANES_STATS") != nullptr;
+    for (int w = 0; w < waves; ++w) {
+        for (int l = 0; l < 64; ++l) {
+            prog[l] = 0;
+            const int pl = l / a.max_rows, row = l % a.max_rows;
+            const int pic = a.pic0 + w * ppw + pl;
+            const bool live =
+                pl < ppw && pic < a.pic0 + a.n_pics && lane_init(lanes[l], pics[pl], lds[l], a, pic, row);
+            if (!live) lanes[l].st = U_DONE;
+        }
+        Env E{&a, lds.data(), prog, 0};
+        long passes = 0, units = 0;
+        for (;; ++passes) {
+            bool any = false, progressed = false;
+            for (int l = 0; l < 64; ++l) any |= lanes[l].st != U_DONE;
+            if (!any) break;
+            // the kernel's pass: every unit kind in syntax order, each on the lanes in it
+            for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
+                for (int l = 0; l < 64; ++l) {
+                    Lane &L = lanes[l];
+                    E.lane = l;
+                    LanePic &P = pics[l / a.max_rows];
+                    if (L.st != kind || (kind == U_CTU && !ctu_ready(L, P, E))) continue;
+                    progressed = true;
+                    ++units;
+                    const Eng G{lds[l].ctx, lds[l].ring, lps, trans, a.bits, P.bits_end};
+                    refill(L, G);
+                    run_unit(kind, L, lds[l], P, E, G);
+                }
+            }
+            if (!progressed) {  // every live lane waits: cannot happen (the top row never waits)
+                for (int l = 0; l < 64; ++l)
+                    if (lanes[l].st != U_DONE) {
+                        lanes[l].status |= ST_SUBSTREAM_END;
+                        atomicOr(&a.status[pics[l / a.max_rows].pic], lanes[l].status);
+                        lanes[l].st = U_DONE;
+                    }
+                break;
+            }
+        }
+        if (stats)
+            printf("wave %d: %ld passes, %.1f units per pass\n", w, passes, (double)units / passes);
+    }
+}
+#else
+// LDS of one wave: LaneLds per used lane, LanePic per picture, progress words, engine tables
+inline size_t lanes_lds_bytes(int ppw, int max_rows) {
+    return sizeof(LaneLds) * (size_t)(ppw * max_rows) + sizeof(LanePic) * (size_t)ppw + 64 * sizeof(uint32_t) + 256 + 64;
+}
+
+__global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int ppw = a.parse_group;  // pictures per wave (launch_parse_lanes)
+    const int nl = ppw * a.max_rows;
+    LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
+    LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + nl);
+    uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + ppw);
+    uint8_t *s_lps = reinterpret_cast<uint8_t *>(s_prog + 64), *s_trans = s_lps + 256;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < 256; i += 64) s_lps[i] = c_lps_l[i];
+    s_trans[lane] = c_trans_l[lane];
+    const int pl = lane / a.max_rows, row = lane % a.max_rows;
+    const int pic = a.pic0 + blockIdx.x * ppw + pl;
+    Lane L;
+    LaneLds &ld = s_lds[lane < nl ? lane : 0];
+    LanePic &P = s_pic[pl < ppw ? pl : 0];
+    s_prog[lane] = 0;
+    const bool live = pl < ppw && pic < a.pic0 + a.n_pics && lane_init(L, P, ld, a, pic, row);
+    if (!live) L.st = U_DONE;
+    __syncthreads();
+    const Env E{&a, s_lds, s_prog, lane};
+    const Eng G{ld.ctx, ld.ring, s_lps, s_trans, a.bits, live ? P.bits_end : 0u};
+#if defined(HG_PARSE_PROF)
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
+    for (uint32_t pass = 0;; ++pass) {
+        if (!__any(L.st != U_DONE)) break;
+        // one pass: every unit kind in syntax order, each run by the lanes in it
+        // (a uniform loop: the units are never linearised into one divergent region)
+        bool progressed = false;
+#pragma unroll
+        for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
+            const bool mine = L.st == kind && (kind != U_CTU || ctu_ready(L, P, E));
+            if (!__any(mine)) continue;
+            progressed = true;
+#if defined(HG_PARSE_PROF)
+            const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
+            if (mine) refill(L, G);
+#if defined(HG_PARSE_PROF)
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+#endif
+            if (mine) run_unit(kind, L, ld, P, E, G);
+#if defined(HG_PARSE_PROF)
+            const uint64_t t2 = __builtin_amdgcn_s_memtime();
+            pf[7] += t1 - t0;
+            pf[kind <= U_CTU ? 2 : kind <= U_TT ? 3 : kind - 1] += t2 - t1;
+#endif
+        }
+#if defined(HG_PARSE_PROF)
+        ++pf[1];
+#endif
+        if (!progressed || pass > (1u << 30)) {  // every live lane waits: cannot happen (the top row never waits)
+            if (L.st != U_DONE) {
+                L.status |= ST_SUBSTREAM_END;
+                atomicOr(&a.status[P.pic], L.status);
+            }
+            break;
+        }
+    }
+#if defined(HG_PARSE_PROF)
+    pf[0] = __builtin_amdgcn_s_memtime() - t_start;
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[k], (unsigned long long)pf[k]);
+#endif
+}
+
+// tuning hook for heifgpu_debug_counters (parse.hip): copies out and zeroes the counters
+int parse_lanes_counters(uint64_t *out8) {
+#if defined(HG_PARSE_PROF)
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_prof_lanes), 8 * sizeof(uint64_t)) != hipSuccess) return -1;
+    const uint64_t zero[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof_lanes), zero, sizeof(zero)) != hipSuccess) return -1;
+    return 8;
+#else
+    (void)out8;
+    return 0;
+#endif
+}
+
+hipError_t launch_parse_lanes(const BatchArgs &a0, hipStream_t s) {
+    BatchArgs a = a0;
+    const int ppw = lanes_pics_per_wave(a.max_rows);
+    a.parse_group = ppw;
+    const int waves = (a.n_pics + ppw - 1) / ppw;
+    hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.max_rows), s, a);
+    return hipGetLastError();
+}
+#endif
+
+}  // namespace hg

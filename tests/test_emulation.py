@@ -29,16 +29,22 @@ def _run(exe, path, env_extra=None):
     return r.returncode, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("group", ["16", "1", "3"])
-def test_emulated_kernels_match_oracle(emu_check, group):
-    rc, out = _run(emu_check, ROOT / "tests/golden/halfmoonbay.heic", {"HEIFGPU_PARSE_GROUP": group})
+# k_parse with 16 / 1 / 3 waves per picture, and k_parse_lanes (one substream per lane)
+PARSERS = {"wave16": {"HEIFGPU_PARSE_GROUP": "16"}, "wave1": {"HEIFGPU_PARSE_GROUP": "1"},
+           "wave3": {"HEIFGPU_PARSE_GROUP": "3"}, "lanes": {"HEIFGPU_PARSE": "lanes"}}
+
+
+@pytest.mark.parametrize("parser", list(PARSERS))
+def test_emulated_kernels_match_oracle(emu_check, parser):
+    rc, out = _run(emu_check, ROOT / "tests/golden/halfmoonbay.heic", PARSERS[parser])
     assert rc == 0 and "EMU PARITY OK" in out, out[-2000:]
 
 
-def test_emulated_kernels_permuted_image(emu_check, tmp_path, halfmoonbay):
+@pytest.mark.parametrize("parser", ["wave16", "lanes"])
+def test_emulated_kernels_permuted_image(emu_check, tmp_path, halfmoonbay, parser):
     p = tmp_path / "perm.heic"
     p.write_bytes(permuted_heic(halfmoonbay, 42))
-    rc, out = _run(emu_check, p)
+    rc, out = _run(emu_check, p, PARSERS[parser])
     assert rc == 0 and "EMU PARITY OK" in out, out[-2000:]
 
 
@@ -61,14 +67,15 @@ def _corrupt(data: bytes, mode: str) -> bytes:
     return bytes(d)
 
 
+@pytest.mark.parametrize("parser", ["wave16", "lanes"])
 @pytest.mark.parametrize("mode", ["random", "zeroed"])
-def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode):
+def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode, parser):
     """Corrupt slice data must end in status bits, never in a crash (the same
     bounds protect the GPU: ring index masks, TU/coefficient caps, clamped
     geometry).  The ASan build (`make emu`) was run on the same inputs."""
     p = tmp_path / f"{mode}.heic"
     p.write_bytes(_corrupt(halfmoonbay, mode))
-    rc, out = _run(emu_check, p)
+    rc, out = _run(emu_check, p, PARSERS[parser])
     assert rc in (0, 1), out[-2000:]
     line = next(l for l in out.splitlines() if l.startswith("parse: status"))
     assert int(line.split()[2].rstrip(","), 16) != 0

@@ -20,6 +20,8 @@ from heif_amd import _lib  # noqa: E402
 from heif_amd.synthetic import permuted_heic  # noqa: E402
 
 NAMES = ["wave", "spin", "bins", "bypass", "refill", "cqt", "resid", "sao"]
+# k_parse_lanes (HEIFGPU_PARSE=lanes): per-wave s_memtime cycles
+LANES = ["l_wave", "l_passes", "l_ctu", "l_tree", "l_tb", "l_sb", "l_ctu_end", "l_refill"]
 
 
 def main():
@@ -41,7 +43,10 @@ def main():
     torch.cuda.synchronize()
     st = ctx.stage_times()
     lib.heifgpu_debug_counters(buf, 16)
-    c = dict(zip(NAMES, buf[:k]))
+    c = dict(zip(NAMES + LANES, buf[:k]))
+    if c.get("l_passes"):
+        print("k_parse_lanes totals:", {n: c[n] for n in LANES}, f"parse {ctx.stage_times()[0]:.3f} ms")
+        return
     info = imgs[0].info
     rows = n * info.num_tiles * ((info.tile_height + 63) // 64)
     print(f"images {n}, waves(rows) {rows}, parse {st[0]:.3f} ms, status {batch.status()}")

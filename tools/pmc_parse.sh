@@ -2,6 +2,7 @@
 # SQ instruction-mix counters of k_parse for one library variant (tuning).
 # usage: tools/pmc_parse.sh <variant-suffix or ''>  -> gpurun_out/pmc_<v>/
 V=$1
+# extra environment (e.g. HEIFGPU_PARSE=lanes) is inherited by the profiled process
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 LIB=$R/heif_amd/libheifgpu${V:+_$V}.so
 cd /tmp && export TMPDIR=/tmp
