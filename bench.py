@@ -209,7 +209,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": traffic,
-                "kernel": "k_parse (CABAC)",
+                "kernel": "k_parse (CABAC, one WPP row per lane)" if os.environ.get("HEIFGPU_PARSE", "lanes")[:1] != "s"
+                          else "k_parse (CABAC, one picture per wave)",
                 "kernel_ms_per_launch": round(parse_ms / chunks, 3),
                 "algorithmic_bytes_per_launch": args.batch * algo_per_image // chunks,
                 "launches_per_step": chunks,

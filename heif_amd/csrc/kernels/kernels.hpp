@@ -68,7 +68,7 @@ size_t parse_group_bytes(int max_width, int max_wctb, int group) {
     return (b + 15) & ~(size_t)15;
 }
 
-// k_parse_lanes (parse_lanes.hip): one substream per lane; HEIFGPU_PARSE=lanes selects it
+// k_parse_lanes (parse_lanes.hip): one substream per lane; the default (HEIFGPU_PARSE=scalar selects k_parse)
 bool parse_lanes_supported(const BatchArgs &a);
 bool parse_lanes_selected(const BatchArgs &a);
 

@@ -1126,7 +1126,7 @@ bool parse_lanes_supported(const BatchArgs &a) { return a.max_rows >= 1 && a.max
 bool parse_lanes_selected(const BatchArgs &a) {
     static const int mode = [] {
         const char *e = std::getenv("HEIFGPU_PARSE");
-        return (e && e[0] == 'l') ? 1 : 0;  // "lanes" | "scalar"
+        return (e && e[0] == 's') ? 0 : 1;  // "lanes" (default) | "scalar"
     }();
     return mode == 1 && parse_lanes_supported(a);
 }

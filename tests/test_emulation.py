@@ -30,8 +30,9 @@ def _run(exe, path, env_extra=None):
 
 
 # k_parse with 16 / 1 / 3 waves per picture, and k_parse_lanes (one substream per lane)
-PARSERS = {"wave16": {"HEIFGPU_PARSE_GROUP": "16"}, "wave1": {"HEIFGPU_PARSE_GROUP": "1"},
-           "wave3": {"HEIFGPU_PARSE_GROUP": "3"}, "lanes": {"HEIFGPU_PARSE": "lanes"}}
+_SCALAR = {"HEIFGPU_PARSE": "scalar"}
+PARSERS = {"wave16": {**_SCALAR, "HEIFGPU_PARSE_GROUP": "16"}, "wave1": {**_SCALAR, "HEIFGPU_PARSE_GROUP": "1"},
+           "wave3": {**_SCALAR, "HEIFGPU_PARSE_GROUP": "3"}, "lanes": {"HEIFGPU_PARSE": "lanes"}}
 
 
 @pytest.mark.parametrize("parser", list(PARSERS))
