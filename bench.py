@@ -133,7 +133,7 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
-    stage_ms = [0.0] * 5
+    stage_ms = [0.0] * 6
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -216,7 +216,7 @@ def main():
                 "launches_per_step": chunks,
             },
             "stage_ms_per_step": {k: round(v, 3) for k, v in zip(
-                ["parse", "transform", "intra", "deblock", "sao_out"], per_step)},
+                ["parse", "transform", "intra", "deblock", "sao_out", "rbsp"], per_step)},
             "pipeline_hbm_gbs": round(args.batch * algo_per_image / (elapsed / args.steps) / 1e9, 2),
             "host_parse_ms_per_image": round(host_parse_ms, 3),
             "upload_s": round(upload_s, 3),

@@ -155,7 +155,7 @@ class DecodeContext:
         return int(lib.heifgpu_last_chunks(self._h))
 
     def stage_times(self) -> List[float]:
-        ms = (ctypes.c_float * 5)()
+        ms = (ctypes.c_float * 6)()
         _lib.check(lib.heifgpu_stage_times(self._h, ms))
         return list(ms)
 

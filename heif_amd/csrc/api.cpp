@@ -35,6 +35,7 @@ struct heifgpu_ctx {
     hipEvent_t fork = nullptr, join = nullptr;       // caller stream <-> recon stream
     hipEvent_t parsed[kMaxChunks] = {};              // chunk i parsed
     hipEvent_t tev[kMaxChunks][7] = {};              // timing: parse start/end, recon start, 4 stage ends
+    hipEvent_t rev[2] = {};                          // timing: k_rbsp start/end
     int timed_chunks = 0;
     int last_chunks = 0;
 };
@@ -77,9 +78,9 @@ struct heifgpu_batch {
     size_t n_images = 0;
     int n_pics = 0;
     BatchArgs args{};
-    DevBuf<uint8_t> bits, sf, maps, recon;
+    DevBuf<uint8_t> bits, rbsp, sf, maps, recon;
     DevBuf<PicDesc> pics;
-    DevBuf<uint32_t> subs, row_counts, status;
+    DevBuf<uint32_t> subs, rsubs, row_counts, status;
     DevBuf<SeqParams> seqs;
     DevBuf<OutImage> outs;
     DevBuf<TuRec> tus;
@@ -153,6 +154,7 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     for (auto &e : c->parsed) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto &row : c->tev)
         for (auto &e : row) HIP_TRY(hipEventCreate(&e));
+    for (auto &e : c->rev) HIP_TRY(hipEventCreate(&e));
     *out = c.release();
     return HEIFGPU_OK;
 }
@@ -164,6 +166,8 @@ void heifgpu_destroy(heifgpu_ctx *ctx) {
         for (auto &e : row)
             if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->parsed)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : ctx->rev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
@@ -179,11 +183,15 @@ int heifgpu_set_timing(heifgpu_ctx *ctx, int enable) {
 
 int heifgpu_last_chunks(const heifgpu_ctx *ctx) { return ctx ? ctx->last_chunks : 0; }
 
-int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[5]) {
+int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[6]) {
     if (!ctx || !ms) return fail(HEIFGPU_E_INVALID, "null argument");
     if (!ctx->timing) return fail(HEIFGPU_E_INVALID, "timing disabled");
     // per stage: summed over chunks (stages of different chunks overlap in time)
-    for (int i = 0; i < 5; ++i) ms[i] = 0.f;
+    for (int i = 0; i < 6; ++i) ms[i] = 0.f;
+    if (ctx->timed_chunks) {
+        HIP_TRY(hipEventSynchronize(ctx->rev[1]));
+        HIP_TRY(hipEventElapsedTime(&ms[5], ctx->rev[0], ctx->rev[1]));
+    }
     for (int k = 0; k < ctx->timed_chunks; ++k) {
         HIP_TRY(hipEventSynchronize(ctx->tev[k][6]));
         float t;
@@ -235,6 +243,8 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
     HIP_TRY(b->bits.alloc(h_bits.size()));
     HIP_TRY(b->pics.alloc(h_pics.size()));
     HIP_TRY(b->subs.alloc(h_subs.size()));
+    HIP_TRY(b->rbsp.alloc(h_bits.size()));
+    HIP_TRY(b->rsubs.alloc(h_subs.size()));
     HIP_TRY(b->seqs.alloc(h_seqs.size()));
     HIP_TRY(b->sf.alloc(h_sf.size()));
     HIP_TRY(b->outs.alloc(n));
@@ -252,10 +262,13 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
     HIP_TRY(hipMemcpy(b->seqs.p, h_seqs.data(), h_seqs.size() * sizeof(SeqParams), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b->sf.p, h_sf.data(), h_sf.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemset(b->status.p, 0, h_pics.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemset(b->rbsp.p, 0, h_bits.size()));
     BatchArgs &a = b->args;
     a.bits = b->bits.p;
     a.pics = b->pics.p;
     a.subs = b->subs.p;
+    a.rbsp = b->rbsp.p;
+    a.rsubs = b->rsubs.p;
     a.seqs = b->seqs.p;
     a.sf = b->sf.p;
     a.outs = b->outs.p;
@@ -309,6 +322,9 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         const char *e = std::getenv("HEIFGPU_STAGES");
         return e ? std::atoi(e) : 5;
     }();
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->rev[0], s));
+    HIP_TRY(launch_rbsp(a, s));
+    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->rev[1], s));
     if (max_stages < 5) {
         hipError_t (*fns[5])(const BatchArgs &, hipStream_t) = {launch_parse, launch_transform, launch_intra,
                                                                 launch_deblock, launch_sao_out};

@@ -50,6 +50,10 @@ int main(int argc, char **argv) {
     a.bits = hb.bits.data();
     a.pics = hb.pics.data();
     a.subs = hb.subs.data();
+    std::vector<uint8_t> rbsp(hb.bits.size(), 0);
+    std::vector<uint32_t> rsubs(hb.subs.size(), 0);
+    a.rbsp = rbsp.data();
+    a.rsubs = rsubs.data();
     a.seqs = hb.seqs.data();
     a.sf = hb.sf.data();
     a.outs = &out;
@@ -68,6 +72,7 @@ int main(int argc, char **argv) {
     a.max_log2ctb = hb.max_log2ctb;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = bps;
+    emu_rbsp(a);
     emu_parse(a);
     uint32_t st = 0;
     for (uint32_t s : status) st |= s;

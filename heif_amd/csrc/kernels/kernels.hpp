@@ -1,6 +1,7 @@
 // kernels.hpp — launch interface of the gfx950 decode pipeline.
 //
-// Pipeline per batch (one HIP stream, 5 launches):
+// Pipeline per batch (6 launches):
+//   0. k_rbsp       emulation-prevention removal + entry-point remap (7.3.1.1)
 //   1. k_parse      CABAC substreams → TU records + coefficients + QP/edge
 //                   maps + SAO parameters        (slice.rs:206-256 + todo!()s)
 //   2. k_transform  dequant (8.6.2-3) + inverse DST/DCT (8.6.4) → residuals
@@ -24,6 +25,8 @@ struct BatchArgs {
     const uint8_t *bits;       // raw NAL payloads
     const PicDesc *pics;
     const uint32_t *subs;      // substream raw start offsets (n_sub + 1 per picture, last = len)
+    uint8_t *rbsp;             // k_rbsp: NAL payloads with emulation prevention removed (same offsets as bits)
+    uint32_t *rsubs;           // k_rbsp: substream start offsets into rbsp (last = RBSP length)
     const SeqParams *seqs;
     const uint8_t *sf;         // ScalingFactor blocks
     const OutImage *outs;
@@ -100,6 +103,7 @@ void emu_launch(K kernel, int gx, int gy, int waves, const BatchArgs &a, bool gr
             std::free(lds);
         }
 }
+void emu_rbsp(const BatchArgs &a);
 void emu_parse(const BatchArgs &a);
 void emu_parse_lanes(const BatchArgs &a);
 void emu_transform(const BatchArgs &a);
@@ -107,6 +111,7 @@ void emu_intra(const BatchArgs &a);
 void emu_deblock(const BatchArgs &a);
 void emu_sao_out(const BatchArgs &a);
 #else
+hipError_t launch_rbsp(const BatchArgs &a, hipStream_t s);
 hipError_t launch_parse(const BatchArgs &a, hipStream_t s);
 hipError_t launch_parse_lanes(const BatchArgs &a, hipStream_t s);
 int parse_lanes_counters(uint64_t *out8);

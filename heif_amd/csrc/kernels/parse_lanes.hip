@@ -47,11 +47,17 @@ __device__ uint64_t g_prof_lanes[8];
 
 namespace {
 
+// engine row of pStateIdx st (Eng::tab): rangeTabLps[st][0..3], transIdxLps, transIdxMps
+HG_HD inline uint64_t state_row(int st) {
+    uint64_t r = 0;
+    for (int q = 0; q < 4; ++q) r |= (uint64_t)c_lps_l[(st << 2) | q] << (8 * q);
+    return r | ((uint64_t)c_trans_l[st] << 32) | ((uint64_t)(st < 62 ? st + 1 : st) << 40);
+}
+
 constexpr uint32_t kProgDone = 0x7fffffffu;
 
 // per-lane LDS block
 struct alignas(16) LaneLds {
-    uint8_t ring[128];           // RBSP bytes of the substream (emulation prevention removed)
     uint8_t ctx[CTX_PAD];
     SaoParams sao;               // SAO parameters of the last CTB (= the left CTB for merge_left)
     uint8_t ipmL[16], ipmA[16];  // IntraPredModeY (4x4 units): last written per row / per column
@@ -102,11 +108,15 @@ enum : uint32_t {
 };
 
 struct Lane {
-    // arithmetic decoder (9.3.4.3, 16-bit-scaled value) and raw byte position
+    // arithmetic decoder (9.3.4.3): ivlOffset carried with k look-ahead bits,
+    // value = ivlOffset * 2^k + next k bits of the substream, so a renormalisation
+    // only lowers k; a bit window tops value up 16 bits at a time
     uint32_t range, value;
-    int bits_needed;
-    uint32_t rd, wr;             // ring read / write counts
-    uint32_t src, prev1, prev2;  // next raw byte (absolute offset into BatchArgs::bits); EP history
+    int k;
+    uint64_t cur;     // next bits of the substream, MSB first (cn valid)
+    int cn;
+    uint32_t nx, lb;  // prefetched next RBSP dword (big-endian) and the offset of the one after it
+    int32_t budget;   // 8 * (bytes from the substream start to the picture's RBSP end) - bits moved into value
     uint32_t status;
     int st;
     uint32_t fl;
@@ -131,9 +141,10 @@ struct Lane {
 
 // engine context of one lane
 struct Eng {
-    uint8_t *ctx, *ring;
-    const uint8_t *lps, *trans, *bits;
-    uint32_t end;
+    uint8_t *ctx;
+    const uint64_t *tab;  // per pStateIdx: rangeTabLps[4] | transIdxLps << 32 | transIdxMps << 40 (LDS)
+    const uint8_t *rbsp;  // BatchArgs::rbsp (emulation prevention removed by k_rbsp)
+    uint32_t lim;         // no loads at or past this offset (the picture's RBSP end + 64)
 };
 
 // ------------------------------------------------------------------ memory helpers
@@ -176,124 +187,83 @@ HG_HD inline uint8_t load_byte_coherent(const uint8_t *p) {
 }
 
 // ------------------------------------------------------------------ bytes
-// The RBSP bytes of each lane's substream flow through a 128-byte LDS ring.
-// The kernel loop tops the ring up before a lane runs a unit (refill), so
-// next_byte inside the units is a single LDS read.  Every unit consumes less
-// than the low-water mark of a conforming stream (SAO of 10-bit video, the
-// largest, < 50 bytes; a 4x4 sub-block < 26 bytes before its
-// coeff_abs_level_remaining values, each of which (<= 72 bypass bins) tops
-// the ring up again when it is below kRingCoefWater).  An overrun of a
-// corrupt stream shows as rd > wr at the CTU end (ST_OVERRUN), as in k_parse.
-constexpr uint32_t kRingSize = 128, kRingLowWater = 96, kRingCoefWater = 24;
-
-HG_HD inline uint32_t next_byte(Lane &L, const Eng &G) { return G.ring[L.rd++ & (kRingSize - 1)]; }
-
-#if !defined(HG_HOST_EMU)
-__device__ __forceinline__ uint4 load16(const uint8_t *bits, uint32_t off) {
-    return *reinterpret_cast<const uint4 *>(bits + off);
-}
-#endif
-
-// raw → RBSP bytes (rbsp_reader.rs:11-39: 00 00 03 followed by a byte <= 3, or
-// by the end of the NAL unit, loses the 03) until the ring holds the low-water
-// mark or the NAL unit ends.  Raw bytes are read 16 at a time.
-HG_HD inline void refill(Lane &L, const Eng &G) {
-    while (L.wr - L.rd < kRingLowWater && L.src < G.end) {
-        const uint32_t base = L.src & ~15u;
+// Each lane reads its substream straight from the RBSP arena, which k_rbsp
+// (rbsp.hip) filled with emulation prevention removed (rbsp_reader.rs:11-39).
+// One dword is always in flight ahead of the bit window, so the load latency
+// hides behind the ~32 bits of bins decoded in between.  Loads stop 64 bytes
+// past the picture's end (arena padding); an overrun of a corrupt stream
+// shows as budget + k < 0 at the CTU end (ST_OVERRUN).
+HG_HD inline uint32_t load_be(const uint8_t *p, uint32_t off, uint32_t lim) {
+    if (off >= lim) return 0u;
 #if defined(HG_HOST_EMU)
-        uint64_t lo = 0, hi = 0;
-        for (int k = 0; k < 8; ++k) {
-            lo |= (uint64_t)G.bits[base + k] << (8 * k);
-            hi |= (uint64_t)G.bits[base + 8 + k] << (8 * k);
-        }
+    return ((uint32_t)p[off] << 24) | ((uint32_t)p[off + 1] << 16) | ((uint32_t)p[off + 2] << 8) | p[off + 3];
 #else
-        const uint4 q = load16(G.bits, base);
-        const uint64_t lo = (uint64_t)q.x | ((uint64_t)q.y << 32), hi = (uint64_t)q.z | ((uint64_t)q.w << 32);
+    return __builtin_bswap32(*reinterpret_cast<const uint32_t *>(p + off));
 #endif
-        const uint32_t stop = base + 16 < G.end ? base + 16 : G.end;
-        for (uint32_t o = L.src; o < stop; ++o) {
-            const uint32_t k = o & 15u;
-            const uint32_t b = (uint32_t)(((k & 8u) ? hi : lo) >> ((k & 7u) << 3)) & 0xffu;
-            bool ep = false;
-            if (b == 3 && L.prev2 == 0 && L.prev1 == 0) {
-                const uint32_t nb = o + 1 >= G.end ? 0u : (k < 15 ? (uint32_t)((((k + 1) & 8u) ? hi : lo) >> (((k + 1) & 7u) << 3)) & 0xffu
-                                                                    : (uint32_t)G.bits[o + 1]);
-                ep = o + 1 >= G.end || nb <= 3;
-            }
-            if (!ep) G.ring[L.wr++ & (kRingSize - 1)] = (uint8_t)b;
-            L.prev2 = L.prev1;
-            L.prev1 = b;
-        }
-        L.src = stop;
-    }
 }
 
-// 9.3.2.5: engine initialisation at raw offset `start` (absolute)
-HG_HD inline void engine_init(Lane &L, const Eng &G, uint32_t start) {
-    L.src = start;
-    L.rd = L.wr = 0;
-    L.prev1 = G.bits[start - 1];  // the 2-byte NAL header precedes every payload
-    L.prev2 = G.bits[start - 2];
-    refill(L, G);
+// value += 16 more look-ahead bits (k < 8 on entry, so k <= 23 and value < 2^32 after)
+HG_HD inline void vfill(Lane &L, const Eng &G) {
+    if (L.cn < 16) {
+        L.cur |= (uint64_t)L.nx << (32 - L.cn);
+        L.cn += 32;
+        L.nx = load_be(G.rbsp, L.lb, G.lim);
+        L.lb += 4;
+    }
+    L.value = (L.value << 16) | (uint32_t)(L.cur >> 48);
+    L.cur <<= 16;
+    L.cn -= 16;
+    L.k += 16;
+    L.budget -= 16;
+}
+
+// 9.3.2.5: engine initialisation at RBSP offset `start` (absolute), picture RBSP end `end`
+HG_HD inline void engine_init(Lane &L, const Eng &G, uint32_t start, uint32_t end) {
+    const uint32_t a0 = start & ~3u, sh = (start & 3u) * 8u;
+    L.cur = (uint64_t)load_be(G.rbsp, a0, G.lim) << (32 + sh);
+    L.cn = 32 - (int)sh;
+    L.nx = load_be(G.rbsp, a0 + 4, G.lim);
+    L.lb = a0 + 8;
+    L.budget = 8 * (int32_t)(end - start);
+    L.value = 0;
+    L.k = -9;  // the first 9 bits are ivlOffset itself
+    vfill(L, G);
+    vfill(L, G);
     L.range = 510;
-    const uint32_t b0 = next_byte(L, G);
-    const uint32_t b1 = next_byte(L, G);
-    L.value = (b0 << 8) | b1;
-    L.bits_needed = -8;
-    if ((L.value >> 7) >= 510) L.status |= ST_CABAC_INIT;
+    if ((L.value >> L.k) >= 510) L.status |= ST_CABAC_INIT;
 }
 
 // ------------------------------------------------------------------ engine (9.3.4.3)
-// DecodeDecision (arithmetic.rs:97-144)
+// DecodeDecision (arithmetic.rs:97-144), branch-free: one LDS row per
+// pStateIdx gives rangeTabLps and both transitions; the renormalisation of
+// either path is a shift by clz and lowers k.
 HG_HD inline int dec(Lane &L, const Eng &G, int ci) {
     const uint32_t s = G.ctx[ci];
-    uint32_t st = s >> 1, mps = s & 1;
-    const uint32_t lps = G.lps[(st << 2) | ((L.range >> 6) & 3)];
-    L.range -= lps;
-    const uint32_t scaled = L.range << 7;
-    int bin;
-    if (L.value < scaled) {
-        bin = (int)mps;
-        st = st < 62 ? st + 1 : st;
-        if (scaled < (256u << 7)) {
-            L.range = scaled >> 6;
-            L.value <<= 1;
-            if (++L.bits_needed == 0) {
-                L.bits_needed = -8;
-                L.value |= next_byte(L, G);
-            }
-        }
-    } else {
-        L.value -= scaled;
-        const int nb = __builtin_clz(lps) - 23;
-        L.value <<= nb;
-        L.range = lps << nb;
-        bin = (int)(mps ^ 1u);
-        if (st == 0) mps ^= 1u;
-        st = G.trans[st];
-        L.bits_needed += nb;
-        if (L.bits_needed >= 0) {
-            L.value |= next_byte(L, G) << L.bits_needed;
-            L.bits_needed -= 8;
-        }
-    }
-    G.ctx[ci] = (uint8_t)((st << 1) | mps);
-    return bin;
+    const uint32_t st = s >> 1, mps = s & 1u;
+    const uint64_t row = G.tab[st];
+    const uint32_t lps = ((uint32_t)row >> (((L.range >> 6) & 3u) << 3)) & 0xffu;
+    const uint32_t rm = L.range - lps;
+    const uint32_t sr = rm << L.k;
+    const bool isl = L.value >= sr;
+    L.value -= isl ? sr : 0u;
+    const uint32_t rn = isl ? lps : rm;
+    const int nb = __builtin_clz(rn) - 23;
+    L.range = rn << nb;
+    L.k -= nb;
+    const uint32_t nst = ((uint32_t)(row >> 32) >> (isl ? 0 : 8)) & 0xffu;
+    G.ctx[ci] = (uint8_t)((nst << 1) | (mps ^ ((isl && st == 0) ? 1u : 0u)));
+    if (L.k < 8) vfill(L, G);
+    return (int)(mps ^ (isl ? 1u : 0u));
 }
 
 // DecodeBypass (arithmetic.rs:146-157)
 HG_HD inline int byp(Lane &L, const Eng &G) {
-    L.value <<= 1;
-    if (++L.bits_needed >= 0) {
-        L.bits_needed = -8;
-        L.value |= next_byte(L, G);
-    }
-    const uint32_t scaled = L.range << 7;
-    if (L.value >= scaled) {
-        L.value -= scaled;
-        return 1;
-    }
-    return 0;
+    L.k -= 1;
+    const uint32_t sr = L.range << L.k;
+    const bool one = L.value >= sr;
+    L.value -= one ? sr : 0u;
+    if (L.k < 8) vfill(L, G);
+    return one ? 1 : 0;
 }
 
 HG_HD inline uint32_t byp_bits(Lane &L, const Eng &G, int n) {
@@ -305,15 +275,12 @@ HG_HD inline uint32_t byp_bits(Lane &L, const Eng &G, int n) {
 // DecodeTerminate (arithmetic.rs:159-169)
 HG_HD inline int term(Lane &L, const Eng &G) {
     L.range -= 2;
-    const uint32_t scaled = L.range << 7;
-    if (L.value >= scaled) return 1;
-    if (scaled < (256u << 7)) {
-        L.range = scaled >> 6;
-        L.value <<= 1;
-        if (++L.bits_needed == 0) {
-            L.bits_needed = -8;
-            L.value |= next_byte(L, G);
-        }
+    const uint32_t sr = L.range << L.k;
+    if (L.value >= sr) return 1;
+    if (L.range < 256) {
+        L.range <<= 1;
+        L.k -= 1;
+        if (L.k < 8) vfill(L, G);
     }
     return 0;
 }
@@ -457,8 +424,8 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
         if (L.row == 0 || P.wctb < 2 || !(L.fl & F_WPP))
 #pragma nounroll
             for (int i = 0; i < CTX_NUM; ++i) ld.ctx[i] = ctx_init_state(c_ctx_init_l[i], P.sliceQp);
-        const uint32_t *subs = E.a->subs + P.sub_first;
-        engine_init(L, G, P.bits_off + subs[(L.fl & F_WPP) ? L.row : 0]);
+        const uint32_t *subs = E.a->rsubs + P.sub_first;
+        engine_init(L, G, P.bits_off + subs[(L.fl & F_WPP) ? L.row : 0], P.bits_end);
         if (L.row == 0) L.fl |= F_FIRST_QG;
     }
     if (P.saoL || P.saoC) {
@@ -935,7 +902,6 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
                     k = k < 4 ? k : 4;
                 }
                 // coeff_abs_level_remaining (decoder.rs:230-261): TR(4 << k, k) prefix, EG(k + 1) escape
-                if (L.wr - L.rd < kRingCoefWater) refill(L, G);
                 int p = 0;
                 while (p < 4 && byp(L, G)) ++p;
                 if (p < 4) {
@@ -1002,7 +968,7 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     const bool last_in_pic = L.row == P.hctb - 1 && L.c == P.wctb - 1;
     if (term(L, G) != (last_in_pic ? 1 : 0)) L.status |= ST_SUBSTREAM_END;
     if (!last_in_pic && (L.fl & F_WPP) && L.c == P.wctb - 1 && !term(L, G)) L.status |= ST_SUBSTREAM_END;
-    if ((int32_t)(L.wr - L.rd) < 0) L.status |= ST_OVERRUN;  // read past the NAL unit
+    if (L.budget + L.k < 0) L.status |= ST_OVERRUN;  // read past the NAL unit
     release_fence();
     ++L.c;
     prog_store(&E.prog[E.lane], (L.fl & F_STOP) ? kProgDone : (uint32_t)L.c);
@@ -1083,7 +1049,7 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
     P.saoC = pd.sao_chroma;
     P.flags = sp.flags;
     P.bits_off = (uint32_t)pd.bits_off;
-    P.bits_end = (uint32_t)pd.bits_off + pd.bits_len;
+    P.bits_end = (uint32_t)pd.bits_off + a.rsubs[pd.sub_first + pd.n_sub];  // RBSP end (k_rbsp)
     P.sub_first = pd.sub_first;
     P.row_off = pd.row_off;
     P.tu_cap = pd.tu_cap_row;
@@ -1096,8 +1062,8 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
     P.tu_base = a.tus + pd.tu_off;
     P.coef_base = a.coefs + pd.coef_off;
     L.status = 0;
-    L.rd = L.wr = 0;
-    L.src = P.bits_end;  // nothing to refill before the substream's engine_init
+    L.cn = 0;
+    L.k = 8;
     L.fl = wpp ? F_WPP : 0u;
     L.row = row;
     L.c = 0;
@@ -1136,9 +1102,8 @@ bool parse_lanes_selected(const BatchArgs &a) {
 void emu_parse_lanes(const BatchArgs &a) {
     const int ppw = lanes_pics_per_wave(a.max_rows);
     const int waves = (a.n_pics + ppw - 1) / ppw;
-    uint8_t lps[256], trans[64];
-    for (int i = 0; i < 256; ++i) lps[i] = c_lps_l[i];
-    for (int i = 0; i < 64; ++i) trans[i] = c_trans_l[i];
+    uint64_t tab[64];
+    for (int i = 0; i < 64; ++i) tab[i] = state_row(i);
     std::vector<LaneLds> lds(64);
     std::vector<LanePic> pics(64);
     std::vector<Lane> lanes(64);
@@ -1168,8 +1133,7 @@ void emu_parse_lanes(const BatchArgs &a) {
                     if (L.st != kind || (kind == U_CTU && !ctu_ready(L, P, E))) continue;
                     progressed = true;
                     ++units;
-                    const Eng G{lds[l].ctx, lds[l].ring, lps, trans, a.bits, P.bits_end};
-                    refill(L, G);
+                    const Eng G{lds[l].ctx, tab, a.rbsp, P.bits_end + 64};
                     run_unit(kind, L, lds[l], P, E, G);
                 }
             }
@@ -1190,7 +1154,8 @@ void emu_parse_lanes(const BatchArgs &a) {
 #else
 // LDS of one wave: LaneLds per used lane, LanePic per picture, progress words, engine tables
 inline size_t lanes_lds_bytes(int ppw, int max_rows) {
-    return sizeof(LaneLds) * (size_t)(ppw * max_rows) + sizeof(LanePic) * (size_t)ppw + 64 * sizeof(uint32_t) + 256 + 64;
+    return sizeof(LaneLds) * (size_t)(ppw * max_rows) + sizeof(LanePic) * (size_t)ppw + 64 * sizeof(uint32_t) +
+           64 * sizeof(uint64_t);
 }
 
 __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
@@ -1200,10 +1165,9 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
     LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + nl);
     uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + ppw);
-    uint8_t *s_lps = reinterpret_cast<uint8_t *>(s_prog + 64), *s_trans = s_lps + 256;
+    uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_prog + 64);
     const int lane = threadIdx.x;
-    for (int i = lane; i < 256; i += 64) s_lps[i] = c_lps_l[i];
-    s_trans[lane] = c_trans_l[lane];
+    s_tab[lane] = state_row(lane);
     const int pl = lane / a.max_rows, row = lane % a.max_rows;
     const int pic = a.pic0 + blockIdx.x * ppw + pl;
     Lane L;
@@ -1214,7 +1178,7 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     if (!live) L.st = U_DONE;
     __syncthreads();
     const Env E{&a, s_lds, s_prog, lane};
-    const Eng G{ld.ctx, ld.ring, s_lps, s_trans, a.bits, live ? P.bits_end : 0u};
+    const Eng G{ld.ctx, s_tab, a.rbsp, live ? P.bits_end + 64 : 0u};
 #if defined(HG_PARSE_PROF)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
@@ -1232,7 +1196,6 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
 #if defined(HG_PARSE_PROF)
             const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-            if (mine) refill(L, G);
 #if defined(HG_PARSE_PROF)
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
 #endif

@@ -104,11 +104,11 @@ int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *batch, uint32_t *statu
 void heifgpu_batch_free(heifgpu_batch *batch);
 /* stage timing of the last decode (ms, from HIP events when enabled with
  * heifgpu_set_timing(ctx, 1)): parse, transform, intra, deblock,
- * sao/output.  A decode runs in heifgpu_last_chunks() picture chunks whose
+ * sao/output, and (last) the emulation-prevention pass k_rbsp.  A decode runs in heifgpu_last_chunks() picture chunks whose
  * parse (caller's stream) overlaps the previous chunk's reconstruction (a
  * second stream); each figure is the sum over chunks. */
 int heifgpu_set_timing(heifgpu_ctx *ctx, int enable);
-int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[5]);
+int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[6]);
 int heifgpu_last_chunks(const heifgpu_ctx *ctx);
 /* convenience: prepare + decode + status + free */
 int heifgpu_decode_batch(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, const heifgpu_planes *out,
