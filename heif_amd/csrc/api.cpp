@@ -22,22 +22,23 @@ struct heifgpu_image {
     ParsedImage img;
 };
 
-// Pipelined decode: the pictures of a batch are cut into chunks; chunk i's
-// k_parse (scalar-issue-bound) runs on the caller's stream while chunk i-1's
-// reconstruction kernels (vector/memory-bound) run on a second stream.
-constexpr int kMaxChunks = 16;
-constexpr int kChunkMinPics = 6144;  // pictures that keep k_parse at ~6 waves/SIMD on 256 CUs
-
+// Pipelined decode.  k_rbsp + k_parse run on an internal parse stream and the
+// four reconstruction kernels on an internal recon stream.  A batch holds two
+// sets of parse outputs (TU records, coefficients, maps, SAO, per-row counts,
+// status) used by alternate decode calls, so the parse of call n + 1 (which
+// depends on nothing the caller can touch: the bitstreams are the batch's own)
+// runs while call n reconstructs.  Ordering with the caller's stream: the
+// reconstruction of a call waits for everything the caller enqueued on its
+// stream before the call (it writes the caller's planes), and the caller's
+// stream waits for that reconstruction.  A parse set is reused only after the
+// reconstruction that read it.  HEIFGPU_PIPELINE=0 keeps one set (no overlap).
 struct heifgpu_ctx {
     int device = 0;
     bool timing = false;
-    hipStream_t recon = nullptr;                     // second stream (reconstruction)
-    hipEvent_t fork = nullptr, join = nullptr;       // caller stream <-> recon stream
-    hipEvent_t parsed[kMaxChunks] = {};              // chunk i parsed
-    hipEvent_t tev[kMaxChunks][7] = {};              // timing: parse start/end, recon start, 4 stage ends
-    hipEvent_t rev[2] = {};                          // timing: k_rbsp start/end
-    int timed_chunks = 0;
-    int last_chunks = 0;
+    hipStream_t parse = nullptr, recon = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    hipEvent_t tev[8] = {};  // timing: rbsp start, rbsp end = parse start, parse end, recon start, 4 stage ends
+    bool timed = false;
 };
 
 namespace {
@@ -73,20 +74,34 @@ struct DevBuf {
 
 }  // namespace
 
+// outputs of one k_parse run (see heifgpu_ctx)
+struct ParseSet {
+    DevBuf<TuRec> tus;
+    DevBuf<Coef> coefs;
+    DevBuf<uint32_t> row_counts, status;
+    DevBuf<uint8_t> maps;
+    DevBuf<SaoParams> sao;
+    hipEvent_t parsed = nullptr, recon_done = nullptr;
+    bool pending = false;  // recon_done recorded and not yet waited for by a parse
+    ~ParseSet() {
+        if (parsed) (void)hipEventDestroy(parsed);
+        if (recon_done) (void)hipEventDestroy(recon_done);
+    }
+};
+
 struct heifgpu_batch {
     int device = 0;
     size_t n_images = 0;
     int n_pics = 0;
     BatchArgs args{};
-    DevBuf<uint8_t> bits, rbsp, sf, maps, recon;
+    DevBuf<uint8_t> bits, rbsp, sf, recon;
     DevBuf<PicDesc> pics;
-    DevBuf<uint32_t> subs, rsubs, row_counts, status;
+    DevBuf<uint32_t> subs, rsubs;
     DevBuf<SeqParams> seqs;
     DevBuf<OutImage> outs;
-    DevBuf<TuRec> tus;
-    DevBuf<Coef> coefs;
     DevBuf<int16_t> resid;
-    DevBuf<SaoParams> sao;
+    ParseSet set[2];
+    int n_sets = 1, next_set = 0, last_set = 0;
     std::vector<OutImage> out_host;
     std::vector<uint32_t> pic_image;  // picture → image
     std::vector<heifgpu_image_info> infos;
@@ -148,13 +163,19 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     HIP_TRY(hipSetDevice(device));
     auto c = std::make_unique<heifgpu_ctx>();
     c->device = device;
+    // the parse is the latency-critical stream: its waves are dispatched ahead
+    // of the reconstruction kernels of the previous decode (HEIFGPU_PARSE_PRIORITY=0: same priority)
+    static const bool prio = [] {
+        const char *e = std::getenv("HEIFGPU_PARSE_PRIORITY");
+        return !e || std::atoi(e) != 0;
+    }();
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamCreateWithPriority(&c->parse, hipStreamNonBlocking, prio ? greatest : least));
     HIP_TRY(hipStreamCreateWithFlags(&c->recon, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
-    for (auto &e : c->parsed) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (auto &row : c->tev)
-        for (auto &e : row) HIP_TRY(hipEventCreate(&e));
-    for (auto &e : c->rev) HIP_TRY(hipEventCreate(&e));
+    for (auto &e : c->tev) HIP_TRY(hipEventCreate(&e));
     *out = c.release();
     return HEIFGPU_OK;
 }
@@ -162,15 +183,12 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
 void heifgpu_destroy(heifgpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    for (auto &row : ctx->tev)
-        for (auto &e : row)
-            if (e) (void)hipEventDestroy(e);
-    for (auto &e : ctx->parsed)
-        if (e) (void)hipEventDestroy(e);
-    for (auto &e : ctx->rev)
+    (void)hipDeviceSynchronize();
+    for (auto &e : ctx->tev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
+    if (ctx->parse) (void)hipStreamDestroy(ctx->parse);
     if (ctx->recon) (void)hipStreamDestroy(ctx->recon);
     delete ctx;
 }
@@ -181,27 +199,17 @@ int heifgpu_set_timing(heifgpu_ctx *ctx, int enable) {
     return HEIFGPU_OK;
 }
 
-int heifgpu_last_chunks(const heifgpu_ctx *ctx) { return ctx ? ctx->last_chunks : 0; }
+int heifgpu_last_chunks(const heifgpu_ctx *ctx) { return ctx && ctx->timed ? 1 : 0; }
 
 int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[6]) {
     if (!ctx || !ms) return fail(HEIFGPU_E_INVALID, "null argument");
     if (!ctx->timing) return fail(HEIFGPU_E_INVALID, "timing disabled");
-    // per stage: summed over chunks (stages of different chunks overlap in time)
     for (int i = 0; i < 6; ++i) ms[i] = 0.f;
-    if (ctx->timed_chunks) {
-        HIP_TRY(hipEventSynchronize(ctx->rev[1]));
-        HIP_TRY(hipEventElapsedTime(&ms[5], ctx->rev[0], ctx->rev[1]));
-    }
-    for (int k = 0; k < ctx->timed_chunks; ++k) {
-        HIP_TRY(hipEventSynchronize(ctx->tev[k][6]));
-        float t;
-        HIP_TRY(hipEventElapsedTime(&t, ctx->tev[k][0], ctx->tev[k][1]));
-        ms[0] += t;
-        for (int i = 1; i < 5; ++i) {
-            HIP_TRY(hipEventElapsedTime(&t, ctx->tev[k][i + 1], ctx->tev[k][i + 2]));
-            ms[i] += t;
-        }
-    }
+    if (!ctx->timed) return HEIFGPU_OK;
+    HIP_TRY(hipEventSynchronize(ctx->tev[7]));
+    HIP_TRY(hipEventElapsedTime(&ms[5], ctx->tev[0], ctx->tev[1]));  // k_rbsp
+    HIP_TRY(hipEventElapsedTime(&ms[0], ctx->tev[1], ctx->tev[2]));  // k_parse
+    for (int i = 1; i < 5; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], ctx->tev[i + 2], ctx->tev[i + 3]));
     return HEIFGPU_OK;
 }
 
@@ -248,20 +256,30 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
     HIP_TRY(b->seqs.alloc(h_seqs.size()));
     HIP_TRY(b->sf.alloc(h_sf.size()));
     HIP_TRY(b->outs.alloc(n));
-    HIP_TRY(b->tus.alloc(tu_n));
-    HIP_TRY(b->coefs.alloc(coef_n));
-    HIP_TRY(b->row_counts.alloc(size_t(2) * rows));
+    static const int pipeline = [] {
+        const char *e = std::getenv("HEIFGPU_PIPELINE");
+        return e ? std::atoi(e) : 1;
+    }();
+    b->n_sets = pipeline ? 2 : 1;
+    for (int k = 0; k < b->n_sets; ++k) {
+        ParseSet &ps = b->set[k];
+        HIP_TRY(ps.tus.alloc(tu_n));
+        HIP_TRY(ps.coefs.alloc(coef_n));
+        HIP_TRY(ps.row_counts.alloc(size_t(2) * rows));
+        HIP_TRY(ps.maps.alloc(map_bytes));
+        HIP_TRY(ps.sao.alloc(sao_n));
+        HIP_TRY(ps.status.alloc(h_pics.size()));
+        HIP_TRY(hipMemset(ps.status.p, 0, h_pics.size() * sizeof(uint32_t)));
+        HIP_TRY(hipEventCreateWithFlags(&ps.parsed, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ps.recon_done, hipEventDisableTiming));
+    }
     HIP_TRY(b->recon.alloc(recon_bytes));
     HIP_TRY(b->resid.alloc(resid_elems));
-    HIP_TRY(b->maps.alloc(map_bytes));
-    HIP_TRY(b->sao.alloc(sao_n));
-    HIP_TRY(b->status.alloc(h_pics.size()));
     HIP_TRY(hipMemcpy(b->bits.p, h_bits.data(), h_bits.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b->pics.p, h_pics.data(), h_pics.size() * sizeof(PicDesc), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b->subs.p, h_subs.data(), h_subs.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b->seqs.p, h_seqs.data(), h_seqs.size() * sizeof(SeqParams), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b->sf.p, h_sf.data(), h_sf.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(b->status.p, 0, h_pics.size() * sizeof(uint32_t)));
     HIP_TRY(hipMemset(b->rbsp.p, 0, h_bits.size()));
     BatchArgs &a = b->args;
     a.bits = b->bits.p;
@@ -272,14 +290,8 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
     a.seqs = b->seqs.p;
     a.sf = b->sf.p;
     a.outs = b->outs.p;
-    a.tus = b->tus.p;
-    a.coefs = b->coefs.p;
-    a.row_counts = b->row_counts.p;
     a.recon = b->recon.p;
     a.resid = b->resid.p;
-    a.maps = b->maps.p;
-    a.sao = b->sao.p;
-    a.status = b->status.p;
     a.n_pics = b->n_pics;
     a.max_width = max_w;
     a.max_wctb = max_wctb;
@@ -315,57 +327,62 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     }
     if (changed)
         HIP_TRY(hipMemcpyAsync(b->outs.p, b->out_host.data(), b->n_images * sizeof(OutImage), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(b->status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), s));
-    const BatchArgs &a = b->args;
-    // bring-up knob: HEIFGPU_STAGES=k launches only the first k stages
+    // parse set of this call
+    const int k = b->next_set;
+    b->next_set = (k + 1) % b->n_sets;
+    b->last_set = k;
+    ParseSet &ps = b->set[k];
+    BatchArgs a = b->args;
+    a.tus = ps.tus.p;
+    a.coefs = ps.coefs.p;
+    a.row_counts = ps.row_counts.p;
+    a.maps = ps.maps.p;
+    a.sao = ps.sao.p;
+    a.status = ps.status.p;
+    // bring-up knob: HEIFGPU_STAGES=k launches only the first k stages (in order, on the caller's stream)
     static const int max_stages = [] {
         const char *e = std::getenv("HEIFGPU_STAGES");
         return e ? std::atoi(e) : 5;
     }();
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->rev[0], s));
-    HIP_TRY(launch_rbsp(a, s));
-    if (ctx->timing) HIP_TRY(hipEventRecord(ctx->rev[1], s));
     if (max_stages < 5) {
+        HIP_TRY(hipStreamSynchronize(ctx->parse));
+        HIP_TRY(hipStreamSynchronize(ctx->recon));
+        HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), s));
+        HIP_TRY(launch_rbsp(a, s));
         hipError_t (*fns[5])(const BatchArgs &, hipStream_t) = {launch_parse, launch_transform, launch_intra,
                                                                 launch_deblock, launch_sao_out};
         for (int i = 0; i < max_stages; ++i) HIP_TRY(fns[i](a, s));
+        ctx->timed = false;
         return HEIFGPU_OK;
     }
-    // chunks: HEIFGPU_CHUNKS overrides.  k_parse needs ~6 waves per SIMD (6144
-    // pictures) in flight to be efficient — measured on 6144 pictures: 1 chunk
-    // 287 ms of parse, 2 chunks 402, 4 chunks 705 — so a batch is only cut
-    // when every chunk still fills the GPU.
-    static const int forced_chunks = [] {
-        const char *e = std::getenv("HEIFGPU_CHUNKS");
-        return e ? std::atoi(e) : 0;
-    }();
-    int nchunks = forced_chunks > 0 ? forced_chunks : std::max(1, a.n_pics / kChunkMinPics);
-    nchunks = std::min(std::max(nchunks, 1), std::min(kMaxChunks, a.n_pics));
+    hipStream_t p = ctx->parse, r = ctx->recon;
+    const bool t = ctx->timing;
+    // parse stream: this set's previous reconstruction must be done with it
+    if (ps.pending) HIP_TRY(hipStreamWaitEvent(p, ps.recon_done, 0));
+    HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), p));
+    if (t) HIP_TRY(hipEventRecord(ctx->tev[0], p));
+    HIP_TRY(launch_rbsp(a, p));
+    if (t) HIP_TRY(hipEventRecord(ctx->tev[1], p));
+    HIP_TRY(launch_parse(a, p));
+    if (t) HIP_TRY(hipEventRecord(ctx->tev[2], p));
+    HIP_TRY(hipEventRecord(ps.parsed, p));
+    // recon stream: after the caller's prior work and this call's parse
     HIP_TRY(hipEventRecord(ctx->fork, s));
-    HIP_TRY(hipStreamWaitEvent(ctx->recon, ctx->fork, 0));
-    for (int k = 0; k < nchunks; ++k) {
-        BatchArgs c = a;
-        c.pic0 = int((int64_t)a.n_pics * k / nchunks);
-        c.n_pics = int((int64_t)a.n_pics * (k + 1) / nchunks) - c.pic0;
-        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][0], s));
-        HIP_TRY(launch_parse(c, s));
-        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][1], s));
-        HIP_TRY(hipEventRecord(ctx->parsed[k], s));
-        HIP_TRY(hipStreamWaitEvent(ctx->recon, ctx->parsed[k], 0));
-        hipStream_t r = ctx->recon;
-        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][2], r));
-        HIP_TRY(launch_transform(c, r));
-        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][3], r));
-        HIP_TRY(launch_intra(c, r));
-        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][4], r));
-        HIP_TRY(launch_deblock(c, r));
-        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][5], r));
-        HIP_TRY(launch_sao_out(c, r));
-        if (ctx->timing) HIP_TRY(hipEventRecord(ctx->tev[k][6], r));
-    }
-    ctx->timed_chunks = ctx->timing ? nchunks : 0;
-    ctx->last_chunks = nchunks;
-    HIP_TRY(hipEventRecord(ctx->join, ctx->recon));
+    HIP_TRY(hipStreamWaitEvent(r, ctx->fork, 0));
+    HIP_TRY(hipStreamWaitEvent(r, ps.parsed, 0));
+    if (t) HIP_TRY(hipEventRecord(ctx->tev[3], r));
+    HIP_TRY(launch_transform(a, r));
+    if (t) HIP_TRY(hipEventRecord(ctx->tev[4], r));
+    HIP_TRY(launch_intra(a, r));
+    if (t) HIP_TRY(hipEventRecord(ctx->tev[5], r));
+    HIP_TRY(launch_deblock(a, r));
+    if (t) HIP_TRY(hipEventRecord(ctx->tev[6], r));
+    HIP_TRY(launch_sao_out(a, r));
+    if (t) HIP_TRY(hipEventRecord(ctx->tev[7], r));
+    HIP_TRY(hipEventRecord(ps.recon_done, r));
+    ps.pending = true;
+    ctx->timed = t;
+    HIP_TRY(hipEventRecord(ctx->join, r));
     HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
     return HEIFGPU_OK;
 }
@@ -375,7 +392,8 @@ int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *b, uint32_t *status, v
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream, as in HIP
     HIP_TRY(hipSetDevice(ctx->device));
     std::vector<uint32_t> st(size_t(b->n_pics));
-    HIP_TRY(hipMemcpyAsync(st.data(), b->status.p, st.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(st.data(), b->set[b->last_set].status.p, st.size() * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     std::vector<uint32_t> per(b->n_images, 0);
     for (size_t p = 0; p < st.size(); ++p) per[b->pic_image[p]] |= st[p];
@@ -390,6 +408,7 @@ int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *b, uint32_t *status, v
 void heifgpu_batch_free(heifgpu_batch *b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
+    (void)hipDeviceSynchronize();  // in-flight parses / reconstructions of this batch
     delete b;
 }
 

@@ -115,7 +115,7 @@ struct Lane {
     int k;
     uint64_t cur;     // next bits of the substream, MSB first (cn valid)
     int cn;
-    uint32_t nx, lb;  // prefetched next RBSP dword (big-endian) and the offset of the one after it
+    uint32_t nx, lb;  // prefetched next RBSP dword (as loaded) and the offset of the one after it
     int32_t budget;   // 8 * (bytes from the substream start to the picture's RBSP end) - bits moved into value
     uint32_t status;
     int st;
@@ -193,21 +193,27 @@ HG_HD inline uint8_t load_byte_coherent(const uint8_t *p) {
 // hides behind the ~32 bits of bins decoded in between.  Loads stop 64 bytes
 // past the picture's end (arena padding); an overrun of a corrupt stream
 // shows as budget + k < 0 at the CTU end (ST_OVERRUN).
-HG_HD inline uint32_t load_be(const uint8_t *p, uint32_t off, uint32_t lim) {
-    if (off >= lim) return 0u;
+// raw (little-endian) dword at `off`, clamped to `lim` instead of branching,
+// so the load issues straight into its register and nothing waits on it
+// until the window needs it (byte-swapped there)
+HG_HD inline uint32_t load_raw(const uint8_t *p, uint32_t off, uint32_t lim) {
+    const uint32_t o = off < lim ? off : lim;
 #if defined(HG_HOST_EMU)
-    return ((uint32_t)p[off] << 24) | ((uint32_t)p[off + 1] << 16) | ((uint32_t)p[off + 2] << 8) | p[off + 3];
+    return (uint32_t)p[o] | ((uint32_t)p[o + 1] << 8) | ((uint32_t)p[o + 2] << 16) | ((uint32_t)p[o + 3] << 24);
 #else
-    return __builtin_bswap32(*reinterpret_cast<const uint32_t *>(p + off));
+    return *reinterpret_cast<const uint32_t *>(p + o);
 #endif
+}
+HG_HD inline uint32_t bswap32(uint32_t w) {
+    return (w >> 24) | ((w >> 8) & 0xff00u) | ((w << 8) & 0xff0000u) | (w << 24);
 }
 
 // value += 16 more look-ahead bits (k < 8 on entry, so k <= 23 and value < 2^32 after)
 HG_HD inline void vfill(Lane &L, const Eng &G) {
     if (L.cn < 16) {
-        L.cur |= (uint64_t)L.nx << (32 - L.cn);
+        L.cur |= (uint64_t)bswap32(L.nx) << (32 - L.cn);
         L.cn += 32;
-        L.nx = load_be(G.rbsp, L.lb, G.lim);
+        L.nx = load_raw(G.rbsp, L.lb, G.lim);
         L.lb += 4;
     }
     L.value = (L.value << 16) | (uint32_t)(L.cur >> 48);
@@ -220,9 +226,9 @@ HG_HD inline void vfill(Lane &L, const Eng &G) {
 // 9.3.2.5: engine initialisation at RBSP offset `start` (absolute), picture RBSP end `end`
 HG_HD inline void engine_init(Lane &L, const Eng &G, uint32_t start, uint32_t end) {
     const uint32_t a0 = start & ~3u, sh = (start & 3u) * 8u;
-    L.cur = (uint64_t)load_be(G.rbsp, a0, G.lim) << (32 + sh);
+    L.cur = (uint64_t)bswap32(load_raw(G.rbsp, a0, G.lim)) << (32 + sh);
     L.cn = 32 - (int)sh;
-    L.nx = load_be(G.rbsp, a0 + 4, G.lim);
+    L.nx = load_raw(G.rbsp, a0 + 4, G.lim);
     L.lb = a0 + 8;
     L.budget = 8 * (int32_t)(end - start);
     L.value = 0;
@@ -237,8 +243,7 @@ HG_HD inline void engine_init(Lane &L, const Eng &G, uint32_t start, uint32_t en
 // DecodeDecision (arithmetic.rs:97-144), branch-free: one LDS row per
 // pStateIdx gives rangeTabLps and both transitions; the renormalisation of
 // either path is a shift by clz and lowers k.
-HG_HD inline int dec(Lane &L, const Eng &G, int ci) {
-    const uint32_t s = G.ctx[ci];
+HG_HD inline int dec_s(Lane &L, const Eng &G, uint32_t &s) {
     const uint32_t st = s >> 1, mps = s & 1u;
     const uint64_t row = G.tab[st];
     const uint32_t lps = ((uint32_t)row >> (((L.range >> 6) & 3u) << 3)) & 0xffu;
@@ -251,9 +256,31 @@ HG_HD inline int dec(Lane &L, const Eng &G, int ci) {
     L.range = rn << nb;
     L.k -= nb;
     const uint32_t nst = ((uint32_t)(row >> 32) >> (isl ? 0 : 8)) & 0xffu;
-    G.ctx[ci] = (uint8_t)((nst << 1) | (mps ^ ((isl && st == 0) ? 1u : 0u)));
+    s = (nst << 1) | (mps ^ ((isl && st == 0) ? 1u : 0u));
     if (L.k < 8) vfill(L, G);
     return (int)(mps ^ (isl ? 1u : 0u));
+}
+
+// the same on context ci in LDS
+HG_HD inline int dec(Lane &L, const Eng &G, int ci) {
+    uint32_t s = G.ctx[ci];
+    const int bin = dec_s(L, G, s);
+    G.ctx[ci] = (uint8_t)s;
+    return bin;
+}
+
+// byte `slot` (0..11) of a 3-word register cache of context states
+HG_HD inline uint32_t cache_get(uint32_t c0, uint32_t c1, uint32_t c2, int slot) {
+    const uint32_t w = slot < 4 ? c0 : (slot < 8 ? c1 : c2);
+    return (w >> ((slot & 3) * 8)) & 0xffu;
+}
+HG_HD inline void cache_put(uint32_t &c0, uint32_t &c1, uint32_t &c2, int slot, uint32_t s) {
+    const int sh = (slot & 3) * 8;
+    const uint32_t w = slot < 4 ? c0 : (slot < 8 ? c1 : c2);
+    const uint32_t nw = (w & ~(0xffu << sh)) | (s << sh);
+    c0 = slot < 4 ? nw : c0;
+    c1 = (slot >> 2) == 1 ? nw : c1;
+    c2 = slot >= 8 ? nw : c2;
 }
 
 // DecodeBypass (arithmetic.rs:146-157)
@@ -266,10 +293,51 @@ HG_HD inline int byp(Lane &L, const Eng &G) {
     return one ? 1 : 0;
 }
 
+// floor(top / r) for top < 2^24 and 256 <= r <= 510: f32 reciprocal estimate, then one correction
+HG_HD inline uint32_t div_range(uint32_t top, uint32_t r) {
+#if defined(HG_HOST_EMU)
+    return top / r;
+#else
+    uint32_t q = (uint32_t)((float)top * __builtin_amdgcn_rcpf((float)r));
+    const int32_t rem = (int32_t)top - (int32_t)(q * r);
+    q = rem < 0 ? q - 1 : (rem >= (int32_t)r ? q + 1 : q);
+    return q;
+#endif
+}
+
+// n (0..8) bypass bins in one step.  n successive DecodeBypass steps are the
+// long division of ivlOffset * 2^n + (the next n bits) by ivlCurrRange: the
+// quotient is the n bins, the remainder the new ivlOffset.
+HG_HD inline uint32_t byp_n(Lane &L, const Eng &G, int n) {
+    L.k -= n;  // k >= 8 >= n on entry
+    const uint32_t q = div_range(L.value >> L.k, L.range);
+    L.value -= (q * L.range) << L.k;
+    if (L.k < 8) vfill(L, G);
+    return q;
+}
+
 HG_HD inline uint32_t byp_bits(Lane &L, const Eng &G, int n) {
     uint32_t v = 0;
-    for (int i = 0; i < n; ++i) v = (v << 1) | (uint32_t)byp(L, G);
+    while (n > 0) {
+        const int c = n < 8 ? n : 8;
+        v = (v << c) | byp_n(L, G, c);
+        n -= c;
+    }
     return v;
+}
+
+// prefix of coeff_abs_level_remaining (TR, cMax 4): the 1-bins before the
+// first 0, at most 4.  The next 4 bins are divided out without consuming them
+// and min(p + 1, 4) are consumed (a prefix of a long-division quotient is the
+// quotient of the shorter division).
+HG_HD inline int byp_prefix4(Lane &L, const Eng &G) {
+    const uint32_t q4 = div_range(L.value >> (L.k - 4), L.range);
+    const int p = __builtin_clz(((~q4) << 28) | (1u << 27));
+    const int m = p < 4 ? p + 1 : 4;
+    L.k -= m;
+    L.value -= ((q4 >> (4 - m)) * L.range) << L.k;
+    if (L.k < 8) vfill(L, G);
+    return p;
 }
 
 // DecodeTerminate (arithmetic.rs:159-169)
@@ -370,30 +438,22 @@ HG_HD inline int scan_inv(int l, int scan, int raster) {
     return (int)((uint32_t)(t >> (4 * raster)) & 15u);
 }
 
-// sig_coeff_flag ctxInc patterns (9.3.4.2.5) per prevCsbf, byte per raster e = x | (y << 2)
-constexpr uint64_t sig_pat_word_l(int pc, int half) {
+// sig_coeff_flag ctxInc patterns (9.3.4.2.5) per prevCsbf, as one nibble per raster position
+// e = x | (y << 2), each + 1 (slot of the sub-block's context cache)
+constexpr uint64_t sig_pat_nib(int pc) {
     uint64_t w = 0;
-    for (int k = 0; k < 8; ++k) {
-        const int e = half * 8 + k, x = e & 3, y = e >> 2;
+    for (int e = 0; e < 16; ++e) {
+        const int x = e & 3, y = e >> 2;
         const int v = pc == 0 ? (x + y == 0 ? 2 : (x + y < 3 ? 1 : 0))
                     : pc == 1 ? (y == 0 ? 2 : (y == 1 ? 1 : 0))
                     : pc == 2 ? (x == 0 ? 2 : (x == 1 ? 1 : 0)) : 2;
-        w |= (uint64_t)v << (8 * k);
+        w |= (uint64_t)(v + 1) << (4 * e);
     }
     return w;
 }
-constexpr uint64_t sig_map4_word_l(int half) {
-    uint64_t w = 0;
-    for (int k = 0; k < 8; ++k) w |= ((kSigCtxMap4 >> (4 * (half * 8 + k))) & 15u) << (8 * k);
-    return w;
+HG_HD inline uint64_t sig_slots(int pcs) {
+    return pcs == 0 ? sig_pat_nib(0) : pcs == 1 ? sig_pat_nib(1) : pcs == 2 ? sig_pat_nib(2) : sig_pat_nib(3);
 }
-HG_HD inline uint64_t sig_pat(int pcs, int half) {
-    return half == 0 ? (pcs == 0 ? sig_pat_word_l(0, 0) : pcs == 1 ? sig_pat_word_l(1, 0)
-                        : pcs == 2 ? sig_pat_word_l(2, 0) : sig_pat_word_l(3, 0))
-                     : (pcs == 0 ? sig_pat_word_l(0, 1) : pcs == 1 ? sig_pat_word_l(1, 1)
-                        : pcs == 2 ? sig_pat_word_l(2, 1) : sig_pat_word_l(3, 1));
-}
-
 HG_HD inline int msb32(uint32_t m) { return 31 - __builtin_clz(m); }
 
 struct Env {
@@ -828,32 +888,52 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
             sig = 1u << L.rc_last_pos;
             nstart = L.rc_last_pos - 1;
         }
-        // ctxInc of sig_coeff_flag per raster position e of the sub-block, one byte each
-        uint64_t t0, t1;
-        if (l2 == 2) {
-            t0 = sig_map4_word_l(0);
-            t1 = sig_map4_word_l(1);
-        } else {
-            const int off = cidx == 0 ? ((xS | yS) ? 3 : 0) + (l2 == 3 ? (L.rc_scan == 0 ? 9 : 15) : 21)
-                                      : (l2 == 3 ? 9 : 12);
-            const uint64_t rep = 0x0101010101010101ull * (uint64_t)off;
-            t0 = sig_pat(pcs, 0) + rep;
-            t1 = sig_pat(pcs, 1) + rep;
-            if ((xS | yS) == 0) t0 &= ~0xffull;  // DC of the TB: sigCtx 0
-        }
+        // sig_coeff_flag contexts of the sub-block (9.3.4.2.5) in a register
+        // cache: a 4x4 TB uses sigCtx 0..8 (ctxIdxMap, slots 0..8); larger TBs
+        // use sigCtx 0 at the TB's DC (slot 0) and off + 0..2 (slots 1..3)
         const int cbase = CTX_SIG + (cidx ? 27 : 0);
+        const uint8_t *cb = G.ctx + cbase;
+        uint64_t slots;
+        uint32_t c0, c1 = 0, c2 = 0;
+        int off = 0;
+        if (l2 == 2) {
+            slots = kSigCtxMap4;
+            c0 = (uint32_t)cb[0] | ((uint32_t)cb[1] << 8) | ((uint32_t)cb[2] << 16) | ((uint32_t)cb[3] << 24);
+            c1 = (uint32_t)cb[4] | ((uint32_t)cb[5] << 8) | ((uint32_t)cb[6] << 16) | ((uint32_t)cb[7] << 24);
+            c2 = cb[8];
+        } else {
+            off = cidx == 0 ? ((xS | yS) ? 3 : 0) + (l2 == 3 ? (L.rc_scan == 0 ? 9 : 15) : 21) : (l2 == 3 ? 9 : 12);
+            slots = sig_slots(pcs);
+            if ((xS | yS) == 0) slots &= ~0xfull;  // DC of the TB: sigCtx 0
+            c0 = (uint32_t)cb[0] | ((uint32_t)cb[off] << 8) | ((uint32_t)cb[off + 1] << 16) |
+                 ((uint32_t)cb[off + 2] << 24);
+        }
         const uint64_t sw = scan4_word(L.rc_scan);
         for (int nn = nstart; nn >= 0; --nn) {
             if (nn > 0 || !infer_dc) {
                 const int e = (int)((sw >> (4 * nn)) & 15u);
-                const uint64_t t = (e & 8) ? t1 : t0;
-                if (dec(L, G, cbase + (int)((t >> ((e & 7) * 8)) & 0xffu))) {
+                const int slot = (int)((slots >> (4 * e)) & 15u);
+                uint32_t cs = cache_get(c0, c1, c2, slot);
+                const int bin = dec_s(L, G, cs);
+                cache_put(c0, c1, c2, slot, cs);
+                if (bin) {
                     sig |= 1u << nn;
                     infer_dc = false;
                 }
             } else {
                 sig |= 1u;  // inferred DC of a coded sub-block
             }
+        }
+        uint8_t *cw = G.ctx + cbase;
+        if (l2 == 2) {
+            for (int k = 0; k < 4; ++k) cw[k] = (uint8_t)(c0 >> (8 * k));
+            for (int k = 0; k < 4; ++k) cw[4 + k] = (uint8_t)(c1 >> (8 * k));
+            cw[8] = (uint8_t)c2;
+        } else {
+            cw[0] = (uint8_t)c0;
+            cw[off] = (uint8_t)(c0 >> 8);
+            cw[off + 1] = (uint8_t)(c0 >> 16);
+            cw[off + 2] = (uint8_t)(c0 >> 24);
         }
     }
     if (sig) {
@@ -863,13 +943,20 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
         L.fl |= F_ANY_SB;
         int c1 = 1;
         uint32_t g1 = 0, g2 = 0;
+        // the ctxSet's four greater1 contexts (9.3.4.2.6) in one register
+        const int gbase = CTX_GT1 + ctx_set * 4 + (cidx ? 16 : 0);
+        uint32_t gc = (uint32_t)G.ctx[gbase] | ((uint32_t)G.ctx[gbase + 1] << 8) | ((uint32_t)G.ctx[gbase + 2] << 16) |
+                      ((uint32_t)G.ctx[gbase + 3] << 24);
         const int first_sig = 31 - __builtin_clz(sig & (0u - sig));
         const int last_sig = msb32(sig);
         int num_g1 = 0, last_g1 = -1;
         for (uint32_t m = sig; m && num_g1 < 8;) {
             const int nn = msb32(m);
             m &= ~(1u << nn);
-            const int f = dec(L, G, CTX_GT1 + ctx_set * 4 + (c1 < 3 ? c1 : 3) + (cidx ? 16 : 0));
+            const int gs = (c1 < 3 ? c1 : 3) * 8;
+            uint32_t cs = (gc >> gs) & 0xffu;
+            const int f = dec_s(L, G, cs);
+            gc = (gc & ~(0xffu << gs)) | (cs << gs);
             ++num_g1;
             if (f) {
                 g1 |= 1u << nn;
@@ -878,6 +965,7 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
             if (c1 > 0) c1 = f ? 0 : c1 + 1;
         }
         L.rc_prev_c1 = c1;
+        for (int k = 0; k < 4; ++k) G.ctx[gbase + k] = (uint8_t)(gc >> (8 * k));
         if (last_g1 >= 0 && dec(L, G, CTX_GT2 + ctx_set + (cidx ? 4 : 0))) g2 = 1u << last_g1;
         const bool sign_hidden = !(L.fl & F_BYPASS) && (last_sig - first_sig > 3);
         const bool hide = (P.flags & SP_SIGN_HIDING) && sign_hidden;
@@ -902,8 +990,7 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
                     k = k < 4 ? k : 4;
                 }
                 // coeff_abs_level_remaining (decoder.rs:230-261): TR(4 << k, k) prefix, EG(k + 1) escape
-                int p = 0;
-                while (p < 4 && byp(L, G)) ++p;
+                const int p = byp_prefix4(L, G);
                 if (p < 4) {
                     rem = (p << k) + (int)byp_bits(L, G, k);
                 } else {
@@ -941,7 +1028,11 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
             if (v > 32767) v = 32767;
             if (v < -32768) v = -32768;
             if (L.ncoef < P.coef_cap)
+#if defined(HG_XP_NO_COEF_STORE)
+                L.ncoef++, (void)v, (void)xC, (void)yC;  // timing experiment only
+#else
                 P.coef_base[L.coef_row + L.ncoef++] = ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC);
+#endif
             else
                 L.status |= ST_CAPACITY;
             ++num_sig;
@@ -1167,6 +1258,11 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + ppw);
     uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_prog + 64);
     const int lane = threadIdx.x;
+#if defined(HG_PARSE_SETPRIO)
+    // the parse is the latency-critical stream: win issue arbitration against
+    // the reconstruction kernels of the previous decode sharing the SIMD
+    __builtin_amdgcn_s_setprio(HG_PARSE_SETPRIO);
+#endif
     s_tab[lane] = state_row(lane);
     const int pl = lane / a.max_rows, row = lane % a.max_rows;
     const int pic = a.pic0 + blockIdx.x * ppw + pl;

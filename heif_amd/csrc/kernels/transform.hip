@@ -9,10 +9,12 @@
 // Mapping: every coded TB is independent, so this stage runs at full chip
 // parallelism: one 256-thread workgroup per CTB row of a picture, each wave
 // taking every 4th TB of the row's TU list.  Coefficients arrive sparse
-// (value, raster position) and are scattered into a per-wave LDS tile; the
-// row pass only spans rows up to the last nonzero coefficient row.  Integer
-// butterflies on VALU — no MFMA (the products are exact int32, and TBs are
-// at most 32x32).
+// (value, raster position) and are scattered into a per-wave int16 LDS tile
+// (17 KiB per workgroup, so blocks fit beside the next decode's k_parse
+// waves); the first stage only runs over the nonzero columns and rows, the
+// second only over the nonzero first-stage columns, and a DC-only TB is a
+// fill.  Integer sums on VALU with the DCT matrix in LDS — no MFMA (the
+// products are exact int32, and TBs are at most 32x32).
 #include "kernels.hpp"
 
 namespace hg {
@@ -58,8 +60,17 @@ __device__ __forceinline__ int clip16(int64_t v) { return v < -32768 ? -32768 : 
 }  // namespace
 
 __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
-    HG_BLOCK_SHARED int32_t tile[kWaves][2][32 * 32];
-    HG_BLOCK_SHARED int32_t maxrow[kWaves];
+    // per wave: the scaled coefficients d and the first-stage output g, both
+    // clipped to 16 bits by 8.6.2 / 8.6.4.2, so int16 tiles (4 KiB per wave);
+    // the 32x32 DCT matrix in LDS (lane-varying rows: LDS, not constant loads)
+    HG_BLOCK_SHARED int16_t tile[kWaves][2][32 * 32];
+    HG_BLOCK_SHARED int32_t extent[kWaves][2];  // last nonzero row / column of d
+    HG_BLOCK_SHARED int8_t s_tm[32 * 32];
+    HG_BLOCK_SHARED int8_t s_dst[16];
+    // every wave fills the tables (same values; the host emulation runs one lane per wave)
+    for (int i = (int)(threadIdx.x & 63); i < 32 * 32; i += kWave) s_tm[i] = c_tm.m[i >> 5][i & 31];
+    for (int i = (int)(threadIdx.x & 63); i < 16; i += kWave) s_dst[i] = c_dst[i >> 2][i & 3];
+    __syncthreads();
     const int pic = a.pic0 + blockIdx.y, row = blockIdx.x;
     const PicDesc pd = a.pics[pic];
     const SeqParams sp = a.seqs[pd.seq];
@@ -75,8 +86,8 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                              a.resid + pd.resid_off + (size_t)W * H + (size_t)cw * ch};
     const int pitch[3] = {W, cw, cw};
     const bool scaling = (sp.flags & SP_SCALING_LIST) != 0;
-    int32_t *d = tile[wave][0];
-    int32_t *g = tile[wave][1];
+    int16_t *d = tile[wave][0];
+    int16_t *g = tile[wave][1];
 
     for (uint32_t t = wave; t < ntu; t += kWaves) {
         const TuRec tu = tus[t];
@@ -87,8 +98,8 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
         const bool bypass = (tu.flags & TU_BYPASS) != 0, ts = (tu.flags & TU_TSKIP) != 0;
         // 1. zero the tile, scatter d[y][x] (scaled unless bypass)
-        for (int i = lane; i < n * n; i += kWave) d[i] = 0;
-        if (lane == 0) maxrow[wave] = 0;
+        for (int i = lane; i < n * n / 2; i += kWave) reinterpret_cast<int32_t *>(d)[i] = 0;
+        if (lane == 0) extent[wave][0] = extent[wave][1] = 0;
         wave_sync();
         const int qp = tu.qp;
         const int bd_shift = bd + log2n - 5;
@@ -96,7 +107,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         const int ls = c_level_scale[qp % 6] << (qp / 6);
         const bool use_m = scaling && !(ts && n > 4);
         const uint8_t *mtab = a.sf + sp.sf_off + sf_size_offset(log2n - 2) + (uint32_t)cidx * (uint32_t)(n * n);
-        int my_max = 0;
+        int my_row = 0, my_col = 0;
         for (int k = lane; k < tu.ncoef; k += kWave) {
             const Coef c = coefs[tu.coef + k];
             const int pos = (int)(c & 0xffffu) & (n * n - 1);
@@ -108,12 +119,14 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                 const int m = use_m ? mtab[pos] : 16;
                 dv = clip16(((int64_t)v * m * ls + rnd) >> bd_shift);
             }
-            d[pos] = dv;
-            my_max = max(my_max, pos >> log2n);
+            d[pos] = (int16_t)dv;
+            my_row = max(my_row, pos >> log2n);
+            my_col = max(my_col, pos & (n - 1));
         }
-        if (my_max) atomicMax(&maxrow[wave], my_max);
+        if (my_row) atomicMax(&extent[wave][0], my_row);
+        if (my_col) atomicMax(&extent[wave][1], my_col);
         wave_sync();
-        const int rows = maxrow[wave] + 1;  // rows of d beyond this are zero
+        const int rows = extent[wave][0] + 1, cols = extent[wave][1] + 1;  // d is zero beyond these
         const int bd2 = 20 - bd;
         int16_t *dst = res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x;
         if (bypass || ts) {
@@ -129,26 +142,35 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         }
         const bool dst_tr = (tu.flags & TU_DST) != 0;
         const int kstep = 32 >> log2n;
-        // 2. vertical (column) pass: e[y][x] = sum_j M[j][y] d[j][x]; g = clip16((e + 64) >> 7)
-        for (int o = lane; o < n * n; o += kWave) {
-            const int y = o >> log2n, x = o & (n - 1);
+        if (!dst_tr && rows == 1 && cols == 1) {
+            // DC only: both stages are constant (transMatrix[0][*] = 64)
+            const int g0 = clip16(((int64_t)64 * d[0] + 64) >> 7);
+            const int16_t r = (int16_t)clip16(((int64_t)64 * g0 + (1 << (bd2 - 1))) >> bd2);
+            for (int i = lane; i < n * n; i += kWave) dst[(i >> log2n) * pitch[cidx] + (i & (n - 1))] = r;
+            wave_sync();
+            continue;
+        }
+        // 2. vertical (column) pass over the nonzero columns:
+        //    e[y][x] = sum_{j < rows} M[j][y] d[j][x]; g = clip16((e + 64) >> 7)
+        for (int o = lane; o < n * cols; o += kWave) {
+            const int y = o / cols, x = o - y * cols;
             int32_t s = 0;
             if (dst_tr) {
-                for (int j = 0; j < rows; ++j) s += (int32_t)c_dst[j][y] * d[j * n + x];
+                for (int j = 0; j < rows; ++j) s += (int32_t)s_dst[j * 4 + y] * d[j * n + x];
             } else {
-                for (int j = 0; j < rows; ++j) s += (int32_t)c_tm.m[j * kstep][y] * d[j * n + x];
+                for (int j = 0; j < rows; ++j) s += (int32_t)s_tm[(j * kstep) * 32 + y] * d[j * n + x];
             }
-            g[o] = clip16(((int64_t)s + 64) >> 7);
+            g[y * n + x] = (int16_t)clip16(((int64_t)s + 64) >> 7);
         }
         wave_sync();
-        // 3. horizontal (row) pass: r[y][x] = sum_j M[j][x] g[y][j]; (r + rnd) >> (20 - bitDepth)
+        // 3. horizontal (row) pass: r[y][x] = sum_{j < cols} M[j][x] g[y][j]; (r + rnd) >> (20 - bitDepth)
         for (int o = lane; o < n * n; o += kWave) {
             const int y = o >> log2n, x = o & (n - 1);
             int64_t s = 0;
             if (dst_tr) {
-                for (int j = 0; j < n; ++j) s += (int32_t)c_dst[j][x] * g[y * n + j];
+                for (int j = 0; j < cols; ++j) s += (int32_t)s_dst[j * 4 + x] * g[y * n + j];
             } else {
-                for (int j = 0; j < n; ++j) s += (int32_t)c_tm.m[j * kstep][x] * g[y * n + j];
+                for (int j = 0; j < cols; ++j) s += (int32_t)s_tm[(j * kstep) * 32 + x] * g[y * n + j];
             }
             dst[y * pitch[cidx] + x] = (int16_t)clip16((s + (1 << (bd2 - 1))) >> bd2);
         }

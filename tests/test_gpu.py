@@ -165,3 +165,24 @@ def test_native_library_is_loaded(H):
 
     maps = pathlib.Path("/proc/self/maps").read_text()
     assert "libheifgpu" in maps
+
+
+def test_pipelined_decodes_back_to_back(H, ctx, oracle_tiles, halfmoonbay):
+    """Several decodes of one batch issued without synchronisation: the parse of
+    call n+1 overlaps the reconstruction of call n (alternate parse sets), and
+    every call's planes must still be exact."""
+    from heif_amd.synthetic import permutation, permuted_heic
+
+    seeds = [7, 8]
+    imgs = [H.HeifImage.parse(permuted_heic(halfmoonbay, s)) for s in seeds]
+    b = ctx.prepare(imgs)
+    outs = [ctx.alloc_outputs(imgs) for _ in range(4)]
+    for o in outs:
+        b.decode_async(o)
+    assert b.status() == [0, 0]
+    for o in outs:
+        for s, oi in zip(seeds, o):
+            want = assemble(oracle_tiles, permutation(48, s))
+            for got, w in zip(planes_np(oi), want):
+                assert np.array_equal(got, w), s
+    b.free()

@@ -6,6 +6,7 @@ V=$1
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 LIB=$R/heif_amd/libheifgpu${V:+_$V}.so
 cd /tmp && export TMPDIR=/tmp
+mkdir -p "$R/gpurun_out/pmc_$V"
 for set in "SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES SQ_INSTS_SMEM SQ_BUSY_CU_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS"; do
     tag=$(echo $set | cut -c1-12 | tr ' ' '_')
