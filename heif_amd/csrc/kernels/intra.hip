@@ -42,6 +42,7 @@ struct alignas(16) IntraScratch {
     int16_t ft[132];
     int16_t ref[200];   // angular reference, index + 64
     int32_t dc;
+    uint32_t done[8];   // decoded 4x4 luma blocks of the current CTU (up to 64x64), row-major
 };
 
 // Per-wave LDS block: scratch, then per component the CTU window.
@@ -87,12 +88,21 @@ int intra_waves(int log2ctb, int chroma, int bps, int max_rows) {
 
 #define wave_sync() HG_WAVE_SYNC()
 
-// 6.4.1 MinTbAddrZs for a luma location
-__device__ __forceinline__ int zscan(int xl, int yl, int log2ctb, int min_tb, int wctb) {
-    const int tbx = xl >> min_tb, tby = yl >> min_tb, sh = log2ctb - min_tb;
-    int v = ((tbx >> sh) + (tby >> sh) * wctb) << (2 * sh);
-    for (int i = 0; i < sh; ++i) v |= (((tbx >> i) & 1) << (2 * i)) | (((tby >> i) & 1) << (2 * i + 1));
-    return v;
+
+// 6.4.1 availability of a neighbouring luma location (xl, yl) for a TB of the
+// CTU at luma (bx0, by0), size csl.  Everything in the CTU row above (up to the
+// above-right CTU, which the wavefront has finished) and in the CTU to the
+// left is decoded; the CTUs below-left and right are not; inside the CTU a
+// block is available iff it precedes the TB in z-scan order, i.e. iff it is
+// already decoded (TBs are reconstructed in decoding order), which the
+// `done` bitmap records.  Replaces the MinTbAddrZs comparison per sample.
+__device__ __forceinline__ bool nb_avail(const uint32_t *done, int xl, int yl, int bx0, int by0, int csl) {
+    const int lx = xl - bx0, ly = yl - by0;
+    if (ly < 0) return true;
+    if (ly >= csl || lx >= csl) return false;
+    if (lx < 0) return true;
+    const int idx = (ly >> 2) * (csl >> 2) + (lx >> 2);
+    return (done[idx >> 5] >> (idx & 31)) & 1u;
 }
 
 // One component's CTU window in LDS.
@@ -119,7 +129,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     const int log2n = tu.log2, n = 1 << log2n, mode = tu.mode;
     const int x0 = tu.x, y0 = tu.y;
     const int sub = cidx ? 1 : 0;  // 4:2:0 chroma → luma = 2x
-    const int zcur = zscan(x0 << sub, y0 << sub, log2ctb, min_tb, wctb);
+    const int bx0 = w.cx0 << sub, by0 = w.cy0 << sub, csl = w.cs << sub;
     const int ns = 4 * n + 1;
     // 1. gather neighbours in search order (8.4.4.2.2): s < 2n left column bottom-up,
     //    s == 2n corner, s > 2n top row left-to-right
@@ -140,8 +150,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
                 xn = x0 + s - 2 * n - 1;
                 yn = y0 - 1;
             }
-            sa[s] = xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
-                    zscan(xn << sub, yn << sub, log2ctb, min_tb, wctb) <= zcur;
+            sa[s] = xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(L->done, xn << sub, yn << sub, bx0, by0, csl);
             sv[s] = sa[s] ? w.fetch(xn, yn) : 0;
             any_av |= sa[s];
         }
@@ -160,6 +169,38 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         }
     }
 #else
+    if (ns <= 64) {  // 4x4 and 8x8 TBs (most of them): one chunk of 4n + 1 <= 33 samples
+        const int s = lane;
+        int xn, yn;
+        if (s < 2 * n) {
+            xn = x0 - 1;
+            yn = y0 + 2 * n - 1 - s;
+        } else if (s == 2 * n) {
+            xn = x0 - 1;
+            yn = y0 - 1;
+        } else {
+            xn = x0 + s - 2 * n - 1;
+            yn = y0 - 1;
+        }
+        const bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
+                        nb_avail(L->done, xn << sub, yn << sub, bx0, by0, csl);
+        const int val = av ? w.fetch(xn, yn) : 0;
+        const uint64_t msk = __ballot(av);
+        int sl = lane;
+        if (!av && msk) {
+            const uint64_t below = msk & ((1ull << lane) - 1ull);
+            sl = below ? 63 - __clzll(below) : __ffsll((unsigned long long)msk) - 1;
+        }
+        const int sv = __shfl(val, sl, 64);
+        const int v = msk ? sv : (1 << (bd - 1));
+        if (s < 2 * n) L->left[2 * n - s] = (int16_t)v;
+        else if (s == 2 * n) {
+            L->left[0] = (int16_t)v;
+            L->top[0] = (int16_t)v;
+        } else if (s < ns) {
+            L->top[s - 2 * n] = (int16_t)v;
+        }
+    } else {
     int val[3];
     uint64_t msk[3];
     for (int k = 0; k < 3; ++k) {
@@ -175,8 +216,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             xn = x0 + s - 2 * n - 1;
             yn = y0 - 1;
         }
-        bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
-                  zscan(xn << sub, yn << sub, log2ctb, min_tb, wctb) <= zcur;
+        bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(L->done, xn << sub, yn << sub, bx0, by0, csl);
         val[k] = av ? w.fetch(xn, yn) : 0;
         msk[k] = __ballot(av);
     }
@@ -216,6 +256,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         } else if (s < ns) {
             L->top[s - 2 * n] = (int16_t)v;
         }
+    }
     }
 #endif
     wave_sync();
@@ -363,11 +404,29 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
         const uint32_t ntu = a.row_counts[2 * (pd.row_off + r)];
         const TuRec *tus = a.tus + pd.tu_off + (uint64_t)r * pd.tu_cap_row;
         int cur = -1;
+#if !defined(HG_HOST_EMU)
+        uint4 tblk = make_uint4(0, 0, 0, 0);  // lane l: TuRec t0 + l (one coalesced load per 64 TBs)
+        uint32_t t0 = 0;
+#endif
         for (uint32_t t = 0; t <= ntu; ++t) {
             TuRec tu{};
             int c = wctb;  // sentinel after the last TB: finish the open CTU
             if (t < ntu) {
+#if defined(HG_HOST_EMU)
                 tu = tus[t];
+#else
+                if ((t & 63u) == 0) {
+                    t0 = t;
+                    const uint32_t i = t + (uint32_t)lane;
+                    tblk = i < ntu ? *reinterpret_cast<const uint4 *>(tus + i) : make_uint4(0, 0, 0, 0);
+                }
+                const int sel = (int)(t - t0);
+                const uint4 r = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)tblk.x, sel),
+                                           (uint32_t)__builtin_amdgcn_readlane((int)tblk.y, sel),
+                                           (uint32_t)__builtin_amdgcn_readlane((int)tblk.z, sel),
+                                           (uint32_t)__builtin_amdgcn_readlane((int)tblk.w, sel));
+                __builtin_memcpy(&tu, &r, sizeof(tu));
+#endif
                 c = (int)HG_UNI((uint32_t)tu.ctu);
             }
             if (c != cur) {
@@ -417,6 +476,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
                         w.res[y * w.cs + x] = resp[k][(size_t)(w.cy0 + y) * PW + w.cx0 + x];
                     }
                 }
+                for (int i = lane; i < 8; i += kWave) S->done[i] = 0u;
                 wave_sync();
             }
             const int cidx = tu.flags & TU_CIDX_MASK;
@@ -430,6 +490,15 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
                 continue;
             predict_tb<Pel>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, log2ctb,
                             sp.log2_min_tb, wctb, lane);
+            if (cidx == 0) {  // the TB's 4x4 blocks are decoded now (a row segment never crosses a word)
+                const int nb = 1 << (tu.log2 - 2), stride = w.cs >> 2;
+                const int bx = (tu.x - w.cx0) >> 2, by = (tu.y - w.cy0) >> 2;
+                for (int i = lane; i < nb; i += kWave) {
+                    const int idx = (by + i) * stride + bx;
+                    atomicOr(&S->done[idx >> 5], ((1u << nb) - 1u) << (idx & 31));
+                }
+                wave_sync();
+            }
         }
         HG_FENCE_REL();
         hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
