@@ -511,13 +511,15 @@ static int intra_launch_waves(const BatchArgs &a) {
     // waves per picture (tuning: fewer waves = more pictures per CU).
     // Measured (128 x 48 tiles): 16 waves/picture 142 ms, 8: 71, 4: 48, 1: 61 —
     // many pictures per CU beat deep per-picture row parallelism, so waves per
-    // picture shrink as the batch grows (floor 4).
+    // picture shrink as the batch grows.  Floor 2: alone 4 and 2 waves tie
+    // (~40 ms), but beside the next decode's k_parse (pipelined) the smaller
+    // workgroup fits the LDS that k_parse leaves free (bench 12.0 -> 12.5-13.0 Gpix/s).
     static const int forced = [] {
         const char *e = std::getenv("HEIFGPU_INTRA_WAVES");
         return e ? std::atoi(e) : 0;
     }();
     int cap = forced > 0 ? forced : kResidentIntraWaves / (a.n_pics > 0 ? a.n_pics : 1);
-    if (forced <= 0) cap = cap < 4 ? 4 : cap;
+    if (forced <= 0) cap = cap < 2 ? 2 : cap;
     const int nw = intra_waves(a.max_log2ctb, 1, a.bytes_per_sample, a.max_rows);
     return cap < nw ? cap : nw;
 }

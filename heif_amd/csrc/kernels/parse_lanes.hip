@@ -180,6 +180,20 @@ __device__ __forceinline__ void store_tu(TuRec *d, uint32_t x, uint32_t y, uint3
 }
 #endif
 
+// n (1..8) bytes of v at p: one store when n is 2, 4 or 8 and p is n-aligned
+HG_HD inline void store_bytes(uint8_t *p, int n, uint64_t v) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    if (n == 8 && !(a & 7)) {
+        *reinterpret_cast<uint64_t *>(p) = v;
+    } else if (n == 4 && !(a & 3)) {
+        *reinterpret_cast<uint32_t *>(p) = (uint32_t)v;
+    } else if (n == 2 && !(a & 1)) {
+        *reinterpret_cast<uint16_t *>(p) = (uint16_t)v;
+    } else {
+        for (int i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * i));
+    }
+}
+
 HG_HD inline uint8_t load_byte_coherent(const uint8_t *p) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     const uint32_t w = load_word_coherent(reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3)));
@@ -469,6 +483,11 @@ HG_HD inline void row_outputs(Lane &L, const LanePic &P) {
     L.ntu = L.ncoef = 0;
 }
 
+// one coefficient, one 4-byte store.  (Grouping four into a 16-byte store
+// through registers measured 5 % slower: the selects run on every lane of
+// every coefficient step, the saved stores were cheap.)
+HG_HD inline void coef_push(Lane &L, const LanePic &P, uint32_t w) { P.coef_base[L.coef_row + L.ncoef++] = w; }
+
 // ------------------------------------------------------------------ units
 // U_CTU: CTU start (7.3.8.2) and sao() (7.3.8.3).  Returns without a state
 // change while the row above is less than two CTUs ahead (WPP).
@@ -682,11 +701,12 @@ HG_HD inline void unit_tt(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
     {  // edge / no-filter flags of every 4x4 luma block of the TB (MF_*)
         const int nb = 1 << (L.tl - 2), gx0 = L.tx >> 2, gy0 = L.ty >> 2;
         const int wx = gx0 + nb <= P.w4 ? nb : P.w4 - gx0, hy = gy0 + nb <= P.h4 ? nb : P.h4 - gy0;
-        const uint8_t nf = (L.fl & F_BYPASS) ? MF_NOFILT : 0;
+        const uint64_t nf = (L.fl & F_BYPASS) ? MF_NOFILT : 0;
+        const uint64_t rep = 0x0101010101010101ull;
         for (int y = 0; y < hy; ++y) {
             uint8_t *row = P.gflags + (size_t)(gy0 + y) * P.w4 + gx0;
-            const uint8_t h = (uint8_t)((y == 0 ? MF_EDGE_H : 0) | nf);
-            for (int x = 0; x < wx; ++x) row[x] = (uint8_t)(h | (x == 0 ? MF_EDGE_V : 0));
+            const uint64_t h = (y == 0 ? (uint64_t)MF_EDGE_H : 0u) | nf;
+            store_bytes(row, wx, (rep * h) | (uint64_t)MF_EDGE_V);
         }
     }
     const int blk = L.td == 0 ? 0 : (((L.tx >> L.tl) & 1) | (((L.ty >> L.tl) & 1) << 1));
@@ -756,7 +776,7 @@ HG_HD inline void tb_done(Lane &L, LaneLds &ld, LanePic &P) {
         const int wx = gx0 + nb <= P.w4 ? nb : P.w4 - gx0, hy = gy0 + nb <= P.h4 ? nb : P.h4 - gy0;
         for (int y = 0; y < hy; ++y) {
             int8_t *row = P.gqpy + (size_t)(gy0 + y) * P.w4 + gx0;
-            for (int x = 0; x < wx; ++x) row[x] = (int8_t)L.qpy_cur;
+            store_bytes(reinterpret_cast<uint8_t *>(row), wx, 0x0101010101010101ull * (uint8_t)L.qpy_cur);
         }
         L.qp_prev_last = L.qpy_cur;
     }
@@ -994,6 +1014,8 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
                 if (p < 4) {
                     rem = (p << k) + (int)byp_bits(L, G, k);
                 } else {
+                    // EG(k + 1) prefix, one bin per step (measured faster here than
+                    // 8-bin divisions: the loop is short and rarely taken by many lanes)
                     int ones = 0;
                     bool bad = false;
                     while (byp(L, G)) {
@@ -1028,11 +1050,7 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
             if (v > 32767) v = 32767;
             if (v < -32768) v = -32768;
             if (L.ncoef < P.coef_cap)
-#if defined(HG_XP_NO_COEF_STORE)
-                L.ncoef++, (void)v, (void)xC, (void)yC;  // timing experiment only
-#else
-                P.coef_base[L.coef_row + L.ncoef++] = ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC);
-#endif
+                coef_push(L, P, ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC));
             else
                 L.status |= ST_CAPACITY;
             ++num_sig;
