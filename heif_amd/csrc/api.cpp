@@ -96,7 +96,7 @@ struct heifgpu_batch {
     BatchArgs args{};
     DevBuf<uint8_t> bits, rbsp, sf, recon;
     DevBuf<PicDesc> pics;
-    DevBuf<uint32_t> subs, rsubs;
+    DevBuf<uint32_t> subs, rsubs, porder;
     DevBuf<SeqParams> seqs;
     DevBuf<OutImage> outs;
     DevBuf<int16_t> resid;
@@ -281,12 +281,17 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
     HIP_TRY(hipMemcpy(b->seqs.p, h_seqs.data(), h_seqs.size() * sizeof(SeqParams), hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b->sf.p, h_sf.data(), h_sf.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemset(b->rbsp.p, 0, h_bits.size()));
+    std::vector<uint32_t> order;
+    lanes_parse_order(h_pics.data(), int(h_pics.size()), max_rows, order);
+    HIP_TRY(b->porder.alloc(order.size()));
+    HIP_TRY(hipMemcpy(b->porder.p, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     BatchArgs &a = b->args;
     a.bits = b->bits.p;
     a.pics = b->pics.p;
     a.subs = b->subs.p;
     a.rbsp = b->rbsp.p;
     a.rsubs = b->rsubs.p;
+    a.parse_order = b->porder.p;
     a.seqs = b->seqs.p;
     a.sf = b->sf.p;
     a.outs = b->outs.p;

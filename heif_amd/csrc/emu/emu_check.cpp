@@ -54,6 +54,9 @@ int main(int argc, char **argv) {
     std::vector<uint32_t> rsubs(hb.subs.size(), 0);
     a.rbsp = rbsp.data();
     a.rsubs = rsubs.data();
+    std::vector<uint32_t> order;
+    lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.max_rows, order);
+    a.parse_order = order.data();
     a.seqs = hb.seqs.data();
     a.sf = hb.sf.data();
     a.outs = &out;

@@ -71,8 +71,9 @@ WinLayout win_layout(int log2ctb, int chroma, int bps) {
         o += (uint32_t)(cs * bps + 15) & ~15u;
         L.above[k] = o;
         o += (uint32_t)((2 * cs + 1) * bps + 15) & ~15u;
-        L.res[k] = o;
-        o += (uint32_t)(cs * cs * 2 + 15) & ~15u;
+        // residuals are read from the k_transform planes, not staged here: half
+        // the block, so twice the workgroups fit beside the next decode's k_parse
+        L.res[k] = 0;
     }
     L.bytes = o;
     return L;
@@ -109,8 +110,8 @@ __device__ __forceinline__ bool nb_avail(const uint32_t *done, int xl, int yl, i
 template <typename Pel>
 struct Win {
     Pel *cur, *left, *above;
-    int16_t *res;
-    int cs, cx0, cy0;  // CTB size and origin in component samples
+    const int16_t *res;  // the component's residual plane (k_transform), pitch = plane width
+    int cs, cx0, cy0;    // CTB size and origin in component samples
     // a decoded neighbour (xn, yn) in picture coordinates; only called for
     // available samples, which lie in the row above, the column to the left
     // or the current CTU
@@ -131,6 +132,10 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     const int sub = cidx ? 1 : 0;  // 4:2:0 chroma → luma = 2x
     const int bx0 = w.cx0 << sub, by0 = w.cy0 << sub, csl = w.cs << sub;
     const int ns = 4 * n + 1;
+    const bool cbf = (tu.flags & TU_CBF) != 0;
+    // residual of a 4x4 / 8x8 TB (one sample per lane): loaded now, used after
+    // the neighbour and filter phases, so the load latency hides behind them
+    const int r0 = (cbf && n <= 8 && lane < n * n) ? w.res[(size_t)(y0 + (lane >> log2n)) * PW + x0 + (lane & (n - 1))] : 0;
     // 1. gather neighbours in search order (8.4.4.2.2): s < 2n left column bottom-up,
     //    s == 2n corner, s > 2n top row left-to-right
 #if defined(HG_HOST_EMU)
@@ -351,7 +356,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             }
         }
         const int li = (ly0 + y) * w.cs + lx0 + x;
-        if (tu.flags & TU_CBF) pv += w.res[li];
+        if (cbf) pv += (n <= 8 && o == lane) ? r0 : w.res[(size_t)(y0 + y) * PW + x0 + x];
         pv = min(max(pv, 0), maxv);
         w.cur[li] = (Pel)pv;
     }
@@ -393,7 +398,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
         win[k].cur = reinterpret_cast<Pel *>(blk + lay.cur[k]);
         win[k].left = reinterpret_cast<Pel *>(blk + lay.left[k]);
         win[k].above = reinterpret_cast<Pel *>(blk + lay.above[k]);
-        win[k].res = reinterpret_cast<int16_t *>(blk + lay.res[k]);
+        win[k].res = resp[k];
         win[k].cs = lay.cs[k];
     }
     progress[wave] = 0;  // every lane writes the same value
@@ -470,11 +475,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
                         const int xg = w.cx0 - 1 + i;
                         w.above[i] = (yg >= 0 && xg >= 0 && xg < PW) ? planes[k][(size_t)yg * PW + xg] : (Pel)0;
                     }
-                    const int vw = min(w.cs, PW - w.cx0), vh = min(w.cs, PH - w.cy0);
-                    for (int o = lane; o < vw * vh; o += kWave) {
-                        const int x = o % vw, y = o / vw;
-                        w.res[y * w.cs + x] = resp[k][(size_t)(w.cy0 + y) * PW + w.cx0 + x];
-                    }
+                    (void)PH;
                 }
                 for (int i = lane; i < 8; i += kWave) S->done[i] = 0u;
                 wave_sync();

@@ -12,11 +12,11 @@
 #include "../common/desc.hpp"
 #include "wave.hpp"
 #include <cstdlib>
+#include <vector>
 
 #if defined(HG_HOST_EMU)
 #include <atomic>
 #include <thread>
-#include <vector>
 #endif
 
 namespace hg {
@@ -27,6 +27,7 @@ struct BatchArgs {
     const uint32_t *subs;      // substream raw start offsets (n_sub + 1 per picture, last = len)
     uint8_t *rbsp;             // k_rbsp: NAL payloads with emulation prevention removed (same offsets as bits)
     uint32_t *rsubs;           // k_rbsp: substream start offsets into rbsp (last = RBSP length)
+    const uint32_t *parse_order;  // k_parse_lanes: picture (minus pic0) of wave slot i; null = identity
     const SeqParams *seqs;
     const uint8_t *sf;         // ScalingFactor blocks
     const OutImage *outs;
@@ -74,6 +75,8 @@ size_t parse_group_bytes(int max_width, int max_wctb, int group) {
 // k_parse_lanes (parse_lanes.hip): one substream per lane; the default (HEIFGPU_PARSE=scalar selects k_parse)
 bool parse_lanes_supported(const BatchArgs &a);
 bool parse_lanes_selected(const BatchArgs &a);
+// host: BatchArgs::parse_order for a batch (size-balanced waves)
+void lanes_parse_order(const PicDesc *pics, int n, int max_rows, std::vector<uint32_t> &order);
 
 #if defined(HG_HOST_EMU)
 // Runs kernel(a) over a gx * gy grid, one block at a time, with `waves` host

@@ -30,6 +30,10 @@
 #include "kernels.hpp"
 #include "tables.hpp"
 
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
 #if defined(HG_HOST_EMU)
 #include <cstdio>
 #endif
@@ -1206,6 +1210,37 @@ bool parse_lanes_selected(const BatchArgs &a) {
     return mode == 1 && parse_lanes_supported(a);
 }
 
+// Wave slot -> picture.  A wave runs until its heaviest picture is parsed,
+// and every extra busy picture in it adds divergent units to each pass, so
+// the critical path is the wave holding the most work.  Pictures are sorted
+// by payload size and dealt snake-wise (wave w of W gets ranks w, 2W-1-w,
+// 2W+w, 4W-1-w, ...): the heaviest pictures share a wave with the lightest.
+// HEIFGPU_PARSE_ORDER=0: batch order.
+void lanes_parse_order(const PicDesc *pics, int n, int max_rows, std::vector<uint32_t> &order) {
+    static const int on = [] {
+        const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
+        return e ? std::atoi(e) : 1;
+    }();
+    order.resize((size_t)n);
+    for (int i = 0; i < n; ++i) order[(size_t)i] = (uint32_t)i;
+    if (!on || n <= 0) return;
+    const int ppw = lanes_pics_per_wave(max_rows);
+    const int W = (n + ppw - 1) / ppw;
+    std::vector<uint32_t> by_size(order);
+    std::stable_sort(by_size.begin(), by_size.end(),
+                     [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
+    std::vector<uint32_t> slots((size_t)W * ppw, UINT32_MAX);
+    for (int r = 0; r < n; ++r) {
+        const int band = r / W, pos = r % W;
+        const int w = (band & 1) ? W - 1 - pos : pos;
+        slots[(size_t)w * ppw + band] = by_size[(size_t)r];
+    }
+    // the last wave may be short: pack the slots so that slot < n holds a picture
+    int k = 0;
+    for (uint32_t s : slots)
+        if (s != UINT32_MAX) order[(size_t)k++] = s;
+}
+
 #if defined(HG_HOST_EMU)
 // one wave at a time, one unit per live lane per pass, lanes in order
 void emu_parse_lanes(const BatchArgs &a) {
@@ -1222,9 +1257,10 @@ void emu_parse_lanes(const BatchArgs &a) {
         for (int l = 0; l < 64; ++l) {
             prog[l] = 0;
             const int pl = l / a.max_rows, row = l % a.max_rows;
-            const int pic = a.pic0 + w * ppw + pl;
-            const bool live =
-                pl < ppw && pic < a.pic0 + a.n_pics && lane_init(lanes[l], pics[pl], lds[l], a, pic, row);
+            const int slot = w * ppw + pl;
+            const bool in = pl < ppw && slot < a.n_pics;
+            const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
+            const bool live = in && lane_init(lanes[l], pics[pl], lds[l], a, pic, row);
             if (!live) lanes[l].st = U_DONE;
         }
         Env E{&a, lds.data(), prog, 0};
@@ -1283,12 +1319,14 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
 #endif
     s_tab[lane] = state_row(lane);
     const int pl = lane / a.max_rows, row = lane % a.max_rows;
-    const int pic = a.pic0 + blockIdx.x * ppw + pl;
+    const int slot = (int)blockIdx.x * ppw + pl;
+    const bool in = pl < ppw && slot < a.n_pics;
+    const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
     Lane L;
     LaneLds &ld = s_lds[lane < nl ? lane : 0];
     LanePic &P = s_pic[pl < ppw ? pl : 0];
     s_prog[lane] = 0;
-    const bool live = pl < ppw && pic < a.pic0 + a.n_pics && lane_init(L, P, ld, a, pic, row);
+    const bool live = in && lane_init(L, P, ld, a, pic, row);
     if (!live) L.st = U_DONE;
     __syncthreads();
     const Env E{&a, s_lds, s_prog, lane};
