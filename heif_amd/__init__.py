@@ -58,9 +58,11 @@ class HeifImage:
         self._h = ctypes.c_void_p(handle)
 
     @classmethod
-    def parse(cls, data: bytes) -> "HeifImage":
+    def parse(cls, data: bytes, item_id: int = 0) -> "HeifImage":
+        """The primary image (item_id 0), or any coded image item, e.g. the
+        auxiliary HDR gain map at `HeifImage.parse(d).info.aux_item_id`."""
         h = ctypes.c_void_p()
-        _lib.check(lib.heifgpu_image_parse(_lib.u8buf(data), len(data), ctypes.byref(h)))
+        _lib.check(lib.heifgpu_image_parse_item(_lib.u8buf(data), len(data), item_id, ctypes.byref(h)))
         return cls(h.value)
 
     @property
@@ -155,9 +157,25 @@ class DecodeContext:
         return int(lib.heifgpu_last_chunks(self._h))
 
     def stage_times(self) -> List[float]:
+        """ms of the last timed decode: parse, transform, intra, deblock, sao_out, rbsp."""
         ms = (ctypes.c_float * 6)()
         _lib.check(lib.heifgpu_stage_times(self._h, ms))
         return list(ms)
+
+    def to_rgb(self, img: DecodedImage, stream: Optional[int] = None):
+        """Interleaved 8-bit RGB (H', W', 3) with the irot rotation applied
+        (heifgpu_ycbcr_to_rgb), as a torch tensor on the device."""
+        torch = self._torch
+        inf = img.info
+        rot = inf.rotation & 3
+        ow, oh = (inf.height, inf.width) if rot & 1 else (inf.width, inf.height)
+        rgb = torch.empty((oh, ow, 3), dtype=torch.uint8, device=torch.device("cuda", self.device))
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        planes = DecodeContext.planes_of([img])
+        _lib.check(lib.heifgpu_ycbcr_to_rgb(self._h, ctypes.byref(inf), planes, ctypes.c_void_p(rgb.data_ptr()),
+                                            rgb.stride(0), ctypes.c_void_p(stream)))
+        return rgb
 
 
 class DeviceBatch:
@@ -201,11 +219,21 @@ class HeicDecoder:
     _ctx: dict = {}
 
     @classmethod
-    def decode(cls, data: bytes, device: int = 0) -> DecodedImage:
+    def context(cls, device: int = 0) -> DecodeContext:
         ctx = cls._ctx.get(device)
         if ctx is None:
             ctx = cls._ctx[device] = DecodeContext(device)
-        img = HeifImage.parse(data)
+        return ctx
+
+    @classmethod
+    def decode_rgb(cls, data: bytes, device: int = 0, item_id: int = 0):
+        """decode() then YCbCr -> RGB8 with the irot rotation (libheif's default output)."""
+        return cls.context(device).to_rgb(cls.decode(data, device, item_id))
+
+    @classmethod
+    def decode(cls, data: bytes, device: int = 0, item_id: int = 0) -> DecodedImage:
+        ctx = cls.context(device)
+        img = HeifImage.parse(data, item_id)
         outs = ctx.alloc_outputs([img])
         batch = ctx.prepare([img])
         try:

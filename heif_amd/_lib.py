@@ -38,7 +38,7 @@ class ImageInfo(ctypes.Structure):
             "width", "height", "chroma_format_idc", "bit_depth", "bytes_per_sample", "grid_rows",
             "grid_cols", "tile_width", "tile_height", "num_tiles", "rotation", "ispe_width",
             "ispe_height", "coded_bytes", "primary_item_id", "num_thumbnails", "matrix_coeffs",
-            "full_range",
+            "full_range", "item_id", "aux_item_id",
         )
     ]
 
@@ -116,6 +116,7 @@ EXPORTS = (
     "heifgpu_decode_batch", "heifgpu_remove_emulation_prevention", "heifgpu_read_ue",
     "heifgpu_read_se", "heifgpu_bins_truncated_rice", "heifgpu_bins_chroma_pred_mode",
     "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb", "heifgpu_image_tile_params", "heifgpu_debug_counters",
+    "heifgpu_image_parse_item", "heifgpu_ycbcr_to_rgb",
 )
 
 
@@ -176,6 +177,8 @@ def _load() -> ctypes.CDLL:
         "heifgpu_bins_exp_golomb": (I32, [u8p, I32, I32, P(I32)]),
         "heifgpu_image_tile_params": (I32, [VP, U32, P(TileParams)]),
         "heifgpu_debug_counters": (I32, [P(ctypes.c_uint64), I32]),
+        "heifgpu_image_parse_item": (I32, [u8p, SZ, U32, P(VP)]),
+        "heifgpu_ycbcr_to_rgb": (I32, [VP, P(ImageInfo), P(Planes), VP, I32, VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -112,11 +112,15 @@ extern "C" {
 const char *heifgpu_last_error(void) { return g_err.c_str(); }
 
 int heifgpu_image_parse(const uint8_t *data, size_t len, heifgpu_image **out) {
+    return heifgpu_image_parse_item(data, len, 0, out);
+}
+
+int heifgpu_image_parse_item(const uint8_t *data, size_t len, uint32_t item_id, heifgpu_image **out) {
     if (!data || !out) return fail(HEIFGPU_E_INVALID, "null argument");
     *out = nullptr;
     try {
         auto im = std::make_unique<heifgpu_image>();
-        im->img = parse_heic(data, len);
+        im->img = parse_heic(data, len, item_id);
         *out = im.release();
         return HEIFGPU_OK;
     } catch (const UnsupportedError &e) {
@@ -149,6 +153,35 @@ int heifgpu_image_get_info(const heifgpu_image *img, heifgpu_image_info *info) {
     info->num_thumbnails = p.num_thumbnails;
     info->matrix_coeffs = uint32_t(s.matrix_coeffs);
     info->full_range = s.video_full_range_flag ? 1u : 0u;
+    info->item_id = p.item_id;
+    info->aux_item_id = p.aux_item_id;
+    return HEIFGPU_OK;
+}
+
+int heifgpu_ycbcr_to_rgb(heifgpu_ctx *ctx, const heifgpu_image_info *info, const heifgpu_planes *in, void *rgb,
+                         int32_t rgb_pitch, void *stream) {
+    if (!ctx || !info || !in || !rgb || !in->plane[0]) return fail(HEIFGPU_E_INVALID, "invalid argument");
+    if (info->chroma_format_idc > 1) return fail(HEIFGPU_E_UNSUPPORTED, "only 4:0:0 and 4:2:0");
+    if (info->chroma_format_idc == 1 && (!in->plane[1] || !in->plane[2])) return fail(HEIFGPU_E_INVALID, "missing chroma plane");
+    if (info->bit_depth < 8 || info->bit_depth > 16) return fail(HEIFGPU_E_INVALID, "bit depth");
+    HIP_TRY(hipSetDevice(ctx->device));
+    ColorArgs c{};
+    for (int k = 0; k < 3; ++k) {
+        c.plane[k] = reinterpret_cast<uint64_t>(in->plane[k]);
+        c.pitch[k] = in->pitch[k];
+    }
+    c.rgb = reinterpret_cast<uint64_t>(rgb);
+    c.rgb_pitch = rgb_pitch;
+    c.w = int32_t(info->width);
+    c.h = int32_t(info->height);
+    c.rotation = int32_t(info->rotation & 3);
+    c.out_w = (c.rotation & 1) ? c.h : c.w;
+    c.out_h = (c.rotation & 1) ? c.w : c.h;
+    if (rgb_pitch < 3 * c.out_w) return fail(HEIFGPU_E_INVALID, "rgb_pitch smaller than 3 * output width");
+    c.chroma = info->chroma_format_idc ? 1 : 0;
+    c.shift = int32_t(info->bit_depth) - 8;
+    color_coefs(info->matrix_coeffs, info->full_range != 0, c);
+    HIP_TRY(launch_ycbcr_rgb(c, int(info->bytes_per_sample), static_cast<hipStream_t>(stream)));
     return HEIFGPU_OK;
 }
 

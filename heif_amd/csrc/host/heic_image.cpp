@@ -28,13 +28,18 @@ void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p
 
 }  // namespace
 
-ParsedImage parse_heic(const uint8_t *data, size_t len) {
+ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id) {
     HeifReader reader(data, len);
     Heif heif = reader.read();
     ParsedImage img;
     img.primary_item_id = heif.primary_item_id;
-    const ItemInfo *pi = heif.item_info_by_item_id(heif.primary_item_id);
-    if (!pi) throw HeifError("primary item " + std::to_string(heif.primary_item_id) + " not found in item_info");
+    img.item_id = item_id ? item_id : heif.primary_item_id;
+    for (const auto &r : heif.references)  // 'auxl' from an auxiliary image to the primary
+        if (r.type == fourcc('a', 'u', 'x', 'l') && !img.aux_item_id)
+            for (uint32_t t : r.to)
+                if (t == heif.primary_item_id) img.aux_item_id = r.from;
+    const ItemInfo *pi = heif.item_info_by_item_id(img.item_id);
+    if (!pi) throw HeifError("item " + std::to_string(img.item_id) + " not found in item_info");
     if (const Property *ispe = heif.item_property(*pi, fourcc('i', 's', 'p', 'e'))) {
         if (ispe->length < 12) throw HeifError("ispe too short");
         const uint8_t *q = data + ispe->offset + 4;

@@ -26,6 +26,8 @@ struct ParsedImage {
     std::vector<ParamSet> params;
     std::vector<TileJob> tiles;  // grid order (row-major)
     uint32_t primary_item_id = 0, ispe_width = 0, ispe_height = 0, rotation = 0, num_thumbnails = 0;
+    uint32_t item_id = 0;      // the decoded image item (the primary unless asked otherwise)
+    uint32_t aux_item_id = 0;  // first auxiliary image of the primary ('auxl'), 0 if none
     uint32_t rows = 1, cols = 1, out_width = 0, out_height = 0;
     uint32_t tile_width = 0, tile_height = 0, coded_bytes = 0;
 };
@@ -34,6 +36,8 @@ struct ParsedImage {
 struct UnsupportedError : HeifError {
     explicit UnsupportedError(const std::string &m) : HeifError(m) {}
 };
-ParsedImage parse_heic(const uint8_t *data, size_t len);
+// item_id 0 = the primary item (heic/decoder.rs:12-112); otherwise any coded
+// image item, e.g. an auxiliary image found through ParsedImage::aux_item_id
+ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id = 0);
 
 }  // namespace hg

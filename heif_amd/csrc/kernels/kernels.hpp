@@ -72,6 +72,35 @@ size_t parse_group_bytes(int max_width, int max_wctb, int group) {
     return (b + 15) & ~(size_t)15;
 }
 
+// k_ycbcr_rgb (color.hip): one decoded image → interleaved RGB8, rotated
+struct ColorArgs {
+    uint64_t plane[3];  // Y, Cb, Cr (device)
+    int32_t pitch[3];   // bytes
+    uint64_t rgb;       // device
+    int32_t rgb_pitch;
+    int32_t w, h;            // decoded (coded-orientation) size
+    int32_t out_w, out_h;    // rotated size
+    int32_t rotation;        // irot, anticlockwise 90-degree units
+    int32_t chroma, shift;   // chroma present; bit depth - 8
+    int32_t yoff, ys;        // luma offset (16 limited range / 0 full) and scale (16.16)
+    int32_t cr_r, cb_g, cr_g, cb_b;  // H.273 chroma weights (16.16, limited range rescaled)
+};
+// H.273 coefficients for matrix_coefficients / video_full_range_flag, rounded to 16.16
+inline void color_coefs(uint32_t matrix, bool full, ColorArgs &c) {
+    double kr = 0.299, kb = 0.114;  // BT.601 (5, 6, and the unspecified default)
+    if (matrix == 1) kr = 0.2126, kb = 0.0722;
+    else if (matrix == 9) kr = 0.2627, kb = 0.0593;
+    const double kg = 1.0 - kr - kb;
+    const double ys = full ? 1.0 : 255.0 / 219.0, cs = full ? 1.0 : 255.0 / 224.0;
+    auto fx = [](double v) { return (int32_t)(v * 65536.0 + 0.5); };
+    c.yoff = full ? 0 : 16;
+    c.ys = fx(ys);
+    c.cr_r = fx(2.0 * (1.0 - kr) * cs);
+    c.cb_b = fx(2.0 * (1.0 - kb) * cs);
+    c.cb_g = fx(2.0 * kb * (1.0 - kb) / kg * cs);
+    c.cr_g = fx(2.0 * kr * (1.0 - kr) / kg * cs);
+}
+
 // k_parse_lanes (parse_lanes.hip): one substream per lane; the default (HEIFGPU_PARSE=scalar selects k_parse)
 bool parse_lanes_supported(const BatchArgs &a);
 bool parse_lanes_selected(const BatchArgs &a);
@@ -115,6 +144,7 @@ void emu_deblock(const BatchArgs &a);
 void emu_sao_out(const BatchArgs &a);
 #else
 hipError_t launch_rbsp(const BatchArgs &a, hipStream_t s);
+hipError_t launch_ycbcr_rgb(const ColorArgs &c, int bytes_per_sample, hipStream_t s);
 hipError_t launch_parse(const BatchArgs &a, hipStream_t s);
 hipError_t launch_parse_lanes(const BatchArgs &a, hipStream_t s);
 int parse_lanes_counters(uint64_t *out8);

@@ -71,6 +71,8 @@ typedef struct {
     uint32_t primary_item_id;
     uint32_t num_thumbnails;
     uint32_t matrix_coeffs, full_range;
+    uint32_t item_id;             /* the decoded item (primary_item_id unless parsed by item) */
+    uint32_t aux_item_id;         /* first auxiliary image of the primary ('auxl'), 0 if none */
 } heifgpu_image_info;
 
 typedef struct {
@@ -81,6 +83,10 @@ typedef struct {
 /* ---- host: demux + parameter sets + slice headers ------------------- */
 /* data is copied; the returned image owns its bytes. */
 int heifgpu_image_parse(const uint8_t *data, size_t len, heifgpu_image **out);
+/* Any coded image item by ID (0 = primary), e.g. the HDR gain map the primary
+ * references through 'auxl' (info.aux_item_id; src/heif/grammar.rs:202-207
+ * parses the reference but nothing decodes it).  Grid or single hvc1 item. */
+int heifgpu_image_parse_item(const uint8_t *data, size_t len, uint32_t item_id, heifgpu_image **out);
 int heifgpu_image_get_info(const heifgpu_image *img, heifgpu_image_info *info);
 void heifgpu_image_free(heifgpu_image *img);
 
@@ -104,15 +110,28 @@ int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *batch, uint32_t *statu
 void heifgpu_batch_free(heifgpu_batch *batch);
 /* stage timing of the last decode (ms, from HIP events when enabled with
  * heifgpu_set_timing(ctx, 1)): parse, transform, intra, deblock,
- * sao/output, and (last) the emulation-prevention pass k_rbsp.  A decode runs in heifgpu_last_chunks() picture chunks whose
- * parse (caller's stream) overlaps the previous chunk's reconstruction (a
- * second stream); each figure is the sum over chunks. */
+ * sao/output, and (last) the emulation-prevention pass k_rbsp.  k_rbsp and
+ * k_parse run on an internal parse stream, the rest on an internal recon
+ * stream, so decode n+1's parse overlaps decode n's reconstruction;
+ * heifgpu_last_chunks() is 1 after a timed decode (ABI v1 compatibility). */
 int heifgpu_set_timing(heifgpu_ctx *ctx, int enable);
 int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[6]);
 int heifgpu_last_chunks(const heifgpu_ctx *ctx);
 /* convenience: prepare + decode + status + free */
 int heifgpu_decode_batch(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, const heifgpu_planes *out,
                          void *stream, uint32_t *status);
+
+/* ---- YCbCr -> RGB with the irot rotation (libheif's default output) -------
+ * Converts one decoded image (planes as written by heifgpu_batch_decode,
+ * `info` from heifgpu_image_get_info) into interleaved 8-bit R,G,B at `rgb`
+ * (device, caller-owned, rgb_pitch bytes per row), rotated anticlockwise by
+ * info->rotation * 90 degrees: the output is height x width for rotation 1
+ * and 3.  Matrix from info->matrix_coeffs (H.273: 1 BT.709, 9 BT.2020 NCL,
+ * anything else BT.601), range from info->full_range, 4:2:0 chroma by sample
+ * replication, samples above 8 bits rounded down to 8.  Fixed point: 16
+ * fractional bits, round half up, clip to 0..255.  Asynchronous on `stream`. */
+int heifgpu_ycbcr_to_rgb(heifgpu_ctx *ctx, const heifgpu_image_info *info, const heifgpu_planes *in, void *rgb,
+                         int32_t rgb_pitch, void *stream);
 
 /* ---- host test hooks (reference unit-test surface) -------------------- */
 size_t heifgpu_remove_emulation_prevention(const uint8_t *in, size_t n, uint8_t *out); /* rbsp_reader.rs:11-39 */

@@ -350,10 +350,29 @@ int oracle_read_meta(const uint8_t *data, size_t len, oracle_meta *out) {
 
 int oracle_list_tiles(const uint8_t *data, size_t len, uint32_t *off, uint32_t *ln, int max,
                       uint32_t *hvcc_off, uint32_t *hvcc_len) {
+    return oracle_list_item_tiles(data, len, 0, off, ln, max, hvcc_off, hvcc_len);
+}
+
+/* First auxiliary image of the primary item: an 'auxl' reference whose
+ * target list holds the primary (heif/grammar.rs:202-207 parses these). */
+uint32_t oracle_aux_item(const uint8_t *data, size_t len) {
+    heif_file *f = (heif_file *)calloc(1, sizeof(heif_file));
+    uint32_t id = 0;
+    if (heif_parse(data, len, f) == 0)
+        for (int r = 0; r < f->n_refs && !id; r++)
+            if (f->refs[r].type == FOURCC('a', 'u', 'x', 'l'))
+                for (int k = 0; k < f->refs[r].n_to; k++)
+                    if (f->refs[r].to[k] == f->primary) id = f->refs[r].from;
+    free(f);
+    return id;
+}
+
+int oracle_list_item_tiles(const uint8_t *data, size_t len, uint32_t item_id, uint32_t *off, uint32_t *ln, int max,
+                           uint32_t *hvcc_off, uint32_t *hvcc_len) {
     heif_file *f = (heif_file *)calloc(1, sizeof(heif_file));
     if (heif_parse(data, len, f)) { free(f); return -1; }
-    heif_item *pi = heif_item_by_id(f, f->primary);
-    if (!pi) { free(f); return oracle_fail("no primary"); }
+    heif_item *pi = heif_item_by_id(f, item_id ? item_id : f->primary);
+    if (!pi) { free(f); return oracle_fail("no such item"); }
     uint32_t ids[HEIF_MAX_TO];
     int n;
     if (pi->type == FOURCC('g', 'r', 'i', 'd')) n = heif_grid_tiles(f, pi->id, ids, HEIF_MAX_TO);

@@ -106,6 +106,11 @@ int oracle_decode_tile(const uint8_t *hvcc, size_t hvcc_len,
  * (into data) and the hvcC property bytes offset/length.  Returns count. */
 int oracle_list_tiles(const uint8_t *data, size_t len, uint32_t *off, uint32_t *ln,
                       int max, uint32_t *hvcc_off, uint32_t *hvcc_len);
+/* The same for any coded image item (item_id 0 = primary), and the first
+ * auxiliary image ('auxl' → primary) of a file, 0 if none. */
+int oracle_list_item_tiles(const uint8_t *data, size_t len, uint32_t item_id, uint32_t *off, uint32_t *ln,
+                           int max, uint32_t *hvcc_off, uint32_t *hvcc_len);
+uint32_t oracle_aux_item(const uint8_t *data, size_t len);
 
 const char *oracle_last_error(void);
 /* bring-up: bit0 skips deblocking, bit1 skips SAO (thread-local) */

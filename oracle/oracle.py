@@ -60,6 +60,10 @@ def _load():
                                        P(ctypes.c_uint16), I]
     lib.oracle_list_tiles.argtypes = [u8p, SZ, P(ctypes.c_uint32), P(ctypes.c_uint32), I,
                                       P(ctypes.c_uint32), P(ctypes.c_uint32)]
+    lib.oracle_list_item_tiles.argtypes = [u8p, SZ, ctypes.c_uint32, P(ctypes.c_uint32), P(ctypes.c_uint32), I,
+                                           P(ctypes.c_uint32), P(ctypes.c_uint32)]
+    lib.oracle_aux_item.argtypes = [u8p, SZ]
+    lib.oracle_aux_item.restype = ctypes.c_uint32
     return lib
 
 
@@ -118,11 +122,17 @@ def decode_heic(data: bytes, with_checks: bool = True) -> OracleImage:
         lib.oracle_image_free(ctypes.byref(img))
 
 
-def list_tiles(data: bytes):
+def aux_item(data: bytes) -> int:
+    """Item ID of the primary image's first auxiliary image ('auxl'), 0 if none."""
+    return int(lib.oracle_aux_item(_buf(data), len(data)))
+
+
+def list_tiles(data: bytes, item_id: int = 0):
+    """Coded pictures of an image item (0 = primary): [(offset, length)], (hvcC offset, length)."""
     off = (ctypes.c_uint32 * 4096)()
     ln = (ctypes.c_uint32 * 4096)()
     ho, hl = ctypes.c_uint32(), ctypes.c_uint32()
-    n = lib.oracle_list_tiles(_buf(data), len(data), off, ln, 4096, ctypes.byref(ho), ctypes.byref(hl))
+    n = lib.oracle_list_item_tiles(_buf(data), len(data), item_id, off, ln, 4096, ctypes.byref(ho), ctypes.byref(hl))
     if n < 0:
         raise OracleError(last_error())
     return [(off[i], ln[i]) for i in range(n)], (ho.value, hl.value)

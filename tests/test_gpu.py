@@ -186,3 +186,32 @@ def test_pipelined_decodes_back_to_back(H, ctx, oracle_tiles, halfmoonbay):
             for got, w in zip(planes_np(oi), want):
                 assert np.array_equal(got, w), s
     b.free()
+
+
+def test_aux_gain_map_bit_exact(H, oracle_mod, halfmoonbay):
+    """§8(f) row 4: the HDR gain map item (4:0:0 monochrome, RExt profile 4,
+    2016x1520 coded, 48 WPP rows in one picture) through the same kernels."""
+    aux = H.HeifImage.parse(halfmoonbay).info.aux_item_id
+    out = H.HeicDecoder.decode(halfmoonbay, item_id=aux)
+    assert out.cb is None and out.cr is None
+    tiles, (ho, hl) = oracle_mod.list_tiles(halfmoonbay, aux)
+    o, n = tiles[0]
+    y, _, _ = oracle_mod.decode_tile(halfmoonbay[ho:ho + hl], halfmoonbay[o:o + n], 2016, 1512)
+    assert np.array_equal(out.y.cpu().numpy().astype(np.uint16), y)
+
+
+def test_rgb_rotated_matches_restatement(H, halfmoonbay):
+    """§8(f) row 2: YCbCr -> RGB8 + irot on the GPU, exact against the numpy
+    restatement of the same fixed-point arithmetic (tests/rgb_ref.py)."""
+    import rgb_ref
+
+    out = H.HeicDecoder.decode(halfmoonbay)
+    inf = out.info
+    rgb = H.HeicDecoder.context().to_rgb(out).cpu().numpy()
+    assert rgb.shape == (4032, 3024, 3)  # irot 3: 4032x3024 stored, shown portrait
+    want = rgb_ref.ycbcr_to_rgb(out.y.cpu().numpy(), out.cb.cpu().numpy(), out.cr.cpu().numpy(),
+                                inf.matrix_coeffs, bool(inf.full_range), inf.rotation)
+    assert np.array_equal(rgb, want)
+    # the monochrome gain map: R = G = B
+    aux = H.HeicDecoder.decode_rgb(halfmoonbay, item_id=inf.aux_item_id).cpu().numpy()
+    assert aux.shape == (2016, 1512, 3) and (aux[..., 0] == aux[..., 2]).all()
