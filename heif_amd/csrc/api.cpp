@@ -151,8 +151,8 @@ int heifgpu_image_get_info(const heifgpu_image *img, heifgpu_image_info *info) {
     info->coded_bytes = p.coded_bytes;
     info->primary_item_id = p.primary_item_id;
     info->num_thumbnails = p.num_thumbnails;
-    info->matrix_coeffs = uint32_t(s.matrix_coeffs);
-    info->full_range = s.video_full_range_flag ? 1u : 0u;
+    info->matrix_coeffs = p.nclx ? p.nclx_matrix : uint32_t(s.matrix_coeffs);
+    info->full_range = p.nclx ? p.nclx_full_range : (s.video_full_range_flag ? 1u : 0u);
     info->item_id = p.item_id;
     info->aux_item_id = p.aux_item_id;
     return HEIFGPU_OK;

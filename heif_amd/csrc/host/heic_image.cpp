@@ -48,6 +48,20 @@ ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id) {
     }
     if (const Property *irot = heif.item_property(*pi, fourcc('i', 'r', 'o', 't')))
         if (irot->length >= 1) img.rotation = data[irot->offset] & 3;
+    // colr of type nclx (ISO/IEC 23008-12 6.5.5; reader.rs:525 leaves it todo!()):
+    // its matrix / range override the SPS VUI for RGB conversion.  An item may
+    // carry both an ICC ('prof') and an nclx colr, so scan all of them.
+    for (uint32_t idx : pi->properties) {
+        if (idx == 0 || idx > heif.properties.size()) continue;
+        const Property &p = heif.properties[idx - 1];
+        if (p.type != fourcc('c', 'o', 'l', 'r') || p.length < 11) continue;
+        const uint8_t *q = data + p.offset;
+        if (((uint32_t(q[0]) << 24) | (uint32_t(q[1]) << 16) | (uint32_t(q[2]) << 8) | q[3]) != fourcc('n', 'c', 'l', 'x'))
+            continue;
+        img.nclx = true;
+        img.nclx_matrix = (uint32_t(q[8]) << 8) | q[9];
+        img.nclx_full_range = q[10] >> 7;
+    }
     img.num_thumbnails = heif.num_thumbnails();
 
     std::vector<uint32_t> tile_ids;

@@ -28,6 +28,8 @@ struct ParsedImage {
     uint32_t primary_item_id = 0, ispe_width = 0, ispe_height = 0, rotation = 0, num_thumbnails = 0;
     uint32_t item_id = 0;      // the decoded image item (the primary unless asked otherwise)
     uint32_t aux_item_id = 0;  // first auxiliary image of the primary ('auxl'), 0 if none
+    bool nclx = false;         // the item has an nclx colr (overrides the VUI colour description)
+    uint32_t nclx_matrix = 0, nclx_full_range = 0;
     uint32_t rows = 1, cols = 1, out_width = 0, out_height = 0;
     uint32_t tile_width = 0, tile_height = 0, coded_bytes = 0;
 };

@@ -73,3 +73,17 @@ def test_rgb_restatement_rotation():
     # anticlockwise: the top-right sample becomes the top-left
     assert out[0, 0, 0] == y[0, 2] and out[2, 0, 0] == y[0, 0]
     assert rgb_ref.ycbcr_to_rgb(y, None, None, 6, True, 3)[0, 0, 0] == y[1, 0]
+
+
+def test_nclx_colr_overrides_vui(halfmoonbay):
+    """§8(f) row 1: an nclx colr (reference: heif/reader.rs:525 todo!()) sets
+    the matrix / range used for RGB; without one the SPS VUI applies."""
+    import heif_amd as H
+
+    base = H.HeifImage.parse(halfmoonbay).info
+    assert (base.matrix_coeffs, base.full_range) == (6, 1)  # VUI (SURVEY Appendix A)
+    i = halfmoonbay.index(b"colrprof") + 4  # colour_type of the primary's ICC colr (548-byte box)
+    patched = bytearray(halfmoonbay)
+    patched[i:i + 11] = b"nclx" + bytes([0, 1, 0, 1, 0, 1, 0x00])  # BT.709 primaries/transfer/matrix, limited
+    inf = H.HeifImage.parse(bytes(patched)).info
+    assert (inf.matrix_coeffs, inf.full_range) == (1, 0)
