@@ -12,8 +12,11 @@ Y/Cb/Cr planes to HBM.  `value` = all ranks' output luma pixels / max-over-
 ranks wall time of K steps.
 
 roofline: the dominant kernel (k_parse) measured with HIP events on the
-decode stream; algorithmic bytes per image = compressed tile bytes +
-reconstructed planes (1,704,187 + 18,874,368 B).
+internal parse stream it runs on, averaged over the timed steps (so the
+slowdown from the overlapping reconstruction is included, as in the rocprofv3
+kernel-trace average of the same command); algorithmic bytes per image =
+compressed tile bytes + reconstructed planes (SURVEY.md §8(d):
+1,704,187 + 18,874,368 B).
 
 cpu_baseline: the CPU oracle (oracle/, spec restatement; the reference Rust
 path cannot decode pixels) decoding tiles on a thread pool for ~10 s.
@@ -132,6 +135,10 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
+    # HIP events around every kernel on the stream it runs on (internal parse /
+    # recon streams), recorded through the timed region: per-kernel means over
+    # the K timed steps, overlap included
+    ctx.set_timing(True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -140,6 +147,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    per_step = ctx.stage_times()
     if world > 1:
         t = torch.tensor([elapsed], device=f"cuda:{local}")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -148,11 +156,9 @@ def main():
     if any(st):
         raise SystemExit(f"rank {rank}: decode status {st}")
 
-    # per-kernel times (HIP events on the internal parse / recon streams) from
-    # one more decode after the timed region, run alone
-    ctx.set_timing(True)
+    # one more decode after the timed region, alone: the single-decode latency
     step()
-    per_step = ctx.stage_times()
+    alone = ctx.stage_times()
     ctx.set_timing(False)
 
     if rank == 0:
@@ -219,9 +225,12 @@ def main():
             },
             "stage_ms_per_step": {k: round(v, 3) for k, v in zip(
                 ["parse", "transform", "intra", "deblock", "sao_out", "rbsp"], per_step)},
+            "stage_ms_alone": {k: round(v, 3) for k, v in zip(
+                ["parse", "transform", "intra", "deblock", "sao_out", "rbsp"], alone)},
             "pipeline": "decode n+1's k_rbsp+k_parse (parse stream) overlap decode n's reconstruction (recon stream); "
-                        "the timed region includes the pipeline fill and drain",
-            "latency_ms_one_step": round(sum(per_step), 3),
+                        "the timed region includes the pipeline fill and drain; stage_ms_per_step are means over the "
+                        "timed steps (overlap included), stage_ms_alone one decode with nothing beside it",
+            "latency_ms_one_step": round(sum(alone), 3),
             "pipeline_hbm_gbs": round(args.batch * algo_per_image / (elapsed / args.steps) / 1e9, 2),
             "host_parse_ms_per_image": round(host_parse_ms, 3),
             "upload_s": round(upload_s, 3),

@@ -32,14 +32,39 @@ struct heifgpu_image {
 // stream before the call (it writes the caller's planes), and the caller's
 // stream waits for that reconstruction.  A parse set is reused only after the
 // reconstruction that read it.  HEIFGPU_PIPELINE=0 keeps one set (no overlap).
+constexpr int kTimingSlots = 32;
 struct heifgpu_ctx {
     int device = 0;
     bool timing = false;
     hipStream_t parse = nullptr, recon = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    hipEvent_t tev[8] = {};  // timing: rbsp start, rbsp end = parse start, parse end, recon start, 4 stage ends
+    // timing ring, one slot per timed decode call: rbsp start, rbsp end = parse
+    // start, parse end, recon start, 4 stage ends.  heifgpu_stage_times folds
+    // every call since the previous query (a slot about to be reused is folded first).
+    hipEvent_t tev[kTimingSlots][8] = {};
+    int timed_calls = 0, folded = 0;
+    double acc[6] = {};
     bool timed = false;
 };
+
+namespace {
+// adds the stage times of the decode call recorded in `slot` to ctx->acc
+hipError_t fold_timing(heifgpu_ctx *ctx, int slot) {
+    hipEvent_t *e = ctx->tev[slot];
+    hipError_t r = hipEventSynchronize(e[7]);
+    if (r != hipSuccess) return r;
+    float t = 0.f;
+    if ((r = hipEventElapsedTime(&t, e[0], e[1])) != hipSuccess) return r;
+    ctx->acc[5] += t;  // k_rbsp
+    if ((r = hipEventElapsedTime(&t, e[1], e[2])) != hipSuccess) return r;
+    ctx->acc[0] += t;  // k_parse
+    for (int i = 1; i < 5; ++i) {
+        if ((r = hipEventElapsedTime(&t, e[i + 2], e[i + 3])) != hipSuccess) return r;
+        ctx->acc[i] += t;
+    }
+    return hipSuccess;
+}
+}  // namespace
 
 namespace {
 
@@ -208,7 +233,8 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     HIP_TRY(hipStreamCreateWithFlags(&c->recon, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
-    for (auto &e : c->tev) HIP_TRY(hipEventCreate(&e));
+    for (auto &row : c->tev)
+        for (auto &e : row) HIP_TRY(hipEventCreate(&e));
     *out = c.release();
     return HEIFGPU_OK;
 }
@@ -217,8 +243,9 @@ void heifgpu_destroy(heifgpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipDeviceSynchronize();
-    for (auto &e : ctx->tev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto &row : ctx->tev)
+        for (auto &e : row)
+            if (e) (void)hipEventDestroy(e);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
     if (ctx->parse) (void)hipStreamDestroy(ctx->parse);
@@ -228,6 +255,10 @@ void heifgpu_destroy(heifgpu_ctx *ctx) {
 
 int heifgpu_set_timing(heifgpu_ctx *ctx, int enable) {
     if (!ctx) return fail(HEIFGPU_E_INVALID, "null ctx");
+    if (enable && !ctx->timing) {  // a fresh accumulation
+        for (double &v : ctx->acc) v = 0.0;
+        ctx->timed_calls = ctx->folded = 0;
+    }
     ctx->timing = enable != 0;
     return HEIFGPU_OK;
 }
@@ -237,12 +268,13 @@ int heifgpu_last_chunks(const heifgpu_ctx *ctx) { return ctx && ctx->timed ? 1 :
 int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[6]) {
     if (!ctx || !ms) return fail(HEIFGPU_E_INVALID, "null argument");
     if (!ctx->timing) return fail(HEIFGPU_E_INVALID, "timing disabled");
+    // mean per decode call over the timed calls since the previous query
     for (int i = 0; i < 6; ++i) ms[i] = 0.f;
-    if (!ctx->timed) return HEIFGPU_OK;
-    HIP_TRY(hipEventSynchronize(ctx->tev[7]));
-    HIP_TRY(hipEventElapsedTime(&ms[5], ctx->tev[0], ctx->tev[1]));  // k_rbsp
-    HIP_TRY(hipEventElapsedTime(&ms[0], ctx->tev[1], ctx->tev[2]));  // k_parse
-    for (int i = 1; i < 5; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], ctx->tev[i + 2], ctx->tev[i + 3]));
+    for (int c = ctx->folded; c < ctx->timed_calls; ++c) HIP_TRY(fold_timing(ctx, c % kTimingSlots));
+    if (ctx->timed_calls)
+        for (int i = 0; i < 6; ++i) ms[i] = float(ctx->acc[i] / ctx->timed_calls);
+    for (double &v : ctx->acc) v = 0.0;
+    ctx->timed_calls = ctx->folded = 0;
     return HEIFGPU_OK;
 }
 
@@ -395,28 +427,38 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     }
     hipStream_t p = ctx->parse, r = ctx->recon;
     const bool t = ctx->timing;
+    hipEvent_t *ev = nullptr;
+    if (t) {  // this call's timing slot; the call that used it last is folded first
+        const int slot = ctx->timed_calls % kTimingSlots;
+        if (ctx->timed_calls - ctx->folded >= kTimingSlots) {
+            HIP_TRY(fold_timing(ctx, slot));
+            ++ctx->folded;
+        }
+        ev = ctx->tev[slot];
+        ++ctx->timed_calls;
+    }
     // parse stream: this set's previous reconstruction must be done with it
     if (ps.pending) HIP_TRY(hipStreamWaitEvent(p, ps.recon_done, 0));
     HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), p));
-    if (t) HIP_TRY(hipEventRecord(ctx->tev[0], p));
+    if (t) HIP_TRY(hipEventRecord(ev[0], p));
     HIP_TRY(launch_rbsp(a, p));
-    if (t) HIP_TRY(hipEventRecord(ctx->tev[1], p));
+    if (t) HIP_TRY(hipEventRecord(ev[1], p));
     HIP_TRY(launch_parse(a, p));
-    if (t) HIP_TRY(hipEventRecord(ctx->tev[2], p));
+    if (t) HIP_TRY(hipEventRecord(ev[2], p));
     HIP_TRY(hipEventRecord(ps.parsed, p));
     // recon stream: after the caller's prior work and this call's parse
     HIP_TRY(hipEventRecord(ctx->fork, s));
     HIP_TRY(hipStreamWaitEvent(r, ctx->fork, 0));
     HIP_TRY(hipStreamWaitEvent(r, ps.parsed, 0));
-    if (t) HIP_TRY(hipEventRecord(ctx->tev[3], r));
+    if (t) HIP_TRY(hipEventRecord(ev[3], r));
     HIP_TRY(launch_transform(a, r));
-    if (t) HIP_TRY(hipEventRecord(ctx->tev[4], r));
+    if (t) HIP_TRY(hipEventRecord(ev[4], r));
     HIP_TRY(launch_intra(a, r));
-    if (t) HIP_TRY(hipEventRecord(ctx->tev[5], r));
+    if (t) HIP_TRY(hipEventRecord(ev[5], r));
     HIP_TRY(launch_deblock(a, r));
-    if (t) HIP_TRY(hipEventRecord(ctx->tev[6], r));
+    if (t) HIP_TRY(hipEventRecord(ev[6], r));
     HIP_TRY(launch_sao_out(a, r));
-    if (t) HIP_TRY(hipEventRecord(ctx->tev[7], r));
+    if (t) HIP_TRY(hipEventRecord(ev[7], r));
     HIP_TRY(hipEventRecord(ps.recon_done, r));
     ps.pending = true;
     ctx->timed = t;

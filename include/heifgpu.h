@@ -108,9 +108,11 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
 int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *batch, const heifgpu_planes *out, void *stream);
 int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *batch, uint32_t *status, void *stream);
 void heifgpu_batch_free(heifgpu_batch *batch);
-/* stage timing of the last decode (ms, from HIP events when enabled with
- * heifgpu_set_timing(ctx, 1)): parse, transform, intra, deblock,
- * sao/output, and (last) the emulation-prevention pass k_rbsp.  k_rbsp and
+/* stage timing (ms per decode call, from HIP events on the streams the
+ * kernels run on, enabled with heifgpu_set_timing(ctx, 1)): the mean over the
+ * decode calls since the previous query (or since timing was enabled) of
+ * parse, transform, intra, deblock, sao/output, and (last) the
+ * emulation-prevention pass k_rbsp; the query resets the mean.  k_rbsp and
  * k_parse run on an internal parse stream, the rest on an internal recon
  * stream, so decode n+1's parse overlaps decode n's reconstruction;
  * heifgpu_last_chunks() is 1 after a timed decode (ABI v1 compatibility). */
