@@ -1,0 +1,953 @@
+/*
+ * hevc_synth.c — synthetic HEVC intra picture generator (SURVEY.md §8(f)
+ * row 3: Main-10 / 8K grid inputs; no 10-bit sample ships with the
+ * reference, tests/ there hold only halfmoonbay.heic).
+ *
+ * This is a *syntax-driven* encoder: it walks the H.265 I-slice syntax
+ * (7.3.8.1-7.3.8.12) exactly as a decoder would, but instead of decoding
+ * each bin it draws the syntax element from a seeded RNG and CABAC-encodes it
+ * with the same context selection (9.3.4.2).  No pixels are ever computed —
+ * the only state it tracks is what context selection and the syntax itself
+ * depend on (IntraPredModeY for MPM derivation and scanIdx, CtDepth for
+ * split_cu_flag, IsCuQpDeltaCoded, coded_sub_block_flag, greater1 state).
+ * The result is a conforming bitstream whose reconstruction exercises every
+ * intra mode, TU size, transform-skip / bypass / sign hiding / scaling list /
+ * cu_qp_delta path at any bit depth, chroma format 4:0:0 or 4:2:0, CTB size
+ * and picture size, with WPP substreams and entry points.
+ *
+ * Arithmetic coder: the standard low/range encoder with carry propagation
+ * through buffered 0xff bytes (the inverse of 9.3.4.3), flushed at every
+ * end_of_slice_segment_flag / end_of_subset_one_bit.
+ *
+ * Not part of the decode path: nothing in libheifgpu.so links this.  It is a
+ * data generator used by tests/ and by bench.py's optional config-5 workload.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "hevc_synth.h"
+
+/* ------------------------------------------------------------------ */
+/* bit writer                                                          */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint8_t *d;
+    size_t n, cap;   /* bytes complete */
+    uint32_t acc;    /* pending bits */
+    int nacc;
+    int err;
+} bw_t;
+
+static void bw_byte(bw_t *w, uint32_t b) {
+    if (w->n >= w->cap) {
+        size_t nc = w->cap ? w->cap * 2 : 4096;
+        uint8_t *nd = (uint8_t *)realloc(w->d, nc);
+        if (!nd) { w->err = 1; return; }
+        w->d = nd;
+        w->cap = nc;
+    }
+    w->d[w->n++] = (uint8_t)b;
+}
+static void bw_bits(bw_t *w, uint32_t v, int n) {
+    for (int i = n - 1; i >= 0; i--) {
+        w->acc = (w->acc << 1) | ((v >> i) & 1);
+        if (++w->nacc == 8) { bw_byte(w, w->acc & 0xff); w->acc = 0; w->nacc = 0; }
+    }
+}
+static void bw_ue(bw_t *w, uint32_t v) {
+    uint64_t x = (uint64_t)v + 1;
+    int len = 0;
+    while ((x >> len) > 1) len++;
+    bw_bits(w, 0, len);
+    bw_bits(w, (uint32_t)x, len + 1);
+}
+static void bw_se(bw_t *w, int32_t v) { bw_ue(w, v > 0 ? (uint32_t)(2 * v - 1) : (uint32_t)(-2 * v)); }
+static void bw_align1(bw_t *w) { /* rbsp_trailing_bits / byte_alignment(): 1 then zeros */
+    bw_bits(w, 1, 1);
+    while (w->nacc) bw_bits(w, 0, 1);
+}
+
+/* ------------------------------------------------------------------ */
+/* RNG (splitmix64)                                                     */
+/* ------------------------------------------------------------------ */
+static uint64_t rng_next(uint64_t *s) {
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static int rnd(uint64_t *s, int n) { return (int)(rng_next(s) % (uint64_t)n); }
+static int pct(uint64_t *s, int p) { return rnd(s, 100) < p; }
+
+/* ------------------------------------------------------------------ */
+/* CABAC tables (H.265 Tables 9-5..9-37 initType 0, 9-52, 9-53)         */
+/* ------------------------------------------------------------------ */
+enum {
+    C_SAO_MERGE = 0, C_SAO_TYPE = 1, C_SPLIT_CU = 2, C_TQ_BYPASS = 5, C_PART_MODE = 6,
+    C_PREV_INTRA = 7, C_CHROMA_MODE = 8, C_SPLIT_TF = 9, C_CBF_LUMA = 12, C_CBF_CHROMA = 14,
+    C_CU_QP_DELTA = 19, C_TS_FLAG = 21, C_LAST_X = 23, C_LAST_Y = 41, C_CSBF = 59,
+    C_SIG = 63, C_GT1 = 107, C_GT2 = 131, C_NUM = 137
+};
+static const uint8_t k_init[C_NUM] = {
+    153, 200, 139, 141, 157, 154, 184, 184, 63, 153, 138, 138, 111, 141, 94, 138, 182, 154, 154, 154, 154,
+    139, 139,
+    110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,
+    110, 110, 124, 125, 140, 153, 125, 127, 140, 109, 111, 143, 127, 111, 79, 108, 123, 63,
+    91, 171, 134, 141,
+    111, 111, 125, 110, 110, 94, 124, 108, 124, 107, 125, 141, 179, 153, 125, 107, 125, 141,
+    179, 153, 125, 107, 125, 141, 179, 153, 125, 140, 139, 182, 182, 152, 136, 152, 136, 153,
+    136, 139, 111, 136, 139, 111, 141, 111,
+    140, 92, 137, 138, 140, 152, 138, 139, 153, 74, 149, 92, 139, 107, 122, 152, 140, 179, 166,
+    182, 140, 227, 122, 197,
+    138, 153, 136, 167, 152, 152,
+};
+static const uint8_t k_lps[64][4] = {
+    {128, 176, 208, 240}, {128, 167, 197, 227}, {128, 158, 187, 216}, {123, 150, 178, 205}, {116, 142, 169, 195},
+    {111, 135, 160, 185}, {105, 128, 152, 175}, {100, 122, 144, 166}, {95, 116, 137, 158}, {90, 110, 130, 150},
+    {85, 104, 123, 142}, {81, 99, 117, 135}, {77, 94, 111, 128}, {73, 89, 105, 122}, {69, 85, 100, 116},
+    {66, 80, 95, 110}, {62, 76, 90, 104}, {59, 72, 86, 99}, {56, 69, 81, 94}, {53, 65, 77, 89},
+    {51, 62, 73, 85}, {48, 59, 69, 80}, {46, 56, 66, 76}, {43, 53, 63, 72}, {41, 50, 59, 69},
+    {39, 48, 56, 65}, {37, 45, 54, 62}, {35, 43, 51, 59}, {33, 41, 48, 56}, {32, 39, 46, 53},
+    {30, 37, 43, 50}, {29, 35, 41, 48}, {27, 33, 39, 45}, {26, 31, 37, 43}, {24, 30, 35, 41},
+    {23, 28, 33, 39}, {22, 27, 32, 37}, {21, 26, 30, 35}, {20, 24, 29, 33}, {19, 23, 27, 31},
+    {18, 22, 26, 30}, {17, 21, 25, 28}, {16, 20, 23, 27}, {15, 19, 22, 25}, {14, 18, 21, 24},
+    {14, 17, 20, 23}, {13, 16, 19, 22}, {12, 15, 18, 21}, {12, 14, 17, 20}, {11, 14, 16, 19},
+    {11, 13, 15, 18}, {10, 12, 15, 17}, {10, 12, 14, 16}, {9, 11, 13, 15}, {9, 11, 12, 14},
+    {8, 10, 12, 14}, {8, 9, 11, 13}, {7, 9, 11, 12}, {7, 9, 10, 12}, {7, 8, 10, 11},
+    {6, 8, 9, 11}, {6, 7, 9, 10}, {6, 7, 8, 9}, {2, 2, 2, 2}};
+static const uint8_t k_trans_lps[64] = {
+    0, 0, 1, 2, 2, 4, 4, 5, 6, 7, 8, 9, 9, 11, 11, 12, 13, 13, 15, 15, 16, 16,
+    18, 18, 19, 19, 21, 21, 22, 22, 23, 24, 24, 25, 26, 26, 27, 27, 28, 29, 29, 30,
+    30, 30, 31, 32, 32, 33, 33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63};
+
+/* ------------------------------------------------------------------ */
+/* arithmetic encoder                                                   */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    bw_t *w;
+    uint32_t low, range;
+    int bits_left, nbuf;
+    uint32_t buf_byte;
+    uint8_t st[C_NUM], mps[C_NUM];
+} cabe_t;
+
+static void ce_init_ctx(cabe_t *c, int qp) {
+    int q = qp < 0 ? 0 : qp > 51 ? 51 : qp;
+    for (int i = 0; i < C_NUM; i++) {
+        int v = k_init[i];
+        int m = (v >> 4) * 5 - 45, nn = ((v & 15) << 3) - 16;
+        int pre = ((m * q) >> 4) + nn;
+        pre = pre < 1 ? 1 : pre > 126 ? 126 : pre;
+        c->mps[i] = pre > 63;
+        c->st[i] = (uint8_t)(c->mps[i] ? pre - 64 : 63 - pre);
+    }
+}
+static void ce_start(cabe_t *c, bw_t *w) {
+    c->w = w;
+    c->low = 0;
+    c->range = 510;
+    c->bits_left = 23;
+    c->nbuf = 0;
+    c->buf_byte = 0xff;
+}
+static void ce_write_out(cabe_t *c) {
+    uint32_t lead = c->low >> (24 - c->bits_left);
+    c->bits_left += 8;
+    c->low &= 0xffffffffu >> c->bits_left;
+    if (lead == 0xff) {
+        c->nbuf++;
+    } else if (c->nbuf > 0) {
+        uint32_t carry = lead >> 8;
+        bw_bits(c->w, (c->buf_byte + carry) & 0xff, 8);
+        c->buf_byte = lead & 0xff;
+        uint32_t fill = (0xff + carry) & 0xff;
+        while (c->nbuf > 1) { bw_bits(c->w, fill, 8); c->nbuf--; }
+    } else {
+        c->nbuf = 1;
+        c->buf_byte = lead;
+    }
+}
+static void ce_test(cabe_t *c) { if (c->bits_left < 12) ce_write_out(c); }
+static void ce_bin(cabe_t *c, int ci, int bin) {
+    uint32_t s = c->st[ci];
+    uint32_t lps = k_lps[s][(c->range >> 6) & 3];
+    c->range -= lps;
+    if (bin != c->mps[ci]) {
+        int nb = 0;
+        while ((lps << nb) < 256) nb++;
+        c->low = (c->low + c->range) << nb;
+        c->range = lps << nb;
+        if (s == 0) c->mps[ci] = (uint8_t)(1 - c->mps[ci]);
+        c->st[ci] = k_trans_lps[s];
+        c->bits_left -= nb;
+    } else {
+        c->st[ci] = (uint8_t)(s < 62 ? s + 1 : s);
+        if (c->range >= 256) return;
+        c->low <<= 1;
+        c->range <<= 1;
+        c->bits_left--;
+    }
+    ce_test(c);
+}
+static void ce_bypass(cabe_t *c, int bin) {
+    c->low <<= 1;
+    if (bin) c->low += c->range;
+    c->bits_left--;
+    ce_test(c);
+}
+static void ce_term(cabe_t *c, int bin) {
+    c->range -= 2;
+    if (bin) {
+        c->low += c->range;
+        c->low <<= 7;
+        c->range = 2 << 7;
+        c->bits_left -= 7;
+    } else if (c->range >= 256) {
+        return;
+    } else {
+        c->low <<= 1;
+        c->range <<= 1;
+        c->bits_left--;
+    }
+    ce_test(c);
+}
+static void ce_finish(cabe_t *c) {
+    if (c->low >> (32 - c->bits_left)) {
+        bw_bits(c->w, (c->buf_byte + 1) & 0xff, 8);
+        while (c->nbuf > 1) { bw_bits(c->w, 0x00, 8); c->nbuf--; }
+        c->low -= 1u << (32 - c->bits_left);
+    } else {
+        if (c->nbuf > 0) bw_bits(c->w, c->buf_byte, 8);
+        while (c->nbuf > 1) { bw_bits(c->w, 0xff, 8); c->nbuf--; }
+    }
+    bw_bits(c->w, c->low >> 8, 24 - c->bits_left);
+}
+static void ce_fl(cabe_t *c, uint32_t v, int n) {
+    for (int i = n - 1; i >= 0; i--) ce_bypass(c, (v >> i) & 1);
+}
+static void ce_egk(cabe_t *c, uint32_t v, int k) {
+    for (;;) {
+        if (v >= (1u << k)) { ce_bypass(c, 1); v -= 1u << k; k++; }
+        else { ce_bypass(c, 0); ce_fl(c, v, k); break; }
+    }
+}
+/* TR (9.3.3.2) with bypass bins */
+static void ce_tr_bypass(cabe_t *c, int v, int cmax, int crice) {
+    int p = v >> crice, pmax = cmax >> crice;
+    for (int i = 0; i < p; i++) ce_bypass(c, 1);
+    if (p < pmax) ce_bypass(c, 0);
+    if (crice > 0 && p < pmax) ce_fl(c, (uint32_t)v & ((1u << crice) - 1), crice);
+}
+/* coeff_abs_level_remaining (9.3.3.11) */
+static void ce_calr(cabe_t *c, int v, int k) {
+    int cmax = 4 << k;
+    if (v < cmax) ce_tr_bypass(c, v, cmax, k);
+    else {
+        for (int i = 0; i < 4; i++) ce_bypass(c, 1);
+        ce_egk(c, (uint32_t)(v - cmax), k + 1);
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* scans (6.5.3-6.5.5), entries (y << 4) | x                            */
+/* ------------------------------------------------------------------ */
+static uint8_t g_scan[4][3][64];
+static void init_scans(void) {
+    static int ready = 0;
+    if (ready) return;
+    for (int l = 0; l < 4; l++) {
+        int n = 1 << l, i = 0, x = 0, y = 0;
+        while (i < n * n) {
+            while (y >= 0) {
+                if (x < n && y < n) g_scan[l][0][i++] = (uint8_t)((y << 4) | x);
+                y--;
+                x++;
+            }
+            y = x;
+            x = 0;
+        }
+        i = 0;
+        for (y = 0; y < n; y++)
+            for (x = 0; x < n; x++) g_scan[l][1][i++] = (uint8_t)((y << 4) | x);
+        i = 0;
+        for (x = 0; x < n; x++)
+            for (y = 0; y < n; y++) g_scan[l][2][i++] = (uint8_t)((y << 4) | x);
+    }
+    ready = 1;
+}
+
+/* ------------------------------------------------------------------ */
+/* picture state                                                        */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    const synth_params *P;
+    uint64_t rng;
+    cabe_t c;
+    int W, H, log2ctb, ctb, wctb, hctb, w4, h4, qpbdY;
+    uint8_t *ipm, *depth;
+    /* current CU */
+    int cu_bypass, intra_split, max_trafo_depth, chroma_mode;
+    int is_qp_coded;
+} pic_t;
+
+static void set_map(pic_t *p, uint8_t *m, int x0, int y0, int n, uint8_t v) {
+    for (int y = y0 >> 2; y < (y0 + n) >> 2 && y < p->h4; y++)
+        for (int x = x0 >> 2; x < (x0 + n) >> 2 && x < p->w4; x++) m[y * p->w4 + x] = v;
+}
+
+static int scan_idx_for(const pic_t *p, int log2n, int cIdx, int mode) {
+    (void)p;
+    if (log2n == 2 || (log2n == 3 && cIdx == 0)) {
+        if (mode >= 6 && mode <= 14) return 2;
+        if (mode >= 22 && mode <= 30) return 1;
+    }
+    return 0;
+}
+
+/* a small non-negative level with a long tail */
+static int draw_remaining(pic_t *p) {
+    int r = rnd(&p->rng, 100);
+    if (r < 60) return rnd(&p->rng, 3);
+    if (r < 90) return rnd(&p->rng, 16);
+    if (r < 99) return rnd(&p->rng, 200);
+    return rnd(&p->rng, 3000);
+}
+
+/* 7.3.8.11 residual_coding, bins drawn at random */
+static void residual_coding(pic_t *p, int log2n, int cIdx, int mode) {
+    cabe_t *c = &p->c;
+    const synth_params *P = p->P;
+    int n = 1 << log2n;
+    if (P->transform_skip && !p->cu_bypass && log2n <= 2) ce_bin(c, C_TS_FLAG + (cIdx ? 1 : 0), pct(&p->rng, 25));
+    int scanIdx = scan_idx_for(p, log2n, cIdx, mode);
+    /* last significant position: biased towards low frequencies */
+    int lx, ly;
+    if (pct(&p->rng, 70)) { lx = rnd(&p->rng, n < 8 ? n : 8); ly = rnd(&p->rng, n < 8 ? n : 8); }
+    else { lx = rnd(&p->rng, n); ly = rnd(&p->rng, n); }
+    if (P->density <= 10) { lx = lx < 4 ? lx : rnd(&p->rng, 4); ly = ly < 4 ? ly : rnd(&p->rng, 4); }
+    int sx = lx, sy = ly;
+    if (scanIdx == 2) { sx = ly; sy = lx; }
+    int cmax = (log2n << 1) - 1, off, shift;
+    if (cIdx == 0) { off = 3 * (log2n - 2) + ((log2n - 1) >> 2); shift = (log2n + 1) >> 2; }
+    else { off = 15; shift = log2n - 2; }
+    int pre[2], suf[2], sk[2];
+    for (int a = 0; a < 2; a++) {
+        int v = a ? sy : sx;
+        if (v < 4) { pre[a] = v; sk[a] = 0; suf[a] = 0; }
+        else {
+            int pp = 4;
+            for (;; pp++) {
+                int k = (pp >> 1) - 1, base = (1 << k) * (2 + (pp & 1));
+                if (v >= base && v < base + (1 << k)) { pre[a] = pp; sk[a] = k; suf[a] = v - base; break; }
+            }
+        }
+    }
+    for (int i = 0; i < pre[0]; i++) ce_bin(c, C_LAST_X + off + (i >> shift), 1);
+    if (pre[0] < cmax) ce_bin(c, C_LAST_X + off + (pre[0] >> shift), 0);
+    for (int i = 0; i < pre[1]; i++) ce_bin(c, C_LAST_Y + off + (i >> shift), 1);
+    if (pre[1] < cmax) ce_bin(c, C_LAST_Y + off + (pre[1] >> shift), 0);
+    if (pre[0] > 3) ce_fl(c, (uint32_t)suf[0], sk[0]);
+    if (pre[1] > 3) ce_fl(c, (uint32_t)suf[1], sk[1]);
+
+    int sbl = log2n - 2, sbw = 1 << sbl;
+    const uint8_t *sbscan = g_scan[sbl][scanIdx], *scan4 = g_scan[2][scanIdx];
+    int lastSub = sbw * sbw - 1, lastPos = 16;
+    for (;;) {
+        if (lastPos == 0) { lastPos = 16; lastSub--; }
+        lastPos--;
+        int xS = sbscan[lastSub] & 15, yS = sbscan[lastSub] >> 4;
+        int xC = (xS << 2) + (scan4[lastPos] & 15), yC = (yS << 2) + (scan4[lastPos] >> 4);
+        if (xC == lx && yC == ly) break;
+    }
+    int dens = P->density;
+    uint8_t csbf[8][8];
+    memset(csbf, 0, sizeof(csbf));
+    int g1prev = 1, first_sb_done = 0;
+    static const uint8_t ctxIdxMap[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+    for (int i = lastSub; i >= 0; i--) {
+        int xS = sbscan[i] & 15, yS = sbscan[i] >> 4;
+        int infer_dc = 0, coded;
+        if (i < lastSub && i > 0) {
+            int r = (xS + 1 < sbw) ? csbf[yS][xS + 1] : 0;
+            int b = (yS + 1 < sbw) ? csbf[yS + 1][xS] : 0;
+            coded = pct(&p->rng, 55);
+            ce_bin(c, C_CSBF + ((r + b) ? 1 : 0) + (cIdx ? 2 : 0), coded);
+            infer_dc = 1;
+        } else {
+            coded = 1;
+        }
+        csbf[yS][xS] = (uint8_t)coded;
+        int sig[16] = {0};
+        int prevCsbf = 0;
+        if (xS < sbw - 1) prevCsbf += csbf[yS][xS + 1];
+        if (yS < sbw - 1) prevCsbf += csbf[yS + 1][xS] << 1;
+        int nstart = (i == lastSub) ? lastPos - 1 : 15;
+        if (i == lastSub) sig[lastPos] = 1;
+        for (int nn = nstart; nn >= 0; nn--) {
+            int xP = scan4[nn] & 15, yP = scan4[nn] >> 4;
+            int xC = (xS << 2) + xP, yC = (yS << 2) + yP;
+            if (coded && (nn > 0 || !infer_dc)) {
+                int sigCtx;
+                if (log2n == 2) sigCtx = ctxIdxMap[(yC << 2) + xC];
+                else if (xC + yC == 0) sigCtx = 0;
+                else {
+                    if (prevCsbf == 0) sigCtx = (xP + yP == 0) ? 2 : (xP + yP < 3) ? 1 : 0;
+                    else if (prevCsbf == 1) sigCtx = (yP == 0) ? 2 : (yP == 1) ? 1 : 0;
+                    else if (prevCsbf == 2) sigCtx = (xP == 0) ? 2 : (xP == 1) ? 1 : 0;
+                    else sigCtx = 2;
+                    if (cIdx == 0) {
+                        if (xS > 0 || yS > 0) sigCtx += 3;
+                        sigCtx += (log2n == 3) ? ((scanIdx == 0) ? 9 : 15) : 21;
+                    } else {
+                        sigCtx += (log2n == 3) ? 9 : 12;
+                    }
+                }
+                sig[nn] = pct(&p->rng, dens);
+                ce_bin(c, C_SIG + (cIdx == 0 ? sigCtx : 27 + sigCtx), sig[nn]);
+                if (sig[nn]) infer_dc = 0;
+            } else if (coded && nn == 0 && infer_dc) {
+                sig[0] = 1;
+            }
+        }
+        int any = 0;
+        for (int nn = 0; nn < 16; nn++) any |= sig[nn];
+        if (!any) continue;
+        int ctxSet = (i == 0 || cIdx > 0) ? 0 : 2;
+        if (first_sb_done && g1prev == 0) ctxSet++;
+        first_sb_done = 1;
+        int g1c = 1, firstSig = 16, lastSig = -1, numG1 = 0, lastG1Pos = -1;
+        int g1[16] = {0}, g2[16] = {0};
+        for (int nn = 15; nn >= 0; nn--) {
+            if (!sig[nn]) continue;
+            if (numG1 < 8) {
+                g1[nn] = pct(&p->rng, 35);
+                ce_bin(c, C_GT1 + ctxSet * 4 + (g1c < 3 ? g1c : 3) + (cIdx ? 16 : 0), g1[nn]);
+                numG1++;
+                if (g1[nn] && lastG1Pos == -1) lastG1Pos = nn;
+                if (g1c > 0) g1c = g1[nn] ? 0 : g1c + 1;
+            }
+            if (lastSig == -1) lastSig = nn;
+            firstSig = nn;
+        }
+        g1prev = g1c;
+        int hidden = p->cu_bypass ? 0 : (lastSig - firstSig > 3);
+        if (lastG1Pos != -1) {
+            g2[lastG1Pos] = pct(&p->rng, 40);
+            ce_bin(c, C_GT2 + ctxSet + (cIdx ? 4 : 0), g2[lastG1Pos]);
+        }
+        for (int nn = 15; nn >= 0; nn--)
+            if (sig[nn] && (!P->sign_hiding || !hidden || nn != firstSig)) ce_bypass(c, pct(&p->rng, 50));
+        int numSig = 0, cLastAbs = 0, cLastRice = 0, firstRem = 1;
+        for (int nn = 15; nn >= 0; nn--) {
+            if (!sig[nn]) continue;
+            int base = 1 + g1[nn] + g2[nn];
+            if (base == ((numSig < 8) ? ((nn == lastG1Pos) ? 3 : 2) : 1)) {
+                int k;
+                if (firstRem) { k = 0; firstRem = 0; }
+                else k = cLastRice + (cLastAbs > 3 * (1 << cLastRice) ? 1 : 0) < 4
+                             ? cLastRice + (cLastAbs > 3 * (1 << cLastRice) ? 1 : 0) : 4;
+                int rem = draw_remaining(p);
+                ce_calr(c, rem, k);
+                cLastAbs = base + rem;
+                cLastRice = k;
+            }
+            numSig++;
+        }
+    }
+}
+
+static void transform_unit(pic_t *p, int x0, int y0, int log2n, int blk, int cbf_l, int cbf_cb, int cbf_cr,
+                           int pcb, int pcr) {
+    const synth_params *P = p->P;
+    int chroma4 = log2n == 2;
+    int cbfChroma = P->chroma_format == 0 ? 0 : (chroma4 ? (pcb || pcr) : (cbf_cb || cbf_cr));
+    if ((cbf_l || cbfChroma) && P->cu_qp_delta && !p->is_qp_coded) {
+        int lim = 26 + p->qpbdY / 2;
+        int v = pct(&p->rng, 70) ? rnd(&p->rng, 5) - 2 : rnd(&p->rng, 2 * lim) - lim;
+        int a = v < 0 ? -v : v;
+        for (int i = 0; i < (a < 5 ? a : 5); i++) ce_bin(&p->c, C_CU_QP_DELTA + (i == 0 ? 0 : 1), 1);
+        if (a < 5) ce_bin(&p->c, C_CU_QP_DELTA + (a == 0 ? 0 : 1), 0);
+        else ce_egk(&p->c, (uint32_t)(a - 5), 0);
+        if (a) ce_bypass(&p->c, v < 0);
+        p->is_qp_coded = 1;
+    }
+    int lmode = p->ipm[(y0 >> 2) * p->w4 + (x0 >> 2)];
+    if (cbf_l) residual_coding(p, log2n, 0, lmode);
+    if (P->chroma_format == 0) return;
+    if (!chroma4) {
+        if (cbf_cb) residual_coding(p, log2n - 1, 1, p->chroma_mode);
+        if (cbf_cr) residual_coding(p, log2n - 1, 2, p->chroma_mode);
+    } else if (blk == 3) {
+        if (pcb) residual_coding(p, 2, 1, p->chroma_mode);
+        if (pcr) residual_coding(p, 2, 2, p->chroma_mode);
+    }
+}
+
+static void transform_tree(pic_t *p, int x0, int y0, int log2n, int depth, int blk, int pcb, int pcr) {
+    const synth_params *P = p->P;
+    int split;
+    if (log2n <= P->log2_max_tb && log2n > P->log2_min_tb && depth < p->max_trafo_depth &&
+        !(p->intra_split && depth == 0)) {
+        split = pct(&p->rng, 40);
+        ce_bin(&p->c, C_SPLIT_TF + 5 - log2n, split);
+    } else {
+        split = (log2n > P->log2_max_tb || (p->intra_split && depth == 0));
+    }
+    int cbf_cb = 0, cbf_cr = 0;
+    if (log2n > 2 && P->chroma_format != 0) {
+        if (depth == 0 || pcb) { cbf_cb = pct(&p->rng, 50); ce_bin(&p->c, C_CBF_CHROMA + depth, cbf_cb); }
+        if (depth == 0 || pcr) { cbf_cr = pct(&p->rng, 50); ce_bin(&p->c, C_CBF_CHROMA + depth, cbf_cr); }
+    }
+    if (split) {
+        int h = 1 << (log2n - 1);
+        transform_tree(p, x0, y0, log2n - 1, depth + 1, 0, cbf_cb, cbf_cr);
+        transform_tree(p, x0 + h, y0, log2n - 1, depth + 1, 1, cbf_cb, cbf_cr);
+        transform_tree(p, x0, y0 + h, log2n - 1, depth + 1, 2, cbf_cb, cbf_cr);
+        transform_tree(p, x0 + h, y0 + h, log2n - 1, depth + 1, 3, cbf_cb, cbf_cr);
+        return;
+    }
+    int cbf_l = pct(&p->rng, 60);
+    ce_bin(&p->c, C_CBF_LUMA + (depth == 0 ? 1 : 0), cbf_l);
+    transform_unit(p, x0, y0, log2n, blk, cbf_l, cbf_cb, cbf_cr, pcb, pcr);
+}
+
+/* 8.4.2 candidate list */
+static void mpm_list(pic_t *p, int xPb, int yPb, int l[3]) {
+    int cand[2];
+    for (int k = 0; k < 2; k++) {
+        int xn = k == 0 ? xPb - 1 : xPb, yn = k == 0 ? yPb : yPb - 1;
+        if (xn < 0 || yn < 0) cand[k] = 1;
+        else if (k == 1 && yPb - 1 < ((yPb >> p->log2ctb) << p->log2ctb)) cand[k] = 1;
+        else cand[k] = p->ipm[(yn >> 2) * p->w4 + (xn >> 2)];
+    }
+    if (cand[0] == cand[1]) {
+        if (cand[0] < 2) { l[0] = 0; l[1] = 1; l[2] = 26; }
+        else { l[0] = cand[0]; l[1] = 2 + ((cand[0] + 29) % 32); l[2] = 2 + ((cand[0] - 2 + 1) % 32); }
+    } else {
+        l[0] = cand[0];
+        l[1] = cand[1];
+        if (l[0] != 0 && l[1] != 0) l[2] = 0;
+        else if (l[0] != 1 && l[1] != 1) l[2] = 1;
+        else l[2] = 26;
+    }
+}
+
+static void coding_unit(pic_t *p, int x0, int y0, int log2cb, int depth) {
+    const synth_params *P = p->P;
+    cabe_t *c = &p->c;
+    int n = 1 << log2cb;
+    p->cu_bypass = 0;
+    if (P->tq_bypass) { p->cu_bypass = pct(&p->rng, 15); ce_bin(c, C_TQ_BYPASS, p->cu_bypass); }
+    int nxn = 0;
+    if (log2cb == P->log2_min_cb) {
+        nxn = log2cb > P->log2_min_tb ? pct(&p->rng, 35) : 0;
+        ce_bin(c, C_PART_MODE, !nxn);
+    }
+    set_map(p, p->depth, x0, y0, n, (uint8_t)depth);
+    int np = nxn ? 4 : 1, pb = nxn ? n / 2 : n;
+    int prev[4], mpm[4] = {0}, rem[4] = {0};
+    for (int i = 0; i < np; i++) {
+        prev[i] = pct(&p->rng, 45);
+        ce_bin(c, C_PREV_INTRA, prev[i]);
+    }
+    for (int i = 0; i < np; i++) {
+        if (prev[i]) {
+            mpm[i] = rnd(&p->rng, 3);
+            ce_bypass(c, mpm[i] > 0);
+            if (mpm[i] > 0) ce_bypass(c, mpm[i] > 1);
+        } else {
+            rem[i] = rnd(&p->rng, 32);
+            ce_fl(c, (uint32_t)rem[i], 5);
+        }
+        int xPb = x0 + (i & 1) * pb, yPb = y0 + (i >> 1) * pb;
+        int l[3], m;
+        mpm_list(p, xPb, yPb, l);
+        if (prev[i]) m = l[mpm[i]];
+        else {
+            if (l[0] > l[1]) { int t = l[0]; l[0] = l[1]; l[1] = t; }
+            if (l[0] > l[2]) { int t = l[0]; l[0] = l[2]; l[2] = t; }
+            if (l[1] > l[2]) { int t = l[1]; l[1] = l[2]; l[2] = t; }
+            m = rem[i];
+            for (int k = 0; k < 3; k++)
+                if (m >= l[k]) m++;
+        }
+        set_map(p, p->ipm, xPb, yPb, pb, (uint8_t)m);
+    }
+    if (P->chroma_format != 0) {
+        int icpm = rnd(&p->rng, 5);
+        ce_bin(c, C_CHROMA_MODE, icpm != 4);
+        if (icpm != 4) ce_fl(c, (uint32_t)icpm, 2);
+        int lm = p->ipm[(y0 >> 2) * p->w4 + (x0 >> 2)];
+        static const int base[4] = {0, 26, 10, 1};
+        p->chroma_mode = icpm == 4 ? lm : (base[icpm] == lm ? 34 : base[icpm]);
+    }
+    p->intra_split = nxn;
+    p->max_trafo_depth = P->max_th_depth_intra + nxn;
+    transform_tree(p, x0, y0, log2cb, 0, 0, 0, 0);
+}
+
+static void coding_quadtree(pic_t *p, int x0, int y0, int log2cb, int depth) {
+    const synth_params *P = p->P;
+    int n = 1 << log2cb, split;
+    if (x0 + n <= p->W && y0 + n <= p->H && log2cb > P->log2_min_cb) {
+        int cond = 0;
+        if (x0 > 0 && p->depth[(y0 >> 2) * p->w4 + ((x0 - 1) >> 2)] > depth) cond++;
+        if (y0 > 0 && p->depth[((y0 - 1) >> 2) * p->w4 + (x0 >> 2)] > depth) cond++;
+        split = pct(&p->rng, log2cb >= 5 ? 60 : 45);
+        ce_bin(&p->c, C_SPLIT_CU + cond, split);
+    } else {
+        split = log2cb > P->log2_min_cb;
+    }
+    if (P->cu_qp_delta && log2cb >= p->log2ctb - P->diff_cu_qp_delta_depth) p->is_qp_coded = 0;
+    if (split) {
+        int h = n >> 1;
+        coding_quadtree(p, x0, y0, log2cb - 1, depth + 1);
+        if (x0 + h < p->W) coding_quadtree(p, x0 + h, y0, log2cb - 1, depth + 1);
+        if (y0 + h < p->H) coding_quadtree(p, x0, y0 + h, log2cb - 1, depth + 1);
+        if (x0 + h < p->W && y0 + h < p->H) coding_quadtree(p, x0 + h, y0 + h, log2cb - 1, depth + 1);
+        return;
+    }
+    coding_unit(p, x0, y0, log2cb, depth);
+}
+
+/* 7.3.8.3 */
+static void sao_syntax(pic_t *p, int rx, int ry, int sao_l, int sao_c) {
+    const synth_params *P = p->P;
+    cabe_t *c = &p->c;
+    if (rx > 0) {
+        int ml = pct(&p->rng, 25);
+        ce_bin(c, C_SAO_MERGE, ml);
+        if (ml) return;
+    }
+    if (ry > 0) {
+        int mu = pct(&p->rng, 25);
+        ce_bin(c, C_SAO_MERGE, mu);
+        if (mu) return;
+    }
+    int ncomp = P->chroma_format ? 3 : 1, type1 = 0;
+    for (int ci = 0; ci < ncomp; ci++) {
+        if (!((sao_l && ci == 0) || (sao_c && ci > 0))) continue;
+        int t;
+        if (ci < 2) {
+            t = rnd(&p->rng, 3);
+            ce_bin(c, C_SAO_TYPE, t != 0);
+            if (t) ce_bypass(c, t == 2);
+            if (ci == 1) type1 = t;
+        } else {
+            t = type1;
+        }
+        if (!t) continue;
+        int bd = P->bit_depth, cmax = (1 << ((bd < 10 ? bd : 10) - 5)) - 1;
+        int a[4];
+        for (int i = 0; i < 4; i++) {
+            a[i] = pct(&p->rng, 30) ? 0 : rnd(&p->rng, cmax + 1);
+            ce_tr_bypass(c, a[i], cmax, 0);
+        }
+        if (t == 1) {
+            for (int i = 0; i < 4; i++)
+                if (a[i]) ce_bypass(c, pct(&p->rng, 50));
+            ce_fl(c, (uint32_t)rnd(&p->rng, 32), 5);
+        } else if (ci < 2) {
+            ce_fl(c, (uint32_t)rnd(&p->rng, 4), 2);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* NAL assembly                                                         */
+/* ------------------------------------------------------------------ */
+static void nal_header(bw_t *w, int type) {
+    bw_bits(w, 0, 1);
+    bw_bits(w, (uint32_t)type, 6);
+    bw_bits(w, 0, 6);
+    bw_bits(w, 1, 3);
+}
+
+/* copy rbsp[hdr..) with emulation prevention (7.4.2); returns bytes written */
+static size_t ep_insert(const uint8_t *in, size_t n, uint8_t *out, size_t cap, int *zeros_io) {
+    size_t o = 0;
+    int z = zeros_io ? *zeros_io : 0;
+    for (size_t i = 0; i < n; i++) {
+        if (z >= 2 && in[i] <= 3) {
+            if (o >= cap) return (size_t)-1;
+            out[o++] = 3;
+            z = 0;
+        }
+        if (o >= cap) return (size_t)-1;
+        out[o++] = in[i];
+        z = in[i] == 0 ? z + 1 : 0;
+    }
+    if (zeros_io) *zeros_io = z;
+    return o;
+}
+
+static int profile_idc(const synth_params *P) {
+    if (P->chroma_format == 0 || P->bit_depth > 10) return 4;
+    return P->bit_depth > 8 ? 2 : 1;
+}
+
+static void ptl(bw_t *w, const synth_params *P) {
+    int pi = profile_idc(P);
+    bw_bits(w, 0, 2);
+    bw_bits(w, 0, 1);
+    bw_bits(w, (uint32_t)pi, 5);
+    uint32_t compat = 1u << (31 - pi);
+    if (pi == 1) compat |= 1u << (31 - 2);
+    bw_bits(w, compat, 32);
+    bw_bits(w, 1, 1); /* progressive */
+    bw_bits(w, 0, 1);
+    bw_bits(w, 0, 1);
+    bw_bits(w, 1, 1); /* frame only */
+    bw_bits(w, 0, 32);
+    bw_bits(w, 0, 11);
+    bw_bits(w, 0, 1);
+    bw_bits(w, 183, 8); /* level 6.1 */
+}
+
+static long finish_nal(bw_t *w, uint8_t *out, size_t cap) {
+    if (w->err) { free(w->d); return -1; }
+    if (cap < 2) { free(w->d); return -1; }
+    out[0] = w->d[0];
+    out[1] = w->d[1];
+    size_t m = ep_insert(w->d + 2, w->n - 2, out + 2, cap - 2, NULL);
+    free(w->d);
+    if (m == (size_t)-1) return -1;
+    return (long)(m + 2);
+}
+
+long synth_vps(const synth_params *P, uint8_t *out, size_t cap) {
+    bw_t w = {0};
+    nal_header(&w, 32);
+    bw_bits(&w, 0, 4);
+    bw_bits(&w, 1, 1);
+    bw_bits(&w, 1, 1);
+    bw_bits(&w, 0, 6);
+    bw_bits(&w, 0, 3);
+    bw_bits(&w, 1, 1);
+    bw_bits(&w, 0xffff, 16);
+    ptl(&w, P);
+    bw_bits(&w, 1, 1);
+    bw_ue(&w, 0);
+    bw_ue(&w, 0);
+    bw_ue(&w, 0);
+    bw_bits(&w, 0, 6);
+    bw_ue(&w, 0);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, 0, 1);
+    bw_align1(&w);
+    return finish_nal(&w, out, cap);
+}
+
+long synth_sps(const synth_params *P, uint8_t *out, size_t cap) {
+    bw_t w = {0};
+    nal_header(&w, 33);
+    bw_bits(&w, 0, 4);
+    bw_bits(&w, 0, 3);
+    bw_bits(&w, 1, 1);
+    ptl(&w, P);
+    bw_ue(&w, 0);
+    bw_ue(&w, (uint32_t)P->chroma_format);
+    bw_ue(&w, (uint32_t)P->width);
+    bw_ue(&w, (uint32_t)P->height);
+    int sub = P->chroma_format == 1 ? 2 : 1;
+    if (P->conf_right || P->conf_bottom) {
+        bw_bits(&w, 1, 1);
+        bw_ue(&w, 0);
+        bw_ue(&w, (uint32_t)(P->conf_right / sub));
+        bw_ue(&w, 0);
+        bw_ue(&w, (uint32_t)(P->conf_bottom / sub));
+    } else {
+        bw_bits(&w, 0, 1);
+    }
+    bw_ue(&w, (uint32_t)(P->bit_depth - 8));
+    bw_ue(&w, (uint32_t)(P->bit_depth - 8));
+    bw_ue(&w, 4);
+    bw_bits(&w, 1, 1);
+    bw_ue(&w, 0);
+    bw_ue(&w, 0);
+    bw_ue(&w, 0);
+    bw_ue(&w, (uint32_t)(P->log2_min_cb - 3));
+    bw_ue(&w, (uint32_t)(P->log2_ctb - P->log2_min_cb));
+    bw_ue(&w, (uint32_t)(P->log2_min_tb - 2));
+    bw_ue(&w, (uint32_t)(P->log2_max_tb - P->log2_min_tb));
+    bw_ue(&w, 0);
+    bw_ue(&w, (uint32_t)P->max_th_depth_intra);
+    bw_bits(&w, P->scaling_list ? 1 : 0, 1);
+    if (P->scaling_list) bw_bits(&w, 0, 1); /* default lists (Tables 7-5 / 7-6) */
+    bw_bits(&w, 0, 1);                      /* amp */
+    bw_bits(&w, P->sao ? 1 : 0, 1);
+    bw_bits(&w, 0, 1);                      /* pcm */
+    bw_ue(&w, 0);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, P->strong_intra ? 1 : 0, 1);
+    bw_bits(&w, 0, 1); /* vui */
+    bw_bits(&w, 0, 1); /* extensions */
+    bw_align1(&w);
+    return finish_nal(&w, out, cap);
+}
+
+long synth_pps(const synth_params *P, uint8_t *out, size_t cap) {
+    bw_t w = {0};
+    nal_header(&w, 34);
+    bw_ue(&w, 0);
+    bw_ue(&w, 0);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, 0, 3);
+    bw_bits(&w, P->sign_hiding ? 1 : 0, 1);
+    bw_bits(&w, 0, 1);
+    bw_ue(&w, 0);
+    bw_ue(&w, 0);
+    bw_se(&w, P->init_qp - 26);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, P->transform_skip ? 1 : 0, 1);
+    bw_bits(&w, P->cu_qp_delta ? 1 : 0, 1);
+    if (P->cu_qp_delta) bw_ue(&w, (uint32_t)P->diff_cu_qp_delta_depth);
+    bw_se(&w, P->cb_qp_offset);
+    bw_se(&w, P->cr_qp_offset);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, P->tq_bypass ? 1 : 0, 1);
+    bw_bits(&w, 0, 1); /* tiles */
+    bw_bits(&w, 1, 1); /* entropy_coding_sync */
+    bw_bits(&w, 0, 1); /* loop filter across slices */
+    bw_bits(&w, 1, 1); /* deblocking control present */
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, P->deblock_disabled ? 1 : 0, 1);
+    if (!P->deblock_disabled) {
+        bw_se(&w, P->beta_offset_div2);
+        bw_se(&w, P->tc_offset_div2);
+    }
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, 0, 1);
+    bw_ue(&w, 0);
+    bw_bits(&w, 0, 1);
+    bw_bits(&w, 0, 1);
+    bw_align1(&w);
+    return finish_nal(&w, out, cap);
+}
+
+int synth_check_params(const synth_params *P) {
+    if (P->chroma_format != 0 && P->chroma_format != 1) return -1;
+    if (P->bit_depth < 8 || P->bit_depth > 10) return -1;
+    if (P->log2_min_cb < 3 || P->log2_ctb < 4 || P->log2_ctb > 6 || P->log2_min_cb > P->log2_ctb) return -1;
+    if (P->log2_min_tb != 2 || P->log2_max_tb < P->log2_min_tb || P->log2_max_tb > 5 ||
+        P->log2_max_tb > P->log2_ctb || P->log2_min_tb >= P->log2_min_cb)
+        return -1;
+    if (P->max_th_depth_intra < 0 || P->max_th_depth_intra > P->log2_ctb - P->log2_min_tb) return -1;
+    if (P->width <= 0 || P->height <= 0 || (P->width & ((1 << P->log2_min_cb) - 1)) ||
+        (P->height & ((1 << P->log2_min_cb) - 1)))
+        return -1;
+    if (P->diff_cu_qp_delta_depth < 0 || P->diff_cu_qp_delta_depth > P->log2_ctb - P->log2_min_cb) return -1;
+    if (P->density < 0 || P->density > 100) return -1;
+    return 0;
+}
+
+long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t cap) {
+    if (synth_check_params(P)) return -2;
+    init_scans();
+    pic_t pic;
+    memset(&pic, 0, sizeof(pic));
+    pic_t *p = &pic;
+    p->P = P;
+    p->rng = seed * 0x2545F4914F6CDD1Dull + 0x1234567ull;
+    p->W = P->width;
+    p->H = P->height;
+    p->log2ctb = P->log2_ctb;
+    p->ctb = 1 << P->log2_ctb;
+    p->wctb = (p->W + p->ctb - 1) >> p->log2ctb;
+    p->hctb = (p->H + p->ctb - 1) >> p->log2ctb;
+    p->w4 = (p->W + 3) >> 2;
+    p->h4 = (p->H + 3) >> 2;
+    p->qpbdY = 6 * (P->bit_depth - 8);
+    p->ipm = (uint8_t *)calloc((size_t)p->w4 * p->h4, 1);
+    p->depth = (uint8_t *)calloc((size_t)p->w4 * p->h4, 1);
+    bw_t *subs = (bw_t *)calloc((size_t)p->hctb, sizeof(bw_t));
+    if (!p->ipm || !p->depth || !subs) { free(p->ipm); free(p->depth); free(subs); return -1; }
+    int slice_qp_delta = P->slice_qp_delta;
+    int slice_qp = P->init_qp + slice_qp_delta;
+    int sao_l = P->sao ? !pct(&p->rng, 10) : 0;
+    int sao_c = (P->sao && P->chroma_format) ? !pct(&p->rng, 10) : 0;
+    uint8_t wst[C_NUM], wmps[C_NUM];
+    int saved = 0;
+    ce_init_ctx(&p->c, slice_qp);
+    for (int ry = 0; ry < p->hctb; ry++) {
+        ce_start(&p->c, &subs[ry]);
+        if (ry > 0) {
+            if (p->wctb > 1 && saved) { memcpy(p->c.st, wst, C_NUM); memcpy(p->c.mps, wmps, C_NUM); }
+            else ce_init_ctx(&p->c, slice_qp);
+        }
+        for (int rx = 0; rx < p->wctb; rx++) {
+            if (sao_l || sao_c) sao_syntax(p, rx, ry, sao_l, sao_c);
+            coding_quadtree(p, rx << p->log2ctb, ry << p->log2ctb, p->log2ctb, 0);
+            if (rx == 1) { memcpy(wst, p->c.st, C_NUM); memcpy(wmps, p->c.mps, C_NUM); saved = 1; }
+            int last = (rx == p->wctb - 1 && ry == p->hctb - 1);
+            ce_term(&p->c, last);
+        }
+        if (ry != p->hctb - 1) ce_term(&p->c, 1); /* end_of_subset_one_bit */
+        ce_finish(&p->c);
+        bw_align1(&subs[ry]); /* byte_alignment() / rbsp_slice_segment_trailing_bits() */
+    }
+    /* substreams with emulation prevention, to size the entry points */
+    long ret = -1;
+    size_t total = 0;
+    int err = 0;
+    for (int r = 0; r < p->hctb; r++) { total += subs[r].n; err |= subs[r].err; }
+    uint8_t *data = (uint8_t *)malloc(total * 3 / 2 + 16);
+    size_t *sub_len = (size_t *)calloc((size_t)p->hctb, sizeof(size_t));
+    if (data && sub_len && !err) {
+        size_t o = 0;
+        int z = 0; /* the slice header ends in a nonzero byte (its alignment bit) */
+        for (int r = 0; r < p->hctb; r++) {
+            size_t m = ep_insert(subs[r].d, subs[r].n, data + o, total * 3 / 2 + 16 - o, &z);
+            sub_len[r] = m;
+            o += m;
+        }
+        bw_t w = {0};
+        nal_header(&w, 19);
+        bw_bits(&w, 1, 1); /* first_slice_segment_in_pic_flag */
+        bw_bits(&w, 0, 1); /* no_output_of_prior_pics_flag */
+        bw_ue(&w, 0);
+        bw_ue(&w, 2);      /* I slice */
+        if (P->sao) {
+            bw_bits(&w, (uint32_t)sao_l, 1);
+            if (P->chroma_format) bw_bits(&w, (uint32_t)sao_c, 1);
+        }
+        bw_se(&w, slice_qp_delta);
+        bw_ue(&w, (uint32_t)(p->hctb - 1));
+        if (p->hctb > 1) {
+            size_t mx = 1;
+            for (int r = 0; r < p->hctb - 1; r++) mx = sub_len[r] > mx ? sub_len[r] : mx;
+            int len = 1;
+            while (((size_t)1 << len) < mx) len++;
+            bw_ue(&w, (uint32_t)(len - 1));
+            for (int r = 0; r < p->hctb - 1; r++) bw_bits(&w, (uint32_t)(sub_len[r] - 1), len);
+        }
+        bw_align1(&w);
+        if (!w.err) {
+            uint8_t *hdr = (uint8_t *)malloc(w.n * 3 / 2 + 4);
+            size_t hm = hdr ? ep_insert(w.d + 2, w.n - 2, hdr, w.n * 3 / 2 + 4, NULL) : (size_t)-1;
+            if (hm != (size_t)-1 && 2 + hm + o <= cap) {
+                out[0] = w.d[0];
+                out[1] = w.d[1];
+                memcpy(out + 2, hdr, hm);
+                memcpy(out + 2 + hm, data, o);
+                ret = (long)(2 + hm + o);
+            } else if (hm != (size_t)-1) {
+                ret = -3; /* capacity */
+            }
+            free(hdr);
+        }
+        free(w.d);
+    }
+    free(data);
+    free(sub_len);
+    for (int r = 0; r < p->hctb; r++) free(subs[r].d);
+    free(subs);
+    free(p->ipm);
+    free(p->depth);
+    return ret;
+}

@@ -1,0 +1,37 @@
+/* hevc_synth.h — synthetic HEVC intra bitstream generator (see hevc_synth.c).
+ * Data generator for tests and benchmarks; not part of the decode path. */
+#ifndef HEVC_SYNTH_H
+#define HEVC_SYNTH_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    int32_t width, height;            /* pic_width/height_in_luma_samples (multiples of MinCbSize) */
+    int32_t conf_right, conf_bottom;  /* conformance-window crop in luma samples (even for 4:2:0) */
+    int32_t chroma_format;            /* 0 = 4:0:0, 1 = 4:2:0 */
+    int32_t bit_depth;                /* 8..10, luma = chroma */
+    int32_t log2_ctb, log2_min_cb, log2_min_tb, log2_max_tb, max_th_depth_intra;
+    int32_t sign_hiding, cu_qp_delta, diff_cu_qp_delta_depth;
+    int32_t transform_skip, tq_bypass, scaling_list, strong_intra;
+    int32_t init_qp, slice_qp_delta, cb_qp_offset, cr_qp_offset;
+    int32_t sao, deblock_disabled, beta_offset_div2, tc_offset_div2;
+    int32_t density;                  /* sig_coeff_flag probability, percent */
+} synth_params;
+
+/* Each returns the NAL unit length (2-byte header included, emulation
+ * prevention applied) or a negative value (-1 allocation / -2 parameters /
+ * -3 capacity). */
+long synth_vps(const synth_params *p, uint8_t *out, size_t cap);
+long synth_sps(const synth_params *p, uint8_t *out, size_t cap);
+long synth_pps(const synth_params *p, uint8_t *out, size_t cap);
+/* One IDR picture (a single I slice, WPP substreams + entry points). */
+long synth_picture(const synth_params *p, uint64_t seed, uint8_t *out, size_t cap);
+int synth_check_params(const synth_params *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

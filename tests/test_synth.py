@@ -1,0 +1,203 @@
+"""Synthetic HEVC-intra inputs (Main-10 / 8K grid,
+BASELINE config 5, plus the coding tools halfmoonbay does not use).
+
+The generator (heif_amd/csrc/synth/hevc_synth.c) draws every syntax element
+at random, so a stream it writes is decodable only if encoder and decoder
+agree on every context selection and binarization: the oracle's per-substream
+self-check (end_of_subset_one_bit at the entry point, alignment bits) fails
+almost surely otherwise.  Reconstruction of these streams is "parity
+unpinned" against the reference (it computes no pixels and ships no 10-bit
+sample); the GPU must equal the oracle bit-exactly.
+"""
+import hashlib
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+S = pytest.importorskip("heif_amd.synth_encoder")
+
+# (name, overrides): every optional tool, bit depths 8/9/10, 4:0:0, CTB 16/32/64,
+# partial CTBs and a conformance crop
+CASES = [
+    ("main8", dict()),
+    ("main10", dict(bit_depth=10)),
+    ("mono10", dict(bit_depth=10, chroma_format=0)),
+    ("mono8", dict(chroma_format=0)),
+    ("b9_ctb16", dict(bit_depth=9, log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2, diff_cu_qp_delta_depth=0)),
+    ("ctb64_tskip_bypass", dict(bit_depth=10, log2_ctb=6, max_th_depth_intra=3, diff_cu_qp_delta_depth=2,
+                                transform_skip=1, tq_bypass=1)),
+    ("scaling_nosdh_qpoff", dict(bit_depth=10, scaling_list=1, sign_hiding=0, strong_intra=0, cb_qp_offset=-3,
+                                 cr_qp_offset=5, init_qp=40, slice_qp_delta=-30)),
+    ("lowqp_dense_dbk_offsets", dict(bit_depth=10, init_qp=22, slice_qp_delta=-33, beta_offset_div2=3,
+                                     tc_offset_div2=-2, density=80)),
+    ("no_loopfilter_cb16", dict(deblock_disabled=1, sao=0, cu_qp_delta=0, log2_min_cb=4)),
+    ("crop_200x120", dict(width=200, height=120, conf_right=6, conf_bottom=2, bit_depth=10)),
+    ("one_cb", dict(width=8, height=8)),
+    ("ctb64_partial", dict(width=72, height=40, log2_ctb=6, bit_depth=10, tq_bypass=1, transform_skip=1,
+                           scaling_list=1)),
+]
+
+
+def params(over):
+    return S.SynthParams(**{**dict(width=128, height=96), **over})
+
+
+def checks_ok(img):
+    return all(c["term_ok"] and c["raw_start"] == c["raw_entry"] for c in img.checks)
+
+
+@pytest.mark.parametrize("name,over", CASES, ids=[c[0] for c in CASES])
+def test_oracle_decodes_synthetic_streams(oracle_mod, name, over):
+    p = params(over)
+    for seed in range(4):
+        data = S.single_heic(p, seed=seed)
+        img = oracle_mod.decode_heic(data)
+        assert checks_ok(img), (name, seed)
+        assert img.bit_depth == p.bit_depth
+        assert img.y.shape == (p.height - p.conf_bottom, p.width - p.conf_right)
+        assert (img.cb is None) == (p.chroma_format == 0)
+        assert int(img.y.max()) < (1 << p.bit_depth)
+
+
+def test_generator_is_deterministic():
+    p = params(dict(bit_depth=10))
+    assert S.picture(p, 3) == S.picture(p, 3)
+    assert S.picture(p, 3) != S.picture(p, 4)
+
+
+def test_generator_rejects_bad_parameters():
+    with pytest.raises(ValueError):
+        S.picture(params(dict(width=100)), 0)      # not a multiple of MinCbSize
+    with pytest.raises(ValueError):
+        S.picture(params(dict(bit_depth=12)), 0)
+    with pytest.raises(ValueError):
+        S.picture(params(dict(log2_max_tb=6, log2_ctb=6)), 0)
+
+
+def test_host_parses_config5_grid(oracle_mod):
+    """BASELINE config 5 geometry: 7680x4320 10-bit -> 15 x 9 tiles of 512x512."""
+    import heif_amd as H
+
+    p = S.SynthParams(bit_depth=10, density=5)
+    pics = [S.picture(p, 0)] * 135           # geometry only: one picture repeated
+    data = S.grid_heic(7680, 4320, p, pictures=pics)
+    meta = oracle_mod.read_meta(data)
+    assert (meta["grid_rows"], meta["grid_cols"], meta["num_tiles"]) == (9, 15, 135)
+    assert (meta["out_width"], meta["out_height"], meta["luma_bits"]) == (7680, 4320, 10)
+    inf = H.HeifImage.parse(data).info
+    assert (inf.width, inf.height, inf.bit_depth, inf.bytes_per_sample) == (7680, 4320, 10, 2)
+
+
+def _golden_hash(img):
+    h = hashlib.sha256()
+    for pl in (img.y, img.cb, img.cr):
+        if pl is not None:
+            h.update(pl.astype("<u2").tobytes())
+    return h.hexdigest()
+
+
+def test_oracle_synthetic_golden_hashes(oracle_mod):
+    """Regression pin of the oracle's reconstruction of two synthetic streams
+    (tests/golden/synth_planes.json, written by tools/make_golden.py)."""
+    g = json.loads((GOLDEN / "synth_planes.json").read_text())
+    for name, ent in g.items():
+        p = S.SynthParams(**ent["params"])
+        data = S.grid_heic(ent["out_w"], ent["out_h"], p, seed=ent["seed"])
+        assert hashlib.sha256(data).hexdigest() == ent["heic_sha256"], name
+        assert _golden_hash(oracle_mod.decode_heic(data, with_checks=False)) == ent["planes_sha256"], name
+
+
+# ------------------------------------------------------------------ GPU parity
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def H():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import heif_amd
+
+    return heif_amd
+
+
+def _planes(o):
+    return [None if t is None else t.cpu().numpy().astype(np.uint16) for t in (o.y, o.cb, o.cr)]
+
+
+def _assert_equal(got, img, tag):
+    for g, r, c in zip(got, (img.y, img.cb, img.cr), "YUV"):
+        if r is None:
+            assert g is None, tag
+            continue
+        assert g.shape == r.shape, (tag, c)
+        bad = int((g != r).sum())
+        assert bad == 0, f"{tag} {c}: {bad} samples differ"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,over", CASES, ids=[c[0] for c in CASES])
+def test_gpu_synthetic_bit_exact(H, oracle_mod, name, over):
+    p = params(over)
+    for seed in range(2):
+        data = S.single_heic(p, seed=seed)
+        out = H.HeicDecoder.decode(data)
+        torch.cuda.synchronize()
+        _assert_equal(_planes(out), oracle_mod.decode_heic(data, with_checks=False), (name, seed))
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_geometry_batch(H, oracle_mod):
+    """One batch of 10-bit 4:2:0 grids whose tiles differ in size, CTB size and
+    coding tools (one SeqParams per distinct SPS/PPS); a batch that mixes bit
+    depth or chroma format is rejected with HEIFGPU_E_UNSUPPORTED."""
+    datas = [S.grid_heic(1000, 700, params(dict(width=256, height=256, bit_depth=10)), seed=1),
+             S.grid_heic(900, 500, params(dict(bit_depth=10, log2_ctb=6, transform_skip=1, tq_bypass=1)), seed=2),
+             S.grid_heic(300, 200, params(dict(width=64, height=64, bit_depth=10, log2_ctb=4, log2_max_tb=4,
+                                               scaling_list=1)), seed=3)]
+    ctx = H.DecodeContext(0)
+    imgs = [H.HeifImage.parse(d) for d in datas]
+    b = ctx.prepare(imgs)
+    outs = ctx.alloc_outputs(imgs)
+    b.decode_async(outs)
+    assert b.status() == [0, 0, 0]
+    for k, (d, o) in enumerate(zip(datas, outs)):
+        _assert_equal(_planes(o), oracle_mod.decode_heic(d, with_checks=False), k)
+    b.free()
+    mixed = [H.HeifImage.parse(datas[0]), H.HeifImage.parse(S.single_heic(params(dict()), seed=4))]
+    with pytest.raises(H.UnsupportedError):
+        ctx.prepare(mixed)
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_config5_8k_main10_grid(H, oracle_mod):
+    """BASELINE config 5 at full size: 7680x4320 Main-10 grid, 135 tiles."""
+    c5 = S.CONFIG5
+    data = S.grid_heic(c5["out_w"], c5["out_h"], c5["params"], seed=5)
+    out = H.HeicDecoder.decode(data)
+    torch.cuda.synchronize()
+    assert out.y.dtype == torch.int16 and out.y.shape == (4320, 7680)
+    _assert_equal(_planes(out), oracle_mod.decode_heic(data, with_checks=False), "config5")
+
+
+# ------------------------------------------- kernels compiled for the host
+@pytest.mark.parametrize("parser", ["lanes", "scalar"])
+def test_emulated_kernels_on_synthetic_streams(tmp_path, parser):
+    """The GPU kernels' source built for the host (HG_HOST_EMU, see
+    test_emulation.py) decodes every synthetic case bit-exactly vs the oracle."""
+    import os
+    import pathlib
+    import subprocess
+
+    csrc = pathlib.Path(__file__).resolve().parents[1] / "heif_amd" / "csrc"
+    subprocess.run(["make", "-s", "-C", str(csrc), "emu-fast"], check=True, capture_output=True)
+    exe = csrc / "build" / "emu_fast" / "emu_check"
+    env = dict(os.environ, HEIFGPU_PARSE=parser)
+    for name, over in CASES:
+        path = tmp_path / f"{name}.heic"
+        path.write_bytes(S.single_heic(params(over), seed=1))
+        r = subprocess.run([str(exe), str(path), "5"], capture_output=True, text=True, env=env, timeout=300)
+        assert r.returncode == 0 and "EMU PARITY OK" in r.stdout + r.stderr, (name, (r.stdout + r.stderr)[-400:])
