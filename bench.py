@@ -18,6 +18,11 @@ kernel-trace average of the same command); algorithmic bytes per image =
 compressed tile bytes + reconstructed planes (SURVEY.md §8(d):
 1,704,187 + 18,874,368 B).
 
+--workload config5 (side measurement, not the headline line): BASELINE
+config 5, 7680x4320 Main-10 grids (15 x 9 tiles of 512x512, 16-bit planes)
+from heif_amd/synth_encoder.py; image i is a permutation (seed i) of one pool
+of 135 synthetic 10-bit tiles.
+
 cpu_baseline: the CPU oracle (oracle/, spec restatement; the reference Rust
 path cannot decode pixels) decoding tiles on a thread pool for ~10 s.
 """
@@ -50,7 +55,7 @@ def shard_seeds(batch_per_rank: int, rank: int) -> list:
     return list(range(rank * batch_per_rank, (rank + 1) * batch_per_rank))
 
 
-def cpu_baseline(data: bytes, seconds: float, threads: int) -> dict:
+def cpu_baseline(data: bytes, seconds: float, threads: int, label: str = "halfmoonbay") -> dict:
     from oracle import oracle
 
     tiles, (ho, hl) = oracle.list_tiles(data)
@@ -80,8 +85,9 @@ def cpu_baseline(data: bytes, seconds: float, threads: int) -> dict:
         "unit": "Mpixels/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{count} halfmoonbay 512x512 tiles decoded by the C oracle in {dt:.1f} s "
-                  f"({threads} threads, output-pixel-equivalent of {count / len(items):.1f} 4032x3024 images)",
+        "sample": f"{count} {label} {tw}x{th} tiles decoded by the C oracle in {dt:.1f} s "
+                  f"({threads} threads, output-pixel-equivalent of {count / len(items):.1f} "
+                  f"{meta['out_width']}x{meta['out_height']} images)",
     }
 
 
@@ -93,6 +99,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["config4", "config5"], default="config4")
     ap.add_argument("--verify", type=int, default=2, help="images checked bit-exact against the oracle (rank 0)")
     args = ap.parse_args()
 
@@ -108,10 +115,23 @@ def main():
     import heif_amd as H
     from heif_amd.synthetic import permuted_heic
 
-    src = SAMPLE.read_bytes()
+    c5 = args.workload == "config5"
+    if c5:
+        from heif_amd import synth_encoder as S
+        from heif_amd.synthetic import permutation
+
+        p5 = S.CONFIG5["params"]
+        pool = [S.picture(p5, 5000 + k) for k in range(135)]
+        src = S.grid_heic(S.CONFIG5["out_w"], S.CONFIG5["out_h"], p5, pictures=pool)
+    else:
+        src = SAMPLE.read_bytes()
     seeds = shard_seeds(args.batch, rank)
     t0 = time.perf_counter()
-    files = [permuted_heic(src, s) for s in seeds]
+    if c5:
+        files = [S.grid_heic(S.CONFIG5["out_w"], S.CONFIG5["out_h"], p5,
+                             pictures=[pool[j] for j in permutation(135, s)]) for s in seeds]
+    else:
+        files = [permuted_heic(src, s) for s in seeds]
     images = [H.HeifImage.parse(f) for f in files]
     host_parse_ms = (time.perf_counter() - t0) * 1e3 / len(files)
     info = images[0].info
@@ -179,7 +199,8 @@ def main():
         parse_ms = per_step[0]  # k_parse time of one launch (one launch per step)
         chunks = 1
         coded_px = info.grid_cols * info.tile_width * info.grid_rows * info.tile_height
-        algo_per_image = info.coded_bytes + coded_px * 3 // 2  # compressed + coded planes
+        bps = info.bytes_per_sample
+        algo_per_image = info.coded_bytes + coded_px * 3 // 2 * bps  # compressed + coded planes
         achieved = args.batch * algo_per_image / (parse_ms / 1e3) / 1e9
         traffic = None
         tfile = ROOT / "profiles" / "pmc_traffic.json"
@@ -191,7 +212,8 @@ def main():
             except Exception:
                 traffic = None
         line = {
-            "metric": "Mpixels/s decoded (bit-exact) on 4032x3024 HEIC batch",
+            "metric": ("Mpixels/s decoded (bit-exact) on 7680x4320 Main-10 HEIC batch" if c5 else
+                       "Mpixels/s decoded (bit-exact) on 4032x3024 HEIC batch"),
             "value": round(value, 2),
             "unit": "Mpixels/s",
             "n_gpus": world,
@@ -201,10 +223,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic: halfmoonbay.heic tiles permuted per image (mt19937_64 Fisher-Yates)",
+            "dtype": "u16" if c5 else "u8",
+            "data": ("synthetic: 135 generated 10-bit tiles (heif_amd/synth_encoder.py) permuted per image" if c5 else
+                     "synthetic: halfmoonbay.heic tiles permuted per image (mt19937_64 Fisher-Yates)"),
             "config": {
-                "workload": f"config4 shard: {args.batch} x 4032x3024 8-bit 4:2:0 intra HEIC grid stills per GPU "
+                "workload": f"config5 shard: {args.batch} x 7680x4320 10-bit 4:2:0 intra HEIC grids per GPU "
+                            f"(135 tiles of 512x512, WPP)" if c5 else f"config4 shard: {args.batch} x 4032x3024 8-bit 4:2:0 intra HEIC grid stills per GPU "
                             f"(48 tiles of 512x512, WPP)",
                 "images_per_gpu": args.batch,
                 "global_batch": total_images,
@@ -238,8 +262,9 @@ def main():
         }
         if not args.no_cpu_baseline:
             threads = min(16, os.cpu_count() or 1)
-            cb = cpu_baseline(src, args.cpu_seconds, threads)
-            one = cpu_baseline(src, min(args.cpu_seconds, 4.0), 1)
+            label = "synthetic 10-bit" if c5 else "halfmoonbay"
+            cb = cpu_baseline(src, args.cpu_seconds, threads, label)
+            one = cpu_baseline(src, min(args.cpu_seconds, 4.0), 1, label)
             cb["value_1core"] = one["value"]
             cb["host_cpus"] = os.cpu_count()
             line["cpu_baseline"] = cb
