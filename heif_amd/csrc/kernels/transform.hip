@@ -91,9 +91,89 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     int16_t *d = tile[wave][0];
     int16_t *g = tile[wave][1];
 
+    // Pass A: 4x4 TBs, four at a time, 16 lanes each (sub-tile q of d / g).
+    // A 4x4 TB has 16 outputs; run one per wave it left 48 lanes idle and paid
+    // a full round of tile zeroing, extent atomics and wave syncs per TB.
+    // Every phase loops over the 64 virtual lanes (one iteration on the GPU;
+    // the host emulation runs one lane per wave).
+    {
+        const uint32_t mine = ntu > (uint32_t)wave ? (ntu - (uint32_t)wave + kWaves - 1) / kWaves : 0;
+        for (uint32_t j = 0; j < mine; j += 4) {
+            // TB of group q = vl >> 4 in this round, if it is a coded 4x4 TB
+            auto group_tb = [&](int vl, TuRec &tu) -> bool {
+                const uint32_t jq = j + (uint32_t)(vl >> 4);
+                if (jq >= mine) return false;
+                tu = tus[(uint32_t)wave + kWaves * jq];
+                const int cidx = tu.flags & TU_CIDX_MASK;
+                return (tu.flags & TU_CBF) && tu.log2 == 2 && cidx <= 2 && tu.x + 4 <= pitch[cidx] &&
+                       tu.y + 4 <= (cidx ? ch : H);
+            };
+            for (int vl = lane; vl < 64; vl += kWave) d[vl] = 0;
+            wave_sync();
+            for (int vl = lane; vl < 64; vl += kWave) {
+                TuRec tu;
+                const int l16 = vl & 15;
+                if (!group_tb(vl, tu) || l16 >= (int)tu.ncoef) continue;
+                const int cidx = tu.flags & TU_CIDX_MASK;
+                const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
+                const Coef c = coefs[tu.coef + l16];
+                const int pos = (int)(c & 15u);
+                int dv = (int)(int16_t)(c >> 16);
+                if (!(tu.flags & TU_BYPASS)) {
+                    const int qp = tu.qp, bd_shift = bd - 3;
+                    const int ls = c_level_scale[qp % 6] << (qp / 6);
+                    // pass B's use_m (scaling && !(ts && n > 4)) is just `scaling` at 4x4
+                    const int m =
+                        scaling ? a.sf[sp.sf_off + sf_size_offset(0) + (uint32_t)cidx * 16u + (uint32_t)pos] : 16;
+                    dv = clip16(((int64_t)dv * m * ls + ((int64_t)1 << (bd_shift - 1))) >> bd_shift);
+                }
+                d[(vl & 48) + pos] = (int16_t)dv;
+            }
+            wave_sync();
+            // first stage: g[y][x] = clip16((sum_k M[k][y] d[k][x] + 64) >> 7)
+            for (int vl = lane; vl < 64; vl += kWave) {
+                TuRec tu;
+                if (!group_tb(vl, tu) || (tu.flags & (TU_BYPASS | TU_TSKIP))) continue;
+                const int16_t *dq = d + (vl & 48);
+                const int y = (vl & 15) >> 2, x = vl & 3;
+                const bool dst_tr = (tu.flags & TU_DST) != 0;
+                int32_t s = 0;
+                for (int k = 0; k < 4; ++k)
+                    s += (int32_t)(dst_tr ? s_dst[k * 4 + y] : s_tm[(k * 8) * 32 + y]) * dq[k * 4 + x];
+                g[vl] = (int16_t)clip16(((int64_t)s + 64) >> 7);
+            }
+            wave_sync();
+            // second stage (or bypass / transform skip) and the residual store
+            for (int vl = lane; vl < 64; vl += kWave) {
+                TuRec tu;
+                if (!group_tb(vl, tu)) continue;
+                const int cidx = tu.flags & TU_CIDX_MASK;
+                const int bd2 = 20 - (cidx ? sp.bit_depth_c : sp.bit_depth_y);
+                const int y = (vl & 15) >> 2, x = vl & 3;
+                const int16_t *dq = d + (vl & 48), *gq = g + (vl & 48);
+                int r;
+                if (tu.flags & TU_BYPASS) {
+                    r = dq[vl & 15];
+                } else if (tu.flags & TU_TSKIP) {
+                    r = ((dq[vl & 15] << 7) + (1 << (bd2 - 1))) >> bd2;  // tsShift = 5 + log2(4)
+                } else {
+                    const bool dst_tr = (tu.flags & TU_DST) != 0;
+                    int64_t s = 0;
+                    for (int k = 0; k < 4; ++k)
+                        s += (int32_t)(dst_tr ? s_dst[k * 4 + x] : s_tm[(k * 8) * 32 + x]) * gq[y * 4 + k];
+                    r = (int)((s + (1 << (bd2 - 1))) >> bd2);
+                }
+                res_plane[cidx][(size_t)(tu.y + y) * pitch[cidx] + tu.x + x] = (int16_t)clip16(r);
+            }
+            wave_sync();
+        }
+    }
+
+    // Pass B: every larger TB, one per wave
     for (uint32_t t = wave; t < ntu; t += kWaves) {
         const TuRec tu = tus[t];
         if (!(tu.flags & TU_CBF)) continue;
+        if (tu.log2 == 2) continue;  // pass A
         const int cidx = tu.flags & TU_CIDX_MASK;
         const int log2n = tu.log2, n = 1 << log2n;
         if (log2n < 2 || log2n > 5 || cidx > 2 || tu.x + n > pitch[cidx] || tu.y + n > (cidx ? ch : H)) continue;
