@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
             const int sx = VERT ? 1 : cw, sk = VERT ? cw : 1;
             for (int k = 0; k < 2; ++k) {
                 const int p0 = q[k * sk - sx], p1 = q[k * sk - 2 * sx], q0 = q[k * sk], q1 = q[k * sk + sx];
-                const int delta = clip3(-tc, tc, ((((q0 - p0) << 2) + p1 - q1 + 4) >> 3));
+                const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
                 if (!(fp & MF_NOFILT)) q[k * sk - sx] = (Pel)clip3(0, maxv, p0 + delta);
                 if (!(fq & MF_NOFILT)) q[k * sk] = (Pel)clip3(0, maxv, q0 - delta);
             }

@@ -184,7 +184,8 @@ __device__ __forceinline__ void store_tu(TuRec *d, uint32_t x, uint32_t y, uint3
 }
 #endif
 
-// n (1..8) bytes of v at p: one store when n is 2, 4 or 8 and p is n-aligned
+// n bytes of v at p (v's 8-byte pattern repeats for n > 8: a 64x64 CU's
+// 16-byte QpY row): one store when n is 2, 4 or 8 and p is n-aligned
 HG_HD inline void store_bytes(uint8_t *p, int n, uint64_t v) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     if (n == 8 && !(a & 7)) {
@@ -194,7 +195,7 @@ HG_HD inline void store_bytes(uint8_t *p, int n, uint64_t v) {
     } else if (n == 2 && !(a & 1)) {
         *reinterpret_cast<uint16_t *>(p) = (uint16_t)v;
     } else {
-        for (int i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * i));
+        for (int i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * (i & 7)));
     }
 }
 

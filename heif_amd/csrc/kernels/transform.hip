@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                 if (tu.flags & TU_BYPASS) {
                     r = dq[vl & 15];
                 } else if (tu.flags & TU_TSKIP) {
-                    r = ((dq[vl & 15] << 7) + (1 << (bd2 - 1))) >> bd2;  // tsShift = 5 + log2(4)
+                    r = (dq[vl & 15] * (1 << 7) + (1 << (bd2 - 1))) >> bd2;  // tsShift = 5 + log2(4)
                 } else {
                     const bool dst_tr = (tu.flags & TU_DST) != 0;
                     int64_t s = 0;
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
             const int ts_shift = 5 + log2n;
             for (int i = lane; i < n * n; i += kWave) {
                 int r = d[i];
-                if (!bypass) r = ((r << ts_shift) + (1 << (bd2 - 1))) >> bd2;
+                if (!bypass) r = (r * (1 << ts_shift) + (1 << (bd2 - 1))) >> bd2;
                 dst[(i >> log2n) * pitch[cidx] + (i & (n - 1))] = (int16_t)clip16(r);
             }
             wave_sync();

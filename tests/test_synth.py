@@ -201,3 +201,61 @@ def test_emulated_kernels_on_synthetic_streams(tmp_path, parser):
         path.write_bytes(S.single_heic(params(over), seed=1))
         r = subprocess.run([str(exe), str(path), "5"], capture_output=True, text=True, env=env, timeout=300)
         assert r.returncode == 0 and "EMU PARITY OK" in r.stdout + r.stderr, (name, (r.stdout + r.stderr)[-400:])
+
+
+# ------------------------------------------- corrupt synthetic streams
+def _corrupt_synth(mode):
+    """A 10-bit CTB-64 grid (transform skip, bypass, scaling lists) with slice
+    data damaged in three tiles (random bytes) or one tile half zeroed."""
+    import random
+
+    from oracle import oracle
+
+    p = params(dict(width=256, height=256, bit_depth=10, log2_ctb=6, transform_skip=1, tq_bypass=1, scaling_list=1))
+    data = bytearray(S.grid_heic(700, 500, p, seed=9))
+    tiles, _ = oracle.list_tiles(bytes(data))
+    rng = random.Random(2)
+    if mode == "random":
+        for k in (0, 2, 5):
+            o, n = tiles[k]
+            for _ in range(40):
+                data[o + 30 + rng.randrange(n - 30)] = rng.randrange(256)
+    else:
+        o, n = tiles[4]
+        data[o + n // 2:o + n] = bytes(n - n // 2)
+    return bytes(data)
+
+
+@pytest.mark.parametrize("mode", ["random", "zeroed"])
+def test_emulated_kernels_survive_corrupt_synthetic(tmp_path, mode):
+    import pathlib
+    import subprocess
+
+    csrc = pathlib.Path(__file__).resolve().parents[1] / "heif_amd" / "csrc"
+    subprocess.run(["make", "-s", "-C", str(csrc), "emu-fast"], check=True, capture_output=True)
+    path = tmp_path / f"{mode}.heic"
+    path.write_bytes(_corrupt_synth(mode))
+    r = subprocess.run([str(csrc / "build" / "emu_fast" / "emu_check"), str(path), "5"], capture_output=True,
+                       text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode in (0, 1), out[-2000:]
+    line = next(l for l in out.splitlines() if l.startswith("parse: status"))
+    assert int(line.split()[2].rstrip(","), 16) != 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["random", "zeroed"])
+def test_gpu_corrupt_synthetic_sets_status(H, oracle_mod, mode):
+    """Damaged 10-bit CTB-64 streams end in status bits, never a device fault;
+    the clean image in the same batch stays bit-exact."""
+    clean = S.grid_heic(700, 500, params(dict(width=256, height=256, bit_depth=10, log2_ctb=6)), seed=10)
+    ctx = H.DecodeContext(0)
+    imgs = [H.HeifImage.parse(_corrupt_synth(mode)), H.HeifImage.parse(clean)]
+    b = ctx.prepare(imgs)
+    outs = ctx.alloc_outputs(imgs)
+    b.decode_async(outs)
+    st = b.status()
+    assert st[0] != 0 and st[1] == 0
+    _assert_equal(_planes(outs[1]), oracle_mod.decode_heic(clean, with_checks=False), "clean")
+    b.free()
+    ctx.close()
