@@ -349,7 +349,7 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
     HIP_TRY(hipMemcpy(b->sf.p, h_sf.data(), h_sf.size(), hipMemcpyHostToDevice));
     HIP_TRY(hipMemset(b->rbsp.p, 0, h_bits.size()));
     std::vector<uint32_t> order;
-    lanes_parse_order(h_pics.data(), int(h_pics.size()), max_rows, order);
+    lanes_parse_order(h_pics.data(), int(h_pics.size()), hb.lane_rows, order);
     HIP_TRY(b->porder.alloc(order.size()));
     HIP_TRY(hipMemcpy(b->porder.p, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     BatchArgs &a = b->args;
@@ -369,6 +369,8 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
     a.max_wctb = max_wctb;
     a.max_rows = max_rows;
     a.max_log2ctb = hb.max_log2ctb;
+    a.lane_rows = hb.lane_rows;
+    a.wpp_ring = hb.wpp_ring;
     a.total_rows = int(rows);
     a.bytes_per_sample = bps;
     b->out_host.assign(n, OutImage{});
@@ -420,6 +422,7 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         HIP_TRY(hipStreamSynchronize(ctx->parse));
         HIP_TRY(hipStreamSynchronize(ctx->recon));
         HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), s));
+        HIP_TRY(hipMemsetAsync(ps.row_counts.p, 0, size_t(2) * uint32_t(b->args.total_rows) * sizeof(uint32_t), s));
         HIP_TRY(launch_rbsp(a, s));
         hipError_t (*fns[5])(const BatchArgs &, hipStream_t) = {launch_parse, launch_transform, launch_intra,
                                                                 launch_deblock, launch_sao_out};
@@ -442,6 +445,8 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     // parse stream: this set's previous reconstruction must be done with it
     if (ps.pending) HIP_TRY(hipStreamWaitEvent(p, ps.recon_done, 0));
     HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), p));
+    // rows a stopped substream never reaches keep zero TBs
+    HIP_TRY(hipMemsetAsync(ps.row_counts.p, 0, size_t(2) * uint32_t(b->args.total_rows) * sizeof(uint32_t), p));
     if (t) HIP_TRY(hipEventRecord(ev[0], p));
     HIP_TRY(launch_rbsp(a, p));
     if (t) HIP_TRY(hipEventRecord(ev[1], p));

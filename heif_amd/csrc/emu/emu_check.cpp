@@ -55,7 +55,7 @@ int main(int argc, char **argv) {
     a.rbsp = rbsp.data();
     a.rsubs = rsubs.data();
     std::vector<uint32_t> order;
-    lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.max_rows, order);
+    lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
     a.parse_order = order.data();
     a.seqs = hb.seqs.data();
     a.sf = hb.sf.data();
@@ -73,6 +73,8 @@ int main(int argc, char **argv) {
     a.max_wctb = hb.max_wctb;
     a.max_rows = hb.max_rows;
     a.max_log2ctb = hb.max_log2ctb;
+    a.lane_rows = hb.lane_rows;
+    a.wpp_ring = hb.wpp_ring;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = bps;
     emu_rbsp(a);

@@ -142,6 +142,9 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n) {
             hb.max_wctb = std::max(hb.max_wctb, wctb);
             hb.max_rows = std::max(hb.max_rows, hctb);
             hb.max_log2ctb = std::max(hb.max_log2ctb, int(sq.log2_ctb));
+            const bool wpp = (sq.flags & SP_WPP) != 0;
+            hb.lane_rows = std::max(hb.lane_rows, wpp ? std::min(hctb, 64) : 1);
+            if (wpp && hctb > 64) hb.wpp_ring = 1;
         }
     }
     hb.bits.resize(hb.bits.size() + 128, 0);

@@ -20,6 +20,7 @@ struct HostBatch {
     uint64_t recon_bytes = 0, resid_elems = 0, map_bytes = 0, sao_n = 0, tu_n = 0, coef_n = 0;
     uint32_t rows = 0;
     int max_w = 0, max_wctb = 0, max_rows = 0, max_log2ctb = 4, bps = 0, chroma = -1;
+    int lane_rows = 1, wpp_ring = 0;  // k_parse_lanes geometry (BatchArgs::lane_rows / wpp_ring)
 };
 
 // Throws HeifError / UnsupportedError.

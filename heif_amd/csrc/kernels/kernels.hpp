@@ -2,8 +2,9 @@
 //
 // Pipeline per batch (6 launches):
 //   0. k_rbsp       emulation-prevention removal + entry-point remap (7.3.1.1)
-//   1. k_parse      CABAC substreams → TU records + coefficients + QP/edge
-//                   maps + SAO parameters        (slice.rs:206-256 + todo!()s)
+//   1. k_parse_lanes CABAC substreams (one per lane) → TU records +
+//                   coefficients + QP/edge maps + SAO parameters
+//                   (slice.rs:206-256 + todo!()s)
 //   2. k_transform  dequant (8.6.2-3) + inverse DST/DCT (8.6.4) → residuals
 //   3. k_intra      intra prediction (8.4.4.2) + reconstruction (8.6.7)
 //   4. k_deblock    vertical then horizontal edges (8.7.2), in place
@@ -46,31 +47,11 @@ struct BatchArgs {
     int max_rows;              // CTB rows, batch max
     int total_rows;            // sum of CTB rows over pictures
     int bytes_per_sample;      // 1 or 2
-    int parse_group;           // k_parse waves per picture (set by launch_parse)
+    int parse_group;           // k_parse_lanes pictures per wave (set by launch_parse)
     int max_log2ctb;           // largest CTB size in the batch (sizes k_intra's LDS)
+    int lane_rows;             // k_parse_lanes lanes per picture: max over pictures of (WPP ? min(rows, 64) : 1)
+    int wpp_ring;              // some WPP picture has more than 64 CTB rows (its rows wrap round its lanes)
 };
-
-constexpr int kParseWaves = 16;              // k_parse block size limit (waves)
-constexpr int kParseSerialMinPics = 1024;    // from this many pictures on: one wave per picture
-constexpr int kParseSerialPicsPerBlock = 4;  // pictures (waves) per block in that mode
-struct ParseShape {
-    int group, pics_per_block, blocks, threads;
-    size_t lds;
-};
-ParseShape parse_shape(const BatchArgs &a);
-// LDS of one picture group: progress[G] (padded to 4), WPP context slots
-// [2][64] words, CtDepth lines [2][dl_stride], SAO lines [2][max_wctb]
-#if defined(HG_HOST_EMU)
-inline
-#else
-__host__ __device__ inline
-#endif
-size_t parse_group_bytes(int max_width, int max_wctb, int group) {
-    const size_t dl_stride = (size_t)(((max_width >> 3) + 15) & ~15);
-    const size_t b = sizeof(uint32_t) * ((group + 3) & ~3) + 2 * 64 * sizeof(uint32_t) + 2 * dl_stride +
-                     2 * (size_t)max_wctb * sizeof(SaoParams);
-    return (b + 15) & ~(size_t)15;
-}
 
 // k_ycbcr_rgb (color.hip): one decoded image → interleaved RGB8, rotated
 struct ColorArgs {
@@ -101,11 +82,8 @@ inline void color_coefs(uint32_t matrix, bool full, ColorArgs &c) {
     c.cr_g = fx(2.0 * kr * (1.0 - kr) / kg * cs);
 }
 
-// k_parse_lanes (parse_lanes.hip): one substream per lane; the default (HEIFGPU_PARSE=scalar selects k_parse)
-bool parse_lanes_supported(const BatchArgs &a);
-bool parse_lanes_selected(const BatchArgs &a);
-// host: BatchArgs::parse_order for a batch (size-balanced waves)
-void lanes_parse_order(const PicDesc *pics, int n, int max_rows, std::vector<uint32_t> &order);
+// host: BatchArgs::parse_order for a batch (size-balanced k_parse_lanes waves)
+void lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uint32_t> &order);
 
 #if defined(HG_HOST_EMU)
 // Runs kernel(a) over a gx * gy grid, one block at a time, with `waves` host
@@ -137,7 +115,6 @@ void emu_launch(K kernel, int gx, int gy, int waves, const BatchArgs &a, bool gr
 }
 void emu_rbsp(const BatchArgs &a);
 void emu_parse(const BatchArgs &a);
-void emu_parse_lanes(const BatchArgs &a);
 void emu_transform(const BatchArgs &a);
 void emu_intra(const BatchArgs &a);
 void emu_deblock(const BatchArgs &a);
@@ -146,8 +123,6 @@ void emu_sao_out(const BatchArgs &a);
 hipError_t launch_rbsp(const BatchArgs &a, hipStream_t s);
 hipError_t launch_ycbcr_rgb(const ColorArgs &c, int bytes_per_sample, hipStream_t s);
 hipError_t launch_parse(const BatchArgs &a, hipStream_t s);
-hipError_t launch_parse_lanes(const BatchArgs &a, hipStream_t s);
-int parse_lanes_counters(uint64_t *out8);
 hipError_t launch_transform(const BatchArgs &a, hipStream_t s);
 hipError_t launch_intra(const BatchArgs &a, hipStream_t s);
 hipError_t launch_deblock(const BatchArgs &a, hipStream_t s);

@@ -1,12 +1,18 @@
-// parse_lanes.hip — CABAC slice-data parser with one substream per LANE
-// (pipeline stage 1; alternative to parse.hip's one-substream-per-wave k_parse).
+// parse_lanes.hip — CABAC slice-data parser (pipeline stage 1), one
+// substream per LANE.
 //
-// Same syntax and the same outputs as k_parse (TU records, coefficients, the
-// QP / edge maps, SAO parameters, per-row counts; see parse.hip for the
-// per-clause references into H.265 and the reference's
-// src/hevc/slice.rs:206-256 / src/cabac), but every lane of a wave runs its
-// own WPP substream: lane = one CTB row of one picture, and a picture's rows
-// sit in consecutive lanes.  Each lane walks its substream as a sequence of
+// Replaces SliceSegmentReader::read_data / read_coding_tree_unit and the
+// todo!() sao() / coding_quadtree() of src/hevc/slice.rs:206-256, with the
+// engine of src/cabac/arithmetic.rs and the binarizations of
+// src/cabac/decoder.rs, plus everything H.265 needs below them (7.3.8.3-14,
+// 9.3.4.2 ctxInc, 8.4.2 MPM, 8.6.1 QP).  Outputs: TU records, coefficients,
+// the QP / edge maps, SAO parameters and per-row counts (desc.hpp).
+//
+// Every lane of a wave runs its own substream: with WPP a lane is one CTB
+// row of a picture and a picture's rows sit in consecutive lanes (R =
+// min(rows, 64) lanes; a picture with more than 64 rows wraps round them, lane
+// r taking rows r, r + R, r + 2R, ...); without WPP the slice is one
+// substream and one lane walks all of its rows.  Each lane walks its substream as a sequence of
 // syntax units (CTU start + SAO, coding-quadtree descent, coding-unit header,
 // transform-tree descent + transform_unit, residual header, one 4x4
 // sub-block, CTU end); one pass of the kernel loop runs one unit on every
@@ -15,9 +21,11 @@
 // inside the units.  So up to 64 substreams share each engine instruction,
 // where k_parse spends a whole wave on one.
 //
-// WPP (9.3.1) inside the wave: lane r+1 starts CTU c once lane r has finished
-// CTU c+1 (per-lane progress words in LDS); lane r writes its contexts after
-// CTU 1 straight into lane r+1's context block.  The CtDepth of a CTB's bottom
+// WPP (9.3.1) inside the wave: row r+1 starts CTU c once row r has finished
+// CTU c+1 (per-lane progress words in LDS, counting r * wctb + CTUs done so
+// they stay monotone when a lane wraps to a later row); row r writes its
+// contexts after CTU 1 straight into row r+1's lane block, or, when rows wrap
+// (that lane may still be parsing an earlier row), into its staging block.  The CtDepth of a CTB's bottom
 // 8x8 row and its SAO parameters reach the row below through global memory
 // (maps arena / SAO array), read with L1-bypassing loads.
 //
@@ -74,6 +82,7 @@ struct LanePic {
     int W, H, log2ctb, wctb, hctb, minCb, minTb, maxTb, maxDepthIntra, chroma;
     int log2qg, bdY, bdC, qpbdY, qpbdC, pcmMin, pcmMax, cbOff, crOff, sliceQp;
     int w4, h4, w8, saoL, saoC;
+    int R, lane0, ring;  // lanes of the picture, its first lane, rows wrap round the lanes (WPP rows > R)
     uint32_t flags, bits_off, bits_end, sub_first, row_off, tu_cap, coef_cap, pic;
     int8_t *gqpy;
     uint8_t *gflags, *gdepth;
@@ -478,9 +487,17 @@ HG_HD inline int msb32(uint32_t m) { return 31 - __builtin_clz(m); }
 struct Env {
     const BatchArgs *a;
     LaneLds *lds;    // the wave's 64 lane blocks
-    uint32_t *prog;  // [64] CTUs finished in the lane's current row
+    uint32_t *prog;  // [64] row * wctb + CTUs finished in the lane's current row
+    uint8_t *wctx;   // [64][CTX_PAD] WPP context staging of wrapping pictures (null when none wraps)
     int lane;
 };
+
+// WPP: the row above is two CTUs ahead of CTU L.c (or finished)
+HG_HD inline bool wpp_ready(const Lane &L, const LanePic &P, const Env &E) {
+    if (!(L.fl & F_WPP) || L.row == 0) return true;
+    const uint32_t need = (uint32_t)(L.row - 1) * (uint32_t)P.wctb + (uint32_t)(L.c + 2 < P.wctb ? L.c + 2 : P.wctb);
+    return prog_load(&E.prog[P.lane0 + (L.row - 1) % P.R]) >= need;
+}
 
 HG_HD inline void row_outputs(Lane &L, const LanePic &P) {
     L.tu_row = (uint32_t)L.row * P.tu_cap;
@@ -497,17 +514,20 @@ HG_HD inline void coef_push(Lane &L, const LanePic &P, uint32_t w) { P.coef_base
 // U_CTU: CTU start (7.3.8.2) and sao() (7.3.8.3).  Returns without a state
 // change while the row above is less than two CTUs ahead (WPP).
 HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const Eng &G) {
-    if ((L.fl & F_WPP) && L.row > 0) {
-        const uint32_t need = (uint32_t)(L.c + 2 < P.wctb ? L.c + 2 : P.wctb);
-        if (prog_load(&E.prog[E.lane - 1]) < need) return;
-    }
+    if (!wpp_ready(L, P, E)) return;
     L.ctbx = L.c << P.log2ctb;
     L.ctby = L.row << P.log2ctb;
     if (L.c == 0 && ((L.fl & F_WPP) || L.row == 0)) {
         // substream start: contexts (init, or the WPP copy already in ld.ctx) + engine
-        if (L.row == 0 || P.wctb < 2 || !(L.fl & F_WPP))
+        if (L.row == 0 || P.wctb < 2 || !(L.fl & F_WPP)) {
 #pragma nounroll
             for (int i = 0; i < CTX_NUM; ++i) ld.ctx[i] = ctx_init_state(c_ctx_init_l[i], P.sliceQp);
+        } else if (P.ring) {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(E.wctx + (size_t)E.lane * CTX_PAD);
+            uint32_t *dst = reinterpret_cast<uint32_t *>(ld.ctx);
+#pragma nounroll
+            for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = src[k];
+        }
         const uint32_t *subs = E.a->rsubs + P.sub_first;
         engine_init(L, G, P.bits_off + subs[(L.fl & F_WPP) ? L.row : 0], P.bits_end);
         if (L.row == 0) L.fl |= F_FIRST_QG;
@@ -1068,8 +1088,10 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
 // end_of_subset_one_bit (slice.rs:214-227), progress, next CTU / row
 HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const Eng &G) {
     if ((L.fl & F_WPP) && L.c == 1 && L.row + 1 < P.hctb) {
-        // 9.3.2.4 storage for the next row's substream: straight into its lane's block
-        uint32_t *dst = reinterpret_cast<uint32_t *>(E.lds[E.lane + 1].ctx);
+        // 9.3.2.4 storage for the next row's substream: into its lane's block, or
+        // its staging block when that lane may still be parsing an earlier row
+        const int nl = P.lane0 + (L.row + 1) % P.R;
+        uint32_t *dst = reinterpret_cast<uint32_t *>(P.ring ? E.wctx + (size_t)nl * CTX_PAD : E.lds[nl].ctx);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(ld.ctx);
 #pragma nounroll
         for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = src[k];
@@ -1085,7 +1107,7 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     if (L.budget + L.k < 0) L.status |= ST_OVERRUN;  // read past the NAL unit
     release_fence();
     ++L.c;
-    prog_store(&E.prog[E.lane], (L.fl & F_STOP) ? kProgDone : (uint32_t)L.c);
+    prog_store(&E.prog[E.lane], (L.fl & F_STOP) ? kProgDone : (uint32_t)L.row * (uint32_t)P.wctb + (uint32_t)L.c);
     if (!(L.fl & F_STOP) && L.c < P.wctb) {
         L.st = U_CTU;
         return;
@@ -1093,8 +1115,9 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     uint32_t *rc = E.a->row_counts + 2 * (size_t)(P.row_off + L.row);
     rc[0] = L.ntu;
     rc[1] = L.ncoef;
-    if (!(L.fl & (F_STOP | F_WPP)) && L.row + 1 < P.hctb) {  // one substream: walk on to the next row
-        ++L.row;
+    const int step = (L.fl & F_WPP) ? P.R : 1;  // one substream (no WPP): walk on to the next row
+    if (!(L.fl & F_STOP) && L.row + step < P.hctb) {
+        L.row += step;
         L.c = 0;
         row_outputs(L, P);
         L.st = U_CTU;
@@ -1122,20 +1145,20 @@ HG_HD inline void run_unit(int kind, Lane &L, LaneLds &ld, LanePic &P, const Env
 }
 
 // a lane in U_CTU can start its CTU (WPP: the row above is two CTUs ahead)
-HG_HD inline bool ctu_ready(const Lane &L, const LanePic &P, const Env &E) {
-    if (!(L.fl & F_WPP) || L.row == 0) return true;
-    const uint32_t need = (uint32_t)(L.c + 2 < P.wctb ? L.c + 2 : P.wctb);
-    return prog_load(&E.prog[E.lane - 1]) >= need;
-}
+HG_HD inline bool ctu_ready(const Lane &L, const LanePic &P, const Env &E) { return wpp_ready(L, P, E); }
 
 // lane setup: picture constants, outputs, first state.  Returns false for an idle lane.
-HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a, int pic, int row) {
+HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a, int pic, int row, int lane0) {
     const PicDesc &pd = a.pics[pic];
     const SeqParams &sp = a.seqs[pd.seq];
     const int log2ctb = sp.log2_ctb, ctb = 1 << log2ctb;
     const int hctb = (sp.height + ctb - 1) >> log2ctb;
     const bool wpp = (sp.flags & SP_WPP) != 0;
-    if (wpp ? row >= hctb : row != 0) return false;
+    const int R = wpp ? (hctb < a.lane_rows ? hctb : a.lane_rows) : 1;
+    if (row >= R) return false;
+    P.R = R;
+    P.lane0 = lane0;
+    P.ring = wpp && hctb > R;
     P.W = sp.width;
     P.H = sp.height;
     P.log2ctb = log2ctb;
@@ -1188,28 +1211,18 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
     return true;
 }
 
-// pictures per wave: a picture's CTB rows occupy consecutive lanes.
+// pictures per wave: a picture's lanes (BatchArgs::lane_rows) are consecutive.
 // HEIFGPU_LANES_PPW lowers it (more, emptier waves) for tuning.
-inline int lanes_pics_per_wave(int max_rows) {
+inline int lanes_pics_per_wave(int lane_rows) {
     static const int forced = [] {
         const char *e = std::getenv("HEIFGPU_LANES_PPW");
         return e ? std::atoi(e) : 0;
     }();
-    const int full = 64 / (max_rows < 1 ? 1 : max_rows);
+    const int full = 64 / (lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows));
     return forced > 0 && forced < full ? forced : full;
 }
 
 }  // namespace
-
-bool parse_lanes_supported(const BatchArgs &a) { return a.max_rows >= 1 && a.max_rows <= 64; }
-
-bool parse_lanes_selected(const BatchArgs &a) {
-    static const int mode = [] {
-        const char *e = std::getenv("HEIFGPU_PARSE");
-        return (e && e[0] == 's') ? 0 : 1;  // "lanes" (default) | "scalar"
-    }();
-    return mode == 1 && parse_lanes_supported(a);
-}
 
 // Wave slot -> picture.  A wave runs until its heaviest picture is parsed,
 // and every extra busy picture in it adds divergent units to each pass, so
@@ -1217,7 +1230,7 @@ bool parse_lanes_selected(const BatchArgs &a) {
 // by payload size and dealt snake-wise (wave w of W gets ranks w, 2W-1-w,
 // 2W+w, 4W-1-w, ...): the heaviest pictures share a wave with the lightest.
 // HEIFGPU_PARSE_ORDER=0: batch order.
-void lanes_parse_order(const PicDesc *pics, int n, int max_rows, std::vector<uint32_t> &order) {
+void lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uint32_t> &order) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
         return e ? std::atoi(e) : 1;
@@ -1225,7 +1238,7 @@ void lanes_parse_order(const PicDesc *pics, int n, int max_rows, std::vector<uin
     order.resize((size_t)n);
     for (int i = 0; i < n; ++i) order[(size_t)i] = (uint32_t)i;
     if (!on || n <= 0) return;
-    const int ppw = lanes_pics_per_wave(max_rows);
+    const int ppw = lanes_pics_per_wave(lane_rows);
     const int W = (n + ppw - 1) / ppw;
     std::vector<uint32_t> by_size(order);
     std::stable_sort(by_size.begin(), by_size.end(),
@@ -1244,27 +1257,28 @@ void lanes_parse_order(const PicDesc *pics, int n, int max_rows, std::vector<uin
 
 #if defined(HG_HOST_EMU)
 // one wave at a time, one unit per live lane per pass, lanes in order
-void emu_parse_lanes(const BatchArgs &a) {
-    const int ppw = lanes_pics_per_wave(a.max_rows);
+void emu_parse(const BatchArgs &a) {
+    const int ppw = lanes_pics_per_wave(a.lane_rows);
     const int waves = (a.n_pics + ppw - 1) / ppw;
     uint64_t tab[64];
     for (int i = 0; i < 64; ++i) tab[i] = state_row(i);
     std::vector<LaneLds> lds(64);
     std::vector<LanePic> pics(64);
     std::vector<Lane> lanes(64);
+    std::vector<uint8_t> wctx(a.wpp_ring ? 64 * CTX_PAD : 0);
     uint32_t prog[64];
     static const bool stats = std::getenv("HEIFGPU_LANES_STATS") != nullptr;
     for (int w = 0; w < waves; ++w) {
         for (int l = 0; l < 64; ++l) {
             prog[l] = 0;
-            const int pl = l / a.max_rows, row = l % a.max_rows;
+            const int pl = l / a.lane_rows, row = l % a.lane_rows;
             const int slot = w * ppw + pl;
             const bool in = pl < ppw && slot < a.n_pics;
             const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
-            const bool live = in && lane_init(lanes[l], pics[pl], lds[l], a, pic, row);
+            const bool live = in && lane_init(lanes[l], pics[pl], lds[l], a, pic, row, pl * a.lane_rows);
             if (!live) lanes[l].st = U_DONE;
         }
-        Env E{&a, lds.data(), prog, 0};
+        Env E{&a, lds.data(), prog, a.wpp_ring ? wctx.data() : nullptr, 0};
         long passes = 0, units = 0;
         for (;; ++passes) {
             bool any = false, progressed = false;
@@ -1275,7 +1289,7 @@ void emu_parse_lanes(const BatchArgs &a) {
                 for (int l = 0; l < 64; ++l) {
                     Lane &L = lanes[l];
                     E.lane = l;
-                    LanePic &P = pics[l / a.max_rows];
+                    LanePic &P = pics[l / a.lane_rows];
                     if (L.st != kind || (kind == U_CTU && !ctu_ready(L, P, E))) continue;
                     progressed = true;
                     ++units;
@@ -1287,7 +1301,7 @@ void emu_parse_lanes(const BatchArgs &a) {
                 for (int l = 0; l < 64; ++l)
                     if (lanes[l].st != U_DONE) {
                         lanes[l].status |= ST_SUBSTREAM_END;
-                        atomicOr(&a.status[pics[l / a.max_rows].pic], lanes[l].status);
+                        atomicOr(&a.status[pics[l / a.lane_rows].pic], lanes[l].status);
                         lanes[l].st = U_DONE;
                     }
                 break;
@@ -1298,20 +1312,22 @@ void emu_parse_lanes(const BatchArgs &a) {
     }
 }
 #else
-// LDS of one wave: LaneLds per used lane, LanePic per picture, progress words, engine tables
-inline size_t lanes_lds_bytes(int ppw, int max_rows) {
-    return sizeof(LaneLds) * (size_t)(ppw * max_rows) + sizeof(LanePic) * (size_t)ppw + 64 * sizeof(uint32_t) +
-           64 * sizeof(uint64_t);
+// LDS of one wave: LaneLds per used lane, LanePic per picture, progress words,
+// engine tables, and the WPP context staging when rows wrap
+inline size_t lanes_lds_bytes(int ppw, int lane_rows, bool ring) {
+    return sizeof(LaneLds) * (size_t)(ppw * lane_rows) + sizeof(LanePic) * (size_t)ppw + 64 * sizeof(uint32_t) +
+           64 * sizeof(uint64_t) + (ring ? 64 * (size_t)CTX_PAD : 0);
 }
 
 __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int ppw = a.parse_group;  // pictures per wave (launch_parse_lanes)
-    const int nl = ppw * a.max_rows;
+    const int ppw = a.parse_group;  // pictures per wave (launch_parse)
+    const int nl = ppw * a.lane_rows;
     LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
     LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + nl);
     uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + ppw);
     uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_prog + 64);
+    uint8_t *s_wctx = a.wpp_ring ? reinterpret_cast<uint8_t *>(s_tab + 64) : nullptr;
     const int lane = threadIdx.x;
 #if defined(HG_PARSE_SETPRIO)
     // the parse is the latency-critical stream: win issue arbitration against
@@ -1319,7 +1335,7 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     __builtin_amdgcn_s_setprio(HG_PARSE_SETPRIO);
 #endif
     s_tab[lane] = state_row(lane);
-    const int pl = lane / a.max_rows, row = lane % a.max_rows;
+    const int pl = lane / a.lane_rows, row = lane % a.lane_rows;
     const int slot = (int)blockIdx.x * ppw + pl;
     const bool in = pl < ppw && slot < a.n_pics;
     const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
@@ -1327,10 +1343,10 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     LaneLds &ld = s_lds[lane < nl ? lane : 0];
     LanePic &P = s_pic[pl < ppw ? pl : 0];
     s_prog[lane] = 0;
-    const bool live = in && lane_init(L, P, ld, a, pic, row);
+    const bool live = in && lane_init(L, P, ld, a, pic, row, pl * a.lane_rows);
     if (!live) L.st = U_DONE;
     __syncthreads();
-    const Env E{&a, s_lds, s_prog, lane};
+    const Env E{&a, s_lds, s_prog, s_wctx, lane};
     const Eng G{ld.ctx, s_tab, a.rbsp, live ? P.bits_end + 64 : 0u};
 #if defined(HG_PARSE_PROF)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1377,27 +1393,36 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
 #endif
 }
 
-// tuning hook for heifgpu_debug_counters (parse.hip): copies out and zeroes the counters
-int parse_lanes_counters(uint64_t *out8) {
-#if defined(HG_PARSE_PROF)
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_prof_lanes), 8 * sizeof(uint64_t)) != hipSuccess) return -1;
-    const uint64_t zero[8] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof_lanes), zero, sizeof(zero)) != hipSuccess) return -1;
-    return 8;
-#else
-    (void)out8;
-    return 0;
-#endif
-}
-
-hipError_t launch_parse_lanes(const BatchArgs &a0, hipStream_t s) {
+hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
     BatchArgs a = a0;
-    const int ppw = lanes_pics_per_wave(a.max_rows);
+    if (a.lane_rows < 1 || a.lane_rows > 64) return hipErrorInvalidValue;
+    const int ppw = lanes_pics_per_wave(a.lane_rows);
     a.parse_group = ppw;
     const int waves = (a.n_pics + ppw - 1) / ppw;
-    hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.max_rows), s, a);
+    hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0), s,
+                       a);
     return hipGetLastError();
 }
 #endif
 
 }  // namespace hg
+
+#if !defined(HG_HOST_EMU)
+// Tuning hook (include/heifgpu.h): copies out and zeroes k_parse_lanes'
+// per-wave s_memtime counters.  Returns the number of counters written, or 0
+// for the product library (counters compiled out; `make prof` has them).
+extern "C" int heifgpu_debug_counters(uint64_t *out, int n) {
+#if defined(HG_PARSE_PROF)
+    uint64_t tmp[8] = {};
+    if (hipMemcpyFromSymbol(tmp, HIP_SYMBOL(hg::g_prof_lanes), sizeof(tmp)) != hipSuccess) return -1;
+    const uint64_t zero[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_prof_lanes), zero, sizeof(zero)) != hipSuccess) return -1;
+    for (int k = 0; k < n && k < 8; ++k) out[k] = tmp[k];
+    return 8;
+#else
+    (void)out;
+    (void)n;
+    return 0;
+#endif
+}
+#endif

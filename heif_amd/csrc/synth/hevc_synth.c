@@ -812,7 +812,7 @@ long synth_pps(const synth_params *P, uint8_t *out, size_t cap) {
     bw_bits(&w, 0, 1);
     bw_bits(&w, P->tq_bypass ? 1 : 0, 1);
     bw_bits(&w, 0, 1); /* tiles */
-    bw_bits(&w, 1, 1); /* entropy_coding_sync */
+    bw_bits(&w, P->wpp ? 1 : 0, 1); /* entropy_coding_sync */
     bw_bits(&w, 0, 1); /* loop filter across slices */
     bw_bits(&w, 1, 1); /* deblocking control present */
     bw_bits(&w, 0, 1);
@@ -843,6 +843,7 @@ int synth_check_params(const synth_params *P) {
         return -1;
     if (P->diff_cu_qp_delta_depth < 0 || P->diff_cu_qp_delta_depth > P->log2_ctb - P->log2_min_cb) return -1;
     if (P->density < 0 || P->density > 100) return -1;
+    if (P->wpp != 0 && P->wpp != 1) return -1;
     return 0;
 }
 
@@ -874,9 +875,14 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
     uint8_t wst[C_NUM], wmps[C_NUM];
     int saved = 0;
     ce_init_ctx(&p->c, slice_qp);
+    /* WPP: one substream per CTB row (9.3.1: contexts after CTU 1 of the row
+     * above, engine restarted at the entry point, end_of_subset_one_bit and
+     * byte_alignment at the row end).  Without WPP the slice is one substream:
+     * the engine and the contexts run on across rows (slice.rs:206-231). */
+    const int nsub = P->wpp ? p->hctb : 1;
     for (int ry = 0; ry < p->hctb; ry++) {
-        ce_start(&p->c, &subs[ry]);
-        if (ry > 0) {
+        if (P->wpp || ry == 0) ce_start(&p->c, &subs[P->wpp ? ry : 0]);
+        if (P->wpp && ry > 0) {
             if (p->wctb > 1 && saved) { memcpy(p->c.st, wst, C_NUM); memcpy(p->c.mps, wmps, C_NUM); }
             else ce_init_ctx(&p->c, slice_qp);
         }
@@ -887,21 +893,22 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
             int last = (rx == p->wctb - 1 && ry == p->hctb - 1);
             ce_term(&p->c, last);
         }
+        if (!P->wpp && ry != p->hctb - 1) continue;
         if (ry != p->hctb - 1) ce_term(&p->c, 1); /* end_of_subset_one_bit */
         ce_finish(&p->c);
-        bw_align1(&subs[ry]); /* byte_alignment() / rbsp_slice_segment_trailing_bits() */
+        bw_align1(&subs[P->wpp ? ry : 0]); /* byte_alignment() / rbsp_slice_segment_trailing_bits() */
     }
     /* substreams with emulation prevention, to size the entry points */
     long ret = -1;
     size_t total = 0;
     int err = 0;
-    for (int r = 0; r < p->hctb; r++) { total += subs[r].n; err |= subs[r].err; }
+    for (int r = 0; r < nsub; r++) { total += subs[r].n; err |= subs[r].err; }
     uint8_t *data = (uint8_t *)malloc(total * 3 / 2 + 16);
     size_t *sub_len = (size_t *)calloc((size_t)p->hctb, sizeof(size_t));
     if (data && sub_len && !err) {
         size_t o = 0;
         int z = 0; /* the slice header ends in a nonzero byte (its alignment bit) */
-        for (int r = 0; r < p->hctb; r++) {
+        for (int r = 0; r < nsub; r++) {
             size_t m = ep_insert(subs[r].d, subs[r].n, data + o, total * 3 / 2 + 16 - o, &z);
             sub_len[r] = m;
             o += m;
@@ -917,14 +924,16 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
             if (P->chroma_format) bw_bits(&w, (uint32_t)sao_c, 1);
         }
         bw_se(&w, slice_qp_delta);
-        bw_ue(&w, (uint32_t)(p->hctb - 1));
-        if (p->hctb > 1) {
-            size_t mx = 1;
-            for (int r = 0; r < p->hctb - 1; r++) mx = sub_len[r] > mx ? sub_len[r] : mx;
-            int len = 1;
-            while (((size_t)1 << len) < mx) len++;
-            bw_ue(&w, (uint32_t)(len - 1));
-            for (int r = 0; r < p->hctb - 1; r++) bw_bits(&w, (uint32_t)(sub_len[r] - 1), len);
+        if (P->wpp) { /* num_entry_point_offsets: present only with tiles or WPP (7.3.6.1) */
+            bw_ue(&w, (uint32_t)(nsub - 1));
+            if (nsub > 1) {
+                size_t mx = 1;
+                for (int r = 0; r < nsub - 1; r++) mx = sub_len[r] > mx ? sub_len[r] : mx;
+                int len = 1;
+                while (((size_t)1 << len) < mx) len++;
+                bw_ue(&w, (uint32_t)(len - 1));
+                for (int r = 0; r < nsub - 1; r++) bw_bits(&w, (uint32_t)(sub_len[r] - 1), len);
+            }
         }
         bw_align1(&w);
         if (!w.err) {
@@ -945,7 +954,7 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
     }
     free(data);
     free(sub_len);
-    for (int r = 0; r < p->hctb; r++) free(subs[r].d);
+    for (int r = 0; r < nsub; r++) free(subs[r].d);
     free(subs);
     free(p->ipm);
     free(p->depth);

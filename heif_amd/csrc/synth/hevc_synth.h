@@ -19,6 +19,8 @@ typedef struct {
     int32_t init_qp, slice_qp_delta, cb_qp_offset, cr_qp_offset;
     int32_t sao, deblock_disabled, beta_offset_div2, tc_offset_div2;
     int32_t density;                  /* sig_coeff_flag probability, percent */
+    int32_t wpp;                      /* entropy_coding_sync_enabled_flag: 1 = one substream per CTB row
+                                         with entry points, 0 = the whole slice in one substream */
 } synth_params;
 
 /* Each returns the NAL unit length (2-byte header included, emulation
@@ -27,7 +29,7 @@ typedef struct {
 long synth_vps(const synth_params *p, uint8_t *out, size_t cap);
 long synth_sps(const synth_params *p, uint8_t *out, size_t cap);
 long synth_pps(const synth_params *p, uint8_t *out, size_t cap);
-/* One IDR picture (a single I slice, WPP substreams + entry points). */
+/* One IDR picture (a single I slice; WPP substreams + entry points when p->wpp). */
 long synth_picture(const synth_params *p, uint64_t seed, uint8_t *out, size_t cap);
 int synth_check_params(const synth_params *p);
 

@@ -30,7 +30,7 @@ class _Params(ctypes.Structure):
         "sign_hiding", "cu_qp_delta", "diff_cu_qp_delta_depth",
         "transform_skip", "tq_bypass", "scaling_list", "strong_intra",
         "init_qp", "slice_qp_delta", "cb_qp_offset", "cr_qp_offset",
-        "sao", "deblock_disabled", "beta_offset_div2", "tc_offset_div2", "density")]
+        "sao", "deblock_disabled", "beta_offset_div2", "tc_offset_div2", "density", "wpp")]
 
 
 @dataclasses.dataclass
@@ -65,6 +65,7 @@ class SynthParams:
     beta_offset_div2: int = 0
     tc_offset_div2: int = 0
     density: int = 35
+    wpp: int = 1  # entropy_coding_sync_enabled_flag (0: one CABAC substream per picture, BASELINE config 2)
 
     def _c(self) -> _Params:
         return _Params(*[getattr(self, n) for n, _ in _Params._fields_])
@@ -137,7 +138,7 @@ def hvcc(p: SynthParams, vps: bytes, sps: bytes, pps: bytes) -> bytes:
     # compatibility/constraint bytes can carry emulation prevention).
     ptl = _unescape(sps[2:])[1:13]
     rec = bytes([1]) + ptl[:1] + ptl[1:5] + ptl[5:11] + ptl[11:12]
-    rec += struct.pack(">H", 0xF000) + bytes([0xFC | 2])          # min_spatial_segmentation, parallelism (WPP)
+    rec += struct.pack(">H", 0xF000) + bytes([0xFC | (2 if p.wpp else 0)])  # min_spatial_segmentation, parallelism
     rec += bytes([0xFC | p.chroma_format, 0xF8 | (p.bit_depth - 8), 0xF8 | (p.bit_depth - 8)])
     rec += struct.pack(">H", 0) + bytes([0x0F])                     # avgFrameRate, 1 layer, nested, 4-byte lengths
     arrays = b""

@@ -29,10 +29,9 @@ def _run(exe, path, env_extra=None):
     return r.returncode, r.stdout + r.stderr
 
 
-# k_parse with 16 / 1 / 3 waves per picture, and k_parse_lanes (one substream per lane)
-_SCALAR = {"HEIFGPU_PARSE": "scalar"}
-PARSERS = {"wave16": {**_SCALAR, "HEIFGPU_PARSE_GROUP": "16"}, "wave1": {**_SCALAR, "HEIFGPU_PARSE_GROUP": "1"},
-           "wave3": {**_SCALAR, "HEIFGPU_PARSE_GROUP": "3"}, "lanes": {"HEIFGPU_PARSE": "lanes"}}
+# k_parse_lanes (one substream per lane) with its default geometry, one
+# picture per wave, and batch (unsorted) wave order
+PARSERS = {"lanes": {}, "ppw1": {"HEIFGPU_LANES_PPW": "1"}, "order0": {"HEIFGPU_PARSE_ORDER": "0"}}
 
 
 @pytest.mark.parametrize("parser", list(PARSERS))
@@ -41,7 +40,7 @@ def test_emulated_kernels_match_oracle(emu_check, parser):
     assert rc == 0 and "EMU PARITY OK" in out, out[-2000:]
 
 
-@pytest.mark.parametrize("parser", ["wave16", "lanes"])
+@pytest.mark.parametrize("parser", ["lanes", "ppw1"])
 def test_emulated_kernels_permuted_image(emu_check, tmp_path, halfmoonbay, parser):
     p = tmp_path / "perm.heic"
     p.write_bytes(permuted_heic(halfmoonbay, 42))
@@ -68,7 +67,7 @@ def _corrupt(data: bytes, mode: str) -> bytes:
     return bytes(d)
 
 
-@pytest.mark.parametrize("parser", ["wave16", "lanes"])
+@pytest.mark.parametrize("parser", ["lanes", "ppw1"])
 @pytest.mark.parametrize("mode", ["random", "zeroed"])
 def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode, parser):
     """Corrupt slice data must end in status bits, never in a crash (the same

@@ -3,8 +3,8 @@
 Bar: bit-exact planes against the CPU oracle on the same input.  At the
 bench's batch sizes the check is size-independent: a permuted image is the
 oracle's 48 independently decoded tiles re-placed by the permutation, so
-every image of a large batch (which also switches k_parse to one wave per
-picture) is checked without re-running the oracle per image.
+every image of a large batch is checked without re-running the oracle per
+image.
 """
 import ctypes
 import hashlib
@@ -87,8 +87,9 @@ def test_permuted_batch_row_parallel(H, ctx, oracle_tiles, halfmoonbay):
     b.free()
 
 
-def test_large_batch_one_wave_per_picture(H, ctx, oracle_tiles, halfmoonbay):
-    """22 images = 1056 pictures >= kParseSerialMinPics: the serial-row parse mode."""
+def test_large_batch_many_waves(H, ctx, oracle_tiles, halfmoonbay):
+    """22 images = 1056 pictures = 264 k_parse_lanes waves (more than one per CU),
+    size-sorted snake order across waves, every image checked."""
     from heif_amd.synthetic import permutation, permuted_heic
 
     seeds = list(range(100, 122))

@@ -38,6 +38,17 @@ CASES = [
     ("one_cb", dict(width=8, height=8)),
     ("ctb64_partial", dict(width=72, height=40, log2_ctb=6, bit_depth=10, tq_bypass=1, transform_skip=1,
                            scaling_list=1)),
+    # entropy_coding_sync_enabled_flag = 0: the slice is one CABAC substream
+    # (BASELINE config 2; the reference's main read_data path, slice.rs:206-231)
+    ("nowpp_512", dict(width=512, height=512, wpp=0)),
+    ("nowpp_ctb16_10b", dict(bit_depth=10, log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2, wpp=0)),
+    # more than 64 CTB rows: WPP rows wrap round a picture's 64 lanes
+    ("rows68_ctb16", dict(width=64, height=1088, log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2)),
+    ("rows135_main10", dict(width=96, height=4320, bit_depth=10)),
+    ("rows68_nowpp", dict(width=64, height=1088, log2_ctb=4, log2_max_tb=4, wpp=0)),
+    # 132 CTBs wide x 70 rows: the row above a wrapped lane's next row is still
+    # being parsed when its contexts are stored (the staging block)
+    ("ring_wide_2112x1120", dict(width=2112, height=1120, log2_ctb=4, log2_max_tb=4, density=10)),
 ]
 
 
@@ -173,6 +184,44 @@ def test_gpu_mixed_geometry_batch(H, oracle_mod):
 
 
 @pytest.mark.gpu
+def test_gpu_mixed_wpp_ring_batch(H, oracle_mod, halfmoonbay):
+    """One batch mixing a 48-tile WPP grid (halfmoonbay), a non-WPP 512x512
+    single-substream picture (config 2) and a 68-row CTB-16 picture whose WPP
+    rows wrap round its 64 lanes: lanes per picture is the batch maximum (64),
+    and each picture keeps its own substream layout."""
+    datas = [halfmoonbay, S.single_heic(params(dict(width=512, height=512, wpp=0)), seed=11),
+             S.single_heic(params(dict(width=64, height=1088, log2_ctb=4, log2_max_tb=4)), seed=12)]
+    ctx = H.DecodeContext(0)
+    imgs = [H.HeifImage.parse(d) for d in datas]
+    b = ctx.prepare(imgs)
+    outs = ctx.alloc_outputs(imgs)
+    for _ in range(2):  # two pipelined decodes (alternate parse sets)
+        b.decode_async(outs)
+    assert b.status() == [0, 0, 0]
+    for k, (d, o) in enumerate(zip(datas, outs)):
+        _assert_equal(_planes(o), oracle_mod.decode_heic(d, with_checks=False), k)
+    b.free()
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_nowpp_batch_64_per_wave(H, oracle_mod):
+    """128 non-WPP pictures: one lane each, 64 pictures per k_parse_lanes wave."""
+    p = params(dict(width=64, height=64, wpp=0))
+    datas = [S.single_heic(p, seed=100 + k) for k in range(128)]
+    ctx = H.DecodeContext(0)
+    imgs = [H.HeifImage.parse(d) for d in datas]
+    b = ctx.prepare(imgs)
+    outs = ctx.alloc_outputs(imgs)
+    b.decode_async(outs)
+    assert not any(b.status())
+    for k in (0, 1, 63, 64, 127):
+        _assert_equal(_planes(outs[k]), oracle_mod.decode_heic(datas[k], with_checks=False), k)
+    b.free()
+    ctx.close()
+
+
+@pytest.mark.gpu
 def test_gpu_config5_8k_main10_grid(H, oracle_mod):
     """BASELINE config 5 at full size: 7680x4320 Main-10 grid, 135 tiles."""
     c5 = S.CONFIG5
@@ -184,7 +233,7 @@ def test_gpu_config5_8k_main10_grid(H, oracle_mod):
 
 
 # ------------------------------------------- kernels compiled for the host
-@pytest.mark.parametrize("parser", ["lanes", "scalar"])
+@pytest.mark.parametrize("parser", ["lanes", "ppw1"])
 def test_emulated_kernels_on_synthetic_streams(tmp_path, parser):
     """The GPU kernels' source built for the host (HG_HOST_EMU, see
     test_emulation.py) decodes every synthetic case bit-exactly vs the oracle."""
@@ -195,7 +244,7 @@ def test_emulated_kernels_on_synthetic_streams(tmp_path, parser):
     csrc = pathlib.Path(__file__).resolve().parents[1] / "heif_amd" / "csrc"
     subprocess.run(["make", "-s", "-C", str(csrc), "emu-fast"], check=True, capture_output=True)
     exe = csrc / "build" / "emu_fast" / "emu_check"
-    env = dict(os.environ, HEIFGPU_PARSE=parser)
+    env = dict(os.environ, **({"HEIFGPU_LANES_PPW": "1"} if parser == "ppw1" else {}))
     for name, over in CASES:
         path = tmp_path / f"{name}.heic"
         path.write_bytes(S.single_heic(params(over), seed=1))
