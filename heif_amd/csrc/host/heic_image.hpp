@@ -35,9 +35,6 @@ struct ParsedImage {
 };
 
 // Throws HeifError (parse) or UnsupportedError (valid stream, tool outside this path).
-struct UnsupportedError : HeifError {
-    explicit UnsupportedError(const std::string &m) : HeifError(m) {}
-};
 // item_id 0 = the primary item (heic/decoder.rs:12-112); otherwise any coded
 // image item, e.g. an auxiliary image found through ParsedImage::aux_item_id
 ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id = 0);

@@ -92,7 +92,8 @@ std::vector<uint8_t> Heif::item_data(const ItemInfo &it) const {
         } else {
             throw HeifError("unsupported construction_method " + std::to_string(it.construction_method));
         }
-        if (e.offset + e.length > limit) throw HeifError("item extent out of bounds");
+        // without overflow: offset and length are up to 64-bit file fields
+        if (e.offset > limit || e.length > limit - e.offset) throw HeifError("item extent out of bounds");
         out.insert(out.end(), base + e.offset, base + e.offset + e.length);
     }
     return out;
@@ -232,6 +233,7 @@ Heif HeifReader::read() {
             for (uint32_t k = 0; k < ne; ++k) {
                 if (idx_sz) c.be(idx_sz);
                 uint64_t o = c.be(off_sz), l = c.be(len_sz);
+                if (o > UINT64_MAX - base) throw HeifError("iloc extent offset overflows");
                 it.extents.push_back({base + o, l});
             }
         }

@@ -78,7 +78,7 @@ void scaling_list_data(RbspReader &r, ScalingLists &s) {
             bool pred_mode = r.read_flag();
             int coef_num = std::min(64, 1 << (4 + (size_id << 1)));
             if (!pred_mode) {
-                int delta = int(r.read_ue());
+                int delta = r.read_ue_max(5, "scaling_list_pred_matrix_id_delta");
                 if (delta == 0) {
                     default_list(size_id, mid, s.list[size_id][mid], s.dc[size_id][mid]);
                 } else {
@@ -90,11 +90,11 @@ void scaling_list_data(RbspReader &r, ScalingLists &s) {
             } else {
                 int next = 8;
                 if (size_id > 1) {
-                    next = r.read_se() + 8;
+                    next = r.read_se_range(-7, 247, "scaling_list_dc_coef_minus8") + 8;
                     s.dc[size_id][mid] = next;
                 }
                 for (int i = 0; i < coef_num; ++i) {
-                    next = (next + r.read_se() + 256) % 256;
+                    next = (next + r.read_se_range(-128, 127, "scaling_list_delta_coef") + 256) % 256;
                     s.list[size_id][mid][i] = uint8_t(next);
                 }
                 if (size_id <= 1) s.dc[size_id][mid] = 16;
@@ -202,7 +202,7 @@ void vui_parameters(RbspReader &r, SequenceParameterSet &s) {
 void st_ref_pic_set(RbspReader &r, int idx, int num_sets, std::vector<int> &num_delta) {
     bool inter = idx != 0 && r.read_flag();
     if (inter) {
-        int delta_idx = idx == num_sets ? int(r.read_ue()) + 1 : 1;
+        int delta_idx = idx == num_sets ? r.read_ue_max(uint32_t(idx - 1), "delta_idx_minus1") + 1 : 1;
         int ref = idx - delta_idx;
         if (ref < 0) throw HeifError("st_ref_pic_set: bad delta_idx");
         r.read_flag();
@@ -215,7 +215,7 @@ void st_ref_pic_set(RbspReader &r, int idx, int num_sets, std::vector<int> &num_
         }
         num_delta[size_t(idx)] = cnt;
     } else {
-        int neg = int(r.read_ue()), pos = int(r.read_ue());
+        int neg = r.read_ue_max(16, "num_negative_pics"), pos = r.read_ue_max(16, "num_positive_pics");
         if (neg > 16 || pos > 16) throw HeifError("st_ref_pic_set: too many pictures");
         for (int i = 0; i < neg + pos; ++i) {
             r.read_ue();
@@ -268,6 +268,27 @@ VideoParameterSet video_parameter_set_rbsp(const std::vector<uint8_t> &rbsp) {
     return v;
 }
 
+// 7.4.3.2 semantic constraints the kernels rely on (block-size ladders, PCM
+// sizes, picture size in whole minimum CBs), then this path's profile limits
+void validate_sps(const SequenceParameterSet &s) {
+    const int min_cb = s.log2_min_luma_coding_block_size, ctb = s.log2_ctb_size;
+    const int min_tb = s.log2_min_tb_size, max_tb = s.log2_max_tb_size;
+    if (ctb < 4 || ctb > 6 || min_cb < 3 || min_cb > ctb) throw HeifError("SPS coding block sizes out of range");
+    if (min_tb < 2 || min_tb >= min_cb || max_tb > 5 || max_tb > ctb)
+        throw HeifError("SPS transform block sizes out of range");
+    if (s.max_transform_hierarchy_depth_intra > ctb - min_tb || s.max_transform_hierarchy_depth_inter > ctb - min_tb)
+        throw HeifError("max_transform_hierarchy_depth out of range");
+    if (s.pic_width_in_luma_samples <= 0 || s.pic_height_in_luma_samples <= 0 ||
+        (s.pic_width_in_luma_samples & ((1 << min_cb) - 1)) || (s.pic_height_in_luma_samples & ((1 << min_cb) - 1)))
+        throw HeifError("picture size is not a multiple of MinCbSizeY");
+    if (s.pcm_enabled_flag &&
+        (s.log2_max_pcm > (ctb < 5 ? ctb : 5) || s.pcm_bit_depth_luma > 8 + s.bit_depth_luma_minus8 ||
+         s.pcm_bit_depth_chroma > 8 + s.bit_depth_chroma_minus8))
+        throw HeifError("PCM parameters out of range");
+    if (s.bit_depth_luma_minus8 > 2 || s.bit_depth_chroma_minus8 > 2)
+        throw UnsupportedError("bit depth above 10 (only 8..10-bit streams are parity-tested on this path)");
+}
+
 SequenceParameterSet sequence_parameter_set_rbsp(const std::vector<uint8_t> &rbsp) {
     RbspReader r(rbsp.data(), rbsp.size());
     SequenceParameterSet s;
@@ -275,35 +296,40 @@ SequenceParameterSet sequence_parameter_set_rbsp(const std::vector<uint8_t> &rbs
     s.max_sub_layers_minus1 = int(r.read_bits(3));
     r.read_flag();
     profile_tier_level(r, s.max_sub_layers_minus1, &s.general_profile_idc, &s.general_level_idc);
-    s.sps_id = int(r.read_ue());
-    s.chroma_format_idc = int(r.read_ue());
-    if (s.chroma_format_idc > 3) throw HeifError("chroma_format_idc out of range");
+    s.sps_id = r.read_ue_max(15, "sps_seq_parameter_set_id");
+    s.chroma_format_idc = r.read_ue_max(3, "chroma_format_idc");
     if (s.chroma_format_idc == 3) s.separate_colour_plane_flag = r.read_flag();
-    s.pic_width_in_luma_samples = int(r.read_ue());
-    s.pic_height_in_luma_samples = int(r.read_ue());
+    // 16888 = sqrt(8 * MaxLumaPs) of level 6.2 (A.4.1), the largest legal dimension
+    s.pic_width_in_luma_samples = r.read_ue_max(16888, "pic_width_in_luma_samples");
+    s.pic_height_in_luma_samples = r.read_ue_max(16888, "pic_height_in_luma_samples");
     int sw = (s.chroma_format_idc == 1 || s.chroma_format_idc == 2) ? 2 : 1;
     int sh = s.chroma_format_idc == 1 ? 2 : 1;
     if (r.read_flag()) {
-        s.conf_win_left = int(r.read_ue()) * sw;
-        s.conf_win_right = int(r.read_ue()) * sw;
-        s.conf_win_top = int(r.read_ue()) * sh;
-        s.conf_win_bottom = int(r.read_ue()) * sh;
+        // 7.4.3.2: SubWidthC * (left + right) < pic_width, likewise vertically
+        const uint32_t l = r.read_ue(), rt = r.read_ue(), t = r.read_ue(), b = r.read_ue();
+        if (uint64_t(sw) * (uint64_t(l) + rt) >= uint64_t(s.pic_width_in_luma_samples) ||
+            uint64_t(sh) * (uint64_t(t) + b) >= uint64_t(s.pic_height_in_luma_samples))
+            throw HeifError("conformance window out of range");
+        s.conf_win_left = int(l) * sw;
+        s.conf_win_right = int(rt) * sw;
+        s.conf_win_top = int(t) * sh;
+        s.conf_win_bottom = int(b) * sh;
     }
-    s.bit_depth_luma_minus8 = int(r.read_ue());
-    s.bit_depth_chroma_minus8 = int(r.read_ue());
-    s.log2_max_pic_order_cnt_lsb = int(r.read_ue()) + 4;
+    s.bit_depth_luma_minus8 = r.read_ue_max(8, "bit_depth_luma_minus8");
+    s.bit_depth_chroma_minus8 = r.read_ue_max(8, "bit_depth_chroma_minus8");
+    s.log2_max_pic_order_cnt_lsb = r.read_ue_max(12, "log2_max_pic_order_cnt_lsb_minus4") + 4;
     bool ordering = r.read_flag();
     for (int i = ordering ? 0 : s.max_sub_layers_minus1; i <= s.max_sub_layers_minus1; ++i) {
         r.read_ue();
         r.read_ue();
         r.read_ue();
     }
-    s.log2_min_luma_coding_block_size = int(r.read_ue()) + 3;
-    s.log2_ctb_size = s.log2_min_luma_coding_block_size + int(r.read_ue());
-    s.log2_min_tb_size = int(r.read_ue()) + 2;
-    s.log2_max_tb_size = s.log2_min_tb_size + int(r.read_ue());
-    s.max_transform_hierarchy_depth_inter = int(r.read_ue());
-    s.max_transform_hierarchy_depth_intra = int(r.read_ue());
+    s.log2_min_luma_coding_block_size = r.read_ue_max(3, "log2_min_luma_coding_block_size_minus3") + 3;
+    s.log2_ctb_size = s.log2_min_luma_coding_block_size + r.read_ue_max(3, "log2_diff_max_min_luma_coding_block_size");
+    s.log2_min_tb_size = r.read_ue_max(3, "log2_min_luma_transform_block_size_minus2") + 2;
+    s.log2_max_tb_size = s.log2_min_tb_size + r.read_ue_max(3, "log2_diff_max_min_luma_transform_block_size");
+    s.max_transform_hierarchy_depth_inter = r.read_ue_max(4, "max_transform_hierarchy_depth_inter");
+    s.max_transform_hierarchy_depth_intra = r.read_ue_max(4, "max_transform_hierarchy_depth_intra");
     s.scaling.set_default();
     s.scaling_list_enabled_flag = r.read_flag();
     if (s.scaling_list_enabled_flag && r.read_flag()) scaling_list_data(r, s.scaling);
@@ -313,18 +339,17 @@ SequenceParameterSet sequence_parameter_set_rbsp(const std::vector<uint8_t> &rbs
     if (s.pcm_enabled_flag) {
         s.pcm_bit_depth_luma = int(r.read_bits(4)) + 1;
         s.pcm_bit_depth_chroma = int(r.read_bits(4)) + 1;
-        s.log2_min_pcm = int(r.read_ue()) + 3;
-        s.log2_max_pcm = s.log2_min_pcm + int(r.read_ue());
+        s.log2_min_pcm = r.read_ue_max(2, "log2_min_pcm_luma_coding_block_size_minus3") + 3;
+        s.log2_max_pcm = s.log2_min_pcm + r.read_ue_max(2, "log2_diff_max_min_pcm_luma_coding_block_size");
         s.pcm_loop_filter_disabled_flag = r.read_flag();
     }
-    s.num_short_term_ref_pic_sets = int(r.read_ue());
-    if (s.num_short_term_ref_pic_sets > 64) throw HeifError("num_short_term_ref_pic_sets > 64");
+    s.num_short_term_ref_pic_sets = r.read_ue_max(64, "num_short_term_ref_pic_sets");
     s.st_rps_num_delta_pocs.assign(65, 0);
     for (int i = 0; i < s.num_short_term_ref_pic_sets; ++i)
         st_ref_pic_set(r, i, s.num_short_term_ref_pic_sets, s.st_rps_num_delta_pocs);
     s.long_term_ref_pics_present_flag = r.read_flag();
     if (s.long_term_ref_pics_present_flag) {
-        s.num_long_term_ref_pics_sps = int(r.read_ue());
+        s.num_long_term_ref_pics_sps = r.read_ue_max(32, "num_long_term_ref_pics_sps");
         for (int i = 0; i < s.num_long_term_ref_pics_sps; ++i) {
             r.read_bits(s.log2_max_pic_order_cnt_lsb);
             r.read_flag();
@@ -338,17 +363,15 @@ SequenceParameterSet sequence_parameter_set_rbsp(const std::vector<uint8_t> &rbs
         r.read_bits(3 + 4);
         if (range) s.range_extension_tools = r.read_bits(9) != 0;
     }
-    if (s.log2_ctb_size > 6 || s.log2_ctb_size < 4 || s.log2_max_tb_size > 5 ||
-        s.log2_min_tb_size >= s.log2_min_luma_coding_block_size || s.bit_depth_luma_minus8 > 8)
-        throw HeifError("SPS values out of range");
+    validate_sps(s);
     return s;
 }
 
 PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp, const SequenceParameterSet &sps) {
     RbspReader r(rbsp.data(), rbsp.size());
     PictureParameterSet p;
-    p.pps_id = int(r.read_ue());
-    p.sps_id = int(r.read_ue());
+    p.pps_id = r.read_ue_max(63, "pps_pic_parameter_set_id");
+    p.sps_id = r.read_ue_max(15, "pps_seq_parameter_set_id");
     p.dependent_slice_segments_enabled_flag = r.read_flag();
     p.output_flag_present_flag = r.read_flag();
     p.num_extra_slice_header_bits = int(r.read_bits(3));
@@ -360,9 +383,11 @@ PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp,
     p.constrained_intra_pred_flag = r.read_flag();
     p.transform_skip_enabled_flag = r.read_flag();
     p.cu_qp_delta_enabled_flag = r.read_flag();
-    if (p.cu_qp_delta_enabled_flag) p.diff_cu_qp_delta_depth = int(r.read_ue());
-    p.pps_cb_qp_offset = r.read_se();
-    p.pps_cr_qp_offset = r.read_se();
+    if (p.cu_qp_delta_enabled_flag)
+        p.diff_cu_qp_delta_depth = r.read_ue_max(uint32_t(sps.log2_ctb_size - sps.log2_min_luma_coding_block_size),
+                                                 "diff_cu_qp_delta_depth");
+    p.pps_cb_qp_offset = r.read_se_range(-12, 12, "pps_cb_qp_offset");
+    p.pps_cr_qp_offset = r.read_se_range(-12, 12, "pps_cr_qp_offset");
     p.pps_slice_chroma_qp_offsets_present_flag = r.read_flag();
     r.read_flag();  // weighted_pred_flag
     r.read_flag();  // weighted_bipred_flag
@@ -370,7 +395,7 @@ PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp,
     p.tiles_enabled_flag = r.read_flag();
     p.entropy_coding_sync_enabled_flag = r.read_flag();
     if (p.tiles_enabled_flag) {
-        int nc = int(r.read_ue()) + 1, nr = int(r.read_ue()) + 1;
+        int nc = r.read_ue_max(19, "num_tile_columns_minus1") + 1, nr = r.read_ue_max(21, "num_tile_rows_minus1") + 1;
         p.uniform_spacing_flag = r.read_flag();
         if (!p.uniform_spacing_flag) {
             for (int i = 0; i < nc - 1; ++i) p.column_widths.push_back(int(r.read_ue()) + 1);
@@ -384,8 +409,8 @@ PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp,
         p.deblocking_filter_override_enabled_flag = r.read_flag();
         p.pps_deblocking_filter_disabled_flag = r.read_flag();
         if (!p.pps_deblocking_filter_disabled_flag) {
-            p.pps_beta_offset_div2 = r.read_se();
-            p.pps_tc_offset_div2 = r.read_se();
+            p.pps_beta_offset_div2 = r.read_se_range(-6, 6, "pps_beta_offset_div2");
+            p.pps_tc_offset_div2 = r.read_se_range(-6, 6, "pps_tc_offset_div2");
         }
     }
     p.scaling = sps.scaling;
@@ -395,7 +420,7 @@ PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp,
         scaling_list_data(r, p.scaling);
     }
     p.lists_modification_present_flag = r.read_flag();
-    p.log2_parallel_merge_level = int(r.read_ue()) + 2;
+    p.log2_parallel_merge_level = r.read_ue_max(uint32_t(sps.log2_ctb_size - 2), "log2_parallel_merge_level_minus2") + 2;
     p.slice_segment_header_extension_present_flag = r.read_flag();
     if (r.read_flag()) {
         bool range = r.read_flag();
@@ -425,10 +450,10 @@ SliceSegmentHeader slice_segment_header(const uint8_t *payload, size_t len, NalU
     int t = nal.nal_unit_type();
     h.first_slice_segment_in_pic_flag = r.read_flag();
     if (t >= 16 && t <= 23) r.read_flag();  // no_output_of_prior_pics_flag
-    h.slice_pic_parameter_set_id = int(r.read_ue());
+    h.slice_pic_parameter_set_id = r.read_ue_max(63, "slice_pic_parameter_set_id");
     if (!h.first_slice_segment_in_pic_flag) throw HeifError("multi-slice pictures are not supported");
     r.read_bits(pps.num_extra_slice_header_bits);
-    h.slice_type = int(r.read_ue());
+    h.slice_type = r.read_ue_max(2, "slice_type");
     if (h.slice_type != 2) throw HeifError("P/B slices are not supported (still images are intra)");
     if (pps.output_flag_present_flag) r.read_flag();
     if (sps.separate_colour_plane_flag) r.read_bits(2);
@@ -441,8 +466,8 @@ SliceSegmentHeader slice_segment_header(const uint8_t *payload, size_t len, NalU
             r.read_bits(ceil_log2(sps.num_short_term_ref_pic_sets));
         }
         if (sps.long_term_ref_pics_present_flag) {
-            int nsps = sps.num_long_term_ref_pics_sps > 0 ? int(r.read_ue()) : 0;
-            int npics = int(r.read_ue());
+            int nsps = sps.num_long_term_ref_pics_sps > 0 ? r.read_ue_max(uint32_t(sps.num_long_term_ref_pics_sps), "num_long_term_sps") : 0;
+            int npics = r.read_ue_max(32, "num_long_term_pics");
             for (int i = 0; i < nsps + npics; ++i) {
                 if (i < nsps) {
                     if (sps.num_long_term_ref_pics_sps > 1) r.read_bits(ceil_log2(sps.num_long_term_ref_pics_sps));
@@ -460,9 +485,16 @@ SliceSegmentHeader slice_segment_header(const uint8_t *payload, size_t len, NalU
         if (sps.chroma_array_type() != 0) h.slice_sao_chroma_flag = r.read_flag();
     }
     h.slice_qp_delta = r.read_se();
+    {  // 7.4.7.1: SliceQpY in [-QpBdOffsetY, +51]
+        const int qp = 26 + pps.init_qp_minus26 + h.slice_qp_delta;
+        if (qp < -6 * sps.bit_depth_luma_minus8 || qp > 51) throw HeifError("SliceQpY out of range");
+    }
     if (pps.pps_slice_chroma_qp_offsets_present_flag) {
-        h.slice_cb_qp_offset = r.read_se();
-        h.slice_cr_qp_offset = r.read_se();
+        h.slice_cb_qp_offset = r.read_se_range(-12, 12, "slice_cb_qp_offset");
+        h.slice_cr_qp_offset = r.read_se_range(-12, 12, "slice_cr_qp_offset");
+        if (pps.pps_cb_qp_offset + h.slice_cb_qp_offset < -12 || pps.pps_cb_qp_offset + h.slice_cb_qp_offset > 12 ||
+            pps.pps_cr_qp_offset + h.slice_cr_qp_offset < -12 || pps.pps_cr_qp_offset + h.slice_cr_qp_offset > 12)
+            throw HeifError("chroma QP offsets out of range");
     }
     bool override_flag = pps.deblocking_filter_override_enabled_flag ? r.read_flag() : false;
     h.slice_deblocking_filter_disabled_flag = pps.pps_deblocking_filter_disabled_flag;
@@ -471,25 +503,23 @@ SliceSegmentHeader slice_segment_header(const uint8_t *payload, size_t len, NalU
     if (override_flag) {
         h.slice_deblocking_filter_disabled_flag = r.read_flag();
         if (!h.slice_deblocking_filter_disabled_flag) {
-            h.slice_beta_offset_div2 = r.read_se();
-            h.slice_tc_offset_div2 = r.read_se();
+            h.slice_beta_offset_div2 = r.read_se_range(-6, 6, "slice_beta_offset_div2");
+            h.slice_tc_offset_div2 = r.read_se_range(-6, 6, "slice_tc_offset_div2");
         }
     }
     if (pps.pps_loop_filter_across_slices_enabled_flag &&
         (h.slice_sao_luma_flag || h.slice_sao_chroma_flag || !h.slice_deblocking_filter_disabled_flag))
         r.read_flag();
     if (pps.tiles_enabled_flag || pps.entropy_coding_sync_enabled_flag) {
-        h.num_entry_point_offsets = int(r.read_ue());
-        int max_entries = sps.pic_height_in_ctbs_y() * (pps.tiles_enabled_flag ? sps.pic_width_in_ctbs_y() : 1);
-        if (h.num_entry_point_offsets > max_entries) throw HeifError("num_entry_point_offsets out of range");
+        const int max_entries = sps.pic_height_in_ctbs_y() * (pps.tiles_enabled_flag ? sps.pic_width_in_ctbs_y() : 1);
+        h.num_entry_point_offsets = r.read_ue_max(uint32_t(max_entries), "num_entry_point_offsets");
         if (h.num_entry_point_offsets > 0) {
-            int bits = int(r.read_ue()) + 1;
-            if (bits > 32) throw HeifError("offset_len_minus1 out of range");
+            const int bits = r.read_ue_max(31, "offset_len_minus1") + 1;
             for (int i = 0; i < h.num_entry_point_offsets; ++i) h.entry_point_offset.push_back(r.read_bits(bits) + 1);
         }
     }
     if (pps.slice_segment_header_extension_present_flag) {
-        uint32_t l = r.read_ue();
+        const int l = r.read_ue_max(256, "slice_segment_header_extension_length");
         r.skip_bits(size_t(l) * 8);
     }
     r.byte_alignment();

@@ -14,6 +14,10 @@ namespace hg {
 struct HeifError : std::runtime_error {
     explicit HeifError(const std::string &m) : std::runtime_error(m) {}
 };
+// a valid stream that uses a tool outside this decode path (HEIFGPU_E_UNSUPPORTED)
+struct UnsupportedError : HeifError {
+    explicit UnsupportedError(const std::string &m) : HeifError(m) {}
+};
 
 class RbspReader {
   public:
@@ -49,10 +53,21 @@ class RbspReader {
         if (lz == 0) return 0;
         return ((1u << lz) - 1u) + read_bits(lz);
     }
+    // ue(v) with its semantic range checked before any narrowing cast
+    int read_ue_max(uint32_t max, const char *what) {
+        const uint32_t v = read_ue();
+        if (v > max) throw HeifError(std::string(what) + " out of range");
+        return int(v);
+    }
     int32_t read_se() {
         uint32_t k = read_ue();
         if (k == 0) return 0;
         return (k & 1) ? int32_t((k + 1) / 2) : -int32_t(k / 2);
+    }
+    int read_se_range(int lo, int hi, const char *what) {
+        const int32_t v = read_se();
+        if (v < lo || v > hi) throw HeifError(std::string(what) + " out of range");
+        return v;
     }
     // byte_alignment(): alignment_bit_equal_to_one then zero bits (rbsp_reader.rs:53-63)
     void byte_alignment() {

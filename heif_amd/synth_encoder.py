@@ -151,31 +151,81 @@ def _ispe(w: int, h: int) -> bytes:
     return _fbox(b"ispe", 0, 0, struct.pack(">II", w, h))
 
 
+@dataclasses.dataclass
+class BoxLayout:
+    """Container variants the reference's reader gets wrong or leaves todo!()
+    (src/heif/reader.rs): items split into several iloc extents (:47), infe
+    version 0/1 entries (:303), unknown ipco properties ahead of the known
+    ones (:460-463 drops them, shifting ipma indices), 16-bit ipma indices
+    (flags & 1, :496-500), and the iloc field widths / base offset (for the
+    overflow cases of the host's bounds checks)."""
+    extents: int = 1            # iloc extents per mdat item (data split evenly)
+    legacy_infe_items: int = 0  # extra metadata items declared with infe version 0 / 1 (alternating)
+    unknown_props: int = 0      # unknown property boxes inserted at the front of ipco
+    ipma_16bit: bool = False    # ipma flags & 1: 15-bit property indices
+    offset_size: int = 4        # iloc offset_size / length_size / base_offset_size (bytes)
+    length_size: int = 4
+    base_offset_size: int = 0
+    base_offset: int = 0        # added to every mdat extent offset (iloc base_offset)
+    first_extent_offset: Optional[int] = None  # raw value written for the first mdat extent's offset (corruption)
+
+
+def _be(v: int, n: int) -> bytes:
+    return (v & ((1 << (8 * n)) - 1)).to_bytes(n, "big") if n else b""
+
+
 def _assemble(items: List[Tuple[int, bytes, bytes]], primary: int, props: List[bytes],
-              assoc: List[Tuple[int, List[int]]], iref: bytes, idat: bytes) -> bytes:
+              assoc: List[Tuple[int, List[int]]], iref: bytes, idat: bytes,
+              layout: Optional[BoxLayout] = None) -> bytes:
     """items: (item_id, item_type, data); data of 'grid' items lives in idat
     (construction_method 1), everything else in mdat."""
+    L = layout or BoxLayout()
     ftyp = _box(b"ftyp", b"heic" + struct.pack(">I", 0) + b"mif1heic")
     hdlr = _fbox(b"hdlr", 0, 0, struct.pack(">I", 0) + b"pict" + bytes(12) + b"\0")
     pitm = _fbox(b"pitm", 0, 0, struct.pack(">H", primary))
     infes = b"".join(_fbox(b"infe", 2, 0, struct.pack(">HH", iid, 0) + typ + b"\0") for iid, typ, _ in items)
+    # ISO/IEC 14496-12 8.11.6 infe v0 / v1: item_ID, protection index, item_name,
+    # content_type, content_encoding (+ v1: extension_type); no item_type.  HEIF
+    # image items need v2+, so these are metadata items the reader must skip.
+    base_id = max(iid for iid, _, _ in items) + 1
+    legacy = [(base_id + k, b"legacy-%d" % k) for k in range(L.legacy_infe_items)]
+    for k, (iid, name) in enumerate(legacy):
+        v = k & 1
+        infes += _fbox(b"infe", v, 0, struct.pack(">HH", iid, 0) + name + b"\0application/octet-stream\0\0" +
+                       (b"fdel" if v else b""))
+        items = items + [(iid, b"meta", b"\x00" * (16 + k))]
     iinf = _fbox(b"iinf", 0, 0, struct.pack(">H", len(items)) + infes)
-    ipco = _box(b"ipco", b"".join(props))
+    unknown = [_box(b"zzz%d" % (k % 10), bytes(4 + k)) for k in range(L.unknown_props)]
+    ipco = _box(b"ipco", b"".join(unknown + props))
+    shift = L.unknown_props
     ipma_p = struct.pack(">I", len(assoc))
     for iid, idxs in assoc:
-        ipma_p += struct.pack(">HB", iid, len(idxs)) + bytes(0x80 | i for i in idxs)
-    iprp = _box(b"iprp", ipco + _fbox(b"ipma", 0, 0, ipma_p))
+        ipma_p += struct.pack(">HB", iid, len(idxs))
+        if L.ipma_16bit:
+            ipma_p += b"".join(struct.pack(">H", 0x8000 | (i + shift)) for i in idxs)
+        else:
+            ipma_p += bytes(0x80 | (i + shift) for i in idxs)
+    iprp = _box(b"iprp", ipco + _fbox(b"ipma", 0, 1 if L.ipma_16bit else 0, ipma_p))
     idat_box = _box(b"idat", idat) if idat else b""
 
     def build(mdat_start: int) -> Tuple[bytes, bytes]:
-        ent = struct.pack(">BBH", 0x44, 0x00, len(items))
+        os_, ls_, bs_ = L.offset_size, L.length_size, L.base_offset_size
+        ent = struct.pack(">BBH", (os_ << 4) | ls_, bs_ << 4, len(items))
         off = mdat_start
         body = b""
         for iid, typ, data in items:
             if typ == b"grid":
-                ent += struct.pack(">HHHHII", iid, 1, 0, 1, 0, len(data))
+                ent += struct.pack(">HHH", iid, 1, 0) + _be(0, bs_) + struct.pack(">H", 1) + _be(0, os_) + \
+                    _be(len(data), ls_)
             else:
-                ent += struct.pack(">HHHHII", iid, 0, 0, 1, off, len(data))
+                n = max(1, min(L.extents, len(data)))
+                cuts = [len(data) * k // n for k in range(n + 1)]
+                ent += struct.pack(">HHH", iid, 0, 0) + _be(L.base_offset, bs_) + struct.pack(">H", n)
+                for k in range(n):
+                    eo = off + cuts[k] - L.base_offset
+                    if L.first_extent_offset is not None and off == mdat_start and k == 0:
+                        eo = L.first_extent_offset
+                    ent += _be(eo, os_) + _be(cuts[k + 1] - cuts[k], ls_)
                 off += len(data)
                 body += data
         iloc = _fbox(b"iloc", 1, 0, ent)
@@ -192,7 +242,8 @@ def _len_prefixed(nal: bytes) -> bytes:
     return struct.pack(">I", len(nal)) + nal
 
 
-def grid_heic(out_w: int, out_h: int, p: SynthParams, seed: int = 0, pictures: Optional[List[bytes]] = None) -> bytes:
+def grid_heic(out_w: int, out_h: int, p: SynthParams, seed: int = 0, pictures: Optional[List[bytes]] = None,
+              layout: Optional[BoxLayout] = None) -> bytes:
     """A grid HEIC of ceil(out_w/W) x ceil(out_h/H) synthetic tiles of p's
     size, tile k drawn with seed (seed << 16) + k."""
     cols = -(-out_w // (p.width - p.conf_right))
@@ -209,15 +260,18 @@ def grid_heic(out_w: int, out_h: int, p: SynthParams, seed: int = 0, pictures: O
     assoc = [(grid_id, [3])] + [(k + 2, [1, 2]) for k in range(n)]
     iref = _fbox(b"iref", 0, 0, _box(b"dimg", struct.pack(">HH", grid_id, n) +
                                      b"".join(struct.pack(">H", k + 2) for k in range(n))))
-    return _assemble(items, grid_id, props, assoc, iref, items[0][2])
+    return _assemble(items, grid_id, props, assoc, iref, items[0][2], layout)
 
 
-def single_heic(p: SynthParams, seed: int = 0) -> bytes:
-    """A single-item (non-grid) HEIC holding one synthetic picture."""
-    vps, sps, pps = parameter_sets(p)
+def single_heic(p: SynthParams, seed: int = 0, layout: Optional[BoxLayout] = None,
+                param_sets: Optional[Tuple[bytes, bytes, bytes]] = None, nal: Optional[bytes] = None) -> bytes:
+    """A single-item (non-grid) HEIC holding one synthetic picture.
+    param_sets / nal replace the generated VPS/SPS/PPS / picture NAL unit
+    (robustness tests hand-craft out-of-range parameter sets)."""
+    vps, sps, pps = param_sets or parameter_sets(p)
     props = [hvcc(p, vps, sps, pps), _ispe(p.width - p.conf_right, p.height - p.conf_bottom)]
-    items = [(1, b"hvc1", _len_prefixed(picture(p, seed)))]
-    return _assemble(items, 1, props, [(1, [1, 2])], b"", b"")
+    items = [(1, b"hvc1", _len_prefixed(nal if nal is not None else picture(p, seed)))]
+    return _assemble(items, 1, props, [(1, [1, 2])], b"", b"", layout)
 
 
 # BASELINE config 5: 8K 10-bit Main-10 grid, 15 x 9 tiles of 512x512

@@ -81,6 +81,7 @@ static void parse_iloc(const uint8_t *d, size_t s, size_t e, heif_file *f) {
             if (index_size) rd(&c, index_size);
             uint64_t off = rd(&c, offset_size);
             uint64_t len = rd(&c, length_size);
+            if (off > UINT64_MAX - base) c.err = 1; /* base_offset + extent_offset wraps */
             if (it && it->n_extents < HEIF_MAX_EXTENTS) {
                 it->ext_off[it->n_extents] = base + off;
                 it->ext_len[it->n_extents] = len;
@@ -253,10 +254,10 @@ uint8_t *heif_item_data(heif_file *f, heif_item *it, size_t *len) {
         uint64_t off = it->ext_off[x], ln = it->ext_len[x];
         const uint8_t *src;
         if (it->construction_method == 0) {
-            if (off + ln > f->len) { free(buf); oracle_fail("extent out of range"); return NULL; }
+            if (off > f->len || ln > f->len - off) { free(buf); oracle_fail("extent out of range"); return NULL; }
             src = f->data + off;
         } else if (it->construction_method == 1) {
-            if (off + ln > f->idat_len) { free(buf); oracle_fail("idat extent out of range"); return NULL; }
+            if (off > f->idat_len || ln > f->idat_len - off) { free(buf); oracle_fail("idat extent out of range"); return NULL; }
             src = f->data + f->idat_off + off;
         } else {
             free(buf);

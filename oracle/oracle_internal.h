@@ -7,7 +7,7 @@
 #define HEIF_MAX_ITEMS 256
 #define HEIF_MAX_EXTENTS 8
 #define HEIF_MAX_PROPS 16
-#define HEIF_MAX_PROPS_TOTAL 128
+#define HEIF_MAX_PROPS_TOTAL 1024
 #define HEIF_MAX_REFS 64
 #define HEIF_MAX_TO 1024
 
