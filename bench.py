@@ -23,8 +23,22 @@ config 5, 7680x4320 Main-10 grids (15 x 9 tiles of 512x512, 16-bit planes)
 from heif_amd/synth_encoder.py; image i is a permutation (seed i) of one pool
 of 135 synthetic 10-bit tiles.
 
+--split tiles (BASELINE config 5 "1->8 GPUs"): every rank
+holds the SAME --batch images and decodes only the grid tiles k with
+k % world == rank (heifgpu_batch_opts), so the total work is fixed
+(`scaling: "strong"`) and `value` = the batch's output pixels / time.  The
+gather to one device (heifgpu_gather_tiles, xGMI peer copies) is not in the
+timed region.
+
+e2e (rank 0, default on): the PCIe-inclusive rate beside `value`: the same
+files re-parsed on the host (heifgpu_image_parse_many on a thread pool),
+flattened into pinned memory and uploaded (heifgpu_batch_prepare_ex, two
+batches reloaded alternately) while the previous batch decodes.
+
 cpu_baseline: the CPU oracle (oracle/, spec restatement; the reference Rust
-path cannot decode pixels) decoding tiles on a thread pool for ~10 s.
+path cannot decode pixels), built -march=native on the measuring host,
+decoding tiles on one thread per CPU this job may use (the cgroup quota) for
+~10 s; the 1-core figure and the node's CPU count are reported beside it.
 """
 from __future__ import annotations
 
@@ -53,6 +67,34 @@ def dist_env():
 def shard_seeds(batch_per_rank: int, rank: int) -> list:
     """Image seeds of this rank: a contiguous block of the global batch."""
     return list(range(rank * batch_per_rank, (rank + 1) * batch_per_rank))
+
+
+def effective_cpus() -> int:
+    """CPUs this process may use: affinity mask, capped by a cgroup v2 cpu.max quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = pathlib.Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def native_oracle() -> str:
+    """Builds the oracle with -march=native for this host (oracle/Makefile
+    `native`) and selects it; returns a note for the JSON line."""
+    import subprocess
+
+    try:
+        subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "native"], check=True, capture_output=True,
+                       timeout=300)
+    except (OSError, subprocess.SubprocessError) as e:
+        return f"-O3 portable build (native build failed: {type(e).__name__})"
+    if "oracle.oracle" in sys.modules:
+        return "-O3 portable build (oracle already loaded)"
+    os.environ["ORACLE_LIBRARY"] = str(ROOT / "oracle" / "build" / "native" / "liboracle.so")
+    return "-O3 -march=native build on this host"
 
 
 def cpu_baseline(data: bytes, seconds: float, threads: int, label: str = "halfmoonbay") -> dict:
@@ -91,6 +133,49 @@ def cpu_baseline(data: bytes, seconds: float, threads: int, label: str = "halfmo
     }
 
 
+def end_to_end(H, ctx, files, outs0, n_batches, threads, stream, info) -> dict:
+    """Host parse + pinned upload + decode of n_batches batches of `files`
+    (re-parsed every time), two device batches reloaded alternately so the
+    host work and upload of batch i+1 overlap the decode of batch i."""
+    import torch
+
+    outs = [outs0, ctx.alloc_outputs(H.HeifImage.parse_many(files[:len(outs0)], threads=threads))]
+    batches = [None, None]
+    t_parse = t_prep = 0.0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(n_batches):
+        ta = time.perf_counter()
+        imgs = H.HeifImage.parse_many(files, threads=threads)
+        tb = time.perf_counter()
+        batches[i % 2] = ctx.prepare(imgs, reuse=batches[i % 2], wait=False)
+        tc = time.perf_counter()
+        batches[i % 2].decode_async(outs[i % 2], stream.cuda_stream)
+        t_parse += tb - ta
+        t_prep += tc - tb
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    for b in batches:
+        if b is not None:
+            if any(b.status(stream.cuda_stream)):
+                raise SystemExit("e2e: decode status")
+            b.free()
+    px = info.width * info.height * len(files) * n_batches
+    return {
+        "value": round(px / dt / 1e6, 2),
+        "unit": "Mpixels/s",
+        "batches": n_batches,
+        "images_per_batch": len(files),
+        "ms_per_batch": round(dt / n_batches * 1e3, 3),
+        "host_parse_ms_per_batch": round(t_parse / n_batches * 1e3, 3),
+        "prepare_ms_per_batch": round(t_prep / n_batches * 1e3, 3),
+        "host_threads": threads,
+        "what": "HEIC files in host memory -> heifgpu_image_parse_many (thread pool) -> heifgpu_batch_prepare_ex "
+                "(flatten into pinned memory, async H2D) -> decode; two batches alternate so host work and "
+                "upload overlap the previous decode; planes stay in HBM",
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -101,7 +186,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=["config4", "config5"], default="config4")
     ap.add_argument("--verify", type=int, default=2, help="images checked bit-exact against the oracle (rank 0)")
+    ap.add_argument("--split", choices=["images", "tiles"], default="images",
+                    help="images: each rank its own shard (weak); tiles: every rank the same images, "
+                         "tiles k %% world == rank (strong)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-parse + upload + decode leg")
+    ap.add_argument("--e2e-batches", type=int, default=6)
     args = ap.parse_args()
+    tiles_split = args.split == "tiles"
 
     import torch
 
@@ -125,20 +216,26 @@ def main():
         src = S.grid_heic(S.CONFIG5["out_w"], S.CONFIG5["out_h"], p5, pictures=pool)
     else:
         src = SAMPLE.read_bytes()
-    seeds = shard_seeds(args.batch, rank)
-    t0 = time.perf_counter()
+    seeds = list(range(args.batch)) if tiles_split else shard_seeds(args.batch, rank)
     if c5:
         files = [S.grid_heic(S.CONFIG5["out_w"], S.CONFIG5["out_h"], p5,
                              pictures=[pool[j] for j in permutation(135, s)]) for s in seeds]
     else:
         files = [permuted_heic(src, s) for s in seeds]
-    images = [H.HeifImage.parse(f) for f in files]
+    # host demux + parameter sets + slice headers alone (heifgpu_image_parse_many)
+    host_threads = effective_cpus()
+    t0 = time.perf_counter()
+    images = H.HeifImage.parse_many(files, threads=1)
     host_parse_ms = (time.perf_counter() - t0) * 1e3 / len(files)
+    t0 = time.perf_counter()
+    images = H.HeifImage.parse_many(files, threads=host_threads)
+    host_parse_ms_mt = (time.perf_counter() - t0) * 1e3 / len(files)
     info = images[0].info
     ctx = H.DecodeContext(local)
     outs = ctx.alloc_outputs(images)
+    stride, offset = (world, rank) if tiles_split else (1, 0)
     t0 = time.perf_counter()
-    batch = ctx.prepare(images)
+    batch = ctx.prepare(images, tile_stride=stride, tile_offset=offset)
     upload_s = time.perf_counter() - t0
     stream = torch.cuda.Stream(device=local)
 
@@ -181,6 +278,10 @@ def main():
     alone = ctx.stage_times()
     ctx.set_timing(False)
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = end_to_end(H, ctx, files, outs, args.e2e_batches, host_threads, stream, info)
+
     if rank == 0:
         verified = 0
         if args.verify:
@@ -189,25 +290,35 @@ def main():
 
             for i in range(min(args.verify, len(files))):
                 ref = oracle.decode_heic(files[i], with_checks=False)
-                for g, r in ((outs[i].y, ref.y), (outs[i].cb, ref.cb), (outs[i].cr, ref.cr)):
-                    if not np.array_equal(g.cpu().numpy().astype(np.uint16), r):
+                for c, (g, r) in enumerate(((outs[i].y, ref.y), (outs[i].cb, ref.cb), (outs[i].cr, ref.cr))):
+                    g = g.cpu().numpy().astype(np.uint16)
+                    if tiles_split:  # only this rank's tiles were decoded
+                        sub = 1 if c else 0
+                        tw, th = info.tile_width >> sub, info.tile_height >> sub
+                        for k in range(offset, info.num_tiles, stride):
+                            ty, tx = (k // info.grid_cols) * th, (k % info.grid_cols) * tw
+                            if not np.array_equal(g[ty:ty + th, tx:tx + tw], r[ty:ty + th, tx:tx + tw]):
+                                raise SystemExit(f"image {i} tile {k}: GPU planes differ from the oracle")
+                    elif not np.array_equal(g, r):
                         raise SystemExit(f"image {i}: GPU planes differ from the oracle")
                 verified += 1
         px = info.width * info.height
-        total_images = args.batch * world
+        total_images = args.batch if tiles_split else args.batch * world
         value = total_images * px * args.steps / elapsed / 1e6  # every step decodes the whole batch
         parse_ms = per_step[0]  # k_parse time of one launch (one launch per step)
         chunks = 1
         coded_px = info.grid_cols * info.tile_width * info.grid_rows * info.tile_height
         bps = info.bytes_per_sample
         algo_per_image = info.coded_bytes + coded_px * 3 // 2 * bps  # compressed + coded planes
-        achieved = args.batch * algo_per_image / (parse_ms / 1e3) / 1e9
+        # algorithmic bytes of this rank's launch (its tile share in a split)
+        launch_bytes = args.batch * algo_per_image * len(range(offset, info.num_tiles, stride)) // info.num_tiles
+        achieved = launch_bytes / (parse_ms / 1e3) / 1e9
         traffic = None
         tfile = ROOT / "profiles" / "pmc_traffic.json"
         if tfile.exists():
             try:
                 tj = json.loads(tfile.read_text())
-                if tj.get("batch") == args.batch and tj.get("chunks", 1) == chunks:
+                if tj.get("batch") == args.batch and tj.get("chunks", 1) == chunks and not tiles_split and not c5:
                     traffic = tj.get("k_parse_hbm_bytes_per_launch")
             except Exception:
                 traffic = None
@@ -221,7 +332,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if tiles_split else "weak",
             "vs_baseline": None,
             "dtype": "u16" if c5 else "u8",
             "data": ("synthetic: 135 generated 10-bit tiles (heif_amd/synth_encoder.py) permuted per image" if c5 else
@@ -232,7 +343,9 @@ def main():
                             f"(48 tiles of 512x512, WPP)",
                 "images_per_gpu": args.batch,
                 "global_batch": total_images,
-                "parallelism": f"images sharded over {world} GPU(s), no collective on the data path",
+                "parallelism": (f"every image's grid tiles split k % {world} == rank over {world} GPU(s), "
+                                "no collective on the data path" if tiles_split else
+                                f"images sharded over {world} GPU(s), no collective on the data path"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -244,7 +357,7 @@ def main():
                 "kernel": "k_parse (CABAC, one WPP row per lane)" if os.environ.get("HEIFGPU_PARSE", "lanes")[:1] != "s"
                           else "k_parse (CABAC, one picture per wave)",
                 "kernel_ms_per_launch": round(parse_ms / chunks, 3),
-                "algorithmic_bytes_per_launch": args.batch * algo_per_image // chunks,
+                "algorithmic_bytes_per_launch": launch_bytes // chunks,
                 "launches_per_step": chunks,
             },
             "stage_ms_per_step": {k: round(v, 3) for k, v in zip(
@@ -257,16 +370,25 @@ def main():
             "latency_ms_one_step": round(sum(alone), 3),
             "pipeline_hbm_gbs": round(args.batch * algo_per_image / (elapsed / args.steps) / 1e9, 2),
             "host_parse_ms_per_image": round(host_parse_ms, 3),
+            "host_parse_ms_per_image_mt": {"threads": host_threads, "ms": round(host_parse_ms_mt, 4)},
             "upload_s": round(upload_s, 3),
             "verified_images": verified,
         }
+        if e2e:
+            line["e2e"] = e2e
         if not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
+            build = native_oracle()
+            threads = effective_cpus()
             label = "synthetic 10-bit" if c5 else "halfmoonbay"
             cb = cpu_baseline(src, args.cpu_seconds, threads, label)
             one = cpu_baseline(src, min(args.cpu_seconds, 4.0), 1, label)
             cb["value_1core"] = one["value"]
             cb["host_cpus"] = os.cpu_count()
+            cb["build"] = build
+            cb["note"] = (f"one thread per CPU this job may use ({threads}: affinity and cgroup cpu.max); "
+                          f"tiles are independent, so {os.cpu_count()} cores would scale to about "
+                          f"{round(one['value'] * os.cpu_count())} Mpixels/s (1-core rate x cores, a projection, "
+                          "not measured)")
             line["cpu_baseline"] = cb
         print(json.dumps(line), flush=True)
     batch.free()

@@ -65,6 +65,21 @@ class HeifImage:
         _lib.check(lib.heifgpu_image_parse_item(_lib.u8buf(data), len(data), item_id, ctypes.byref(h)))
         return cls(h.value)
 
+    @classmethod
+    def parse_many(cls, files: Sequence[bytes], threads: int = 0) -> List["HeifImage"]:
+        """Primary images of many files, parsed on `threads` native host threads
+        (heifgpu_image_parse_many; 0 = every hardware thread)."""
+        n = len(files)
+        bufs = [_lib.u8buf(f) for f in files]
+        data = (ctypes.POINTER(ctypes.c_uint8) * max(n, 1))(
+            *[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in files])
+        hs = (ctypes.c_void_p * max(n, 1))()
+        rc = lib.heifgpu_image_parse_many(data, lens, n, threads, hs, None)
+        imgs = [cls(h) if h else None for h in hs[:n]]
+        _lib.check(rc)
+        return imgs
+
     @property
     def info(self) -> _lib.ImageInfo:
         info = _lib.ImageInfo()
@@ -143,18 +158,40 @@ class DecodeContext:
                     arr[i].pitch[c] = t.stride(0) * t.element_size()
         return arr
 
-    def prepare(self, images: Sequence[HeifImage]) -> "DeviceBatch":
+    def prepare(self, images: Sequence[HeifImage], tile_stride: int = 1, tile_offset: int = 0,
+                reuse: Optional["DeviceBatch"] = None, wait: bool = True) -> "DeviceBatch":
+        """Device batch of `images` (heifgpu_batch_prepare_ex).  tile_stride /
+        tile_offset select the grid tiles k % tile_stride == tile_offset (the
+        single-image tile split across GPUs); `reuse` reloads an existing batch
+        in place; wait=False returns before the upload has finished (the next
+        decode of the batch waits for it)."""
         arr = (ctypes.c_void_p * len(images))(*[im._h.value for im in images])
-        b = ctypes.c_void_p()
-        _lib.check(lib.heifgpu_batch_prepare(self._h, arr, len(images), ctypes.byref(b)))
-        return DeviceBatch(self, b, list(images))
+        opts = _lib.BatchOpts(tile_stride, tile_offset)
+        if reuse is not None:
+            _lib.check(lib.heifgpu_batch_prepare_ex(self._h, arr, len(images), ctypes.byref(opts),
+                                                    ctypes.byref(reuse._h)))
+            reuse.images = list(images)
+            batch = reuse
+        else:
+            b = ctypes.c_void_p()
+            _lib.check(lib.heifgpu_batch_prepare_ex(self._h, arr, len(images), ctypes.byref(opts), ctypes.byref(b)))
+            batch = DeviceBatch(self, b, list(images))
+        if wait:
+            self._torch.cuda.synchronize(self.device)
+        return batch
+
+    def gather_tiles(self, dst: DecodedImage, src: DecodedImage, tile_stride: int, tile_offset: int,
+                     stream: Optional[int] = None):
+        """Copy the tiles k % tile_stride == tile_offset of `src` (decoded with
+        those options, on any device) into `dst` on this context's device."""
+        if stream is None:
+            stream = self._torch.cuda.current_stream(self.device).cuda_stream
+        _lib.check(lib.heifgpu_gather_tiles(ctypes.byref(dst.info), DecodeContext.planes_of([dst]),
+                                            DecodeContext.planes_of([src]), tile_stride, tile_offset,
+                                            ctypes.c_void_p(stream)))
 
     def set_timing(self, enable: bool):
         _lib.check(lib.heifgpu_set_timing(self._h, 1 if enable else 0))
-
-    def last_chunks(self) -> int:
-        """Picture chunks the last decode was pipelined in (parse ∥ reconstruction)."""
-        return int(lib.heifgpu_last_chunks(self._h))
 
     def stage_times(self) -> List[float]:
         """ms of the last timed decode: parse, transform, intra, deblock, sao_out, rbsp."""

@@ -108,15 +108,21 @@ class Planes(ctypes.Structure):
     _fields_ = [("plane", ctypes.c_void_p * 3), ("pitch", ctypes.c_int32 * 3)]
 
 
+class BatchOpts(ctypes.Structure):
+    """heifgpu_batch_opts: decode only grid tiles k with k % tile_stride == tile_offset."""
+    _fields_ = [("tile_stride", ctypes.c_uint32), ("tile_offset", ctypes.c_uint32)]
+
+
 # every symbol include/heifgpu.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "heifgpu_image_parse", "heifgpu_image_get_info", "heifgpu_image_free", "heifgpu_create",
     "heifgpu_destroy", "heifgpu_last_error", "heifgpu_batch_prepare", "heifgpu_batch_decode",
-    "heifgpu_batch_status", "heifgpu_batch_free", "heifgpu_set_timing", "heifgpu_stage_times", "heifgpu_last_chunks",
+    "heifgpu_batch_status", "heifgpu_batch_free", "heifgpu_set_timing", "heifgpu_stage_times",
     "heifgpu_decode_batch", "heifgpu_remove_emulation_prevention", "heifgpu_read_ue",
     "heifgpu_read_se", "heifgpu_bins_truncated_rice", "heifgpu_bins_chroma_pred_mode",
     "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb", "heifgpu_image_tile_params", "heifgpu_debug_counters",
-    "heifgpu_image_parse_item", "heifgpu_ycbcr_to_rgb",
+    "heifgpu_image_parse_item", "heifgpu_ycbcr_to_rgb", "heifgpu_batch_prepare_ex", "heifgpu_gather_tiles",
+    "heifgpu_image_parse_many",
 )
 
 
@@ -166,7 +172,6 @@ def _load() -> ctypes.CDLL:
         "heifgpu_batch_free": (None, [VP]),
         "heifgpu_set_timing": (I32, [VP, I32]),
         "heifgpu_stage_times": (I32, [VP, P(ctypes.c_float)]),
-        "heifgpu_last_chunks": (I32, [VP]),
         "heifgpu_decode_batch": (I32, [VP, P(VP), SZ, P(Planes), VP, P(U32)]),
         "heifgpu_remove_emulation_prevention": (SZ, [u8p, SZ, u8p]),
         "heifgpu_read_ue": (I32, [u8p, SZ, P(U32)]),
@@ -179,6 +184,9 @@ def _load() -> ctypes.CDLL:
         "heifgpu_debug_counters": (I32, [P(ctypes.c_uint64), I32]),
         "heifgpu_image_parse_item": (I32, [u8p, SZ, U32, P(VP)]),
         "heifgpu_ycbcr_to_rgb": (I32, [VP, P(ImageInfo), P(Planes), VP, I32, VP]),
+        "heifgpu_batch_prepare_ex": (I32, [VP, P(VP), SZ, P(BatchOpts), P(VP)]),
+        "heifgpu_gather_tiles": (I32, [P(ImageInfo), P(Planes), P(Planes), U32, U32, VP]),
+        "heifgpu_image_parse_many": (I32, [P(P(ctypes.c_uint8)), P(SZ), SZ, I32, P(VP), P(I32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -5,8 +5,10 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/heifgpu.h"
@@ -22,6 +24,12 @@ struct heifgpu_image {
     ParsedImage img;
 };
 
+// the C structs' layouts are part of the ABI (INTEGRATION.md's Rust binding mirrors them)
+static_assert(sizeof(heifgpu_image_info) == 80, "heifgpu_image_info: 20 x uint32");
+static_assert(sizeof(heifgpu_planes) == 40, "heifgpu_planes: 3 pointers + 3 int32 (+ padding)");
+static_assert(sizeof(heifgpu_batch_opts) == 8, "heifgpu_batch_opts: 2 x uint32");
+static_assert(sizeof(heifgpu_tile_params) == 55 * 4 + 64 * 4, "heifgpu_tile_params: 55 int32 + 64 uint32");
+
 // Pipelined decode.  k_rbsp + k_parse run on an internal parse stream and the
 // four reconstruction kernels on an internal recon stream.  A batch holds two
 // sets of parse outputs (TU records, coefficients, maps, SAO, per-row counts,
@@ -36,7 +44,7 @@ constexpr int kTimingSlots = 32;
 struct heifgpu_ctx {
     int device = 0;
     bool timing = false;
-    hipStream_t parse = nullptr, recon = nullptr;
+    hipStream_t parse = nullptr, recon = nullptr, upload = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     // timing ring, one slot per timed decode call: rbsp start, rbsp end = parse
     // start, parse end, recon start, 4 stage ends.  heifgpu_stage_times folds
@@ -44,7 +52,6 @@ struct heifgpu_ctx {
     hipEvent_t tev[kTimingSlots][8] = {};
     int timed_calls = 0, folded = 0;
     double acc[6] = {};
-    bool timed = false;
 };
 
 namespace {
@@ -91,9 +98,44 @@ struct DevBuf {
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
+    size_t cap = 0;
+    // count elements, reusing the allocation when it is large enough (a
+    // reloaded batch, heifgpu_batch_prepare_ex); the caller has drained every
+    // use of the old contents before a reallocation
     hipError_t alloc(size_t count) {
         n = count;
-        return hipMalloc(reinterpret_cast<void **>(&p), std::max<size_t>(count, 1) * sizeof(T));
+        if (p && count <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            p = nullptr;
+            cap = 0;
+            if (e != hipSuccess) return e;
+        }
+        cap = std::max<size_t>(count, 1);
+        return hipMalloc(reinterpret_cast<void **>(&p), cap * sizeof(T));
+    }
+};
+
+// page-locked host staging of a batch's uploads (one hipMemcpyAsync source)
+struct PinnedBuf {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf &) = delete;
+    PinnedBuf &operator=(const PinnedBuf &) = delete;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t reserve(size_t bytes) {
+        if (p && bytes <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+            if (e != hipSuccess) return e;
+        }
+        cap = std::max<size_t>(bytes, 4096);
+        return hipHostMalloc(reinterpret_cast<void **>(&p), cap, hipHostMallocDefault);
     }
 };
 
@@ -118,6 +160,10 @@ struct heifgpu_batch {
     int device = 0;
     size_t n_images = 0;
     int n_pics = 0;
+    uint32_t tile_stride = 1, tile_offset = 0;
+    PinnedBuf stage;
+    hipEvent_t uploaded = nullptr;  // the last load's H2D copies (upload stream)
+    bool loaded = false;
     BatchArgs args{};
     DevBuf<uint8_t> bits, rbsp, sf, recon;
     DevBuf<PicDesc> pics;
@@ -130,6 +176,9 @@ struct heifgpu_batch {
     std::vector<OutImage> out_host;
     std::vector<uint32_t> pic_image;  // picture → image
     std::vector<heifgpu_image_info> infos;
+    ~heifgpu_batch() {
+        if (uploaded) (void)hipEventDestroy(uploaded);
+    }
 };
 
 extern "C" {
@@ -153,6 +202,93 @@ int heifgpu_image_parse_item(const uint8_t *data, size_t len, uint32_t item_id, 
     } catch (const std::exception &e) {
         return fail(HEIFGPU_E_PARSE, e.what());
     }
+}
+
+int heifgpu_image_parse_many(const uint8_t *const *data, const size_t *len, size_t n, int threads,
+                             heifgpu_image **out, int *rc) {
+    if (!data || !len || !out) return fail(HEIFGPU_E_INVALID, "null argument");
+    for (size_t i = 0; i < n; ++i) out[i] = nullptr;
+    std::vector<int> codes(n, HEIFGPU_OK);
+    std::vector<std::string> msgs(n);
+    std::atomic<size_t> next{0};
+    auto worker = [&] {
+        for (size_t i; (i = next.fetch_add(1)) < n;) {
+            if (!data[i]) {
+                codes[i] = HEIFGPU_E_INVALID;
+                msgs[i] = "null data";
+                continue;
+            }
+            try {
+                auto im = std::make_unique<heifgpu_image>();
+                im->img = parse_heic(data[i], len[i], 0);
+                out[i] = im.release();
+            } catch (const UnsupportedError &e) {
+                codes[i] = HEIFGPU_E_UNSUPPORTED;
+                msgs[i] = e.what();
+            } catch (const std::exception &e) {
+                codes[i] = HEIFGPU_E_PARSE;
+                msgs[i] = e.what();
+            }
+        }
+    };
+    size_t nt = threads > 0 ? size_t(threads) : size_t(std::max(1u, std::thread::hardware_concurrency()));
+    nt = std::min(nt, n);
+    std::vector<std::thread> pool;
+    for (size_t t = 1; t < nt; ++t) pool.emplace_back(worker);
+    worker();
+    for (auto &th : pool) th.join();
+    int first = HEIFGPU_OK;
+    for (size_t i = 0; i < n; ++i) {
+        if (rc) rc[i] = codes[i];
+        if (codes[i] != HEIFGPU_OK && first == HEIFGPU_OK) {
+            first = codes[i];
+            g_err = "image " + std::to_string(i) + ": " + msgs[i];
+        }
+    }
+    return first;
+}
+
+int heifgpu_gather_tiles(const heifgpu_image_info *info, const heifgpu_planes *dst, const heifgpu_planes *src,
+                         uint32_t tile_stride, uint32_t tile_offset, void *stream) {
+    if (!info || !dst || !src) return fail(HEIFGPU_E_INVALID, "null argument");
+    if (tile_stride == 0) tile_stride = 1;
+    if (tile_offset >= tile_stride) return fail(HEIFGPU_E_INVALID, "tile_offset must be below tile_stride");
+    if (info->chroma_format_idc > 1) return fail(HEIFGPU_E_UNSUPPORTED, "only 4:0:0 and 4:2:0");
+    const int planes = info->chroma_format_idc ? 3 : 1;
+    for (int c = 0; c < planes; ++c)
+        if (!dst->plane[c] || !src->plane[c]) return fail(HEIFGPU_E_INVALID, "missing plane");
+    hipPointerAttribute_t ad{}, as{};
+    HIP_TRY(hipPointerGetAttributes(&ad, dst->plane[0]));
+    HIP_TRY(hipPointerGetAttributes(&as, src->plane[0]));
+    if (ad.device != as.device) {  // peer copy over xGMI
+        int cur = 0;
+        HIP_TRY(hipGetDevice(&cur));
+        HIP_TRY(hipSetDevice(ad.device));
+        const hipError_t e = hipDeviceEnablePeerAccess(as.device, 0);
+        (void)hipGetLastError();
+        HIP_TRY(hipSetDevice(cur));
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_TRY(e);
+    }
+    const uint32_t W = info->width, H = info->height, bps = info->bytes_per_sample;
+    const uint32_t cols = std::max(1u, info->grid_cols), tw = info->tile_width ? info->tile_width : W,
+                   th = info->tile_height ? info->tile_height : H;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    for (uint32_t k = tile_offset; k < std::max(1u, info->num_tiles); k += tile_stride) {
+        const uint32_t x0 = (k % cols) * tw, y0 = (k / cols) * th;
+        if (x0 >= W || y0 >= H) continue;  // a tile wholly inside the crop
+        for (int c = 0; c < planes; ++c) {
+            const uint32_t sx = c ? 1 : 0;  // 4:2:0 chroma halves both axes
+            const uint32_t pw = (W + sx) >> sx, ph = (H + sx) >> sx;
+            const uint32_t x = x0 >> sx, y = y0 >> sx;
+            const uint32_t w = std::min(tw >> sx, pw - x), h = std::min(th >> sx, ph - y);
+            const size_t so = size_t(y) * size_t(src->pitch[c]) + size_t(x) * bps;
+            const size_t d0 = size_t(y) * size_t(dst->pitch[c]) + size_t(x) * bps;
+            HIP_TRY(hipMemcpy2DAsync(static_cast<uint8_t *>(dst->plane[c]) + d0, size_t(dst->pitch[c]),
+                                     static_cast<const uint8_t *>(src->plane[c]) + so, size_t(src->pitch[c]),
+                                     size_t(w) * bps, h, hipMemcpyDefault, s));
+        }
+    }
+    return HEIFGPU_OK;
 }
 
 int heifgpu_image_get_info(const heifgpu_image *img, heifgpu_image_info *info) {
@@ -233,6 +369,7 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIP_TRY(hipStreamCreateWithPriority(&c->parse, hipStreamNonBlocking, prio ? greatest : least));
     HIP_TRY(hipStreamCreateWithFlags(&c->recon, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&c->upload, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
     for (auto &row : c->tev)
@@ -252,6 +389,7 @@ void heifgpu_destroy(heifgpu_ctx *ctx) {
     if (ctx->join) (void)hipEventDestroy(ctx->join);
     if (ctx->parse) (void)hipStreamDestroy(ctx->parse);
     if (ctx->recon) (void)hipStreamDestroy(ctx->recon);
+    if (ctx->upload) (void)hipStreamDestroy(ctx->upload);
     delete ctx;
 }
 
@@ -264,8 +402,6 @@ int heifgpu_set_timing(heifgpu_ctx *ctx, int enable) {
     ctx->timing = enable != 0;
     return HEIFGPU_OK;
 }
-
-int heifgpu_last_chunks(const heifgpu_ctx *ctx) { return ctx && ctx->timed ? 1 : 0; }
 
 int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[6]) {
     if (!ctx || !ms) return fail(HEIFGPU_E_INVALID, "null argument");
@@ -280,79 +416,122 @@ int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[6]) {
     return HEIFGPU_OK;
 }
 
-int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, heifgpu_batch **out) {
-    if (!ctx || !imgs || !out || n == 0) return fail(HEIFGPU_E_INVALID, "invalid argument");
-    *out = nullptr;
+int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n,
+                             const heifgpu_batch_opts *opts, heifgpu_batch **inout) {
+    if (!ctx || !imgs || !inout || n == 0) return fail(HEIFGPU_E_INVALID, "invalid argument");
+    const uint32_t stride = opts && opts->tile_stride ? opts->tile_stride : 1u;
+    const uint32_t offset = opts ? opts->tile_offset : 0u;
+    if (offset >= stride) return fail(HEIFGPU_E_INVALID, "tile_offset must be below tile_stride");
+    if (*inout && (*inout)->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
     HIP_TRY(hipSetDevice(ctx->device));
-    auto b = std::make_unique<heifgpu_batch>();
-    b->device = ctx->device;
-    b->n_images = n;
     std::vector<const ParsedImage *> parsed;
+    std::vector<heifgpu_image_info> infos;
     for (size_t i = 0; i < n; ++i) {
         if (!imgs[i]) return fail(HEIFGPU_E_INVALID, "null image");
         parsed.push_back(&imgs[i]->img);
         heifgpu_image_info info;
         heifgpu_image_get_info(imgs[i], &info);
-        b->infos.push_back(info);
+        infos.push_back(info);
     }
     HostBatch hb;
     try {
-        hb = build_batch(parsed.data(), n);
+        hb = build_batch(parsed.data(), n, stride, offset);
     } catch (const UnsupportedError &e) {
         return fail(HEIFGPU_E_UNSUPPORTED, e.what());
     } catch (const std::exception &e) {
         return fail(HEIFGPU_E_PARSE, e.what());
     }
-    std::vector<uint8_t> &h_bits = hb.bits;
-    std::vector<PicDesc> &h_pics = hb.pics;
-    std::vector<uint32_t> &h_subs = hb.subs;
-    std::vector<SeqParams> &h_seqs = hb.seqs;
-    std::vector<uint8_t> &h_sf = hb.sf;
-    const uint64_t recon_bytes = hb.recon_bytes, resid_elems = hb.resid_elems, map_bytes = hb.map_bytes,
-                   sao_n = hb.sao_n, tu_n = hb.tu_n, coef_n = hb.coef_n;
-    const uint32_t rows = hb.rows;
-    const int max_w = hb.max_w, max_wctb = hb.max_wctb, max_rows = hb.max_rows, bps = hb.bps;
+    std::unique_ptr<heifgpu_batch> fresh;
+    heifgpu_batch *b = *inout;
+    if (!b) {
+        fresh = std::make_unique<heifgpu_batch>();
+        b = fresh.get();
+        b->device = ctx->device;
+        HIP_TRY(hipEventCreateWithFlags(&b->uploaded, hipEventDisableTiming));
+        static const int pipeline = [] {
+            const char *e = std::getenv("HEIFGPU_PIPELINE");
+            return e ? std::atoi(e) : 1;
+        }();
+        b->n_sets = pipeline ? 2 : 1;
+        for (int k = 0; k < b->n_sets; ++k) {
+            HIP_TRY(hipEventCreateWithFlags(&b->set[k].parsed, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&b->set[k].recon_done, hipEventDisableTiming));
+        }
+    }
+    // A reloaded batch: the upload stream waits for every decode still
+    // reading the old contents; the staging buffer is rewritten only after the
+    // previous load's copies (long finished in a double-buffered loop).
+    if (b->loaded) HIP_TRY(hipEventSynchronize(b->uploaded));
+    for (int k = 0; k < b->n_sets; ++k)
+        if (b->set[k].pending) HIP_TRY(hipStreamWaitEvent(ctx->upload, b->set[k].recon_done, 0));
+    const bool grows = b->loaded && (hb.bits.size() > b->bits.cap || hb.pics.size() > b->pics.cap ||
+                                     hb.subs.size() > b->subs.cap || hb.seqs.size() > b->seqs.cap ||
+                                     hb.sf.size() > b->sf.cap || n > b->outs.cap || hb.recon_bytes > b->recon.cap ||
+                                     hb.resid_elems > b->resid.cap || hb.tu_n > b->set[0].tus.cap ||
+                                     hb.coef_n > b->set[0].coefs.cap || hb.map_bytes > b->set[0].maps.cap ||
+                                     hb.sao_n > b->set[0].sao.cap || 2 * size_t(hb.rows) > b->set[0].row_counts.cap ||
+                                     hb.pics.size() > b->set[0].status.cap);
+    if (grows) HIP_TRY(hipStreamSynchronize(ctx->upload));  // reallocation: old contents fully drained
+    b->n_images = n;
+    b->tile_stride = stride;
+    b->tile_offset = offset;
+    b->infos = std::move(infos);
     b->pic_image = hb.pic_image;
-    b->n_pics = int(h_pics.size());
-    // ---- device arenas
-    HIP_TRY(b->bits.alloc(h_bits.size()));
-    HIP_TRY(b->pics.alloc(h_pics.size()));
-    HIP_TRY(b->subs.alloc(h_subs.size()));
-    HIP_TRY(b->rbsp.alloc(h_bits.size()));
-    HIP_TRY(b->rsubs.alloc(h_subs.size()));
-    HIP_TRY(b->seqs.alloc(h_seqs.size()));
-    HIP_TRY(b->sf.alloc(h_sf.size()));
+    b->n_pics = int(hb.pics.size());
+    // ---- device arenas (reused when large enough)
+    HIP_TRY(b->bits.alloc(hb.bits.size()));
+    HIP_TRY(b->pics.alloc(hb.pics.size()));
+    HIP_TRY(b->subs.alloc(hb.subs.size()));
+    HIP_TRY(b->rbsp.alloc(hb.bits.size()));
+    HIP_TRY(b->rsubs.alloc(hb.subs.size()));
+    HIP_TRY(b->seqs.alloc(hb.seqs.size()));
+    HIP_TRY(b->sf.alloc(hb.sf.size()));
     HIP_TRY(b->outs.alloc(n));
-    static const int pipeline = [] {
-        const char *e = std::getenv("HEIFGPU_PIPELINE");
-        return e ? std::atoi(e) : 1;
-    }();
-    b->n_sets = pipeline ? 2 : 1;
     for (int k = 0; k < b->n_sets; ++k) {
         ParseSet &ps = b->set[k];
-        HIP_TRY(ps.tus.alloc(tu_n));
-        HIP_TRY(ps.coefs.alloc(coef_n));
-        HIP_TRY(ps.row_counts.alloc(size_t(2) * rows));
-        HIP_TRY(ps.maps.alloc(map_bytes));
-        HIP_TRY(ps.sao.alloc(sao_n));
-        HIP_TRY(ps.status.alloc(h_pics.size()));
-        HIP_TRY(hipMemset(ps.status.p, 0, h_pics.size() * sizeof(uint32_t)));
-        HIP_TRY(hipEventCreateWithFlags(&ps.parsed, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ps.recon_done, hipEventDisableTiming));
+        HIP_TRY(ps.tus.alloc(hb.tu_n));
+        HIP_TRY(ps.coefs.alloc(hb.coef_n));
+        HIP_TRY(ps.row_counts.alloc(size_t(2) * hb.rows));
+        HIP_TRY(ps.maps.alloc(hb.map_bytes));
+        HIP_TRY(ps.sao.alloc(hb.sao_n));
+        HIP_TRY(ps.status.alloc(hb.pics.size()));
+        HIP_TRY(hipMemsetAsync(ps.status.p, 0, hb.pics.size() * sizeof(uint32_t), ctx->upload));
     }
-    HIP_TRY(b->recon.alloc(recon_bytes));
-    HIP_TRY(b->resid.alloc(resid_elems));
-    HIP_TRY(hipMemcpy(b->bits.p, h_bits.data(), h_bits.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(b->pics.p, h_pics.data(), h_pics.size() * sizeof(PicDesc), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(b->subs.p, h_subs.data(), h_subs.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(b->seqs.p, h_seqs.data(), h_seqs.size() * sizeof(SeqParams), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(b->sf.p, h_sf.data(), h_sf.size(), hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(b->rbsp.p, 0, h_bits.size()));
+    HIP_TRY(b->recon.alloc(hb.recon_bytes));
+    HIP_TRY(b->resid.alloc(hb.resid_elems));
     std::vector<uint32_t> order;
-    lanes_parse_order(h_pics.data(), int(h_pics.size()), hb.lane_rows, order);
+    lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
     HIP_TRY(b->porder.alloc(order.size()));
-    HIP_TRY(hipMemcpy(b->porder.p, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    // ---- one pinned staging image of every upload, copied asynchronously
+    struct Seg {
+        const void *src;
+        size_t bytes;
+        void *dst;
+    };
+    const Seg segs[] = {
+        {hb.bits.data(), hb.bits.size(), b->bits.p},
+        {hb.pics.data(), hb.pics.size() * sizeof(PicDesc), b->pics.p},
+        {hb.subs.data(), hb.subs.size() * sizeof(uint32_t), b->subs.p},
+        {hb.seqs.data(), hb.seqs.size() * sizeof(SeqParams), b->seqs.p},
+        {hb.sf.data(), hb.sf.size(), b->sf.p},
+        {order.data(), order.size() * sizeof(uint32_t), b->porder.p},
+    };
+    size_t total = 0;
+    for (const Seg &g : segs) total += (g.bytes + 255) & ~size_t(255);
+    HIP_TRY(b->stage.reserve(total));
+    size_t off = 0;
+    for (const Seg &g : segs) {
+        if (g.bytes) {
+            std::memcpy(b->stage.p + off, g.src, g.bytes);
+            HIP_TRY(hipMemcpyAsync(g.dst, b->stage.p + off, g.bytes, hipMemcpyHostToDevice, ctx->upload));
+        }
+        off += (g.bytes + 255) & ~size_t(255);
+    }
+    HIP_TRY(hipMemsetAsync(b->rbsp.p, 0, hb.bits.size(), ctx->upload));
+    HIP_TRY(hipEventRecord(b->uploaded, ctx->upload));
+    b->loaded = true;
     BatchArgs &a = b->args;
+    a = BatchArgs{};
     a.bits = b->bits.p;
     a.pics = b->pics.p;
     a.subs = b->subs.p;
@@ -365,16 +544,25 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
     a.recon = b->recon.p;
     a.resid = b->resid.p;
     a.n_pics = b->n_pics;
-    a.max_width = max_w;
-    a.max_wctb = max_wctb;
-    a.max_rows = max_rows;
+    a.max_width = hb.max_w;
+    a.max_wctb = hb.max_wctb;
+    a.max_rows = hb.max_rows;
     a.max_log2ctb = hb.max_log2ctb;
     a.lane_rows = hb.lane_rows;
     a.wpp_ring = hb.wpp_ring;
-    a.total_rows = int(rows);
-    a.bytes_per_sample = bps;
+    a.total_rows = int(hb.rows);
+    a.bytes_per_sample = hb.bps;
     b->out_host.assign(n, OutImage{});
-    *out = b.release();
+    if (fresh) *inout = fresh.release();
+    return HEIFGPU_OK;
+}
+
+int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, heifgpu_batch **out) {
+    if (!out) return fail(HEIFGPU_E_INVALID, "invalid argument");
+    *out = nullptr;
+    const int rc = heifgpu_batch_prepare_ex(ctx, imgs, n, nullptr, out);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->upload));  // v1 semantics: uploaded on return
     return HEIFGPU_OK;
 }
 
@@ -419,6 +607,7 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         return e ? std::atoi(e) : 5;
     }();
     if (max_stages < 5) {
+        HIP_TRY(hipStreamSynchronize(ctx->upload));
         HIP_TRY(hipStreamSynchronize(ctx->parse));
         HIP_TRY(hipStreamSynchronize(ctx->recon));
         HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), s));
@@ -427,10 +616,12 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         hipError_t (*fns[5])(const BatchArgs &, hipStream_t) = {launch_parse, launch_transform, launch_intra,
                                                                 launch_deblock, launch_sao_out};
         for (int i = 0; i < max_stages; ++i) HIP_TRY(fns[i](a, s));
-        ctx->timed = false;
         return HEIFGPU_OK;
     }
     hipStream_t p = ctx->parse, r = ctx->recon;
+    if (b->n_pics == 0) {  // a tile subset without pictures: nothing to decode
+        return HEIFGPU_OK;
+    }
     const bool t = ctx->timing;
     hipEvent_t *ev = nullptr;
     if (t) {  // this call's timing slot; the call that used it last is folded first
@@ -442,7 +633,8 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         ev = ctx->tev[slot];
         ++ctx->timed_calls;
     }
-    // parse stream: this set's previous reconstruction must be done with it
+    // parse stream: the batch's uploads, and this set's previous reconstruction must be done with it
+    HIP_TRY(hipStreamWaitEvent(p, b->uploaded, 0));
     if (ps.pending) HIP_TRY(hipStreamWaitEvent(p, ps.recon_done, 0));
     HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), p));
     // rows a stopped substream never reaches keep zero TBs
@@ -468,7 +660,6 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     if (t) HIP_TRY(hipEventRecord(ev[7], r));
     HIP_TRY(hipEventRecord(ps.recon_done, r));
     ps.pending = true;
-    ctx->timed = t;
     HIP_TRY(hipEventRecord(ctx->join, r));
     HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
     return HEIFGPU_OK;
@@ -479,8 +670,9 @@ int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *b, uint32_t *status, v
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream, as in HIP
     HIP_TRY(hipSetDevice(ctx->device));
     std::vector<uint32_t> st(size_t(b->n_pics));
-    HIP_TRY(hipMemcpyAsync(st.data(), b->set[b->last_set].status.p, st.size() * sizeof(uint32_t),
-                           hipMemcpyDeviceToHost, s));
+    if (!st.empty())
+        HIP_TRY(hipMemcpyAsync(st.data(), b->set[b->last_set].status.p, st.size() * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     std::vector<uint32_t> per(b->n_images, 0);
     for (size_t p = 0; p < st.size(); ++p) per[b->pic_image[p]] |= st[p];

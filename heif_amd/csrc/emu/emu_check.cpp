@@ -1,7 +1,11 @@
 // emu_check.cpp — TEST-ONLY driver: runs the decode kernels' own sources as
 // host C++ (HG_HOST_EMU, see kernels/wave.hpp) and diffs every plane against
 // the CPU oracle.  Never part of the product library.
-//   emu_check file.heic [stages=5]   stages: 1 parse .. 5 full (3 = before deblocking)
+//   emu_check file.heic [stages=5] [tile_stride tile_offset]
+//   stages: 1 parse .. 5 full (3 = before deblocking); with a tile stride only
+//   the grid tiles k % stride == offset are decoded (the tile split across GPUs):
+//   their windows must match the oracle and every other sample must keep the
+//   sentinel the planes start with
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -19,6 +23,7 @@ using namespace hg;
 int main(int argc, char **argv) {
     if (argc < 2) return 2;
     int stages = argc > 2 ? atoi(argv[2]) : 5;
+    const uint32_t tstride = argc > 4 ? uint32_t(atoi(argv[3])) : 1u, toff = argc > 4 ? uint32_t(atoi(argv[4])) : 0u;
     FILE *f = fopen(argv[1], "rb");
     fseek(f, 0, SEEK_END);
     long n = ftell(f);
@@ -28,7 +33,7 @@ int main(int argc, char **argv) {
     fclose(f);
     ParsedImage im = parse_heic(data.data(), data.size());
     const ParsedImage *ims[1] = {&im};
-    HostBatch hb = build_batch(ims, 1);
+    HostBatch hb = build_batch(ims, 1, tstride, toff);
     std::vector<TuRec> tus(hb.tu_n);
     std::vector<Coef> coefs(hb.coef_n);
     std::vector<uint32_t> rc(2 * hb.rows), status(hb.pics.size());
@@ -37,7 +42,9 @@ int main(int argc, char **argv) {
     std::vector<SaoParams> sao(hb.sao_n);
     const int W = int(im.out_width), H = int(im.out_height), bps = hb.bps;
     const int CW = (W + 1) / 2, CH = (H + 1) / 2;
-    std::vector<uint8_t> oy(size_t(W) * H * bps), ocb(size_t(CW) * CH * bps), ocr(size_t(CW) * CH * bps);
+    constexpr uint8_t kSentinel = 0xa5;
+    std::vector<uint8_t> oy(size_t(W) * H * bps, kSentinel), ocb(size_t(CW) * CH * bps, kSentinel),
+        ocr(size_t(CW) * CH * bps, kSentinel);
     OutImage out{};
     out.plane[0] = uint64_t(oy.data());
     out.plane[1] = uint64_t(ocb.data());
@@ -125,10 +132,14 @@ int main(int argc, char **argv) {
         int pw = int(ref.pw[c]), ph = int(ref.ph[c]);
         long bad = 0;
         int fx = -1, fy = -1;
+        const int s = c ? 1 : 0;
         for (int y = 0; y < ph; ++y)
             for (int x = 0; x < pw; ++x) {
                 int gv = bps == 1 ? g[size_t(y) * pw + x] : reinterpret_cast<const uint16_t *>(g)[size_t(y) * pw + x];
-                if (gv != ref.plane[c][size_t(y) * pw + x]) {
+                const uint32_t tile = uint32_t((y << s) / int(im.tile_height)) * im.cols + uint32_t((x << s) / int(im.tile_width));
+                const int want = tile % tstride == toff ? int(ref.plane[c][size_t(y) * pw + x])
+                                                        : (bps == 1 ? kSentinel : kSentinel * 0x101);
+                if (gv != want) {
                     if (!bad) fx = x, fy = y;
                     ++bad;
                 }

@@ -57,7 +57,9 @@ void fill_scaling(const ParamSet &ps, uint8_t *blk) {
 
 }  // namespace
 
-HostBatch build_batch(const ParsedImage *const *imgs, size_t n) {
+HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_stride, uint32_t tile_offset) {
+    if (tile_stride == 0) tile_stride = 1;
+    if (tile_offset >= tile_stride) throw HeifError("tile_offset must be below tile_stride");
     HostBatch hb;
     std::vector<std::vector<uint8_t>> seq_keys;
     for (size_t i = 0; i < n; ++i) {
@@ -70,7 +72,7 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n) {
         } else if (hb.bps != bps || hb.chroma != s0.chroma_array_type()) {
             throw UnsupportedError("a batch must share bit depth and chroma format");
         }
-        for (size_t t = 0; t < im.tiles.size(); ++t) {
+        for (size_t t = tile_offset; t < im.tiles.size(); t += tile_stride) {
             const TileJob &tj = im.tiles[t];
             const ParamSet &ps = im.params[size_t(tj.param)];
             uint32_t seq;

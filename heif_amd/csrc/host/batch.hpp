@@ -23,7 +23,9 @@ struct HostBatch {
     int lane_rows = 1, wpp_ring = 0;  // k_parse_lanes geometry (BatchArgs::lane_rows / wpp_ring)
 };
 
-// Throws HeifError / UnsupportedError.
-HostBatch build_batch(const ParsedImage *const *imgs, size_t n);
+// Throws HeifError / UnsupportedError.  Only grid tiles k (row-major) with
+// k % tile_stride == tile_offset become pictures (the single-image tile split
+// across GPUs); the default takes every tile.
+HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_stride = 1, uint32_t tile_offset = 0);
 
 }  // namespace hg

@@ -52,8 +52,8 @@ __constant__ uint8_t c_lps_l[256] = {HG_LPS_TABLE};
 __constant__ uint8_t c_trans_l[64] = {HG_TRANS_LPS};
 __constant__ uint8_t c_ctx_init_l[CTX_NUM] = {HG_CTX_INIT_VALUES};
 #if defined(HG_PARSE_PROF) && !defined(HG_HOST_EMU)
-// s_memtime cycles per wave: [0] kernel, [1] passes, [2..7] unit kinds CTU, tree (CQT+CU+TT), TB, SB,
-// CTU_END, refill (tuning build only; heifgpu_debug_counters slots 8..15)
+// s_memtime cycles per wave: [0] kernel, [1] passes, [2..6] unit kinds CTU, tree (CQT+CU+TT), TB, SB,
+// CTU_END; [7] units run (lanes x unit executions) (tuning build only; heifgpu_debug_counters slots 8..15)
 __device__ uint64_t g_prof_lanes[8];
 #endif
 
@@ -1363,15 +1363,12 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
             if (!__any(mine)) continue;
             progressed = true;
 #if defined(HG_PARSE_PROF)
-            const uint64_t t0 = __builtin_amdgcn_s_memtime();
-#endif
-#if defined(HG_PARSE_PROF)
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            pf[7] += (uint64_t)__popcll(__ballot(mine));  // lanes running a unit
 #endif
             if (mine) run_unit(kind, L, ld, P, E, G);
 #if defined(HG_PARSE_PROF)
             const uint64_t t2 = __builtin_amdgcn_s_memtime();
-            pf[7] += t1 - t0;
             pf[kind <= U_CTU ? 2 : kind <= U_TT ? 3 : kind - 1] += t2 - t1;
 #endif
         }

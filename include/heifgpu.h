@@ -12,7 +12,7 @@
  *     the reconstructed Y/Cb/Cr planes.
  * The test hooks at the end expose the host pieces the reference unit-tests
  * (src/hevc/rbsp_reader.rs:139-303, src/cabac/decoder.rs:286-373,
- * tests/libheif_comparison.rs:173-276).
+ * tests/libheif_comparison.rs:9-112).
  *
  * Conventions: functions return 0 on success and a negative HEIFGPU_E_*
  * code on failure (the reference's anyhow::Result / ensure! / bail!);
@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define HEIFGPU_ABI_VERSION 1
+#define HEIFGPU_ABI_VERSION 2
 
 enum {
     HEIFGPU_OK = 0,
@@ -80,9 +80,24 @@ typedef struct {
     int32_t pitch[3];             /* bytes per row */
 } heifgpu_planes;
 
+/* decode options of heifgpu_batch_prepare_ex */
+typedef struct {
+    /* Single-image tile split across GPUs: only grid tiles k
+     * (row-major) with k % tile_stride == tile_offset are decoded, each into
+     * its window of the full-size output planes; the other windows are not
+     * written.  0 or 1 = every tile.  Tiles are independent IDR pictures
+     * (src/heic/decoder.rs:98-119 decodes them one by one). */
+    uint32_t tile_stride, tile_offset;
+} heifgpu_batch_opts;
+
 /* ---- host: demux + parameter sets + slice headers ------------------- */
 /* data is copied; the returned image owns its bytes. */
 int heifgpu_image_parse(const uint8_t *data, size_t len, heifgpu_image **out);
+/* n independent files parsed on `threads` host threads (<= 0: all hardware
+ * threads).  out[i] is NULL when file i failed; rc[i] (optional) receives its
+ * code.  Returns 0 when every file parsed, else the first failure's code. */
+int heifgpu_image_parse_many(const uint8_t *const *data, const size_t *len, size_t n, int threads,
+                             heifgpu_image **out, int *rc);
 /* Any coded image item by ID (0 = primary), e.g. the HDR gain map the primary
  * references through 'auxl' (info.aux_item_id; src/heif/grammar.rs:202-207
  * parses the reference but nothing decodes it).  Grid or single hvc1 item. */
@@ -98,13 +113,24 @@ const char *heifgpu_last_error(void);
 /* ---- batched decode ----------------------------------------------------
  * heifgpu_batch_prepare flattens n images (all must share bit depth and
  * chroma format) into device descriptors, uploads their bitstreams
- * (synchronously) and allocates the work arenas.  heifgpu_batch_decode
+ * (complete on return) and allocates the work arenas.
+ * heifgpu_batch_prepare_ex does the same with options (NULL = defaults) and
+ * without waiting for the upload: the host work (flattening into a pinned
+ * staging buffer) is done on return, the host-to-device copies run on an
+ * internal upload stream that the next heifgpu_batch_decode of the batch
+ * waits for.  With *inout == NULL it creates a batch; otherwise it reloads
+ * *inout with the new images, reusing its device arenas when they are large
+ * enough (the copies wait for every decode still reading the old contents).
+ * Two batches reloaded alternately overlap host parsing and upload of batch
+ * n + 1 with the decode of batch n.  heifgpu_batch_decode
  * then enqueues the five decode stages on `stream` (a hipStream_t; NULL =
  * the device's null stream, as everywhere in HIP) and returns immediately; out[i] receives
  * image i.  It may be called repeatedly on the same batch (the bench times
  * exactly this call).  heifgpu_batch_status synchronises the stream and
  * returns the per-image status words (0 = ok). */
 int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, heifgpu_batch **out);
+int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n,
+                             const heifgpu_batch_opts *opts, heifgpu_batch **inout);
 int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *batch, const heifgpu_planes *out, void *stream);
 int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *batch, uint32_t *status, void *stream);
 void heifgpu_batch_free(heifgpu_batch *batch);
@@ -114,14 +140,21 @@ void heifgpu_batch_free(heifgpu_batch *batch);
  * parse, transform, intra, deblock, sao/output, and (last) the
  * emulation-prevention pass k_rbsp; the query resets the mean.  k_rbsp and
  * k_parse run on an internal parse stream, the rest on an internal recon
- * stream, so decode n+1's parse overlaps decode n's reconstruction;
- * heifgpu_last_chunks() is 1 after a timed decode (ABI v1 compatibility). */
+ * stream, so decode n+1's parse overlaps decode n's reconstruction. */
 int heifgpu_set_timing(heifgpu_ctx *ctx, int enable);
 int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[6]);
-int heifgpu_last_chunks(const heifgpu_ctx *ctx);
 /* convenience: prepare + decode + status + free */
 int heifgpu_decode_batch(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, const heifgpu_planes *out,
                          void *stream, uint32_t *status);
+
+/* Gather of a tile split: copies the visible windows of the grid tiles k with
+ * k % tile_stride == tile_offset from `src` (planes decoded by a batch with
+ * those options, possibly on another device) into `dst` (full-size planes),
+ * with 2-D copies on `stream` (a stream of dst's device; peer copies over
+ * xGMI when the devices differ, peer access enabled here).  `info` describes
+ * the image (heifgpu_image_get_info). */
+int heifgpu_gather_tiles(const heifgpu_image_info *info, const heifgpu_planes *dst, const heifgpu_planes *src,
+                         uint32_t tile_stride, uint32_t tile_offset, void *stream);
 
 /* ---- YCbCr -> RGB with the irot rotation (libheif's default output) -------
  * Converts one decoded image (planes as written by heifgpu_batch_decode,
@@ -169,8 +202,8 @@ typedef struct {
 int heifgpu_image_tile_params(const heifgpu_image *img, uint32_t tile, heifgpu_tile_params *out);
 
 /* ---- tuning hook ------------------------------------------------------ */
-/* k_parse cycle/bin counters (wave cycles, WPP wait cycles, context bins,
- * bypass bins, ring refills, coding_quadtree / residual_coding / SAO cycles),
+/* k_parse_lanes counters (s_memtime cycles: whole wave, passes, per unit
+ * kind CTU / tree / TB / sub-block / CTU end; lanes that ran a unit),
  * summed over waves since the last call, then reset.  Returns the number of
  * counters written, or 0 for the product build (counters compiled out; the
  * `make prof` library has them). */

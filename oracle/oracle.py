@@ -7,13 +7,16 @@ See oracle/oracle.h for what the oracle restates and how it is pinned.
 from __future__ import annotations
 
 import ctypes
+import os
 import pathlib
 from dataclasses import dataclass
 
 import numpy as np
 
 _HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = _HERE / "build" / "liboracle.so"
+# ORACLE_LIBRARY: another build of the same oracle (bench.py's cpu_baseline
+# builds `make -C oracle native`, -march=native for the host it runs on)
+LIB_PATH = pathlib.Path(os.environ.get("ORACLE_LIBRARY", _HERE / "build" / "liboracle.so"))
 
 
 class _Meta(ctypes.Structure):

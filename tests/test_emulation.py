@@ -79,3 +79,18 @@ def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonb
     assert rc in (0, 1), out[-2000:]
     line = next(l for l in out.splitlines() if l.startswith("parse: status"))
     assert int(line.split()[2].rstrip(","), 16) != 0
+
+
+@pytest.mark.parametrize("split", [(2, 0), (2, 1), (3, 0), (3, 1), (3, 2), (8, 5)])
+def test_emulated_tile_split_subsets(emu_check, split):
+    """Row e2 (single-image tile split): rank g of G decodes only
+    tiles k % G == g.  Its windows must equal the oracle's decode of the whole
+    image and nothing else may be written, so the union over g — what
+    heifgpu_gather_tiles assembles — is the single-rank decode bit for bit."""
+    G, g = split
+    r = subprocess.run([str(emu_check), str(ROOT / "tests/golden/halfmoonbay.heic"), "5", str(G), str(g)],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "EMU PARITY OK" in r.stdout, (r.stdout + r.stderr)[-2000:]
+    line = next(l for l in r.stdout.splitlines() if l.startswith("parse: status"))
+    tbs = int(line.split()[3])
+    assert 0 < tbs < 207654  # a strict subset of the image's TBs

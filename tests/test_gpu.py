@@ -216,3 +216,76 @@ def test_rgb_rotated_matches_restatement(H, halfmoonbay):
     # the monochrome gain map: R = G = B
     aux = H.HeicDecoder.decode_rgb(halfmoonbay, item_id=inf.aux_item_id).cpu().numpy()
     assert aux.shape == (2016, 1512, 3) and (aux[..., 0] == aux[..., 2]).all()
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_tile_split_gather_bit_exact(H, ctx, oracle_halfmoonbay, halfmoonbay, G):
+    """Row e2: one image split by grid tile over G "ranks" (here G batches on
+    one device; on a node, one per GPU), each decoding tiles k % G == g into
+    its own full-size planes, then gathered (heifgpu_gather_tiles) into one
+    image: bit-exact with the oracle, and each rank wrote only its tiles."""
+    img = H.HeifImage.parse(halfmoonbay)
+    dst = ctx.alloc_outputs([img])[0]
+    for t in (dst.y, dst.cb, dst.cr):
+        t.fill_(0)
+    for g in range(G):
+        part = ctx.alloc_outputs([img])[0]
+        for t in (part.y, part.cb, part.cr):
+            t.fill_(0xA5)
+        b = ctx.prepare([img], tile_stride=G, tile_offset=g)
+        b.decode_async([part])
+        assert b.status() == [0]
+        b.free()
+        y = part.y.cpu().numpy()
+        for k in range(48):
+            r, c = divmod(k, 8)
+            win = y[512 * r:512 * (r + 1), 512 * c:512 * (c + 1)]
+            ref = oracle_halfmoonbay.y[512 * r:512 * (r + 1), 512 * c:512 * (c + 1)]
+            if k % G == g:
+                assert np.array_equal(win, ref), (g, k)
+            else:
+                assert (win == 0xA5).all(), (g, k)
+        ctx.gather_tiles(dst, part, G, g)
+    torch.cuda.synchronize()
+    y, cb, cr = planes_np(dst)
+    assert np.array_equal(y, oracle_halfmoonbay.y)
+    assert np.array_equal(cb, oracle_halfmoonbay.cb)
+    assert np.array_equal(cr, oracle_halfmoonbay.cr)
+
+
+def test_tile_subset_without_pictures(H, ctx, oracle_mod, halfmoonbay):
+    """A subset that selects no picture (a 1x1 item, offset 1 of 2) decodes nothing and reports clean."""
+    aux = H.HeifImage.parse(halfmoonbay, H.HeifImage.parse(halfmoonbay).info.aux_item_id)
+    out = ctx.alloc_outputs([aux])[0]
+    out.y.fill_(7)
+    b = ctx.prepare([aux], tile_stride=2, tile_offset=1)
+    b.decode_async([out])
+    assert b.status() == [0]
+    assert int((out.y != 7).sum()) == 0
+    b.free()
+
+
+def test_reloaded_batches_alternate(H, ctx, oracle_tiles, halfmoonbay):
+    """f1: two batches reloaded in turn (heifgpu_batch_prepare_ex with a batch
+    to reuse, uploads not waited for) while the other decodes; every load's
+    planes exact, including a reload with more images (arena growth)."""
+    from heif_amd.synthetic import permutation, permuted_heic
+
+    loads = [[11], [12, 13], [14], [15, 16, 17], [18]]
+    batches = [None, None]
+    results = []
+    for i, seeds in enumerate(loads):
+        imgs = H.HeifImage.parse_many([permuted_heic(halfmoonbay, s) for s in seeds], threads=4)
+        outs = ctx.alloc_outputs(imgs)
+        batches[i % 2] = ctx.prepare(imgs, reuse=batches[i % 2], wait=False)
+        batches[i % 2].decode_async(outs)
+        results.append((seeds, outs))
+    torch.cuda.synchronize()
+    for seeds, outs in results:
+        for s, o in zip(seeds, outs):
+            want = assemble(oracle_tiles, permutation(48, s))
+            for got, w in zip(planes_np(o), want):
+                assert np.array_equal(got, w), s
+    for b in batches:
+        assert not any(b.status())
+        b.free()

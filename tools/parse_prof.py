@@ -1,12 +1,14 @@
-"""k_parse cycle breakdown (tuning only).
+"""k_parse_lanes cycle breakdown (tuning only).
 
-usage: HEIFGPU_LIBRARY=heif_amd/libheifgpu_prof.so python tools/parse_prof.py [n_images]
+usage: HEIFGPU_LIBRARY=heif_amd/libheifgpu_prof.so python tools/parse_prof.py [n_images] [out.json]
 
 Decodes a batch of permuted halfmoonbay images with the counter-instrumented
-library (`make -C heif_amd/csrc prof`) and prints the per-wave averages of
-the k_parse counters (s_memtime cycles) and cycles per bin.
+library (`make -C heif_amd/csrc prof`) and prints per-wave averages of the
+k_parse_lanes counters (s_memtime cycles per unit kind, passes, lanes that
+ran a unit), i.e. the mean active lanes per unit execution and per pass.
 """
 import ctypes
+import json
 import pathlib
 import sys
 
@@ -19,9 +21,9 @@ import heif_amd as H  # noqa: E402
 from heif_amd import _lib  # noqa: E402
 from heif_amd.synthetic import permuted_heic  # noqa: E402
 
-NAMES = ["wave", "spin", "bins", "bypass", "refill", "cqt", "resid", "sao"]
-# k_parse_lanes (HEIFGPU_PARSE=lanes): per-wave s_memtime cycles
-LANES = ["l_wave", "l_passes", "l_ctu", "l_tree", "l_tb", "l_sb", "l_ctu_end", "l_refill"]
+# slots of heifgpu_debug_counters (parse_lanes.hip g_prof_lanes), summed over waves
+LANES = ["cycles", "passes", "ctu", "tree", "tb", "sb", "ctu_end", "units"]
+BINS_PER_IMAGE = 15358022  # context + bypass + terminate bins of one halfmoonbay image (oracle count)
 
 
 def main():
@@ -41,21 +43,26 @@ def main():
         raise SystemExit("library has no counters: build with `make -C heif_amd/csrc prof` and set HEIFGPU_LIBRARY")
     batch.decode_async(outs)
     torch.cuda.synchronize()
-    st = ctx.stage_times()
+    parse_ms = ctx.stage_times()[0]
     lib.heifgpu_debug_counters(buf, 16)
-    c = dict(zip(NAMES + LANES, buf[:k]))
-    if c.get("l_passes"):
-        print("k_parse_lanes totals:", {n: c[n] for n in LANES}, f"parse {ctx.stage_times()[0]:.3f} ms")
-        return
-    info = imgs[0].info
-    rows = n * info.num_tiles * ((info.tile_height + 63) // 64)
-    print(f"images {n}, waves(rows) {rows}, parse {st[0]:.3f} ms, status {batch.status()}")
-    for name in NAMES:
-        print(f"  {name:7s} total {c[name]:16d}  per wave {c[name] / rows:14.1f}")
-    bins = c["bins"] + c["bypass"]
-    busy = c["wave"] - c["spin"]
-    print(f"  cycles/bin (busy) {busy / max(bins, 1):.1f}; cqt cycles/bin {c['cqt'] / max(bins, 1):.1f}; "
-          f"spin share {c['spin'] / max(c['wave'], 1):.3f}")
+    c = dict(zip(LANES, buf[:k]))
+    pics = sum(im.info.num_tiles for im in imgs)
+    waves = (pics + 3) // 4
+    res = {
+        "images": n,
+        "waves": waves,
+        "parse_ms": round(parse_ms, 3),
+        "per_wave": {name: round(c[name] / waves, 1) for name in LANES},
+        "cycles_per_pass": round(c["cycles"] / max(c["passes"], 1), 1),
+        "lanes_per_pass": round(c["units"] / max(c["passes"], 1), 2),
+        "unit_cycle_share": {name: round(c[name] / max(c["cycles"], 1), 3)
+                             for name in ("ctu", "tree", "tb", "sb", "ctu_end")},
+        "bins_per_wave": round(n * BINS_PER_IMAGE / waves, 1),
+        "note": "s_memtime shader cycles of the instrumented build (+~11% over the product build)",
+    }
+    print(json.dumps(res))
+    if len(sys.argv) > 2:
+        pathlib.Path(sys.argv[2]).write_text(json.dumps(res, indent=1) + "\n")
 
 
 if __name__ == "__main__":

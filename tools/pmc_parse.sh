@@ -1,26 +1,46 @@
 #!/bin/bash
-# SQ instruction-mix counters of k_parse for one library variant (tuning).
-# usage: tools/pmc_parse.sh <variant-suffix or ''>  -> gpurun_out/pmc_<v>/
+# SQ counters of k_parse_lanes (one rocprofv3 --pmc pass per counter set,
+# each within the 8-SQ-counter limit), reduced to per-launch and per-bin
+# figures in gpurun_out/pmc_parse/parse_counters.json.
+# usage: tools/pmc_parse.sh [library-suffix]   (on the GPU box, repo root)
 V=$1
-# extra environment (e.g. HEIFGPU_PARSE=lanes) is inherited by the profiled process
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 LIB=$R/heif_amd/libheifgpu${V:+_$V}.so
+OUT=$R/gpurun_out/pmc_parse${V:+_$V}
+BATCH=${PMC_BATCH:-128}
 cd /tmp && export TMPDIR=/tmp
-mkdir -p "$R/gpurun_out/pmc_$V"
-for set in "SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVES SQ_INSTS_SMEM SQ_BUSY_CU_CYCLES" \
-           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS"; do
-    tag=$(echo $set | cut -c1-12 | tr ' ' '_')
-    HEIFGPU_LIBRARY=$LIB timeout -k 10 300 rocprofv3 --pmc $set -d "$R/gpurun_out/pmc_$V/$tag" -o p --output-format csv -- \
-        python3 "$R/bench.py" --batch 64 --steps 1 --warmup 1 --no-cpu-baseline --verify 0 > "$R/gpurun_out/pmc_$V/$tag.log" 2>&1 || exit 1
+mkdir -p "$OUT"
+i=0
+for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_BRANCH" \
+           "SQ_WAIT_INST_LDS SQ_INST_LEVEL_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA" \
+           "SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_IFETCH"; do
+    i=$((i + 1))
+    HEIFGPU_LIBRARY=$LIB timeout -s KILL 300 rocprofv3 --pmc $set -d "$OUT/set$i" -o p --output-format csv -- \
+        python3 "$R/bench.py" --batch "$BATCH" --steps 1 --warmup 1 --no-cpu-baseline --verify 0 > "$OUT/set$i.log" 2>&1 || { [ $i -eq 3 ] || exit 1; }
 done
-python3 - "$R/gpurun_out/pmc_$V" <<'PY'
-import csv, collections, glob, sys
-acc = collections.defaultdict(float); disp = set()
-for f in glob.glob(sys.argv[1] + "/*/p_counter_collection.csv"):
+python3 - "$OUT" "$BATCH" <<'PY'
+import csv, collections, glob, json, sys
+out, batch = sys.argv[1], int(sys.argv[2])
+acc = collections.defaultdict(float)
+disp = collections.defaultdict(set)
+for f in glob.glob(out + "/set*/**/p_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if "k_parse" in r["Kernel_Name"]:
-            acc[r["Counter_Name"]] += float(r["Counter_Value"]); disp.add((f, r["Dispatch_Id"]))
-nd = len(disp) / 2
-bins = 64 * 15358022
-print({k: round(v / nd / bins, 2) for k, v in sorted(acc.items())}, "per bin")
+            acc[r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[r["Counter_Name"]].add((f, r["Dispatch_Id"]))
+per_launch = {k: v / len(disp[k]) for k, v in sorted(acc.items())}
+bins = batch * 15358022  # bins per halfmoonbay image (oracle count)
+res = {
+    "kernel": "k_parse_lanes",
+    "batch_images": batch,
+    "bins_per_launch": bins,
+    "per_launch": {k: round(v) for k, v in per_launch.items()},
+    "per_bin": {k: round(v / bins, 4) for k, v in per_launch.items()},
+    "note": "SQ_*_CYCLES / WAIT / ACTIVE count quad-cycles (MI355X_MICROARCH.md); one pass per counter set",
+}
+w = per_launch.get("SQ_WAVES")
+if w:
+    res["per_wave"] = {k: round(v / w, 1) for k, v in per_launch.items()}
+json.dump(res, open(out + "/parse_counters.json", "w"), indent=1)
+print(json.dumps(res["per_bin"]))
 PY
