@@ -197,6 +197,8 @@ def main():
     import torch
 
     rank, world, local = dist_env()
+    # the CPU baseline's -march=native oracle must be selected before anything imports the oracle
+    cpu_build = native_oracle() if rank == 0 and not args.no_cpu_baseline else None
     if world > 1:
         import torch.distributed as dist
 
@@ -377,7 +379,7 @@ def main():
         if e2e:
             line["e2e"] = e2e
         if not args.no_cpu_baseline:
-            build = native_oracle()
+            build = cpu_build
             threads = effective_cpus()
             label = "synthetic 10-bit" if c5 else "halfmoonbay"
             cb = cpu_baseline(src, args.cpu_seconds, threads, label)

@@ -70,9 +70,10 @@ class HeifImage:
         """Primary images of many files, parsed on `threads` native host threads
         (heifgpu_image_parse_many; 0 = every hardware thread)."""
         n = len(files)
-        bufs = [_lib.u8buf(f) for f in files]
+        files = [bytes(f) for f in files]  # no copy for bytes; the library copies what it keeps
+        # pointers straight into the bytes objects (no Python-side copy of the files)
         data = (ctypes.POINTER(ctypes.c_uint8) * max(n, 1))(
-            *[ctypes.cast(b, ctypes.POINTER(ctypes.c_uint8)) for b in bufs])
+            *[ctypes.cast(ctypes.c_char_p(f), ctypes.POINTER(ctypes.c_uint8)) for f in files])
         lens = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in files])
         hs = (ctypes.c_void_p * max(n, 1))()
         rc = lib.heifgpu_image_parse_many(data, lens, n, threads, hs, None)

@@ -435,7 +435,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     }
     HostBatch hb;
     try {
-        hb = build_batch(parsed.data(), n, stride, offset);
+        hb = build_batch(parsed.data(), n, stride, offset, /*defer_bits=*/true);
     } catch (const UnsupportedError &e) {
         return fail(HEIFGPU_E_UNSUPPORTED, e.what());
     } catch (const std::exception &e) {
@@ -464,7 +464,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     if (b->loaded) HIP_TRY(hipEventSynchronize(b->uploaded));
     for (int k = 0; k < b->n_sets; ++k)
         if (b->set[k].pending) HIP_TRY(hipStreamWaitEvent(ctx->upload, b->set[k].recon_done, 0));
-    const bool grows = b->loaded && (hb.bits.size() > b->bits.cap || hb.pics.size() > b->pics.cap ||
+    const bool grows = b->loaded && (hb.bits_size > b->bits.cap || hb.pics.size() > b->pics.cap ||
                                      hb.subs.size() > b->subs.cap || hb.seqs.size() > b->seqs.cap ||
                                      hb.sf.size() > b->sf.cap || n > b->outs.cap || hb.recon_bytes > b->recon.cap ||
                                      hb.resid_elems > b->resid.cap || hb.tu_n > b->set[0].tus.cap ||
@@ -479,10 +479,10 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     b->pic_image = hb.pic_image;
     b->n_pics = int(hb.pics.size());
     // ---- device arenas (reused when large enough)
-    HIP_TRY(b->bits.alloc(hb.bits.size()));
+    HIP_TRY(b->bits.alloc(hb.bits_size));
     HIP_TRY(b->pics.alloc(hb.pics.size()));
     HIP_TRY(b->subs.alloc(hb.subs.size()));
-    HIP_TRY(b->rbsp.alloc(hb.bits.size()));
+    HIP_TRY(b->rbsp.alloc(hb.bits_size));
     HIP_TRY(b->rsubs.alloc(hb.subs.size()));
     HIP_TRY(b->seqs.alloc(hb.seqs.size()));
     HIP_TRY(b->sf.alloc(hb.sf.size()));
@@ -509,7 +509,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         void *dst;
     };
     const Seg segs[] = {
-        {hb.bits.data(), hb.bits.size(), b->bits.p},
+        {nullptr, hb.bits_size, b->bits.p},  // the payload pieces, copied below
         {hb.pics.data(), hb.pics.size() * sizeof(PicDesc), b->pics.p},
         {hb.subs.data(), hb.subs.size() * sizeof(uint32_t), b->subs.p},
         {hb.seqs.data(), hb.seqs.size() * sizeof(SeqParams), b->seqs.p},
@@ -519,15 +519,36 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     size_t total = 0;
     for (const Seg &g : segs) total += (g.bytes + 255) & ~size_t(255);
     HIP_TRY(b->stage.reserve(total));
+    {  // the bitstreams (most of the bytes) straight from the parsed images into staging, on a few threads
+        uint8_t *dst = b->stage.p;
+        const size_t np = hb.pieces.size();
+        const size_t nt = std::min<size_t>(std::max(1u, std::min(16u, std::thread::hardware_concurrency())),
+                                           (hb.bits_size >> 22) + 1);  // ~4 MB per thread at least
+        std::atomic<size_t> next{0};
+        auto copy = [&] {
+            for (size_t i; (i = next.fetch_add(64)) < np;)
+                for (size_t j = i; j < std::min(np, i + 64); ++j) {
+                    const HostBatch::Piece &pc = hb.pieces[j];
+                    std::memcpy(dst + pc.dst, pc.src, pc.len);
+                    const size_t end = j + 1 < np ? hb.pieces[j + 1].dst : hb.bits_size;
+                    std::memset(dst + pc.dst + pc.len, 0, end - pc.dst - pc.len);  // alignment padding
+                }
+        };
+        std::vector<std::thread> pool;
+        for (size_t t = 1; t < nt; ++t) pool.emplace_back(copy);
+        copy();
+        for (auto &th : pool) th.join();
+        if (np == 0) std::memset(dst, 0, hb.bits_size);
+    }
     size_t off = 0;
     for (const Seg &g : segs) {
         if (g.bytes) {
-            std::memcpy(b->stage.p + off, g.src, g.bytes);
+            if (g.src) std::memcpy(b->stage.p + off, g.src, g.bytes);
             HIP_TRY(hipMemcpyAsync(g.dst, b->stage.p + off, g.bytes, hipMemcpyHostToDevice, ctx->upload));
         }
         off += (g.bytes + 255) & ~size_t(255);
     }
-    HIP_TRY(hipMemsetAsync(b->rbsp.p, 0, hb.bits.size(), ctx->upload));
+    HIP_TRY(hipMemsetAsync(b->rbsp.p, 0, hb.bits_size, ctx->upload));
     HIP_TRY(hipEventRecord(b->uploaded, ctx->upload));
     b->loaded = true;
     BatchArgs &a = b->args;
@@ -835,7 +856,7 @@ int heifgpu_image_tile_params(const heifgpu_image *img, uint32_t tile, heifgpu_t
     o->slice_qp_y = 26 + pps.init_qp_minus26 + sh.slice_qp_delta;
     o->num_entry_point_offsets = sh.num_entry_point_offsets;
     o->slice_data_raw_offset = int32_t(sh.slice_data_raw_offset);
-    o->payload_bytes = int32_t(t.payload.size());
+    o->payload_bytes = int32_t(t.payload_len);
     for (size_t i = 0; i < sh.entry_point_offset.size() && i < 64; ++i) o->entry_point_offset[i] = sh.entry_point_offset[i];
     return HEIFGPU_OK;
 }

@@ -57,7 +57,8 @@ void fill_scaling(const ParamSet &ps, uint8_t *blk) {
 
 }  // namespace
 
-HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_stride, uint32_t tile_offset) {
+HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_stride, uint32_t tile_offset,
+                      bool defer_bits) {
     if (tile_stride == 0) tile_stride = 1;
     if (tile_offset >= tile_stride) throw HeifError("tile_offset must be below tile_stride");
     HostBatch hb;
@@ -93,10 +94,10 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
             const int w4 = (sq.width + 3) >> 2, h4 = (sq.height + 3) >> 2;
             const uint64_t samples = uint64_t(sq.width) * sq.height * (sq.chroma_format ? 3 : 2) / 2;
             PicDesc pd{};
-            pd.bits_off = hb.bits.size();
-            pd.bits_len = uint32_t(tj.payload.size());
-            hb.bits.insert(hb.bits.end(), tj.payload.begin(), tj.payload.end());
-            hb.bits.resize((hb.bits.size() + 63) & ~size_t(63));
+            pd.bits_off = hb.bits_size;
+            pd.bits_len = uint32_t(tj.payload_len);
+            hb.pieces.push_back({tj.payload, tj.payload_len, hb.bits_size});
+            hb.bits_size = (hb.bits_size + tj.payload_len + 63) & ~size_t(63);
             pd.sub_first = uint32_t(hb.subs.size());
             pd.n_sub = uint32_t(tj.sh.num_entry_point_offsets + 1);
             uint32_t o = tj.sh.slice_data_raw_offset;
@@ -149,7 +150,12 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
             if (wpp && hctb > 64) hb.wpp_ring = 1;
         }
     }
-    hb.bits.resize(hb.bits.size() + 128, 0);
+    hb.bits_size += 128;
+    if (!defer_bits) {
+        hb.bits.assign(hb.bits_size, 0);
+        for (const HostBatch::Piece &pc : hb.pieces) std::copy(pc.src, pc.src + pc.len, hb.bits.data() + pc.dst);
+        hb.pieces.clear();
+    }
     return hb;
 }
 

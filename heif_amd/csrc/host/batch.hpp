@@ -11,7 +11,15 @@
 namespace hg {
 
 struct HostBatch {
-    std::vector<uint8_t> bits;
+    std::vector<uint8_t> bits;  // every picture's payload, 64-byte aligned (+128 B tail), unless deferred
+    // deferred bits (build_batch(..., defer_bits = true)): where each payload
+    // goes in the bits arena, copied by the caller straight into its staging
+    struct Piece {
+        const uint8_t *src;
+        size_t len, dst;
+    };
+    std::vector<Piece> pieces;
+    size_t bits_size = 0;  // bytes of the bits arena
     std::vector<PicDesc> pics;
     std::vector<uint32_t> subs;
     std::vector<SeqParams> seqs;
@@ -26,6 +34,7 @@ struct HostBatch {
 // Throws HeifError / UnsupportedError.  Only grid tiles k (row-major) with
 // k % tile_stride == tile_offset become pictures (the single-image tile split
 // across GPUs); the default takes every tile.
-HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_stride = 1, uint32_t tile_offset = 0);
+HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_stride = 1, uint32_t tile_offset = 0,
+                      bool defer_bits = false);
 
 }  // namespace hg

@@ -80,11 +80,27 @@ ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id) {
         throw UnsupportedError("unsupported primary item type");
     }
 
-    std::map<size_t, int> param_of_prop;  // hvcC property offset → params index
+    // one owned copy of every tile item's bytes; the tiles' payloads are views into it
+    std::vector<const ItemInfo *> items;
+    size_t coded_total = 0;
     for (uint32_t id : tile_ids) {
         const ItemInfo *it = heif.item_info_by_item_id(id);
         if (!it) throw HeifError("tile item " + std::to_string(id) + " not found");
         if (it->type != fourcc('h', 'v', 'c', '1')) throw UnsupportedError("grid tile is not hvc1");
+        items.push_back(it);
+        coded_total += heif.item_data(*it, nullptr);
+    }
+    img.coded.reserve(coded_total);
+    std::vector<size_t> item_off;
+    for (const ItemInfo *it : items) {
+        item_off.push_back(img.coded.size());
+        heif.item_data(*it, &img.coded);
+    }
+    item_off.push_back(img.coded.size());
+
+    std::map<size_t, int> param_of_prop;  // hvcC property offset → params index
+    for (size_t ti = 0; ti < items.size(); ++ti) {
+        const ItemInfo *it = items[ti];
         const Property *hv = heif.item_property(*it, fourcc('h', 'v', 'c', 'C'));
         if (!hv) throw HeifError("missing HEVC decoder configuration");
         int param;
@@ -110,30 +126,32 @@ ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id) {
         const ParamSet &ps = img.params[size_t(param)];
         // read_item_nal_unit (decoder.rs:146-164), generalised: length-prefixed NAL units,
         // exactly one VCL NAL (one slice segment per picture), non-VCL units skipped
-        std::vector<uint8_t> item = heif.item_data(*it);
-        img.coded_bytes += uint32_t(item.size());
+        const uint8_t *item = img.coded.data() + item_off[ti];
+        const size_t item_len = item_off[ti + 1] - item_off[ti];
+        img.coded_bytes += uint32_t(item_len);
         int lsz = cfg.length_size_minus_one + 1;
         size_t pos = 0;
         bool have_vcl = false;
         TileJob job;
         job.param = param;
-        while (pos < item.size()) {
-            if (pos + size_t(lsz) > item.size()) throw HeifError("truncated NAL length prefix");
+        while (pos < item_len) {
+            if (pos + size_t(lsz) > item_len) throw HeifError("truncated NAL length prefix");
             size_t nl = 0;
             for (int k = 0; k < lsz; ++k) nl = (nl << 8) | item[pos + size_t(k)];
             pos += size_t(lsz);
-            if (nl < 3 || pos + nl > item.size()) throw HeifError("NAL unit length out of range");
+            if (nl < 3 || nl > item_len - pos) throw HeifError("NAL unit length out of range");
             NalUnitHeader h{uint16_t((item[pos] << 8) | item[pos + 1])};
             if (h.nal_unit_type() < 32) {
                 if (have_vcl) throw UnsupportedError("more than one slice segment per picture");
                 have_vcl = true;
                 job.nal = h;
-                job.payload.assign(item.begin() + long(pos) + 2, item.begin() + long(pos + nl));
+                job.payload = item + pos + 2;
+                job.payload_len = nl - 2;
             }
             pos += nl;
         }
         if (!have_vcl) throw HeifError("tile item holds no VCL NAL unit");
-        job.sh = slice_segment_header(job.payload.data(), job.payload.size(), job.nal, ps.sps, ps.pps);
+        job.sh = slice_segment_header(job.payload, job.payload_len, job.nal, ps.sps, ps.pps);
         img.tiles.push_back(std::move(job));
     }
     const SequenceParameterSet &s0 = img.params[0].sps;

@@ -16,13 +16,22 @@ struct ParamSet {
 };
 
 struct TileJob {
-    std::vector<uint8_t> payload;  // raw NAL payload after the 2-byte header (EP bytes kept)
+    // raw NAL payload after the 2-byte header (EP bytes kept): a view into ParsedImage::coded
+    const uint8_t *payload = nullptr;
+    size_t payload_len = 0;
     NalUnitHeader nal;
     SliceSegmentHeader sh;
     int param = 0;
 };
 
 struct ParsedImage {
+    // move-only: the tiles' payload views point into `coded`, whose buffer a move keeps
+    ParsedImage() = default;
+    ParsedImage(const ParsedImage &) = delete;
+    ParsedImage &operator=(const ParsedImage &) = delete;
+    ParsedImage(ParsedImage &&) = default;
+    ParsedImage &operator=(ParsedImage &&) = default;
+    std::vector<uint8_t> coded;  // the coded items' bytes, one copy (TileJob payloads point into it)
     std::vector<ParamSet> params;
     std::vector<TileJob> tiles;  // grid order (row-major)
     uint32_t primary_item_id = 0, ispe_width = 0, ispe_height = 0, rotation = 0, num_thumbnails = 0;

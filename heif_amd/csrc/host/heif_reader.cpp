@@ -78,8 +78,8 @@ const Property *Heif::item_property(const ItemInfo &it, uint32_t type) const {
     return nullptr;
 }
 
-std::vector<uint8_t> Heif::item_data(const ItemInfo &it) const {
-    std::vector<uint8_t> out;
+size_t Heif::item_data(const ItemInfo &it, std::vector<uint8_t> *out) const {
+    size_t total = 0;
     for (auto &e : it.extents) {
         const uint8_t *base;
         size_t limit;
@@ -94,8 +94,15 @@ std::vector<uint8_t> Heif::item_data(const ItemInfo &it) const {
         }
         // without overflow: offset and length are up to 64-bit file fields
         if (e.offset > limit || e.length > limit - e.offset) throw HeifError("item extent out of bounds");
-        out.insert(out.end(), base + e.offset, base + e.offset + e.length);
+        if (out) out->insert(out->end(), base + e.offset, base + e.offset + e.length);
+        total += size_t(e.length);
     }
+    return total;
+}
+
+std::vector<uint8_t> Heif::item_data(const ItemInfo &it) const {
+    std::vector<uint8_t> out;
+    item_data(it, &out);
     return out;
 }
 

@@ -59,6 +59,8 @@ struct Heif {
     const ItemInfo *item_info_by_item_id(uint32_t id) const;
     const Property *item_property(const ItemInfo &it, uint32_t type) const;
     std::vector<uint8_t> item_data(const ItemInfo &it) const;  // concatenated extents
+    // the item's byte count (extents bounds-checked), appending its bytes to *out when out is set
+    size_t item_data(const ItemInfo &it, std::vector<uint8_t> *out) const;
     std::vector<uint32_t> references_from(uint32_t type, uint32_t from) const;
     ImageGrid grid(const ItemInfo &it) const;
     // tests/libheif_comparison.rs:240-250: 'thmb' references pointing at the primary

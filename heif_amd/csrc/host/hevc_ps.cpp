@@ -440,9 +440,31 @@ PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp,
     return p;
 }
 
+namespace {
+SliceSegmentHeader slice_segment_header_prefix(const uint8_t *payload, size_t len, size_t full_len, NalUnitHeader nal,
+                                               const SequenceParameterSet &sps, const PictureParameterSet &pps);
+}  // namespace
+
 SliceSegmentHeader slice_segment_header(const uint8_t *payload, size_t len, NalUnitHeader nal,
                                         const SequenceParameterSet &sps, const PictureParameterSet &pps) {
-    // the header is short: strip EP from a bounded prefix, remembering removed bytes
+    // The header is short: parse it from an EP-stripped prefix of the payload
+    // (stripping the whole 35 KB payload of a tile dominated host parse time),
+    // and only when it does not fit there from the whole payload.
+    constexpr size_t kPrefix = 4096;
+    if (len > kPrefix) {
+        try {
+            return slice_segment_header_prefix(payload, kPrefix, len, nal, sps, pps);
+        } catch (const HeifError &) {
+            // fall through: a header longer than the prefix, or a genuine error reported from the full payload
+        }
+    }
+    return slice_segment_header_prefix(payload, len, len, nal, sps, pps);
+}
+
+namespace {
+// the header from the first `len` bytes of a payload of `full_len` bytes
+SliceSegmentHeader slice_segment_header_prefix(const uint8_t *payload, size_t len, size_t full_len, NalUnitHeader nal,
+                                               const SequenceParameterSet &sps, const PictureParameterSet &pps) {
     std::vector<uint32_t> ep;
     std::vector<uint8_t> rbsp = RbspReader::remove_emulation_prevention(payload, len, &ep);
     RbspReader r(rbsp.data(), rbsp.size());
@@ -541,9 +563,10 @@ SliceSegmentHeader slice_segment_header(const uint8_t *payload, size_t len, NalU
     h.slice_data_raw_offset = uint32_t(raw);
     uint64_t total = raw;
     for (uint32_t o : h.entry_point_offset) total += o;
-    if (total >= len) throw HeifError("entry points exceed the NAL unit");
+    if (total >= full_len) throw HeifError("entry points exceed the NAL unit");
     return h;
 }
+}  // namespace
 
 HevcConfig parse_hvcc(const uint8_t *p, size_t n) {
     if (n < 23) throw HeifError("hvcC too short");
