@@ -559,6 +559,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.rbsp = b->rbsp.p;
     a.rsubs = b->rsubs.p;
     a.parse_order = b->porder.p;
+    a.n_slots = int(order.size());
     a.seqs = b->seqs.p;
     a.sf = b->sf.p;
     a.outs = b->outs.p;

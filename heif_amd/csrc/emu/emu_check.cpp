@@ -64,6 +64,7 @@ int main(int argc, char **argv) {
     std::vector<uint32_t> order;
     lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
     a.parse_order = order.data();
+    a.n_slots = int(order.size());
     a.seqs = hb.seqs.data();
     a.sf = hb.sf.data();
     a.outs = &out;

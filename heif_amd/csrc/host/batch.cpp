@@ -2,6 +2,7 @@
 #include "batch.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace hg {
 
@@ -46,6 +47,18 @@ SeqParams make_seq(const ParamSet &ps, uint32_t sf_off) {
     q.out_h = s.out_height();
     q.sf_off = sf_off;
     return q;
+}
+
+// k_parse_lanes lanes per WPP picture: a picture with more CTB rows wraps
+// them round its lanes (lane r parses rows r, r + R, ...).  HEIFGPU_LANE_ROWS
+// caps R (tuning).
+int max_lane_rows() {
+    static const int cap = [] {
+        const char *e = std::getenv("HEIFGPU_LANE_ROWS");
+        const int v = e ? std::atoi(e) : 64;
+        return v < 1 ? 1 : (v > 64 ? 64 : v);
+    }();
+    return cap;
 }
 
 void fill_scaling(const ParamSet &ps, uint8_t *blk) {
@@ -146,8 +159,8 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
             hb.max_rows = std::max(hb.max_rows, hctb);
             hb.max_log2ctb = std::max(hb.max_log2ctb, int(sq.log2_ctb));
             const bool wpp = (sq.flags & SP_WPP) != 0;
-            hb.lane_rows = std::max(hb.lane_rows, wpp ? std::min(hctb, 64) : 1);
-            if (wpp && hctb > 64) hb.wpp_ring = 1;
+            hb.lane_rows = std::max(hb.lane_rows, wpp ? std::min(hctb, max_lane_rows()) : 1);
+            if (wpp && hctb > max_lane_rows()) hb.wpp_ring = 1;
         }
     }
     hb.bits_size += 128;

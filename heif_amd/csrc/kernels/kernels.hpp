@@ -28,7 +28,8 @@ struct BatchArgs {
     const uint32_t *subs;      // substream raw start offsets (n_sub + 1 per picture, last = len)
     uint8_t *rbsp;             // k_rbsp: NAL payloads with emulation prevention removed (same offsets as bits)
     uint32_t *rsubs;           // k_rbsp: substream start offsets into rbsp (last = RBSP length)
-    const uint32_t *parse_order;  // k_parse_lanes: picture (minus pic0) of wave slot i; null = identity
+    const uint32_t *parse_order;  // k_parse_lanes: picture (minus pic0) of wave slot i (~0u: empty); null = identity
+    int n_slots;               // entries of parse_order (wave slots; a multiple of the pictures per wave)
     const SeqParams *seqs;
     const uint8_t *sf;         // ScalingFactor blocks
     const OutImage *outs;

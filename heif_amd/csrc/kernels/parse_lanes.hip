@@ -128,7 +128,13 @@ struct Lane {
     int k;
     uint64_t cur;     // next bits of the substream, MSB first (cn valid)
     int cn;
-    uint32_t nx, lb;  // prefetched next RBSP dword (as loaded) and the offset of the one after it
+    // RBSP queue, dwords as loaded (little endian): a (ai consumed), then b (valid: bv), then f (in
+    // flight: fp); lb = offset of the 16 bytes after the last loaded block.  f is issued at a pass
+    // start and lands at the next one, after the pass's one memory wait, so refills inside a pass
+    // never wait on memory (a wait for a load also waits for every older store)
+    uint32_t a0, a1, a2, a3, b0, b1, b2, b3, f0, f1, f2, f3;
+    int ai, bv, fp;
+    uint32_t lb;
     int32_t budget;   // 8 * (bytes from the substream start to the picture's RBSP end) - bits moved into value
     uint32_t status;
     int st;
@@ -217,32 +223,77 @@ HG_HD inline uint8_t load_byte_coherent(const uint8_t *p) {
 // ------------------------------------------------------------------ bytes
 // Each lane reads its substream straight from the RBSP arena, which k_rbsp
 // (rbsp.hip) filled with emulation prevention removed (rbsp_reader.rs:11-39).
-// One dword is always in flight ahead of the bit window, so the load latency
-// hides behind the ~32 bits of bins decoded in between.  Loads stop 64 bytes
-// past the picture's end (arena padding); an overrun of a corrupt stream
-// shows as budget + k < 0 at the CTU end (ST_OVERRUN).
-// raw (little-endian) dword at `off`, clamped to `lim` instead of branching,
-// so the load issues straight into its register and nothing waits on it
-// until the window needs it (byte-swapped there)
-HG_HD inline uint32_t load_raw(const uint8_t *p, uint32_t off, uint32_t lim) {
-    const uint32_t o = off < lim ? off : lim;
+// The bit window refills from a per-lane queue of up to 8 dwords in registers;
+// 16 more bytes are loaded at each pass start and used from the next pass on,
+// after the pass's single s_waitcnt, so no refill inside a pass waits on
+// memory (a wait for a load also drains every older store of the wave: with a
+// one-dword prefetch it cost ~5 % of the parse).  Loads stop 64 bytes past
+// the picture's end (arena padding); an overrun of a corrupt stream shows as
+// budget + k < 0 at the CTU end (ST_OVERRUN).
+// 16 bytes at `off` (dword aligned), clamped to `lim` (inside the arena's padding)
 #if defined(HG_HOST_EMU)
-    return (uint32_t)p[o] | ((uint32_t)p[o + 1] << 8) | ((uint32_t)p[o + 2] << 16) | ((uint32_t)p[o + 3] << 24);
-#else
-    return *reinterpret_cast<const uint32_t *>(p + o);
-#endif
+inline void load_x4(const uint8_t *p, uint32_t off, uint32_t lim, uint32_t &x, uint32_t &y, uint32_t &z, uint32_t &w) {
+    uint32_t v[4];
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t o = std::min(off + 4u * (uint32_t)i, lim);
+        v[i] = (uint32_t)p[o] | ((uint32_t)p[o + 1] << 8) | ((uint32_t)p[o + 2] << 16) | ((uint32_t)p[o + 3] << 24);
+    }
+    x = v[0], y = v[1], z = v[2], w = v[3];
 }
+// the pass start's one memory wait (host emulation: nothing in flight)
+inline void pass_wait() {}
+#else
+__device__ __forceinline__ void load_x4(const uint8_t *p, uint32_t off, uint32_t lim, uint32_t &x, uint32_t &y,
+                                        uint32_t &z, uint32_t &w) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(p + (off < lim ? off : lim));
+    x = v.x, y = v.y, z = v.z, w = v.w;
+}
+// s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): every global access of this wave so far
+__device__ __forceinline__ void pass_wait() { __builtin_amdgcn_s_waitcnt(0x0f70); }
+#endif
 HG_HD inline uint32_t bswap32(uint32_t w) {
     return (w >> 24) | ((w >> 8) & 0xff00u) | ((w << 8) & 0xff0000u) | (w << 24);
+}
+
+// next RBSP dword of the queue.  Normally a or b; a lane that drained both
+// inside one pass takes f (waiting for it) or loads synchronously.
+HG_HD inline uint32_t q_pop(Lane &L, const Eng &G) {
+    const uint32_t w = L.ai == 0 ? L.a0 : (L.ai == 1 ? L.a1 : (L.ai == 2 ? L.a2 : L.a3));
+    if (++L.ai == 4) {
+        L.ai = 0;
+        if (L.bv) {
+            L.a0 = L.b0, L.a1 = L.b1, L.a2 = L.b2, L.a3 = L.b3;
+            L.bv = 0;
+        } else if (L.fp) {
+            L.a0 = L.f0, L.a1 = L.f1, L.a2 = L.f2, L.a3 = L.f3;
+            L.fp = 0;
+        } else {
+            load_x4(G.rbsp, L.lb, G.lim, L.a0, L.a1, L.a2, L.a3);
+            L.lb += 16;
+        }
+    }
+    return w;
+}
+
+// pass start (after pass_wait): land f, issue the next block
+HG_HD inline void q_refill(Lane &L, const Eng &G) {
+    if (L.fp && !L.bv) {
+        L.b0 = L.f0, L.b1 = L.f1, L.b2 = L.f2, L.b3 = L.f3;
+        L.bv = 1;
+        L.fp = 0;
+    }
+    if (!L.fp && L.lb) {
+        load_x4(G.rbsp, L.lb, G.lim, L.f0, L.f1, L.f2, L.f3);
+        L.lb += 16;
+        L.fp = 1;
+    }
 }
 
 // value += 16 more look-ahead bits (k < 8 on entry, so k <= 23 and value < 2^32 after)
 HG_HD inline void vfill(Lane &L, const Eng &G) {
     if (L.cn < 16) {
-        L.cur |= (uint64_t)bswap32(L.nx) << (32 - L.cn);
+        L.cur |= (uint64_t)bswap32(q_pop(L, G)) << (32 - L.cn);
         L.cn += 32;
-        L.nx = load_raw(G.rbsp, L.lb, G.lim);
-        L.lb += 4;
     }
     L.value = (L.value << 16) | (uint32_t)(L.cur >> 48);
     L.cur <<= 16;
@@ -254,10 +305,14 @@ HG_HD inline void vfill(Lane &L, const Eng &G) {
 // 9.3.2.5: engine initialisation at RBSP offset `start` (absolute), picture RBSP end `end`
 HG_HD inline void engine_init(Lane &L, const Eng &G, uint32_t start, uint32_t end) {
     const uint32_t a0 = start & ~3u, sh = (start & 3u) * 8u;
-    L.cur = (uint64_t)bswap32(load_raw(G.rbsp, a0, G.lim)) << (32 + sh);
+    load_x4(G.rbsp, a0, G.lim, L.a0, L.a1, L.a2, L.a3);
+    load_x4(G.rbsp, a0 + 16, G.lim, L.b0, L.b1, L.b2, L.b3);
+    L.ai = 0;
+    L.bv = 1;
+    L.fp = 0;
+    L.lb = a0 + 32;
+    L.cur = (uint64_t)bswap32(q_pop(L, G)) << (32 + sh);
     L.cn = 32 - (int)sh;
-    L.nx = load_raw(G.rbsp, a0 + 4, G.lim);
-    L.lb = a0 + 8;
     L.budget = 8 * (int32_t)(end - start);
     L.value = 0;
     L.k = -9;  // the first 9 bits are ivlOffset itself
@@ -1201,6 +1256,8 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
     L.status = 0;
     L.cn = 0;
     L.k = 8;
+    L.ai = L.bv = L.fp = 0;
+    L.lb = 0;
     L.fl = wpp ? F_WPP : 0u;
     L.row = row;
     L.c = 0;
@@ -1227,39 +1284,50 @@ inline int lanes_pics_per_wave(int lane_rows) {
 // Wave slot -> picture.  A wave runs until its heaviest picture is parsed,
 // and every extra busy picture in it adds divergent units to each pass, so
 // the critical path is the wave holding the most work.  Pictures are sorted
-// by payload size and dealt snake-wise (wave w of W gets ranks w, 2W-1-w,
-// 2W+w, 4W-1-w, ...): the heaviest pictures share a wave with the lightest.
-// HEIFGPU_PARSE_ORDER=0: batch order.
+// by payload size; the `heavy` largest each get a wave to themselves (their
+// WPP chain is the kernel's critical path, and a pass over one picture's
+// lanes is cheaper than over four), the rest are dealt snake-wise (wave w of
+// W gets ranks w, 2W-1-w, 2W+w, 4W-1-w, ...): heavy beside light.  Empty
+// slots are ~0u.  HEIFGPU_PARSE_ORDER=0: batch order; HEIFGPU_PARSE_HEAVY
+// overrides the heavy count.
 void lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uint32_t> &order) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
         return e ? std::atoi(e) : 1;
     }();
-    order.resize((size_t)n);
-    for (int i = 0; i < n; ++i) order[(size_t)i] = (uint32_t)i;
-    if (!on || n <= 0) return;
+    static const int heavy_env = [] {
+        const char *e = std::getenv("HEIFGPU_PARSE_HEAVY");
+        return e ? std::atoi(e) : -1;
+    }();
     const int ppw = lanes_pics_per_wave(lane_rows);
-    const int W = (n + ppw - 1) / ppw;
-    std::vector<uint32_t> by_size(order);
+    if (!on || n <= 0) {
+        order.resize((size_t)n);
+        for (int i = 0; i < n; ++i) order[(size_t)i] = (uint32_t)i;
+        order.resize((size_t)((n + ppw - 1) / ppw) * ppw, ~0u);
+        return;
+    }
+    std::vector<uint32_t> by_size((size_t)n);
+    for (int i = 0; i < n; ++i) by_size[(size_t)i] = (uint32_t)i;
     std::stable_sort(by_size.begin(), by_size.end(),
                      [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
-    std::vector<uint32_t> slots((size_t)W * ppw, UINT32_MAX);
-    for (int r = 0; r < n; ++r) {
+    int heavy = heavy_env >= 0 ? heavy_env : 0;
+    heavy = ppw > 1 ? std::min(heavy, n) : 0;
+    const int rest = n - heavy, W = (rest + ppw - 1) / ppw;
+    order.assign((size_t)(heavy + W) * ppw, ~0u);
+    for (int h = 0; h < heavy; ++h) order[(size_t)h * ppw] = by_size[(size_t)h];
+    for (int r = 0; r < rest; ++r) {
         const int band = r / W, pos = r % W;
         const int w = (band & 1) ? W - 1 - pos : pos;
-        slots[(size_t)w * ppw + band] = by_size[(size_t)r];
+        order[(size_t)(heavy + w) * ppw + band] = by_size[(size_t)(heavy + r)];
     }
-    // the last wave may be short: pack the slots so that slot < n holds a picture
-    int k = 0;
-    for (uint32_t s : slots)
-        if (s != UINT32_MAX) order[(size_t)k++] = s;
 }
 
 #if defined(HG_HOST_EMU)
 // one wave at a time, one unit per live lane per pass, lanes in order
 void emu_parse(const BatchArgs &a) {
     const int ppw = lanes_pics_per_wave(a.lane_rows);
-    const int waves = (a.n_pics + ppw - 1) / ppw;
+    const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
+    const int waves = (n_slots + ppw - 1) / ppw;
     uint64_t tab[64];
     for (int i = 0; i < 64; ++i) tab[i] = state_row(i);
     std::vector<LaneLds> lds(64);
@@ -1273,7 +1341,7 @@ void emu_parse(const BatchArgs &a) {
             prog[l] = 0;
             const int pl = l / a.lane_rows, row = l % a.lane_rows;
             const int slot = w * ppw + pl;
-            const bool in = pl < ppw && slot < a.n_pics;
+            const bool in = pl < ppw && slot < n_slots && (!a.parse_order || a.parse_order[slot] != ~0u);
             const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
             const bool live = in && lane_init(lanes[l], pics[pl], lds[l], a, pic, row, pl * a.lane_rows);
             if (!live) lanes[l].st = U_DONE;
@@ -1284,6 +1352,12 @@ void emu_parse(const BatchArgs &a) {
             bool any = false, progressed = false;
             for (int l = 0; l < 64; ++l) any |= lanes[l].st != U_DONE;
             if (!any) break;
+            for (int l = 0; l < 64; ++l)
+                if (lanes[l].st != U_DONE) {
+                    const LanePic &P = pics[l / a.lane_rows];
+                    const Eng G{lds[l].ctx, tab, a.rbsp, (P.bits_end + 64u) & ~3u};
+                    q_refill(lanes[l], G);
+                }
             // the kernel's pass: every unit kind in syntax order, each on the lanes in it
             for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
                 for (int l = 0; l < 64; ++l) {
@@ -1293,7 +1367,7 @@ void emu_parse(const BatchArgs &a) {
                     if (L.st != kind || (kind == U_CTU && !ctu_ready(L, P, E))) continue;
                     progressed = true;
                     ++units;
-                    const Eng G{lds[l].ctx, tab, a.rbsp, P.bits_end + 64};
+                    const Eng G{lds[l].ctx, tab, a.rbsp, (P.bits_end + 64u) & ~3u};
                     run_unit(kind, L, lds[l], P, E, G);
                 }
             }
@@ -1337,7 +1411,8 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     s_tab[lane] = state_row(lane);
     const int pl = lane / a.lane_rows, row = lane % a.lane_rows;
     const int slot = (int)blockIdx.x * ppw + pl;
-    const bool in = pl < ppw && slot < a.n_pics;
+    const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
+    const bool in = pl < ppw && slot < n_slots && (!a.parse_order || a.parse_order[slot] != ~0u);
     const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
     Lane L;
     LaneLds &ld = s_lds[lane < nl ? lane : 0];
@@ -1347,13 +1422,15 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     if (!live) L.st = U_DONE;
     __syncthreads();
     const Env E{&a, s_lds, s_prog, s_wctx, lane};
-    const Eng G{ld.ctx, s_tab, a.rbsp, live ? P.bits_end + 64 : 0u};
+    const Eng G{ld.ctx, s_tab, a.rbsp, live ? (P.bits_end + 64u) & ~3u : 0u};
 #if defined(HG_PARSE_PROF)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
     for (uint32_t pass = 0;; ++pass) {
         if (!__any(L.st != U_DONE)) break;
+        pass_wait();
+        if (live) q_refill(L, G);
         // one pass: every unit kind in syntax order, each run by the lanes in it
         // (a uniform loop: the units are never linearised into one divergent region)
         bool progressed = false;
@@ -1395,7 +1472,7 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
     if (a.lane_rows < 1 || a.lane_rows > 64) return hipErrorInvalidValue;
     const int ppw = lanes_pics_per_wave(a.lane_rows);
     a.parse_group = ppw;
-    const int waves = (a.n_pics + ppw - 1) / ppw;
+    const int waves = ((a.parse_order ? a.n_slots : a.n_pics) + ppw - 1) / ppw;
     hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0), s,
                        a);
     return hipGetLastError();
