@@ -162,6 +162,7 @@ struct Lane {
 struct Eng {
     uint8_t *ctx;
     const uint64_t *tab;  // per pStateIdx: rangeTabLps[4] | transIdxLps << 32 | transIdxMps << 40 (LDS)
+    const uint64_t *seq;  // sig_seq(scan, pattern): slot of every scan position of a sub-block (LDS)
     const uint8_t *rbsp;  // BatchArgs::rbsp (emulation prevention removed by k_rbsp)
     uint32_t lim;         // no loads at or past this offset (the picture's RBSP end + 64)
 };
@@ -409,16 +410,32 @@ HG_HD inline uint32_t byp_bits(Lane &L, const Eng &G, int n) {
     return v;
 }
 
-// prefix of coeff_abs_level_remaining (TR, cMax 4): the 1-bins before the
-// first 0, at most 4.  The next 4 bins are divided out without consuming them
-// and min(p + 1, 4) are consumed (a prefix of a long-division quotient is the
-// quotient of the shorter division).
-HG_HD inline int byp_prefix4(Lane &L, const Eng &G) {
-    const uint32_t q4 = div_range(L.value >> (L.k - 4), L.range);
-    const int p = __builtin_clz(((~q4) << 28) | (1u << 27));
-    const int m = p < 4 ? p + 1 : 4;
-    L.k -= m;
-    L.value -= ((q4 >> (4 - m)) * L.range) << L.k;
+// coeff_abs_level_remaining's non-escape part (decoder.rs:230-261: prefix
+// TR(cMax 4 << k, k), i.e. up to 4 one-bins, a 0, then k suffix bins) in ONE
+// division: the next 8 bins are divided out without consuming them, the
+// prefix p is their leading ones (at most 4), and when p < 4 the whole code
+// (p + 1 + k <= 8 bins) is a prefix of those 8, consumed at once (a prefix of
+// a long-division quotient is the quotient of the shorter division).  Returns
+// the value, or -1 after consuming the 4 ones of an escape.
+HG_HD inline int byp_rem(Lane &L, const Eng &G, int k) {
+    const uint32_t q8 = div_range(L.value >> (L.k - 8), L.range);  // k >= 8 on entry
+    const int p = __builtin_clz(((~q8) << 24) | (1u << 27));        // leading ones, at most 4
+    const int used = p < 4 ? p + 1 + k : 4;
+    const uint32_t q = q8 >> (8 - used);
+    L.k -= used;
+    L.value -= (q * L.range) << L.k;
+    if (L.k < 8) vfill(L, G);
+    return p < 4 ? (p << k) + (int)(q & ((1u << k) - 1u)) : -1;
+}
+
+// a unary bypass prefix of at most m (1..8) bins: the number p of 1-bins
+// before the first 0, consuming min(p + 1, m) bins
+HG_HD inline int byp_unary(Lane &L, const Eng &G, int m) {
+    const uint32_t q = div_range(L.value >> (L.k - m), L.range);
+    const int p = __builtin_clz(((~q) << (32 - m)) | (1u << (31 - m)));
+    const int used = p < m ? p + 1 : m;
+    L.k -= used;
+    L.value -= ((q >> (m - used)) * L.range) << L.k;
     if (L.k < 8) vfill(L, G);
     return p;
 }
@@ -538,6 +555,21 @@ HG_HD inline uint64_t sig_slots(int pcs) {
     return pcs == 0 ? sig_pat_nib(0) : pcs == 1 ? sig_pat_nib(1) : pcs == 2 ? sig_pat_nib(2) : sig_pat_nib(3);
 }
 HG_HD inline int msb32(uint32_t m) { return 31 - __builtin_clz(m); }
+
+// context slot of sig_coeff_flag per scan position n of a 4x4 sub-block
+// (nibble n), for scanIdx 0..2 and slot pattern 0..3 (prevCsbf, sizes > 4x4)
+// or 4 (ctxIdxMap, 4x4 TBs): 15 words, computed into LDS at kernel start
+HG_HD inline uint64_t sig_seq(int idx) {
+    const int scan = idx / 5, pat = idx % 5;
+    const uint64_t slots = pat == 4 ? kSigCtxMap4 : sig_slots(pat);
+    const uint64_t sw = scan4_word(scan);
+    uint64_t q = 0;
+    for (int n = 0; n < 16; ++n) {
+        const int e = (int)((sw >> (4 * n)) & 15u);
+        q |= ((slots >> (4 * e)) & 15u) << (4 * n);
+    }
+    return q;
+}
 
 struct Env {
     const BatchArgs *a;
@@ -993,26 +1025,22 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
         // use sigCtx 0 at the TB's DC (slot 0) and off + 0..2 (slots 1..3)
         const int cbase = CTX_SIG + (cidx ? 27 : 0);
         const uint8_t *cb = G.ctx + cbase;
-        uint64_t slots;
+        uint64_t seq = G.seq[L.rc_scan * 5 + (l2 == 2 ? 4 : pcs)];  // slot per scan position
         uint32_t c0, c1 = 0, c2 = 0;
         int off = 0;
         if (l2 == 2) {
-            slots = kSigCtxMap4;
             c0 = (uint32_t)cb[0] | ((uint32_t)cb[1] << 8) | ((uint32_t)cb[2] << 16) | ((uint32_t)cb[3] << 24);
             c1 = (uint32_t)cb[4] | ((uint32_t)cb[5] << 8) | ((uint32_t)cb[6] << 16) | ((uint32_t)cb[7] << 24);
             c2 = cb[8];
         } else {
             off = cidx == 0 ? ((xS | yS) ? 3 : 0) + (l2 == 3 ? (L.rc_scan == 0 ? 9 : 15) : 21) : (l2 == 3 ? 9 : 12);
-            slots = sig_slots(pcs);
-            if ((xS | yS) == 0) slots &= ~0xfull;  // DC of the TB: sigCtx 0
+            if ((xS | yS) == 0) seq &= ~0xfull;  // DC of the TB (scan position 0 of sub-block 0): sigCtx 0
             c0 = (uint32_t)cb[0] | ((uint32_t)cb[off] << 8) | ((uint32_t)cb[off + 1] << 16) |
                  ((uint32_t)cb[off + 2] << 24);
         }
-        const uint64_t sw = scan4_word(L.rc_scan);
         for (int nn = nstart; nn >= 0; --nn) {
             if (nn > 0 || !infer_dc) {
-                const int e = (int)((sw >> (4 * nn)) & 15u);
-                const int slot = (int)((slots >> (4 * e)) & 15u);
+                const int slot = (int)((seq >> (4 * nn)) & 15u);
                 uint32_t cs = cache_get(c0, c1, c2, slot);
                 const int bin = dec_s(L, G, cs);
                 cache_put(c0, c1, c2, slot, cs);
@@ -1090,21 +1118,18 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
                     k = k < 4 ? k : 4;
                 }
                 // coeff_abs_level_remaining (decoder.rs:230-261): TR(4 << k, k) prefix, EG(k + 1) escape
-                const int p = byp_prefix4(L, G);
-                if (p < 4) {
-                    rem = (p << k) + (int)byp_bits(L, G, k);
-                } else {
-                    // EG(k + 1) prefix, one bin per step (measured faster here than
-                    // 8-bin divisions: the loop is short and rarely taken by many lanes)
+                rem = byp_rem(L, G, k);
+                if (rem < 0) {
+                    // EG(k + 1) prefix: unary ones, up to 8 per division, at most 31 - (k + 1)
+                    const int lim = 31 - (k + 1);
                     int ones = 0;
-                    bool bad = false;
-                    while (byp(L, G)) {
-                        if (++ones > 31 - (k + 1)) {
-                            bad = true;
-                            break;
-                        }
+                    for (;;) {
+                        const int mm = lim + 1 - ones < 8 ? lim + 1 - ones : 8;
+                        const int p = byp_unary(L, G, mm);
+                        ones += p;
+                        if (p < mm || ones > lim) break;  // the terminating 0 read, or too many ones
                     }
-                    if (bad) {
+                    if (ones > lim) {
                         L.status |= ST_SYNTAX;
                         rem = 0;
                     } else {
@@ -1328,8 +1353,9 @@ void emu_parse(const BatchArgs &a) {
     const int ppw = lanes_pics_per_wave(a.lane_rows);
     const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
     const int waves = (n_slots + ppw - 1) / ppw;
-    uint64_t tab[64];
+    uint64_t tab[64], seq[15];
     for (int i = 0; i < 64; ++i) tab[i] = state_row(i);
+    for (int i = 0; i < 15; ++i) seq[i] = sig_seq(i);
     std::vector<LaneLds> lds(64);
     std::vector<LanePic> pics(64);
     std::vector<Lane> lanes(64);
@@ -1355,7 +1381,7 @@ void emu_parse(const BatchArgs &a) {
             for (int l = 0; l < 64; ++l)
                 if (lanes[l].st != U_DONE) {
                     const LanePic &P = pics[l / a.lane_rows];
-                    const Eng G{lds[l].ctx, tab, a.rbsp, (P.bits_end + 64u) & ~3u};
+                    const Eng G{lds[l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
                     q_refill(lanes[l], G);
                 }
             // the kernel's pass: every unit kind in syntax order, each on the lanes in it
@@ -1367,7 +1393,7 @@ void emu_parse(const BatchArgs &a) {
                     if (L.st != kind || (kind == U_CTU && !ctu_ready(L, P, E))) continue;
                     progressed = true;
                     ++units;
-                    const Eng G{lds[l].ctx, tab, a.rbsp, (P.bits_end + 64u) & ~3u};
+                    const Eng G{lds[l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
                     run_unit(kind, L, lds[l], P, E, G);
                 }
             }
@@ -1390,7 +1416,7 @@ void emu_parse(const BatchArgs &a) {
 // engine tables, and the WPP context staging when rows wrap
 inline size_t lanes_lds_bytes(int ppw, int lane_rows, bool ring) {
     return sizeof(LaneLds) * (size_t)(ppw * lane_rows) + sizeof(LanePic) * (size_t)ppw + 64 * sizeof(uint32_t) +
-           64 * sizeof(uint64_t) + (ring ? 64 * (size_t)CTX_PAD : 0);
+           (64 + 16) * sizeof(uint64_t) + (ring ? 64 * (size_t)CTX_PAD : 0);
 }
 
 __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
@@ -1401,7 +1427,8 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + nl);
     uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + ppw);
     uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_prog + 64);
-    uint8_t *s_wctx = a.wpp_ring ? reinterpret_cast<uint8_t *>(s_tab + 64) : nullptr;
+    uint64_t *s_seq = s_tab + 64;
+    uint8_t *s_wctx = a.wpp_ring ? reinterpret_cast<uint8_t *>(s_seq + 16) : nullptr;
     const int lane = threadIdx.x;
 #if defined(HG_PARSE_SETPRIO)
     // the parse is the latency-critical stream: win issue arbitration against
@@ -1409,6 +1436,7 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     __builtin_amdgcn_s_setprio(HG_PARSE_SETPRIO);
 #endif
     s_tab[lane] = state_row(lane);
+    if (lane < 15) s_seq[lane] = sig_seq(lane);
     const int pl = lane / a.lane_rows, row = lane % a.lane_rows;
     const int slot = (int)blockIdx.x * ppw + pl;
     const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
@@ -1422,7 +1450,7 @@ __global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
     if (!live) L.st = U_DONE;
     __syncthreads();
     const Env E{&a, s_lds, s_prog, s_wctx, lane};
-    const Eng G{ld.ctx, s_tab, a.rbsp, live ? (P.bits_end + 64u) & ~3u : 0u};
+    const Eng G{ld.ctx, s_tab, s_seq, a.rbsp, live ? (P.bits_end + 64u) & ~3u : 0u};
 #if defined(HG_PARSE_PROF)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
