@@ -42,7 +42,6 @@ struct alignas(16) IntraScratch {
     int16_t ft[132];
     int16_t ref[200];   // angular reference, index + 64
     int32_t dc;
-    uint32_t done[8];   // decoded 4x4 luma blocks of the current CTU (up to 64x64), row-major
 };
 
 // Per-wave LDS block: scratch, then per component the CTU window.
@@ -94,16 +93,23 @@ int intra_waves(int log2ctb, int chroma, int bps, int max_rows) {
 // CTU at luma (bx0, by0), size csl.  Everything in the CTU row above (up to the
 // above-right CTU, which the wavefront has finished) and in the CTU to the
 // left is decoded; the CTUs below-left and right are not; inside the CTU a
-// block is available iff it precedes the TB in z-scan order, i.e. iff it is
-// already decoded (TBs are reconstructed in decoding order), which the
-// `done` bitmap records.  Replaces the MinTbAddrZs comparison per sample.
-__device__ __forceinline__ bool nb_avail(const uint32_t *done, int xl, int yl, int bx0, int by0, int csl) {
+// block is available iff it precedes the TB in z-scan order (MinTbAddrZs of
+// 6.5.2 at 4x4 granularity: the CTU's quadtrees are decoded in z-order, so a
+// 4x4 block is decoded before the TB iff its z-index is below the z-index zc
+// of the TB's first luma 4x4 block).
+__device__ __forceinline__ int zidx(int bx, int by) {  // bits of bx, by interleaved (bx, by < 16)
+    auto spread = [](int v) {
+        v = (v | (v << 2)) & 0x33;
+        return (v | (v << 1)) & 0x55;
+    };
+    return spread(bx) | (spread(by) << 1);
+}
+__device__ __forceinline__ bool nb_avail(int zc, int xl, int yl, int bx0, int by0, int csl) {
     const int lx = xl - bx0, ly = yl - by0;
     if (ly < 0) return true;
     if (ly >= csl || lx >= csl) return false;
     if (lx < 0) return true;
-    const int idx = (ly >> 2) * (csl >> 2) + (lx >> 2);
-    return (done[idx >> 5] >> (idx & 31)) & 1u;
+    return zidx(lx >> 2, ly >> 2) < zc;
 }
 
 // One component's CTU window in LDS.
@@ -133,6 +139,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     const int bx0 = w.cx0 << sub, by0 = w.cy0 << sub, csl = w.cs << sub;
     const int ns = 4 * n + 1;
     const bool cbf = (tu.flags & TU_CBF) != 0;
+    const int zc = zidx(((x0 << sub) - bx0) >> 2, ((y0 << sub) - by0) >> 2);
     // residual of a 4x4 / 8x8 TB (one sample per lane): loaded now, used after
     // the neighbour and filter phases, so the load latency hides behind them
     const int r0 = (cbf && n <= 8 && lane < n * n) ? w.res[(size_t)(y0 + (lane >> log2n)) * PW + x0 + (lane & (n - 1))] : 0;
@@ -155,7 +162,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
                 xn = x0 + s - 2 * n - 1;
                 yn = y0 - 1;
             }
-            sa[s] = xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(L->done, xn << sub, yn << sub, bx0, by0, csl);
+            sa[s] = xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(zc, xn << sub, yn << sub, bx0, by0, csl);
             sv[s] = sa[s] ? w.fetch(xn, yn) : 0;
             any_av |= sa[s];
         }
@@ -188,7 +195,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             yn = y0 - 1;
         }
         const bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
-                        nb_avail(L->done, xn << sub, yn << sub, bx0, by0, csl);
+                        nb_avail(zc, xn << sub, yn << sub, bx0, by0, csl);
         const int val = av ? w.fetch(xn, yn) : 0;
         const uint64_t msk = __ballot(av);
         int sl = lane;
@@ -221,7 +228,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             xn = x0 + s - 2 * n - 1;
             yn = y0 - 1;
         }
-        bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(L->done, xn << sub, yn << sub, bx0, by0, csl);
+        bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(zc, xn << sub, yn << sub, bx0, by0, csl);
         val[k] = av ? w.fetch(xn, yn) : 0;
         msk[k] = __ballot(av);
     }
@@ -477,7 +484,6 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
                     }
                     (void)PH;
                 }
-                for (int i = lane; i < 8; i += kWave) S->done[i] = 0u;
                 wave_sync();
             }
             const int cidx = tu.flags & TU_CIDX_MASK;
@@ -491,15 +497,6 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
                 continue;
             predict_tb<Pel>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, log2ctb,
                             sp.log2_min_tb, wctb, lane);
-            if (cidx == 0) {  // the TB's 4x4 blocks are decoded now (a row segment never crosses a word)
-                const int nb = 1 << (tu.log2 - 2), stride = w.cs >> 2;
-                const int bx = (tu.x - w.cx0) >> 2, by = (tu.y - w.cy0) >> 2;
-                for (int i = lane; i < nb; i += kWave) {
-                    const int idx = (by + i) * stride + bx;
-                    atomicOr(&S->done[idx >> 5], ((1u << nb) - 1u) << (idx & 31));
-                }
-                wave_sync();
-            }
         }
         HG_FENCE_REL();
         hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
