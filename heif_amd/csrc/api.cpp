@@ -30,26 +30,31 @@ static_assert(sizeof(heifgpu_planes) == 40, "heifgpu_planes: 3 pointers + 3 int3
 static_assert(sizeof(heifgpu_batch_opts) == 8, "heifgpu_batch_opts: 2 x uint32");
 static_assert(sizeof(heifgpu_tile_params) == 55 * 4 + 64 * 4, "heifgpu_tile_params: 55 int32 + 64 uint32");
 
-// Pipelined decode.  k_rbsp + k_parse run on an internal parse stream and the
+// Pipelined decode.  k_rbsp + k_parse run on an internal parse stream, the
 // four reconstruction kernels on an internal recon stream.  A batch holds two
 // sets of parse outputs (TU records, coefficients, maps, SAO, per-row counts,
-// status) used by alternate decode calls, so the parse of call n + 1 (which
-// depends on nothing the caller can touch: the bitstreams are the batch's own)
-// runs while call n reconstructs.  Ordering with the caller's stream: the
-// reconstruction of a call waits for everything the caller enqueued on its
-// stream before the call (it writes the caller's planes), and the caller's
-// stream waits for that reconstruction.  A parse set is reused only after the
-// reconstruction that read it.  HEIFGPU_PIPELINE=0 keeps one set (no overlap).
+// status, residual planes) used by alternate decode calls, so the parse of
+// call n + 1 runs while call n reconstructs: neither depends on anything the
+// caller can touch (the bitstreams are the batch's own) except k_sao_out,
+// which writes the caller's planes and so waits for everything the caller
+// enqueued on its stream before the call; the caller's stream waits for
+// k_sao_out.  A set is reused only after the reconstruction that read it.
+// HEIFGPU_PIPELINE=0 keeps one set (no overlap); HEIFGPU_PIPELINE=3 uses three
+// sets and a third stream for k_transform, so parse n + 2, transform n + 1 and
+// reconstruction n overlap (A/B at 20 steps: 15.32 / 15.33 vs 15.67 / 15.64
+// Gpix/s for two streams: the parse, the critical path, slows from 88 to 93 ms
+// beside two other streams).
 constexpr int kTimingSlots = 32;
 struct heifgpu_ctx {
     int device = 0;
     bool timing = false;
-    hipStream_t parse = nullptr, recon = nullptr, upload = nullptr;
+    hipStream_t parse = nullptr, xform = nullptr, recon = nullptr, upload = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     // timing ring, one slot per timed decode call: rbsp start, rbsp end = parse
-    // start, parse end, recon start, 4 stage ends.  heifgpu_stage_times folds
-    // every call since the previous query (a slot about to be reused is folded first).
-    hipEvent_t tev[kTimingSlots][8] = {};
+    // start, parse end, transform start, transform end, recon start, 3 stage
+    // ends.  heifgpu_stage_times folds every call since the previous query (a
+    // slot about to be reused is folded first).
+    hipEvent_t tev[kTimingSlots][9] = {};
     int timed_calls = 0, folded = 0;
     double acc[6] = {};
 };
@@ -58,15 +63,17 @@ namespace {
 // adds the stage times of the decode call recorded in `slot` to ctx->acc
 hipError_t fold_timing(heifgpu_ctx *ctx, int slot) {
     hipEvent_t *e = ctx->tev[slot];
-    hipError_t r = hipEventSynchronize(e[7]);
+    hipError_t r = hipEventSynchronize(e[8]);
     if (r != hipSuccess) return r;
     float t = 0.f;
     if ((r = hipEventElapsedTime(&t, e[0], e[1])) != hipSuccess) return r;
     ctx->acc[5] += t;  // k_rbsp
     if ((r = hipEventElapsedTime(&t, e[1], e[2])) != hipSuccess) return r;
     ctx->acc[0] += t;  // k_parse
-    for (int i = 1; i < 5; ++i) {
-        if ((r = hipEventElapsedTime(&t, e[i + 2], e[i + 3])) != hipSuccess) return r;
+    if ((r = hipEventElapsedTime(&t, e[3], e[4])) != hipSuccess) return r;
+    ctx->acc[1] += t;  // k_transform
+    for (int i = 2; i < 5; ++i) {  // k_intra, k_deblock, k_sao_out
+        if ((r = hipEventElapsedTime(&t, e[i + 3], e[i + 4])) != hipSuccess) return r;
         ctx->acc[i] += t;
     }
     return hipSuccess;
@@ -148,10 +155,12 @@ struct ParseSet {
     DevBuf<uint32_t> row_counts, status;
     DevBuf<uint8_t> maps;
     DevBuf<SaoParams> sao;
-    hipEvent_t parsed = nullptr, recon_done = nullptr;
+    DevBuf<int16_t> resid;  // k_transform -> k_intra
+    hipEvent_t parsed = nullptr, transformed = nullptr, recon_done = nullptr;
     bool pending = false;  // recon_done recorded and not yet waited for by a parse
     ~ParseSet() {
         if (parsed) (void)hipEventDestroy(parsed);
+        if (transformed) (void)hipEventDestroy(transformed);
         if (recon_done) (void)hipEventDestroy(recon_done);
     }
 };
@@ -170,8 +179,7 @@ struct heifgpu_batch {
     DevBuf<uint32_t> subs, rsubs, porder;
     DevBuf<SeqParams> seqs;
     DevBuf<OutImage> outs;
-    DevBuf<int16_t> resid;
-    ParseSet set[2];
+    ParseSet set[3];
     int n_sets = 1, next_set = 0, last_set = 0;
     std::vector<OutImage> out_host;
     std::vector<uint32_t> pic_image;  // picture → image
@@ -368,6 +376,7 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     int least = 0, greatest = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIP_TRY(hipStreamCreateWithPriority(&c->parse, hipStreamNonBlocking, prio ? greatest : least));
+    HIP_TRY(hipStreamCreateWithFlags(&c->xform, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&c->recon, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&c->upload, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
@@ -388,6 +397,7 @@ void heifgpu_destroy(heifgpu_ctx *ctx) {
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->join) (void)hipEventDestroy(ctx->join);
     if (ctx->parse) (void)hipStreamDestroy(ctx->parse);
+    if (ctx->xform) (void)hipStreamDestroy(ctx->xform);
     if (ctx->recon) (void)hipStreamDestroy(ctx->recon);
     if (ctx->upload) (void)hipStreamDestroy(ctx->upload);
     delete ctx;
@@ -450,11 +460,12 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         HIP_TRY(hipEventCreateWithFlags(&b->uploaded, hipEventDisableTiming));
         static const int pipeline = [] {
             const char *e = std::getenv("HEIFGPU_PIPELINE");
-            return e ? std::atoi(e) : 1;
+            return e ? std::atoi(e) : 2;
         }();
-        b->n_sets = pipeline ? 2 : 1;
+        b->n_sets = pipeline == 0 ? 1 : (pipeline == 3 ? 3 : 2);
         for (int k = 0; k < b->n_sets; ++k) {
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].parsed, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&b->set[k].transformed, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].recon_done, hipEventDisableTiming));
         }
     }
@@ -467,7 +478,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     const bool grows = b->loaded && (hb.bits_size > b->bits.cap || hb.pics.size() > b->pics.cap ||
                                      hb.subs.size() > b->subs.cap || hb.seqs.size() > b->seqs.cap ||
                                      hb.sf.size() > b->sf.cap || n > b->outs.cap || hb.recon_bytes > b->recon.cap ||
-                                     hb.resid_elems > b->resid.cap || hb.tu_n > b->set[0].tus.cap ||
+                                     hb.resid_elems > b->set[0].resid.cap || hb.tu_n > b->set[0].tus.cap ||
                                      hb.coef_n > b->set[0].coefs.cap || hb.map_bytes > b->set[0].maps.cap ||
                                      hb.sao_n > b->set[0].sao.cap || 2 * size_t(hb.rows) > b->set[0].row_counts.cap ||
                                      hb.pics.size() > b->set[0].status.cap);
@@ -495,10 +506,10 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         HIP_TRY(ps.maps.alloc(hb.map_bytes));
         HIP_TRY(ps.sao.alloc(hb.sao_n));
         HIP_TRY(ps.status.alloc(hb.pics.size()));
+        HIP_TRY(ps.resid.alloc(hb.resid_elems));
         HIP_TRY(hipMemsetAsync(ps.status.p, 0, hb.pics.size() * sizeof(uint32_t), ctx->upload));
     }
     HIP_TRY(b->recon.alloc(hb.recon_bytes));
-    HIP_TRY(b->resid.alloc(hb.resid_elems));
     std::vector<uint32_t> order;
     lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
     HIP_TRY(b->porder.alloc(order.size()));
@@ -564,7 +575,6 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.sf = b->sf.p;
     a.outs = b->outs.p;
     a.recon = b->recon.p;
-    a.resid = b->resid.p;
     a.n_pics = b->n_pics;
     a.max_width = hb.max_w;
     a.max_wctb = hb.max_wctb;
@@ -623,6 +633,7 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     a.maps = ps.maps.p;
     a.sao = ps.sao.p;
     a.status = ps.status.p;
+    a.resid = ps.resid.p;
     // bring-up knob: HEIFGPU_STAGES=k launches only the first k stages (in order, on the caller's stream)
     static const int max_stages = [] {
         const char *e = std::getenv("HEIFGPU_STAGES");
@@ -631,6 +642,7 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     if (max_stages < 5) {
         HIP_TRY(hipStreamSynchronize(ctx->upload));
         HIP_TRY(hipStreamSynchronize(ctx->parse));
+        HIP_TRY(hipStreamSynchronize(ctx->xform));
         HIP_TRY(hipStreamSynchronize(ctx->recon));
         HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), s));
         HIP_TRY(hipMemsetAsync(ps.row_counts.p, 0, size_t(2) * uint32_t(b->args.total_rows) * sizeof(uint32_t), s));
@@ -667,19 +679,24 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     HIP_TRY(launch_parse(a, p));
     if (t) HIP_TRY(hipEventRecord(ev[2], p));
     HIP_TRY(hipEventRecord(ps.parsed, p));
-    // recon stream: after the caller's prior work and this call's parse
+    // transform stream (the recon stream with two sets): this set's parse
+    hipStream_t x = b->n_sets >= 3 ? ctx->xform : r;
+    HIP_TRY(hipStreamWaitEvent(x, ps.parsed, 0));
+    if (t) HIP_TRY(hipEventRecord(ev[3], x));
+    HIP_TRY(launch_transform(a, x));
+    if (t) HIP_TRY(hipEventRecord(ev[4], x));
+    HIP_TRY(hipEventRecord(ps.transformed, x));
+    // recon stream: this set's transform, and the caller's prior work before the planes are written
     HIP_TRY(hipEventRecord(ctx->fork, s));
-    HIP_TRY(hipStreamWaitEvent(r, ctx->fork, 0));
-    HIP_TRY(hipStreamWaitEvent(r, ps.parsed, 0));
-    if (t) HIP_TRY(hipEventRecord(ev[3], r));
-    HIP_TRY(launch_transform(a, r));
-    if (t) HIP_TRY(hipEventRecord(ev[4], r));
-    HIP_TRY(launch_intra(a, r));
+    HIP_TRY(hipStreamWaitEvent(r, ps.transformed, 0));
     if (t) HIP_TRY(hipEventRecord(ev[5], r));
-    HIP_TRY(launch_deblock(a, r));
+    HIP_TRY(launch_intra(a, r));
     if (t) HIP_TRY(hipEventRecord(ev[6], r));
-    HIP_TRY(launch_sao_out(a, r));
+    HIP_TRY(launch_deblock(a, r));
     if (t) HIP_TRY(hipEventRecord(ev[7], r));
+    HIP_TRY(hipStreamWaitEvent(r, ctx->fork, 0));
+    HIP_TRY(launch_sao_out(a, r));
+    if (t) HIP_TRY(hipEventRecord(ev[8], r));
     HIP_TRY(hipEventRecord(ps.recon_done, r));
     ps.pending = true;
     HIP_TRY(hipEventRecord(ctx->join, r));
