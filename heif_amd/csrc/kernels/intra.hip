@@ -36,11 +36,14 @@ __constant__ int16_t c_inv_angle[35] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -4096, 
                                         -256, -315, -390, -482, -630, -910, -1638, -4096, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
 struct alignas(16) IntraScratch {
-    int16_t left[132];  // [0] = p[-1][-1], [1+y] = p[-1][y]
-    int16_t top[132];   // [0] = p[-1][-1], [1+x] = p[x][-1]
-    int16_t fl[132];
-    int16_t ft[132];
-    int16_t ref[200];   // angular reference, index + 64
+    // TBs are at most 32x32 (MaxTbLog2SizeY <= 5): 2n + 1 <= 65 reference samples
+    // per side.  Sized to that, not to the CTB, so more workgroups fit beside the
+    // next decode's k_parse_lanes (which holds ~120 KB of each CU's LDS).
+    int16_t left[66];  // [0] = p[-1][-1], [1+y] = p[-1][y]
+    int16_t top[66];   // [0] = p[-1][-1], [1+x] = p[x][-1]
+    int16_t fl[66];
+    int16_t ft[66];
+    int16_t ref[100];  // angular reference ref[-32 .. 65], index + 32
     int32_t dc;
 };
 
@@ -321,7 +324,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         wave_sync();
     } else if (mode >= 2) {
         const int ang = c_angle[mode];
-        int16_t *ref = L->ref + 64;
+        int16_t *ref = L->ref + 32;
         const int16_t *main_ = mode >= 18 ? tp : lf;
         const int16_t *side = mode >= 18 ? lf : tp;
         for (int i = lane; i <= 2 * n; i += kWave) {
@@ -353,7 +356,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             }
         } else {
             const int ang = c_angle[mode];
-            const int16_t *ref = L->ref + 64;
+            const int16_t *ref = L->ref + 32;
             const int a = mode >= 18 ? x : y, b = mode >= 18 ? y : x;  // a along the main direction
             const int idx = ((b + 1) * ang) >> 5, fact = ((b + 1) * ang) & 31;
             pv = fact ? ((32 - fact) * ref[a + idx + 1] + fact * ref[a + idx + 2] + 16) >> 5 : ref[a + idx + 1];
