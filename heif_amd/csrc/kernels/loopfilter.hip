@@ -163,7 +163,38 @@ __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
     }
 }
 
-// SAO + crop + grid placement: one thread per output sample
+// SAO (8.7.3) of one sample at picture position (xs, ys) of component cidx
+template <typename Pel>
+__device__ __forceinline__ int sao_sample(const Pel *P, int PW, int PH, int xs, int ys, int cidx, int sub,
+                                          const SaoParams *sao, int wctb, int log2ctb, const uint8_t *flg, int w4,
+                                          int bd) {
+    int v = P[(size_t)ys * PW + xs];
+    const SaoParams &s = sao[(ys >> (log2ctb - sub)) * wctb + (xs >> (log2ctb - sub))];
+    const int type = s.type[cidx];
+    if (!type || (flg[((ys << sub) >> 2) * w4 + ((xs << sub) >> 2)] & MF_NOFILT)) return v;
+    int o = 0;
+    if (type == 2) {
+        const int cl = s.band_eo[cidx];
+        const int hx = cl == 0 ? 1 : (cl == 1 ? 0 : (cl == 2 ? 1 : -1));
+        const int vy = cl == 0 ? 0 : 1;
+        const int ax = xs - hx, ay = ys - vy, bx = xs + hx, by = ys + vy;
+        if (ax >= 0 && ay >= 0 && ax < PW && ay < PH && bx >= 0 && by >= 0 && bx < PW && by < PH) {
+            const int na = P[(size_t)ay * PW + ax], nb = P[(size_t)by * PW + bx];
+            int e = 2 + (v > na) - (v < na) + (v > nb) - (v < nb);
+            if (e <= 2) e = e == 2 ? 0 : e + 1;
+            o = e ? s.off[cidx][e - 1] : 0;
+        }
+    } else {
+        const int band = v >> (bd - 5);
+        const int k = (band - s.band_eo[cidx]) & 31;
+        o = k < 4 ? s.off[cidx][k] : 0;
+    }
+    return clip3(0, (1 << bd) - 1, v + o);
+}
+
+// SAO + crop + grid placement: one thread per four consecutive output samples
+// of a row (one 4- or 8-byte store; per sample at a row's ragged end or an
+// unaligned caller plane)
 template <typename Pel>
 __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
     const int pic = a.pic0 + blockIdx.y;
@@ -181,60 +212,53 @@ __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
     const int vw = min(sp.out_w, oi.width - pd.out_x), vh = min(sp.out_h, oi.height - pd.out_y);
     if (vw <= 0 || vh <= 0) return;
     const int vcw = sp.chroma_format ? (vw + 1) >> 1 : 0, vch = sp.chroma_format ? (vh + 1) >> 1 : 0;
-    const int nl = vw * vh, nc = vcw * vch;
+    const int qw = (vw + 3) >> 2, qcw = (vcw + 3) >> 2;  // quads per row
+    const int nl = qw * vh, nc = qcw * vch;
     const int total = nl + 2 * nc;
-    const bool any_sao = pd.sao_luma || pd.sao_chroma;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
-        int cidx, x, y, PW, PH, sub;
+        int cidx, q, y;
         if (t < nl) {
             cidx = 0;
-            x = t % vw;
-            y = t / vw;
+            q = t % qw;
+            y = t / qw;
         } else {
             const int u = t - nl;
             cidx = 1 + u / nc;
-            x = (u % nc) % vcw;
-            y = (u % nc) / vcw;
+            q = (u % nc) % qcw;
+            y = (u % nc) / qcw;
         }
-        sub = cidx ? 1 : 0;
-        PW = cidx ? cw : W;
-        PH = cidx ? ch : H;
+        const int sub = cidx ? 1 : 0;
+        const int PW = cidx ? cw : W, PH = cidx ? ch : H;
+        const int vwc = cidx ? vcw : vw;
         const Pel *P = cidx == 0 ? Y : Y + (size_t)W * H + (size_t)(cidx - 1) * cw * ch;
-        const int xs = x + (sp.conf_l >> sub), ys = y + (sp.conf_t >> sub);  // picture coords
-        int v = P[(size_t)ys * PW + xs];
-        if (any_sao) {
-            const SaoParams &s = sao[(ys >> (log2ctb - sub)) * wctb + (xs >> (log2ctb - sub))];
-            const int type = s.type[cidx];
-            const bool nof = flg[((ys << sub) >> 2) * w4 + ((xs << sub) >> 2)] & MF_NOFILT;
-            if (type && !nof) {
-                const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
-                int o = 0;
-                if (type == 2) {
-                    const int cl = s.band_eo[cidx];
-                    const int hx = cl == 0 ? 1 : (cl == 1 ? 0 : (cl == 2 ? 1 : -1));
-                    const int vy = cl == 0 ? 0 : 1;
-                    const int ax = xs - hx, ay = ys - vy, bx = xs + hx, by = ys + vy;
-                    if (ax >= 0 && ay >= 0 && ax < PW && ay < PH && bx >= 0 && by >= 0 && bx < PW && by < PH) {
-                        const int na = P[(size_t)ay * PW + ax], nb = P[(size_t)by * PW + bx];
-                        int e = 2 + (v > na) - (v < na) + (v > nb) - (v < nb);
-                        if (e <= 2) e = e == 2 ? 0 : e + 1;
-                        o = e ? s.off[cidx][e - 1] : 0;
-                    }
-                } else {
-                    const int band = v >> (bd - 5);
-                    const int k = (band - s.band_eo[cidx]) & 31;
-                    o = k < 4 ? s.off[cidx][k] : 0;
-                }
-                v = clip3(0, (1 << bd) - 1, v + o);
-            }
+        const int x0 = q * 4, n = min(4, vwc - x0);
+        const int ys = y + (sp.conf_t >> sub), xs0 = x0 + (sp.conf_l >> sub);  // picture coords
+        const bool on = pd.sao_luma || pd.sao_chroma;  // SaoTypeIdx is 0 for a component whose flag is off
+        const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
+        int v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            v[j] = 0;
+            if (j < n)
+                v[j] = on ? sao_sample(P, PW, PH, xs0 + j, ys, cidx, sub, sao, wctb, log2ctb, flg, w4, bd)
+                          : (int)P[(size_t)ys * PW + xs0 + j];
         }
-        const int ox = (pd.out_x >> sub) + x, oy = (pd.out_y >> sub) + y;
         // component fields by select: a lane-varying index into the OutImage copy made
         // the compiler keep it in LDS (12 KB per workgroup, 519 M bank-conflict cycles per launch)
         const uint64_t plane = cidx == 0 ? oi.plane[0] : (cidx == 1 ? oi.plane[1] : oi.plane[2]);
         const int pitch = cidx == 0 ? oi.pitch[0] : (cidx == 1 ? oi.pitch[1] : oi.pitch[2]);
+        const int ox = (pd.out_x >> sub) + x0, oy = (pd.out_y >> sub) + y;
         Pel *dst = reinterpret_cast<Pel *>(plane + (size_t)oy * pitch) + ox;
-        *dst = (Pel)v;
+        if (n == 4 && (reinterpret_cast<uintptr_t>(dst) & (4 * sizeof(Pel) - 1)) == 0) {
+            if (sizeof(Pel) == 1)
+                *reinterpret_cast<uint32_t *>(dst) = (uint32_t)v[0] | (uint32_t)v[1] << 8 | (uint32_t)v[2] << 16 |
+                                                     (uint32_t)v[3] << 24;
+            else
+                *reinterpret_cast<uint64_t *>(dst) = (uint64_t)v[0] | (uint64_t)v[1] << 16 | (uint64_t)v[2] << 32 |
+                                                     (uint64_t)v[3] << 48;
+        } else {
+            for (int j = 0; j < n; ++j) dst[j] = (Pel)v[j];
+        }
     }
 }
 
