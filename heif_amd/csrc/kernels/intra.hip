@@ -43,8 +43,6 @@ struct alignas(16) IntraScratch {
     int16_t top[66];   // [0] = p[-1][-1], [1+x] = p[x][-1]
     int16_t fl[66];
     int16_t ft[66];
-    int16_t ref[100];  // angular reference ref[-32 .. 65], index + 32
-    int32_t dc;
 };
 
 // Per-wave LDS block: scratch, then per component the CTU window.
@@ -89,6 +87,35 @@ int intra_waves(int log2ctb, int chroma, int bps, int max_rows) {
     return nw < 1 ? 1 : nw;
 }
 
+// Bottom-row line buffers in LDS: the wave of CTB row r leaves each finished
+// CTU's bottom sample row in line buffer r % nbuf (nbuf = max(waves, 2)), and
+// row r + 1 reads its above / above-right neighbours from there instead of
+// re-reading the picture in HBM after every progress wait.  The buffer is
+// only overwritten by row r + nbuf, whose progress wait (transitively through
+// rows r + 1 ..) puts row r + 1 past every CTU that reads the overwritten
+// samples.  Luma at 0, Cb at max_width, Cr at max_width + ceil(max_width / 2).
+#if defined(HG_HOST_EMU)
+inline
+#else
+__host__ __device__ inline
+#endif
+uint32_t intra_line_bytes(int max_width, int bps) {
+    return ((uint32_t)(max_width + 2 * ((max_width + 1) >> 1)) * (uint32_t)bps + 15u) & ~15u;
+}
+#if defined(HG_HOST_EMU)
+inline
+#else
+__host__ __device__ inline
+#endif
+bool intra_use_lines(int nw, uint32_t block_bytes, uint32_t line_bytes) {
+#if defined(HG_INTRA_NO_LINE)
+    return false;
+#else
+    const uint32_t nbuf = nw < 2 ? 2u : (uint32_t)nw;
+    return 64u + (uint32_t)nw * block_bytes + nbuf * line_bytes <= (uint32_t)kIntraLdsBudget;
+#endif
+}
+
 #define wave_sync() HG_WAVE_SYNC()
 
 
@@ -114,6 +141,27 @@ __device__ __forceinline__ bool nb_avail(int zc, int xl, int yl, int bx0, int by
     if (lx < 0) return true;
     return zidx(lx >> 2, ly >> 2) < zc;
 }
+
+// ref[k] of 8.4.4.2.6 read in place: the main-side neighbour for k >= 0, the
+// projected side-side neighbour for k < 0 (only reached when
+// (nTbS * intraPredAngle) >> 5 < -1, exactly where the spec extends ref)
+__device__ __forceinline__ const int16_t *ang_ref(const int16_t *main_, const int16_t *side, int inv, int k) {
+    return k >= 0 ? main_ + k : side + ((k * inv + 128) >> 8);
+}
+
+// four samples as one store unit
+template <typename Pel>
+struct QuadT;
+template <>
+struct QuadT<uint8_t> {
+    using type = uint32_t;
+};
+template <>
+struct QuadT<uint16_t> {
+    using type = uint64_t;
+};
+template <typename Pel>
+using Quad = typename QuadT<Pel>::type;
 
 // One component's CTU window in LDS.
 template <typename Pel>
@@ -216,9 +264,11 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             L->top[s - 2 * n] = (int16_t)v;
         }
     } else {
-    int val[3];
-    uint64_t msk[3];
-    for (int k = 0; k < 3; ++k) {
+    // 16x16 (65 samples) needs two chunks, 32x32 (129) three
+    const int nch = ns <= 128 ? 2 : 3;
+    int val[3] = {0, 0, 0};
+    uint64_t msk[3] = {0, 0, 0};
+    for (int k = 0; k < nch; ++k) {
         const int s = lane + 64 * k;
         int xn, yn;
         if (s < 2 * n) {
@@ -237,7 +287,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     }
     // 2. substitution: nearest available predecessor in search order, else the first available
     const bool any = (msk[0] | msk[1] | msk[2]) != 0;
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < nch; ++k) {
         const int s = lane + 64 * k;
         int sc = k, sl = lane;  // source (chunk, lane) of this sample's value
         if (any && !((msk[k] >> lane) & 1)) {
@@ -262,7 +312,8 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             }
         }
         // all lanes active for the cross-lane reads
-        const int v0 = __shfl(val[0], sl, 64), v1 = __shfl(val[1], sl, 64), v2 = __shfl(val[2], sl, 64);
+        const int v0 = __shfl(val[0], sl, 64), v1 = __shfl(val[1], sl, 64);
+        const int v2 = nch > 2 ? __shfl(val[2], sl, 64) : 0;
         const int v = !any ? (1 << (bd - 1)) : (sc == 0 ? v0 : (sc == 1 ? v1 : v2));
         if (s < 2 * n) L->left[2 * n - s] = (int16_t)v;
         else if (s == 2 * n) {
@@ -314,32 +365,15 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     }
     const int maxv = (1 << bd) - 1;
     // 4. prediction (+ residual)
-    if (mode == 1) {  // DC: wave reduction of the 2n references
+    int dc = 0;
+    if (mode == 1) {  // DC: wave reduction of the 2n references (every lane ends with the sum)
         int sum = 0;
         for (int i = lane; i < 2 * n; i += kWave) sum += i < n ? tp[1 + i] : lf[1 + i - n];
 #if !defined(HG_HOST_EMU)
         for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
 #endif
-        L->dc = (sum + n) >> (log2n + 1);
-        wave_sync();
-    } else if (mode >= 2) {
-        const int ang = c_angle[mode];
-        int16_t *ref = L->ref + 32;
-        const int16_t *main_ = mode >= 18 ? tp : lf;
-        const int16_t *side = mode >= 18 ? lf : tp;
-        for (int i = lane; i <= 2 * n; i += kWave) {
-            if (i <= n || ang >= 0) ref[i] = main_[i];
-        }
-        if (ang < 0) {
-            const int lo = (n * ang) >> 5;
-            if (lo < -1) {
-                const int inv = c_inv_angle[mode];
-                for (int xx = lo + lane; xx <= -1; xx += kWave) ref[xx] = side[(xx * inv + 128) >> 8];
-            }
-        }
-        wave_sync();
+        dc = (sum + n) >> (log2n + 1);
     }
-    const int dc = mode == 1 ? L->dc : 0;
     const int lx0 = x0 - w.cx0, ly0 = y0 - w.cy0;
     for (int o = lane; o < n * n; o += kWave) {
         const int x = o & (n - 1), y = o >> log2n;
@@ -355,11 +389,12 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
                 else if (x == 0) pv = (lf[1 + y] + 3 * dc + 2) >> 2;
             }
         } else {
-            const int ang = c_angle[mode];
-            const int16_t *ref = L->ref + 32;
+            const int ang = c_angle[mode], inv = c_inv_angle[mode];
+            const int16_t *main_ = mode >= 18 ? tp : lf, *side = mode >= 18 ? lf : tp;
             const int a = mode >= 18 ? x : y, b = mode >= 18 ? y : x;  // a along the main direction
             const int idx = ((b + 1) * ang) >> 5, fact = ((b + 1) * ang) & 31;
-            pv = fact ? ((32 - fact) * ref[a + idx + 1] + fact * ref[a + idx + 2] + 16) >> 5 : ref[a + idx + 1];
+            const int p0 = *ang_ref(main_, side, inv, a + idx + 1);
+            pv = fact ? ((32 - fact) * p0 + fact * *ang_ref(main_, side, inv, a + idx + 2) + 16) >> 5 : p0;
             if (cidx == 0 && n < 32) {
                 if (mode == 26 && x == 0) pv = min(max(tp[1] + ((lf[1 + y] - lf[0]) >> 1), 0), maxv);
                 if (mode == 10 && y == 0) pv = min(max(lf[1] + ((tp[1 + x] - tp[0]) >> 1), 0), maxv);
@@ -373,10 +408,142 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     wave_sync();
 }
 
+#if !defined(HG_HOST_EMU)
+// The Cb and Cr TBs of one 4:2:0 chroma TU (n = 4 or 8) in one pass: lanes
+// 0-31 predict Cb, lanes 32-63 Cr.  The two TBs share position, size,
+// IntraPredModeC and neighbour availability, and chroma has no reference
+// filtering (8.4.4.2.3) and no DC / angular edge filters (8.4.4.2.6, cIdx 0
+// only), so each step of predict_tb runs once for both: 4n + 1 <= 33
+// neighbours per half (a second chunk for the 33rd of an 8x8), a 32-lane DC
+// reduction, and n * n <= 64 samples in two rounds of 32.  Scratch halves:
+// left / top at + 33 * h.
+template <typename Pel>
+__device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch *L, const TuRec &tb, const TuRec &tr,
+                                                                   const Win<Pel> &wb, const Win<Pel> &wr, int PW,
+                                                                   int PH, int bd, int lane) {
+    const int log2n = tb.log2, n = 1 << log2n, mode = tb.mode;
+    const int x0 = tb.x, y0 = tb.y;
+    const int h = lane >> 5, sl = lane & 31;
+    // per-field selects (a lane-dependent reference into the caller's win[] would put it in scratch)
+    Win<Pel> w;
+    w.cur = h ? wr.cur : wb.cur;
+    w.left = h ? wr.left : wb.left;
+    w.above = h ? wr.above : wb.above;
+    w.res = h ? wr.res : wb.res;
+    w.cs = wb.cs;
+    w.cx0 = wb.cx0;
+    w.cy0 = wb.cy0;
+    const bool cbf = ((h ? tr.flags : tb.flags) & TU_CBF) != 0;
+    const int bx0 = w.cx0 << 1, by0 = w.cy0 << 1, csl = w.cs << 1;
+    const int ns = 4 * n + 1, nch = n == 8 ? 2 : 1;
+    const int zc = zidx(((x0 << 1) - bx0) >> 2, ((y0 << 1) - by0) >> 2);
+    // residuals (sample sl and sl + 32 of this half), used after the neighbour phase
+    int r0 = 0, r1 = 0;
+    if (cbf && sl < n * n) r0 = w.res[(size_t)(y0 + (sl >> log2n)) * PW + x0 + (sl & (n - 1))];
+    if (cbf && sl + 32 < n * n) r1 = w.res[(size_t)(y0 + ((sl + 32) >> log2n)) * PW + x0 + ((sl + 32) & (n - 1))];
+    int16_t *left = L->left + 33 * h, *top = L->top + 33 * h;
+    // 1. neighbours in search order (8.4.4.2.2), chunk k = search positions sl + 32 k
+    int val[2] = {0, 0};
+    uint32_t hm[2] = {0, 0};
+    for (int k = 0; k < nch; ++k) {
+        const int s = sl + 32 * k;
+        int xn, yn;
+        if (s < 2 * n) {
+            xn = x0 - 1;
+            yn = y0 + 2 * n - 1 - s;
+        } else if (s == 2 * n) {
+            xn = x0 - 1;
+            yn = y0 - 1;
+        } else {
+            xn = x0 + s - 2 * n - 1;
+            yn = y0 - 1;
+        }
+        const bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
+                        nb_avail(zc, xn << 1, yn << 1, bx0, by0, csl);
+        val[k] = av ? w.fetch(xn, yn) : 0;
+        hm[k] = (uint32_t)(__ballot(av) >> (32 * h));
+    }
+    // 2. substitution: nearest available predecessor, else the first available
+    const bool any = (hm[0] | hm[1]) != 0;
+    for (int k = 0; k < nch; ++k) {
+        const int s = sl + 32 * k;
+        int sc = k, src = sl;
+        if (any && !((hm[k] >> sl) & 1u)) {
+            const uint32_t below = hm[k] & ((1u << sl) - 1u);
+            if (below) {
+                src = 31 - __builtin_clz(below);
+            } else if (k == 1 && hm[0]) {
+                sc = 0;
+                src = 31 - __builtin_clz(hm[0]);
+            } else {
+                sc = hm[0] ? 0 : 1;
+                src = __builtin_ctz(hm[sc]);
+            }
+        }
+        const int v0 = __shfl(val[0], 32 * h + src, 64);
+        const int v1 = nch > 1 ? __shfl(val[1], 32 * h + src, 64) : 0;
+        const int v = !any ? (1 << (bd - 1)) : (sc == 0 ? v0 : v1);
+        if (s < 2 * n) left[2 * n - s] = (int16_t)v;
+        else if (s == 2 * n) {
+            left[0] = (int16_t)v;
+            top[0] = (int16_t)v;
+        } else if (s < ns) {
+            top[s - 2 * n] = (int16_t)v;
+        }
+    }
+    wave_sync();
+    const int16_t *lf = left, *tp = top;
+    const int maxv = (1 << bd) - 1;
+    int dc = 0;
+    const int ang = c_angle[mode], inv = c_inv_angle[mode];
+    const int16_t *main_ = mode >= 18 ? tp : lf, *side = mode >= 18 ? lf : tp;
+    if (mode == 1) {
+        int sum = sl < 2 * n ? (sl < n ? tp[1 + sl] : lf[1 + sl - n]) : 0;
+        for (int off = 16; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+        dc = (sum + n) >> (log2n + 1);
+    }
+    const int lx0 = x0 - w.cx0, ly0 = y0 - w.cy0;
+    for (int it = 0; it < nch; ++it) {
+        const int o = sl + 32 * it;
+        if (o < n * n) {
+            const int x = o & (n - 1), y = o >> log2n;
+            int pv;
+            if (mode == 0) {
+                pv = ((n - 1 - x) * lf[1 + y] + (x + 1) * tp[1 + n] + (n - 1 - y) * tp[1 + x] + (y + 1) * lf[1 + n] +
+                      n) >> (log2n + 1);
+            } else if (mode == 1) {
+                pv = dc;
+            } else {
+                const int a = mode >= 18 ? x : y, b = mode >= 18 ? y : x;
+                const int idx = ((b + 1) * ang) >> 5, fact = ((b + 1) * ang) & 31;
+                const int p0 = *ang_ref(main_, side, inv, a + idx + 1);
+                pv = fact ? ((32 - fact) * p0 + fact * *ang_ref(main_, side, inv, a + idx + 2) + 16) >> 5 : p0;
+            }
+            if (cbf) pv += it ? r1 : r0;
+            pv = min(max(pv, 0), maxv);
+            w.cur[(ly0 + y) * w.cs + lx0 + x] = (Pel)pv;
+        }
+    }
+    wave_sync();
+}
+#endif
+
 }  // namespace
 
+// Register budget: at 7 waves per SIMD (<= 72 VGPRs) more reconstruction waves
+// fit beside the next decode's k_parse_lanes (176 VGPRs per wave) than at the
+// compiler's own 84; 8 (64 VGPRs) and the unconstrained build measured slower
+// (DESIGN.md section 5).  HG_INTRA_WPE=0 leaves it to the compiler.
+#ifndef HG_INTRA_WPE
+#define HG_INTRA_WPE 7
+#endif
+#if HG_INTRA_WPE > 0
+#define HG_INTRA_ATTR __attribute__((amdgpu_waves_per_eu(HG_INTRA_WPE)))
+#else
+#define HG_INTRA_ATTR
+#endif
 template <typename Pel>
-__global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
+__global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArgs a) {
 #if defined(HG_HOST_EMU)
     unsigned char *smem = g_emu.smem;
 #else
@@ -411,6 +578,17 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
         win[k].res = resp[k];
         win[k].cs = lay.cs[k];
     }
+    // sized as intra_lds_bytes sizes the launch (largest CTB of the batch, chroma present)
+    const uint32_t launch_block = win_layout(a.max_log2ctb, 1, (int)sizeof(Pel)).bytes;
+    const uint32_t line_bytes = intra_line_bytes(a.max_width, (int)sizeof(Pel));
+    const bool lines = intra_use_lines(nw, launch_block, line_bytes);
+    const int nbuf = nw < 2 ? 2 : nw, cwmax = (a.max_width + 1) >> 1;
+    unsigned char *line0 = smem + 64 + (size_t)nw * launch_block;
+    // component k of the line buffer of CTB row `row`
+    auto line_of = [&](int row, int k) -> Pel * {
+        return reinterpret_cast<Pel *>(line0 + (size_t)(row % nbuf) * line_bytes) +
+               (k == 0 ? 0 : (k == 1 ? a.max_width : a.max_width + cwmax));
+    };
     progress[wave] = 0;  // every lane writes the same value
     __syncthreads();
     const uint32_t stride = (uint32_t)wctb + 1;
@@ -447,15 +625,31 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
             if (c != cur) {
                 if (cur >= 0) {
                     // finish CTU `cur`: write the window back, keep its last column as `left`
-                    for (int k = 0; k < ncomp; ++k) {
+                    _Pragma("unroll") for (int k = 0; k < 3; ++k) {
+                        if (k >= ncomp) break;
                         const Win<Pel> &w = win[k];
                         const int PW = k ? cw : W, PH = k ? ch : H;
                         const int vw = min(w.cs, PW - w.cx0), vh = min(w.cs, PH - w.cy0);
-                        for (int o = lane; o < vw * vh; o += kWave) {
-                            const int x = o % vw, y = o / vw;
-                            planes[k][(size_t)(w.cy0 + y) * PW + w.cx0 + x] = w.cur[y * w.cs + x];
+                        if (vw == w.cs && !(PW & 3) &&
+                            !(reinterpret_cast<uintptr_t>(planes[k]) & (4 * sizeof(Pel) - 1))) {
+                            // full-width CTU: four samples per lane, one 4- (8-) byte store
+                            const int lq = __builtin_ctz((unsigned)w.cs) - 2;
+                            for (int o = lane; o < (vh << lq); o += kWave) {
+                                const int x = (o & ((1 << lq) - 1)) << 2, y = o >> lq;
+                                *reinterpret_cast<Quad<Pel> *>(planes[k] + (size_t)(w.cy0 + y) * PW + w.cx0 + x) =
+                                    *reinterpret_cast<const Quad<Pel> *>(w.cur + y * w.cs + x);
+                            }
+                        } else {
+                            for (int o = lane; o < vw * vh; o += kWave) {
+                                const int x = o % vw, y = o / vw;
+                                planes[k][(size_t)(w.cy0 + y) * PW + w.cx0 + x] = w.cur[y * w.cs + x];
+                            }
                         }
                         for (int y = lane; y < w.cs; y += kWave) w.left[y] = w.cur[y * w.cs + w.cs - 1];
+                        if (lines && r + 1 < hctb) {  // a row below exists, so this CTU is full height
+                            Pel *lw = line_of(r, k) + w.cx0;
+                            for (int x = lane; x < vw; x += kWave) lw[x] = w.cur[(w.cs - 1) * w.cs + x];
+                        }
                     }
                     wave_sync();
                     HG_FENCE_REL();
@@ -475,12 +669,18 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
                     HG_FENCE_ACQ();
                 }
                 // start CTU c: the row above (corner .. above-right) and the residuals
-                for (int k = 0; k < ncomp; ++k) {
+                _Pragma("unroll") for (int k = 0; k < 3; ++k) {
+                    if (k >= ncomp) break;
                     Win<Pel> &w = win[k];
                     const int PW = k ? cw : W, PH = k ? ch : H;
                     w.cx0 = c * w.cs;
                     w.cy0 = r * w.cs;
                     const int yg = w.cy0 - 1;
+                    if (lines) {
+                        // fetch() reads above[xn - cx0 + 1] only for available (decoded) xn
+                        w.above = line_of(r - 1 < 0 ? 0 : r - 1, k) + w.cx0 - 1;
+                        continue;
+                    }
                     for (int i = lane; i <= 2 * w.cs; i += kWave) {
                         const int xg = w.cx0 - 1 + i;
                         w.above[i] = (yg >= 0 && xg >= 0 && xg < PW) ? planes[k][(size_t)yg * PW + xg] : (Pel)0;
@@ -491,13 +691,41 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra(BatchArgs a) {
             }
             const int cidx = tu.flags & TU_CIDX_MASK;
             if (cidx >= ncomp) continue;
-            const Win<Pel> &w = win[cidx];
+            // field-wise selects on the wave-uniform cidx: indexing win[] with it (or
+            // selecting one of its elements by reference) keeps the array in scratch memory
+            Win<Pel> w;
+            w.cur = cidx == 0 ? win[0].cur : (cidx == 1 ? win[1].cur : win[2].cur);
+            w.left = cidx == 0 ? win[0].left : (cidx == 1 ? win[1].left : win[2].left);
+            w.above = cidx == 0 ? win[0].above : (cidx == 1 ? win[1].above : win[2].above);
+            w.res = cidx == 0 ? win[0].res : (cidx == 1 ? win[1].res : win[2].res);
+            w.cs = cidx == 0 ? win[0].cs : (cidx == 1 ? win[1].cs : win[2].cs);
+            w.cx0 = cidx == 0 ? win[0].cx0 : (cidx == 1 ? win[1].cx0 : win[2].cx0);
+            w.cy0 = cidx == 0 ? win[0].cy0 : (cidx == 1 ? win[1].cy0 : win[2].cy0);
             const int PW = cidx ? cw : W, PH = cidx ? ch : H;
             // a TB must lie inside the picture and inside its CTU window
             if (tu.log2 < 2 || tu.log2 > 5 || tu.x + (1 << tu.log2) > PW || tu.y + (1 << tu.log2) > PH ||
                 tu.x < w.cx0 || tu.y < w.cy0 || tu.x + (1 << tu.log2) > w.cx0 + w.cs ||
                 tu.y + (1 << tu.log2) > w.cy0 + w.cs)
                 continue;
+#if !defined(HG_HOST_EMU) && !defined(HG_INTRA_NO_PAIR)
+            // a 4x4 / 8x8 Cb TB followed by its Cr TB (same TU; the next record of this 64-record block):
+            // both in one pass
+            if (cidx == 1 && chroma == 1 && tu.log2 <= 3 && t + 1 < ntu && ((t + 1) & 63u) != 0) {
+                const int sel = (int)(t + 1 - t0);
+                const uint4 r = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)tblk.x, sel),
+                                           (uint32_t)__builtin_amdgcn_readlane((int)tblk.y, sel),
+                                           (uint32_t)__builtin_amdgcn_readlane((int)tblk.z, sel),
+                                           (uint32_t)__builtin_amdgcn_readlane((int)tblk.w, sel));
+                TuRec tr;
+                __builtin_memcpy(&tr, &r, sizeof(tr));
+                if ((tr.flags & TU_CIDX_MASK) == 2 && tr.x == tu.x && tr.y == tu.y && tr.log2 == tu.log2 &&
+                    tr.mode == tu.mode && tr.ctu == tu.ctu) {
+                    predict_pair<Pel>(S, tu, tr, win[1], win[2], PW, PH, sp.bit_depth_c, lane);
+                    ++t;
+                    continue;
+                }
+            }
+#endif
             predict_tb<Pel>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, log2ctb,
                             sp.log2_min_tb, wctb, lane);
         }
@@ -526,7 +754,9 @@ static int intra_launch_waves(const BatchArgs &a) {
 }
 
 static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
-    return 64 + (size_t)nw * win_layout(a.max_log2ctb, 1, a.bytes_per_sample).bytes;
+    const uint32_t block = win_layout(a.max_log2ctb, 1, a.bytes_per_sample).bytes;
+    const uint32_t line = intra_line_bytes(a.max_width, a.bytes_per_sample);
+    return 64 + (size_t)nw * block + (intra_use_lines(nw, block, line) ? (size_t)(nw < 2 ? 2 : nw) * line : 0);
 }
 
 #if defined(HG_HOST_EMU)

@@ -1419,7 +1419,12 @@ inline size_t lanes_lds_bytes(int ppw, int lane_rows, bool ring) {
            (64 + 16) * sizeof(uint64_t) + (ring ? 64 * (size_t)CTX_PAD : 0);
 }
 
-__global__ void __launch_bounds__(64) k_parse_lanes(BatchArgs a) {
+#if defined(HG_PARSE_WPE)
+#define HG_PARSE_ATTR __attribute__((amdgpu_waves_per_eu(HG_PARSE_WPE)))
+#else
+#define HG_PARSE_ATTR
+#endif
+__global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ppw = a.parse_group;  // pictures per wave (launch_parse)
     const int nl = ppw * a.lane_rows;
