@@ -87,35 +87,6 @@ int intra_waves(int log2ctb, int chroma, int bps, int max_rows) {
     return nw < 1 ? 1 : nw;
 }
 
-// Bottom-row line buffers in LDS: the wave of CTB row r leaves each finished
-// CTU's bottom sample row in line buffer r % nbuf (nbuf = max(waves, 2)), and
-// row r + 1 reads its above / above-right neighbours from there instead of
-// re-reading the picture in HBM after every progress wait.  The buffer is
-// only overwritten by row r + nbuf, whose progress wait (transitively through
-// rows r + 1 ..) puts row r + 1 past every CTU that reads the overwritten
-// samples.  Luma at 0, Cb at max_width, Cr at max_width + ceil(max_width / 2).
-#if defined(HG_HOST_EMU)
-inline
-#else
-__host__ __device__ inline
-#endif
-uint32_t intra_line_bytes(int max_width, int bps) {
-    return ((uint32_t)(max_width + 2 * ((max_width + 1) >> 1)) * (uint32_t)bps + 15u) & ~15u;
-}
-#if defined(HG_HOST_EMU)
-inline
-#else
-__host__ __device__ inline
-#endif
-bool intra_use_lines(int nw, uint32_t block_bytes, uint32_t line_bytes) {
-#if defined(HG_INTRA_NO_LINE)
-    return false;
-#else
-    const uint32_t nbuf = nw < 2 ? 2u : (uint32_t)nw;
-    return 64u + (uint32_t)nw * block_bytes + nbuf * line_bytes <= (uint32_t)kIntraLdsBudget;
-#endif
-}
-
 #define wave_sync() HG_WAVE_SYNC()
 
 
@@ -578,17 +549,6 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
         win[k].res = resp[k];
         win[k].cs = lay.cs[k];
     }
-    // sized as intra_lds_bytes sizes the launch (largest CTB of the batch, chroma present)
-    const uint32_t launch_block = win_layout(a.max_log2ctb, 1, (int)sizeof(Pel)).bytes;
-    const uint32_t line_bytes = intra_line_bytes(a.max_width, (int)sizeof(Pel));
-    const bool lines = intra_use_lines(nw, launch_block, line_bytes);
-    const int nbuf = nw < 2 ? 2 : nw, cwmax = (a.max_width + 1) >> 1;
-    unsigned char *line0 = smem + 64 + (size_t)nw * launch_block;
-    // component k of the line buffer of CTB row `row`
-    auto line_of = [&](int row, int k) -> Pel * {
-        return reinterpret_cast<Pel *>(line0 + (size_t)(row % nbuf) * line_bytes) +
-               (k == 0 ? 0 : (k == 1 ? a.max_width : a.max_width + cwmax));
-    };
     progress[wave] = 0;  // every lane writes the same value
     __syncthreads();
     const uint32_t stride = (uint32_t)wctb + 1;
@@ -646,10 +606,6 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                             }
                         }
                         for (int y = lane; y < w.cs; y += kWave) w.left[y] = w.cur[y * w.cs + w.cs - 1];
-                        if (lines && r + 1 < hctb) {  // a row below exists, so this CTU is full height
-                            Pel *lw = line_of(r, k) + w.cx0;
-                            for (int x = lane; x < vw; x += kWave) lw[x] = w.cur[(w.cs - 1) * w.cs + x];
-                        }
                     }
                     wave_sync();
                     HG_FENCE_REL();
@@ -676,11 +632,6 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                     w.cx0 = c * w.cs;
                     w.cy0 = r * w.cs;
                     const int yg = w.cy0 - 1;
-                    if (lines) {
-                        // fetch() reads above[xn - cx0 + 1] only for available (decoded) xn
-                        w.above = line_of(r - 1 < 0 ? 0 : r - 1, k) + w.cx0 - 1;
-                        continue;
-                    }
                     for (int i = lane; i <= 2 * w.cs; i += kWave) {
                         const int xg = w.cx0 - 1 + i;
                         w.above[i] = (yg >= 0 && xg >= 0 && xg < PW) ? planes[k][(size_t)yg * PW + xg] : (Pel)0;
@@ -754,9 +705,7 @@ static int intra_launch_waves(const BatchArgs &a) {
 }
 
 static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
-    const uint32_t block = win_layout(a.max_log2ctb, 1, a.bytes_per_sample).bytes;
-    const uint32_t line = intra_line_bytes(a.max_width, a.bytes_per_sample);
-    return 64 + (size_t)nw * block + (intra_use_lines(nw, block, line) ? (size_t)(nw < 2 ? 2 : nw) * line : 0);
+    return 64 + (size_t)nw * win_layout(a.max_log2ctb, 1, a.bytes_per_sample).bytes;
 }
 
 #if defined(HG_HOST_EMU)
