@@ -108,12 +108,24 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                 return (tu.flags & TU_CBF) && tu.log2 == 2 && cidx <= 2 && tu.x + 4 <= pitch[cidx] &&
                        tu.y + 4 <= (cidx ? ch : H);
             };
+            // the lane's record, loaded once per round (each phase below would
+            // otherwise re-load it after the wave syncs)
+#if defined(HG_HOST_EMU)
+            auto grp = group_tb;
+#else
+            TuRec tu_c;
+            const bool ok_c = group_tb(lane, tu_c);
+            auto grp = [&](int, TuRec &tu) -> bool {
+                tu = tu_c;
+                return ok_c;
+            };
+#endif
             for (int vl = lane; vl < 64; vl += kWave) d[vl] = 0;
             wave_sync();
             for (int vl = lane; vl < 64; vl += kWave) {
                 TuRec tu;
                 const int l16 = vl & 15;
-                if (!group_tb(vl, tu) || l16 >= (int)tu.ncoef) continue;
+                if (!grp(vl, tu) || l16 >= (int)tu.ncoef) continue;
                 const int cidx = tu.flags & TU_CIDX_MASK;
                 const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
                 const Coef c = coefs[tu.coef + l16];
@@ -133,7 +145,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
             // first stage: g[y][x] = clip16((sum_k M[k][y] d[k][x] + 64) >> 7)
             for (int vl = lane; vl < 64; vl += kWave) {
                 TuRec tu;
-                if (!group_tb(vl, tu) || (tu.flags & (TU_BYPASS | TU_TSKIP))) continue;
+                if (!grp(vl, tu) || (tu.flags & (TU_BYPASS | TU_TSKIP))) continue;
                 const int16_t *dq = d + (vl & 48);
                 const int y = (vl & 15) >> 2, x = vl & 3;
                 const bool dst_tr = (tu.flags & TU_DST) != 0;
@@ -146,7 +158,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
             // second stage (or bypass / transform skip) and the residual store
             for (int vl = lane; vl < 64; vl += kWave) {
                 TuRec tu;
-                if (!group_tb(vl, tu)) continue;
+                if (!grp(vl, tu)) continue;
                 const int cidx = tu.flags & TU_CIDX_MASK;
                 const int bd2 = 20 - (cidx ? sp.bit_depth_c : sp.bit_depth_y);
                 const int y = (vl & 15) >> 2, x = vl & 3;
