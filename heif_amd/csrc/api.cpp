@@ -511,7 +511,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     }
     HIP_TRY(b->recon.alloc(hb.recon_bytes));
     std::vector<uint32_t> order;
-    lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
+    const int parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
     HIP_TRY(b->porder.alloc(order.size()));
     // ---- one pinned staging image of every upload, copied asynchronously
     struct Seg {
@@ -571,6 +571,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.rsubs = b->rsubs.p;
     a.parse_order = b->porder.p;
     a.n_slots = int(order.size());
+    a.parse_group = parse_group;
     a.seqs = b->seqs.p;
     a.sf = b->sf.p;
     a.outs = b->outs.p;

@@ -62,9 +62,10 @@ int main(int argc, char **argv) {
     a.rbsp = rbsp.data();
     a.rsubs = rsubs.data();
     std::vector<uint32_t> order;
-    lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
+    const int parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
     a.parse_order = order.data();
     a.n_slots = int(order.size());
+    a.parse_group = parse_group;
     a.seqs = hb.seqs.data();
     a.sf = hb.sf.data();
     a.outs = &out;

@@ -48,7 +48,7 @@ struct BatchArgs {
     int max_rows;              // CTB rows, batch max
     int total_rows;            // sum of CTB rows over pictures
     int bytes_per_sample;      // 1 or 2
-    int parse_group;           // k_parse_lanes pictures per wave (set by launch_parse)
+    int parse_group;           // k_parse_lanes pictures per wave (lanes_parse_order's choice; launch_parse otherwise)
     int max_log2ctb;           // largest CTB size in the batch (sizes k_intra's LDS)
     int lane_rows;             // k_parse_lanes lanes per picture: max over pictures of (WPP ? min(rows, 64) : 1)
     int wpp_ring;              // some WPP picture has more than 64 CTB rows (its rows wrap round its lanes)
@@ -83,8 +83,9 @@ inline void color_coefs(uint32_t matrix, bool full, ColorArgs &c) {
     c.cr_g = fx(2.0 * kr * (1.0 - kr) / kg * cs);
 }
 
-// host: BatchArgs::parse_order for a batch (size-balanced k_parse_lanes waves)
-void lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uint32_t> &order);
+// host: BatchArgs::parse_order for a batch (size-balanced k_parse_lanes waves);
+// returns the pictures per wave it dealt for (BatchArgs::parse_group)
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uint32_t> &order);
 
 #if defined(HG_HOST_EMU)
 // Runs kernel(a) over a gx * gy grid, one block at a time, with `waves` host

@@ -1294,14 +1294,44 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
 }
 
 // pictures per wave: a picture's lanes (BatchArgs::lane_rows) are consecutive.
-// HEIFGPU_LANES_PPW lowers it (more, emptier waves) for tuning.
-inline int lanes_pics_per_wave(int lane_rows) {
+// A wave's time is its pictures' WPP chains times the cost of a pass, and a
+// pass costs more with more pictures' lanes in it (more unit kinds and longer
+// divergent loops), so a batch that cannot fill every SIMD takes the fewest
+// pictures per wave that still fit one wave per SIMD (single 4032x3024
+// image on MI355X: parse 85 -> 66 ms at 1 picture per wave instead of 4);
+// a full batch packs 64 lanes (config 4: 1536 waves).  HEIFGPU_LANES_PPW
+// forces a value (tuning); HEIFGPU_PARSE_ADAPT=0 always packs.
+inline int lanes_simds() {
+    static const int simds = [] {
+        const char *e = std::getenv("HEIFGPU_PARSE_SIMDS");
+        if (e) return std::atoi(e);
+#if !defined(HG_HOST_EMU)
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+            return 4 * cus;
+#endif
+        return 1024;
+    }();
+    return simds;
+}
+inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
     static const int forced = [] {
         const char *e = std::getenv("HEIFGPU_LANES_PPW");
         return e ? std::atoi(e) : 0;
     }();
+    static const bool adapt = [] {
+        const char *e = std::getenv("HEIFGPU_PARSE_ADAPT");
+        return !e || std::atoi(e) != 0;
+    }();
     const int full = 64 / (lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows));
-    return forced > 0 && forced < full ? forced : full;
+    if (forced > 0) return forced < full ? forced : full;
+    if (adapt && n_pics > 0) {
+        const long S = lanes_simds();
+        for (int p = 1; p < full; ++p)
+            if ((n_pics + p - 1) / p <= S) return p;
+    }
+    return full;
 }
 
 }  // namespace
@@ -1315,7 +1345,7 @@ inline int lanes_pics_per_wave(int lane_rows) {
 // W gets ranks w, 2W-1-w, 2W+w, 4W-1-w, ...): heavy beside light.  Empty
 // slots are ~0u.  HEIFGPU_PARSE_ORDER=0: batch order; HEIFGPU_PARSE_HEAVY
 // overrides the heavy count.
-void lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uint32_t> &order) {
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uint32_t> &order) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
         return e ? std::atoi(e) : 1;
@@ -1324,12 +1354,12 @@ void lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<ui
         const char *e = std::getenv("HEIFGPU_PARSE_HEAVY");
         return e ? std::atoi(e) : -1;
     }();
-    const int ppw = lanes_pics_per_wave(lane_rows);
+    const int ppw = lanes_pics_per_wave(lane_rows, n);
     if (!on || n <= 0) {
         order.resize((size_t)n);
         for (int i = 0; i < n; ++i) order[(size_t)i] = (uint32_t)i;
         order.resize((size_t)((n + ppw - 1) / ppw) * ppw, ~0u);
-        return;
+        return ppw;
     }
     std::vector<uint32_t> by_size((size_t)n);
     for (int i = 0; i < n; ++i) by_size[(size_t)i] = (uint32_t)i;
@@ -1345,12 +1375,13 @@ void lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<ui
         const int w = (band & 1) ? W - 1 - pos : pos;
         order[(size_t)(heavy + w) * ppw + band] = by_size[(size_t)(heavy + r)];
     }
+    return ppw;
 }
 
 #if defined(HG_HOST_EMU)
 // one wave at a time, one unit per live lane per pass, lanes in order
 void emu_parse(const BatchArgs &a) {
-    const int ppw = lanes_pics_per_wave(a.lane_rows);
+    const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : lanes_pics_per_wave(a.lane_rows, a.n_pics);
     const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
     const int waves = (n_slots + ppw - 1) / ppw;
     uint64_t tab[64], seq[15];
@@ -1503,7 +1534,8 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
 hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
     BatchArgs a = a0;
     if (a.lane_rows < 1 || a.lane_rows > 64) return hipErrorInvalidValue;
-    const int ppw = lanes_pics_per_wave(a.lane_rows);
+    // the dealing of parse_order fixed the pictures per wave (lanes_parse_order)
+    const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : lanes_pics_per_wave(a.lane_rows, a.n_pics);
     a.parse_group = ppw;
     const int waves = ((a.parse_order ? a.n_slots : a.n_pics) + ppw - 1) / ppw;
     hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0), s,
