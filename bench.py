@@ -189,6 +189,9 @@ def main():
     ap.add_argument("--split", choices=["images", "tiles"], default="images",
                     help="images: each rank its own shard (weak); tiles: every rank the same images, "
                          "tiles k %% world == rank (strong)")
+    ap.add_argument("--parse", choices=["auto", "lanes", "solo"], default="auto",
+                    help="CABAC parse mode (auto: solo for small batches, lanes otherwise)")
+    ap.add_argument("--ppw", type=int, default=0, help="lanes mode: pictures per wave (0 = adaptive)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-parse + upload + decode leg")
     ap.add_argument("--e2e-batches", type=int, default=6)
     args = ap.parse_args()
@@ -237,7 +240,7 @@ def main():
     outs = ctx.alloc_outputs(images)
     stride, offset = (world, rank) if tiles_split else (1, 0)
     t0 = time.perf_counter()
-    batch = ctx.prepare(images, tile_stride=stride, tile_offset=offset)
+    batch = ctx.prepare(images, tile_stride=stride, tile_offset=offset, parse=args.parse, pics_per_wave=args.ppw)
     upload_s = time.perf_counter() - t0
     stream = torch.cuda.Stream(device=local)
 

@@ -160,14 +160,17 @@ class DecodeContext:
         return arr
 
     def prepare(self, images: Sequence[HeifImage], tile_stride: int = 1, tile_offset: int = 0,
-                reuse: Optional["DeviceBatch"] = None, wait: bool = True) -> "DeviceBatch":
+                reuse: Optional["DeviceBatch"] = None, wait: bool = True, parse: str = "auto",
+                pics_per_wave: int = 0) -> "DeviceBatch":
         """Device batch of `images` (heifgpu_batch_prepare_ex).  tile_stride /
         tile_offset select the grid tiles k % tile_stride == tile_offset (the
         single-image tile split across GPUs); `reuse` reloads an existing batch
         in place; wait=False returns before the upload has finished (the next
-        decode of the batch waits for it)."""
+        decode of the batch waits for it).  parse: "auto" (by batch size),
+        "lanes" (one substream per lane, `pics_per_wave` pictures per wave, 0 =
+        adaptive) or "solo" (one substream per wave: small-batch latency)."""
         arr = (ctypes.c_void_p * len(images))(*[im._h.value for im in images])
-        opts = _lib.BatchOpts(tile_stride, tile_offset)
+        opts = _lib.BatchOpts(tile_stride, tile_offset, _lib.PARSE_MODES[parse], pics_per_wave)
         if reuse is not None:
             _lib.check(lib.heifgpu_batch_prepare_ex(self._h, arr, len(images), ctypes.byref(opts),
                                                     ctypes.byref(reuse._h)))
@@ -238,6 +241,14 @@ class DeviceBatch:
         if rc not in (_lib.HEIFGPU_OK, _lib.HEIFGPU_E_DECODE):
             _lib.check(rc)
         return list(st)
+
+    def parse_geometry(self) -> dict:
+        """The CABAC parse launch of this batch (heifgpu_batch_parse_geometry)."""
+        v = [ctypes.c_uint32() for _ in range(4)]
+        _lib.check(lib.heifgpu_batch_parse_geometry(self._h, *[ctypes.byref(x) for x in v]))
+        mode = {_lib.PARSE_LANES: "lanes", _lib.PARSE_SOLO: "solo"}[v[0].value]
+        return {"mode": mode, "workgroups": v[1].value, "pics_per_wave": v[2].value,
+                "waves_per_workgroup": v[3].value}
 
     def free(self):
         if self._h is not None and self._h.value:

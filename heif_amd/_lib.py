@@ -109,8 +109,14 @@ class Planes(ctypes.Structure):
 
 
 class BatchOpts(ctypes.Structure):
-    """heifgpu_batch_opts: decode only grid tiles k with k % tile_stride == tile_offset."""
-    _fields_ = [("tile_stride", ctypes.c_uint32), ("tile_offset", ctypes.c_uint32)]
+    """heifgpu_batch_opts: decode only grid tiles k with k % tile_stride == tile_offset;
+    parse_mode (PARSE_*) and, in lanes mode, pictures per wave (0 = adaptive)."""
+    _fields_ = [("tile_stride", ctypes.c_uint32), ("tile_offset", ctypes.c_uint32),
+                ("parse_mode", ctypes.c_uint32), ("pics_per_wave", ctypes.c_uint32)]
+
+
+PARSE_AUTO, PARSE_LANES, PARSE_SOLO = 0, 1, 2
+PARSE_MODES = {"auto": PARSE_AUTO, "lanes": PARSE_LANES, "solo": PARSE_SOLO}
 
 
 # every symbol include/heifgpu.h declares (checked by tests/test_abi.py)
@@ -122,7 +128,7 @@ EXPORTS = (
     "heifgpu_read_se", "heifgpu_bins_truncated_rice", "heifgpu_bins_chroma_pred_mode",
     "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb", "heifgpu_image_tile_params", "heifgpu_debug_counters",
     "heifgpu_image_parse_item", "heifgpu_ycbcr_to_rgb", "heifgpu_batch_prepare_ex", "heifgpu_gather_tiles",
-    "heifgpu_image_parse_many",
+    "heifgpu_image_parse_many", "heifgpu_batch_parse_geometry",
 )
 
 
@@ -187,6 +193,7 @@ def _load() -> ctypes.CDLL:
         "heifgpu_batch_prepare_ex": (I32, [VP, P(VP), SZ, P(BatchOpts), P(VP)]),
         "heifgpu_gather_tiles": (I32, [P(ImageInfo), P(Planes), P(Planes), U32, U32, VP]),
         "heifgpu_image_parse_many": (I32, [P(P(ctypes.c_uint8)), P(SZ), SZ, I32, P(VP), P(I32)]),
+        "heifgpu_batch_parse_geometry": (I32, [VP, P(U32), P(U32), P(U32), P(U32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -27,7 +27,9 @@ struct heifgpu_image {
 // the C structs' layouts are part of the ABI (INTEGRATION.md's Rust binding mirrors them)
 static_assert(sizeof(heifgpu_image_info) == 80, "heifgpu_image_info: 20 x uint32");
 static_assert(sizeof(heifgpu_planes) == 40, "heifgpu_planes: 3 pointers + 3 int32 (+ padding)");
-static_assert(sizeof(heifgpu_batch_opts) == 8, "heifgpu_batch_opts: 2 x uint32");
+static_assert(sizeof(heifgpu_batch_opts) == 16, "heifgpu_batch_opts: 4 x uint32");
+static_assert(HEIFGPU_PARSE_AUTO == PARSE_AUTO && HEIFGPU_PARSE_LANES == PARSE_LANES && HEIFGPU_PARSE_SOLO == PARSE_SOLO,
+              "parse modes");
 static_assert(sizeof(heifgpu_tile_params) == 55 * 4 + 64 * 4, "heifgpu_tile_params: 55 int32 + 64 uint32");
 
 // Pipelined decode.  k_rbsp + k_parse run on an internal parse stream, the
@@ -432,6 +434,9 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     const uint32_t stride = opts && opts->tile_stride ? opts->tile_stride : 1u;
     const uint32_t offset = opts ? opts->tile_offset : 0u;
     if (offset >= stride) return fail(HEIFGPU_E_INVALID, "tile_offset must be below tile_stride");
+    const uint32_t mode_req = opts ? opts->parse_mode : 0u;
+    if (mode_req > HEIFGPU_PARSE_SOLO) return fail(HEIFGPU_E_INVALID, "parse_mode");
+    const int ppw_req = opts ? int(std::min<uint32_t>(opts->pics_per_wave, 64u)) : 0;
     if (*inout && (*inout)->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
     HIP_TRY(hipSetDevice(ctx->device));
     std::vector<const ParsedImage *> parsed;
@@ -475,7 +480,12 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     if (b->loaded) HIP_TRY(hipEventSynchronize(b->uploaded));
     for (int k = 0; k < b->n_sets; ++k)
         if (b->set[k].pending) HIP_TRY(hipStreamWaitEvent(ctx->upload, b->set[k].recon_done, 0));
-    const bool grows = b->loaded && (hb.bits_size > b->bits.cap || hb.pics.size() > b->pics.cap ||
+    std::vector<uint32_t> order;
+    const int mode = parse_mode_for(int(mode_req), int(hb.pics.size()));
+    const int solo_waves = solo_waves_for(hb.lane_rows);
+    const int parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows,
+                                              mode == PARSE_SOLO ? 1 : ppw_req, order);
+    const bool grows = (order.size() > b->porder.cap || hb.bits_size > b->bits.cap || hb.pics.size() > b->pics.cap ||
                                      hb.subs.size() > b->subs.cap || hb.seqs.size() > b->seqs.cap ||
                                      hb.sf.size() > b->sf.cap || n > b->outs.cap || hb.recon_bytes > b->recon.cap ||
                                      hb.resid_elems > b->set[0].resid.cap || hb.tu_n > b->set[0].tus.cap ||
@@ -483,12 +493,9 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
                                      hb.sao_n > b->set[0].sao.cap || 2 * size_t(hb.rows) > b->set[0].row_counts.cap ||
                                      hb.pics.size() > b->set[0].status.cap);
     if (grows) HIP_TRY(hipStreamSynchronize(ctx->upload));  // reallocation: old contents fully drained
-    b->n_images = n;
-    b->tile_stride = stride;
-    b->tile_offset = offset;
-    b->infos = std::move(infos);
-    b->pic_image = hb.pic_image;
-    b->n_pics = int(hb.pics.size());
+    // A failure from here on leaves the batch unusable until a reload succeeds
+    // (its arguments may point at freed arenas): `loaded` is set again last.
+    b->loaded = false;
     // ---- device arenas (reused when large enough)
     HIP_TRY(b->bits.alloc(hb.bits_size));
     HIP_TRY(b->pics.alloc(hb.pics.size()));
@@ -510,8 +517,6 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         HIP_TRY(hipMemsetAsync(ps.status.p, 0, hb.pics.size() * sizeof(uint32_t), ctx->upload));
     }
     HIP_TRY(b->recon.alloc(hb.recon_bytes));
-    std::vector<uint32_t> order;
-    const int parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
     HIP_TRY(b->porder.alloc(order.size()));
     // ---- one pinned staging image of every upload, copied asynchronously
     struct Seg {
@@ -561,6 +566,12 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     }
     HIP_TRY(hipMemsetAsync(b->rbsp.p, 0, hb.bits_size, ctx->upload));
     HIP_TRY(hipEventRecord(b->uploaded, ctx->upload));
+    b->n_images = n;
+    b->tile_stride = stride;
+    b->tile_offset = offset;
+    b->infos = std::move(infos);
+    b->pic_image = hb.pic_image;
+    b->n_pics = int(hb.pics.size());
     b->loaded = true;
     BatchArgs &a = b->args;
     a = BatchArgs{};
@@ -582,7 +593,10 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.max_rows = hb.max_rows;
     a.max_log2ctb = hb.max_log2ctb;
     a.lane_rows = hb.lane_rows;
-    a.wpp_ring = hb.wpp_ring;
+    a.parse_mode = mode;
+    a.solo_waves = solo_waves;
+    // rows wrap round the lanes (waves) of a picture: the WPP context staging
+    a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = hb.bps;
     b->out_host.assign(n, OutImage{});
@@ -602,6 +616,7 @@ int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, si
 int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_planes *out, void *stream) {
     if (!ctx || !b || !out) return fail(HEIFGPU_E_INVALID, "invalid argument");
     if (b->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
+    if (!b->loaded) return fail(HEIFGPU_E_INVALID, "batch not loaded (its last prepare failed)");
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream, as in HIP
     HIP_TRY(hipSetDevice(ctx->device));
     bool changed = false;
@@ -702,6 +717,19 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     ps.pending = true;
     HIP_TRY(hipEventRecord(ctx->join, r));
     HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
+    return HEIFGPU_OK;
+}
+
+int heifgpu_batch_parse_geometry(const heifgpu_batch *b, uint32_t *mode, uint32_t *workgroups,
+                                 uint32_t *pics_per_wave, uint32_t *waves_per_workgroup) {
+    if (!b || !b->loaded) return fail(HEIFGPU_E_INVALID, "invalid batch");
+    const BatchArgs &a = b->args;
+    const bool solo = a.parse_mode == PARSE_SOLO;
+    const uint32_t ppw = solo ? 1u : uint32_t(std::max(1, a.parse_group));
+    if (mode) *mode = solo ? HEIFGPU_PARSE_SOLO : HEIFGPU_PARSE_LANES;
+    if (workgroups) *workgroups = (uint32_t(a.n_slots) + ppw - 1) / ppw;
+    if (pics_per_wave) *pics_per_wave = ppw;
+    if (waves_per_workgroup) *waves_per_workgroup = solo ? uint32_t(a.solo_waves) : 1u;
     return HEIFGPU_OK;
 }
 

@@ -62,7 +62,10 @@ int main(int argc, char **argv) {
     a.rbsp = rbsp.data();
     a.rsubs = rsubs.data();
     std::vector<uint32_t> order;
-    const int parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, order);
+    const int mode = parse_mode_for(PARSE_AUTO, int(hb.pics.size()));
+    const int solo_waves = solo_waves_for(hb.lane_rows);
+    const int parse_group =
+        lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0, order);
     a.parse_order = order.data();
     a.n_slots = int(order.size());
     a.parse_group = parse_group;
@@ -83,7 +86,9 @@ int main(int argc, char **argv) {
     a.max_rows = hb.max_rows;
     a.max_log2ctb = hb.max_log2ctb;
     a.lane_rows = hb.lane_rows;
-    a.wpp_ring = hb.wpp_ring;
+    a.parse_mode = mode;
+    a.solo_waves = solo_waves;
+    a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = bps;
     emu_rbsp(a);
@@ -95,6 +100,7 @@ int main(int argc, char **argv) {
         ntu += rc[2 * r];
         ncoef += rc[2 * r + 1];
     }
+    printf("parse mode: %s\n", mode == PARSE_SOLO ? "solo" : "lanes");
     printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);
     if (stages >= 2) emu_transform(a);
     if (stages >= 3) emu_intra(a);

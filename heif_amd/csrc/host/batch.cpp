@@ -161,6 +161,7 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
             const bool wpp = (sq.flags & SP_WPP) != 0;
             hb.lane_rows = std::max(hb.lane_rows, wpp ? std::min(hctb, max_lane_rows()) : 1);
             if (wpp && hctb > max_lane_rows()) hb.wpp_ring = 1;
+            if (wpp) hb.max_wpp_rows = std::max(hb.max_wpp_rows, hctb);
         }
     }
     hb.bits_size += 128;

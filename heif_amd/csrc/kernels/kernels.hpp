@@ -51,7 +51,9 @@ struct BatchArgs {
     int parse_group;           // k_parse_lanes pictures per wave (lanes_parse_order's choice; launch_parse otherwise)
     int max_log2ctb;           // largest CTB size in the batch (sizes k_intra's LDS)
     int lane_rows;             // k_parse_lanes lanes per picture: max over pictures of (WPP ? min(rows, 64) : 1)
-    int wpp_ring;              // some WPP picture has more than 64 CTB rows (its rows wrap round its lanes)
+    int wpp_ring;              // some WPP picture has more CTB rows than lanes (its rows wrap round its lanes)
+    int parse_mode;            // PARSE_LANES (k_parse_lanes) or PARSE_SOLO (k_parse_solo)
+    int solo_waves;            // k_parse_solo waves per workgroup (solo_waves_for(lane_rows))
 };
 
 // k_ycbcr_rgb (color.hip): one decoded image → interleaved RGB8, rotated
@@ -83,9 +85,17 @@ inline void color_coefs(uint32_t matrix, bool full, ColorArgs &c) {
     c.cr_g = fx(2.0 * kr * (1.0 - kr) / kg * cs);
 }
 
-// host: BatchArgs::parse_order for a batch (size-balanced k_parse_lanes waves);
-// returns the pictures per wave it dealt for (BatchArgs::parse_group)
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uint32_t> &order);
+// parse modes (BatchArgs::parse_mode; heifgpu_batch_opts::parse_mode)
+enum : int { PARSE_AUTO = 0, PARSE_LANES = 1, PARSE_SOLO = 2 };
+constexpr int kSoloMaxWaves = 16;
+// host: BatchArgs::parse_order for a batch (size-balanced k_parse_lanes waves,
+// or for solo mode with ppw_force = 1 one picture per workgroup, heaviest
+// first); returns the pictures per wave it dealt for (BatchArgs::parse_group).
+// ppw_force = 0: the adaptive choice.
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order);
+// the parse mode a batch of n_pics pictures runs in (requested: PARSE_*)
+int parse_mode_for(int requested, int n_pics);
+int solo_waves_for(int lane_rows);
 
 #if defined(HG_HOST_EMU)
 // Runs kernel(a) over a gx * gy grid, one block at a time, with `waves` host

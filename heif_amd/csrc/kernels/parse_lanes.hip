@@ -158,13 +158,115 @@ struct Lane {
     uint32_t tu_row, coef_row;  // TuRec / Coef index of the current row's outputs
 };
 
-// engine context of one lane
+// engine context of one lane (lanes mode: every lane its own substream)
 struct Eng {
+    static constexpr bool kSolo = false;
     uint8_t *ctx;
     const uint64_t *tab;  // per pStateIdx: rangeTabLps[4] | transIdxLps << 32 | transIdxMps << 40 (LDS)
     const uint64_t *seq;  // sig_seq(scan, pattern): slot of every scan position of a sub-block (LDS)
     const uint8_t *rbsp;  // BatchArgs::rbsp (emulation prevention removed by k_rbsp)
     uint32_t lim;         // no loads at or past this offset (the picture's RBSP end + 64)
+    HG_HD uint64_t row(uint32_t st) const { return tab[st]; }
+};
+
+// Solo mode (k_parse_solo): one substream per WAVE, run by its lane 0 alone,
+// so the engine state is wave-uniform.  The state rows live in two VGPRs
+// across the lanes (lane s = pStateIdx s) and are read with v_readlane, and
+// the RBSP comes from a 512-byte window in two VGPRs (dword d of the arena at
+// lane d % 64 of register (d / 64) % 2), filled between units by whole-wave
+// coalesced 256-byte loads through a staging VGPR: a chunk is loaded one
+// chunk ahead of use and copied into the window (the copy is where the
+// compiler waits for it) only when the reader enters the chunk before it, so
+// a bin never waits on LDS for its state row and a refill almost never waits
+// on memory.
+#if defined(HG_HOST_EMU)
+struct Win {
+    const uint32_t *w;  // [2 * 64]
+    uint32_t get(uint32_t d) const { return w[d & 127u]; }
+};
+#else
+struct Win {
+    uint32_t r0, r1;
+    __device__ __forceinline__ uint32_t get(uint32_t d) const {
+        const int ln = __builtin_amdgcn_readfirstlane((int)(d & 63u));
+        const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)((d >> 6) & 1u));
+        return (uint32_t)__builtin_amdgcn_readlane((int)(k ? r1 : r0), ln);
+    }
+};
+#endif
+struct EngSolo {
+    static constexpr bool kSolo = true;
+    uint8_t *ctx;
+    uint32_t tlo, thi;    // lane s: state_row(s) (GPU); unused under emulation
+    const uint64_t *seq;
+    const uint8_t *rbsp;
+    uint32_t lim;
+    Win win;
+#if defined(HG_HOST_EMU)
+    uint64_t row(uint32_t st) const { return state_row((int)st); }
+#else
+    __device__ __forceinline__ uint64_t row(uint32_t st) const {
+        const int s = __builtin_amdgcn_readfirstlane((int)st);
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)tlo, s);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)thi, s);
+        return (uint64_t)lo | ((uint64_t)hi << 32);
+    }
+#endif
+};
+
+// driver side of a solo wave's RBSP window: chunks (64 dwords, 256 bytes) c
+// and c + 1 of the reader in the window, c + 2 staged (in flight)
+struct SoloWin {
+#if defined(HG_HOST_EMU)
+    uint32_t *w, *f;  // [128], [64]
+    void load(const uint8_t *rbsp, uint32_t chunk, uint32_t lim, int) {
+        for (int l = 0; l < 64; ++l) {
+            const uint32_t o = std::min((chunk * 64u + (uint32_t)l) * 4u, lim);
+            f[l] = (uint32_t)rbsp[o] | ((uint32_t)rbsp[o + 1] << 8) | ((uint32_t)rbsp[o + 2] << 16) |
+                   ((uint32_t)rbsp[o + 3] << 24);
+        }
+    }
+    void commit(uint32_t chunk) {
+        for (int l = 0; l < 64; ++l) w[(chunk & 1u) * 64u + (uint32_t)l] = f[l];
+    }
+    Win view() const { return Win{w}; }
+#else
+    uint32_t r0, r1, f;
+    // every lane loads its dword of the chunk (one coalesced 256-byte load)
+    __device__ __forceinline__ void load(const uint8_t *rbsp, uint32_t chunk, uint32_t lim, int lane) {
+        const uint32_t o = (chunk * 64u + (uint32_t)lane) * 4u;
+        f = *reinterpret_cast<const uint32_t *>(rbsp + (o < lim ? o : lim));
+    }
+    // the copy is the first use of the staged load: the compiler waits for it here
+    __device__ __forceinline__ void commit(uint32_t chunk) {
+        if (chunk & 1u) r1 = f;
+        else r0 = f;
+    }
+    __device__ __forceinline__ Win view() const { return Win{r0, r1}; }
+#endif
+    uint32_t ck;  // the staged chunk
+    // a substream (re)starts at byte `start`
+    HG_HD void restart(const uint8_t *rbsp, uint32_t start, uint32_t lim, int lane) {
+        const uint32_t c0 = start >> 8;
+        load(rbsp, c0, lim, lane);
+        commit(c0);
+        load(rbsp, c0 + 1, lim, lane);
+        commit(c0 + 1);
+        load(rbsp, c0 + 2, lim, lane);
+        ck = c0 + 2;
+    }
+    // before a unit, the reader at dword rd: keep its chunk and the next in the window
+    HG_HD void advance(const uint8_t *rbsp, uint32_t rd, uint32_t lim, int lane) {
+        const uint32_t cc = rd >> 6;
+        if (cc + 1 < ck) return;
+        if (cc >= ck) {  // a unit ran past the window (corrupt stream): reload
+            restart(rbsp, cc << 8, lim, lane);
+            return;
+        }
+        commit(ck);
+        load(rbsp, ck + 1, lim, lane);
+        ++ck;
+    }
 };
 
 // ------------------------------------------------------------------ memory helpers
@@ -257,8 +359,11 @@ HG_HD inline uint32_t bswap32(uint32_t w) {
 }
 
 // next RBSP dword of the queue.  Normally a or b; a lane that drained both
-// inside one pass takes f (waiting for it) or loads synchronously.
-HG_HD inline uint32_t q_pop(Lane &L, const Eng &G) {
+// inside one pass takes f (waiting for it) or loads synchronously.  Solo
+// mode: dword L.lb of the register window (filled between units).
+template <class EG>
+HG_HD inline uint32_t q_pop(Lane &L, const EG &G) {
+    if constexpr (EG::kSolo) return G.win.get(L.lb++);
     const uint32_t w = L.ai == 0 ? L.a0 : (L.ai == 1 ? L.a1 : (L.ai == 2 ? L.a2 : L.a3));
     if (++L.ai == 4) {
         L.ai = 0;
@@ -291,7 +396,8 @@ HG_HD inline void q_refill(Lane &L, const Eng &G) {
 }
 
 // value += 16 more look-ahead bits (k < 8 on entry, so k <= 23 and value < 2^32 after)
-HG_HD inline void vfill(Lane &L, const Eng &G) {
+template <class EG>
+HG_HD inline void vfill(Lane &L, const EG &G) {
     if (L.cn < 16) {
         L.cur |= (uint64_t)bswap32(q_pop(L, G)) << (32 - L.cn);
         L.cn += 32;
@@ -304,14 +410,20 @@ HG_HD inline void vfill(Lane &L, const Eng &G) {
 }
 
 // 9.3.2.5: engine initialisation at RBSP offset `start` (absolute), picture RBSP end `end`
-HG_HD inline void engine_init(Lane &L, const Eng &G, uint32_t start, uint32_t end) {
+// (solo mode: the driver has filled the window from `start` on)
+template <class EG>
+HG_HD inline void engine_init(Lane &L, const EG &G, uint32_t start, uint32_t end) {
     const uint32_t a0 = start & ~3u, sh = (start & 3u) * 8u;
-    load_x4(G.rbsp, a0, G.lim, L.a0, L.a1, L.a2, L.a3);
-    load_x4(G.rbsp, a0 + 16, G.lim, L.b0, L.b1, L.b2, L.b3);
-    L.ai = 0;
-    L.bv = 1;
-    L.fp = 0;
-    L.lb = a0 + 32;
+    if constexpr (EG::kSolo) {
+        L.lb = a0 >> 2;
+    } else {
+        load_x4(G.rbsp, a0, G.lim, L.a0, L.a1, L.a2, L.a3);
+        load_x4(G.rbsp, a0 + 16, G.lim, L.b0, L.b1, L.b2, L.b3);
+        L.ai = 0;
+        L.bv = 1;
+        L.fp = 0;
+        L.lb = a0 + 32;
+    }
     L.cur = (uint64_t)bswap32(q_pop(L, G)) << (32 + sh);
     L.cn = 32 - (int)sh;
     L.budget = 8 * (int32_t)(end - start);
@@ -327,9 +439,10 @@ HG_HD inline void engine_init(Lane &L, const Eng &G, uint32_t start, uint32_t en
 // DecodeDecision (arithmetic.rs:97-144), branch-free: one LDS row per
 // pStateIdx gives rangeTabLps and both transitions; the renormalisation of
 // either path is a shift by clz and lowers k.
-HG_HD inline int dec_s(Lane &L, const Eng &G, uint32_t &s) {
+template <class EG>
+HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
     const uint32_t st = s >> 1, mps = s & 1u;
-    const uint64_t row = G.tab[st];
+    const uint64_t row = G.row(st);
     const uint32_t lps = ((uint32_t)row >> (((L.range >> 6) & 3u) << 3)) & 0xffu;
     const uint32_t rm = L.range - lps;
     const uint32_t sr = rm << L.k;
@@ -346,7 +459,8 @@ HG_HD inline int dec_s(Lane &L, const Eng &G, uint32_t &s) {
 }
 
 // the same on context ci in LDS
-HG_HD inline int dec(Lane &L, const Eng &G, int ci) {
+template <class EG>
+HG_HD inline int dec(Lane &L, const EG &G, int ci) {
     uint32_t s = G.ctx[ci];
     const int bin = dec_s(L, G, s);
     G.ctx[ci] = (uint8_t)s;
@@ -368,7 +482,8 @@ HG_HD inline void cache_put(uint32_t &c0, uint32_t &c1, uint32_t &c2, int slot, 
 }
 
 // DecodeBypass (arithmetic.rs:146-157)
-HG_HD inline int byp(Lane &L, const Eng &G) {
+template <class EG>
+HG_HD inline int byp(Lane &L, const EG &G) {
     L.k -= 1;
     const uint32_t sr = L.range << L.k;
     const bool one = L.value >= sr;
@@ -392,7 +507,8 @@ HG_HD inline uint32_t div_range(uint32_t top, uint32_t r) {
 // n (0..8) bypass bins in one step.  n successive DecodeBypass steps are the
 // long division of ivlOffset * 2^n + (the next n bits) by ivlCurrRange: the
 // quotient is the n bins, the remainder the new ivlOffset.
-HG_HD inline uint32_t byp_n(Lane &L, const Eng &G, int n) {
+template <class EG>
+HG_HD inline uint32_t byp_n(Lane &L, const EG &G, int n) {
     L.k -= n;  // k >= 8 >= n on entry
     const uint32_t q = div_range(L.value >> L.k, L.range);
     L.value -= (q * L.range) << L.k;
@@ -400,7 +516,8 @@ HG_HD inline uint32_t byp_n(Lane &L, const Eng &G, int n) {
     return q;
 }
 
-HG_HD inline uint32_t byp_bits(Lane &L, const Eng &G, int n) {
+template <class EG>
+HG_HD inline uint32_t byp_bits(Lane &L, const EG &G, int n) {
     uint32_t v = 0;
     while (n > 0) {
         const int c = n < 8 ? n : 8;
@@ -417,7 +534,8 @@ HG_HD inline uint32_t byp_bits(Lane &L, const Eng &G, int n) {
 // (p + 1 + k <= 8 bins) is a prefix of those 8, consumed at once (a prefix of
 // a long-division quotient is the quotient of the shorter division).  Returns
 // the value, or -1 after consuming the 4 ones of an escape.
-HG_HD inline int byp_rem(Lane &L, const Eng &G, int k) {
+template <class EG>
+HG_HD inline int byp_rem(Lane &L, const EG &G, int k) {
     const uint32_t q8 = div_range(L.value >> (L.k - 8), L.range);  // k >= 8 on entry
     const int p = __builtin_clz(((~q8) << 24) | (1u << 27));        // leading ones, at most 4
     const int used = p < 4 ? p + 1 + k : 4;
@@ -430,7 +548,8 @@ HG_HD inline int byp_rem(Lane &L, const Eng &G, int k) {
 
 // a unary bypass prefix of at most m (1..8) bins: the number p of 1-bins
 // before the first 0, consuming min(p + 1, m) bins
-HG_HD inline int byp_unary(Lane &L, const Eng &G, int m) {
+template <class EG>
+HG_HD inline int byp_unary(Lane &L, const EG &G, int m) {
     const uint32_t q = div_range(L.value >> (L.k - m), L.range);
     const int p = __builtin_clz(((~q) << (32 - m)) | (1u << (31 - m)));
     const int used = p < m ? p + 1 : m;
@@ -441,7 +560,8 @@ HG_HD inline int byp_unary(Lane &L, const Eng &G, int m) {
 }
 
 // DecodeTerminate (arithmetic.rs:159-169)
-HG_HD inline int term(Lane &L, const Eng &G) {
+template <class EG>
+HG_HD inline int term(Lane &L, const EG &G) {
     L.range -= 2;
     const uint32_t sr = L.range << L.k;
     if (L.value >= sr) return 1;
@@ -586,6 +706,14 @@ HG_HD inline bool wpp_ready(const Lane &L, const LanePic &P, const Env &E) {
     return prog_load(&E.prog[P.lane0 + (L.row - 1) % P.R]) >= need;
 }
 
+// RBSP offset (absolute) at which a lane about to run U_CTU starts its
+// substream (engine and context initialisation, unit_ctu), or ~0u
+HG_HD inline uint32_t substream_start(const Lane &L, const LanePic &P, const BatchArgs &a) {
+    if (L.c == 0 && ((L.fl & F_WPP) || L.row == 0))
+        return P.bits_off + a.rsubs[P.sub_first + ((L.fl & F_WPP) ? L.row : 0)];
+    return ~0u;
+}
+
 HG_HD inline void row_outputs(Lane &L, const LanePic &P) {
     L.tu_row = (uint32_t)L.row * P.tu_cap;
     L.coef_row = (uint32_t)L.row * P.coef_cap;
@@ -600,7 +728,8 @@ HG_HD inline void coef_push(Lane &L, const LanePic &P, uint32_t w) { P.coef_base
 // ------------------------------------------------------------------ units
 // U_CTU: CTU start (7.3.8.2) and sao() (7.3.8.3).  Returns without a state
 // change while the row above is less than two CTUs ahead (WPP).
-HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const Eng &G) {
+template <class EG>
+HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const EG &G) {
     if (!wpp_ready(L, P, E)) return;
     L.ctbx = L.c << P.log2ctb;
     L.ctby = L.row << P.log2ctb;
@@ -615,8 +744,7 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
 #pragma nounroll
             for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = src[k];
         }
-        const uint32_t *subs = E.a->rsubs + P.sub_first;
-        engine_init(L, G, P.bits_off + subs[(L.fl & F_WPP) ? L.row : 0], P.bits_end);
+        engine_init(L, G, substream_start(L, P, *E.a), P.bits_end);
         if (L.row == 0) L.fl |= F_FIRST_QG;
     }
     if (P.saoL || P.saoC) {
@@ -669,7 +797,8 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
 }
 
 // U_CQT: split_cu_flag descent (7.3.8.4) from the current node to a CU
-HG_HD inline void unit_cqt(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+template <class EG>
+HG_HD inline void unit_cqt(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     for (;;) {
         const int n = 1 << L.ql;
         bool split;
@@ -700,7 +829,8 @@ HG_HD inline void unit_cqt(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
 }
 
 // U_CU: coding_unit (7.3.8.5) up to its transform_tree
-HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+template <class EG>
+HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     if (L.fl & F_QG_NEW) {
         derive_qp_pred(L, ld, P);
         L.fl &= ~F_QG_NEW;
@@ -763,7 +893,8 @@ HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
 
 // U_TT: transform_tree descent (7.3.8.8) from the current node to a leaf,
 // then transform_unit (7.3.8.10) up to its first TB
-HG_HD inline void unit_tt(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+template <class EG>
+HG_HD inline void unit_tt(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     const bool nxn = (L.fl & F_NXN) != 0;
     const int max_depth = P.maxDepthIntra + (nxn ? 1 : 0);
     for (;;) {
@@ -915,7 +1046,8 @@ HG_HD inline void tb_done(Lane &L, LaneLds &ld, LanePic &P) {
 
 // U_TB: TB tb_t of the TU; without coefficients it is done here, otherwise
 // residual_coding's header (transform_skip_flag, last position) is parsed
-HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+template <class EG>
+HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     const int t = L.tb_t;
     const bool chroma4 = P.chroma == 1 && L.tl == 2;
     bool cbf;
@@ -999,7 +1131,8 @@ HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
 }
 
 // U_SB: sub-block rc_i of residual_coding (7.3.8.11, 9.3.4.2.5-7)
-HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
+template <class EG>
+HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     const int l2 = L.tb_log2, cidx = L.tb_cidx, i = L.rc_i;
     const int sbl = l2 - 2, sbw = 1 << sbl;
     const int sp = scan_pos(sbl, L.rc_scan, i);
@@ -1166,7 +1299,8 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const Eng &G) {
 
 // U_CTU_END: WPP context storage, the depth line, end_of_slice_segment_flag /
 // end_of_subset_one_bit (slice.rs:214-227), progress, next CTU / row
-HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const Eng &G) {
+template <class EG>
+HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const EG &G) {
     if ((L.fl & F_WPP) && L.c == 1 && L.row + 1 < P.hctb) {
         // 9.3.2.4 storage for the next row's substream: into its lane's block, or
         // its staging block when that lane may still be parsing an earlier row
@@ -1211,7 +1345,8 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
 // only lanes in that unit).  One unit kind per pass keeps the dispatch a
 // uniform branch: a divergent switch over the units would linearise them, and
 // every L field a unit updates would then need a register per unit.
-HG_HD inline void run_unit(int kind, Lane &L, LaneLds &ld, LanePic &P, const Env &E, const Eng &G) {
+template <class EG>
+HG_HD inline void run_unit(int kind, Lane &L, LaneLds &ld, LanePic &P, const Env &E, const EG &G) {
     switch (kind) {
     case U_SB: unit_sb(L, ld, P, G); break;
     case U_TB: unit_tb(L, ld, P, G); break;
@@ -1228,13 +1363,15 @@ HG_HD inline void run_unit(int kind, Lane &L, LaneLds &ld, LanePic &P, const Env
 HG_HD inline bool ctu_ready(const Lane &L, const LanePic &P, const Env &E) { return wpp_ready(L, P, E); }
 
 // lane setup: picture constants, outputs, first state.  Returns false for an idle lane.
-HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a, int pic, int row, int lane0) {
+// `cap` lanes (waves, solo mode) at most per picture.
+HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a, int pic, int row, int lane0,
+                            int cap) {
     const PicDesc &pd = a.pics[pic];
     const SeqParams &sp = a.seqs[pd.seq];
     const int log2ctb = sp.log2_ctb, ctb = 1 << log2ctb;
     const int hctb = (sp.height + ctb - 1) >> log2ctb;
     const bool wpp = (sp.flags & SP_WPP) != 0;
-    const int R = wpp ? (hctb < a.lane_rows ? hctb : a.lane_rows) : 1;
+    const int R = wpp ? (hctb < cap ? hctb : cap) : 1;
     if (row >= R) return false;
     P.R = R;
     P.lane0 = lane0;
@@ -1345,7 +1482,7 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
 // W gets ranks w, 2W-1-w, 2W+w, 4W-1-w, ...): heavy beside light.  Empty
 // slots are ~0u.  HEIFGPU_PARSE_ORDER=0: batch order; HEIFGPU_PARSE_HEAVY
 // overrides the heavy count.
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uint32_t> &order) {
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
         return e ? std::atoi(e) : 1;
@@ -1354,7 +1491,8 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uin
         const char *e = std::getenv("HEIFGPU_PARSE_HEAVY");
         return e ? std::atoi(e) : -1;
     }();
-    const int ppw = lanes_pics_per_wave(lane_rows, n);
+    const int full = 64 / (lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows));
+    const int ppw = ppw_force > 0 ? std::min(ppw_force, full) : lanes_pics_per_wave(lane_rows, n);
     if (!on || n <= 0) {
         order.resize((size_t)n);
         for (int i = 0; i < n; ++i) order[(size_t)i] = (uint32_t)i;
@@ -1378,9 +1516,34 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, std::vector<uin
     return ppw;
 }
 
+// Parse mode of a batch.  Solo mode parses each substream on a wave of its own
+// (lane 0), which is far faster per substream than a lane of a packed wave
+// but leaves 63 lanes idle: it is the latency path of small batches, where
+// the packed waves cannot fill the SIMDs anyway.  HEIFGPU_PARSE=lanes|solo
+// forces a mode for every batch, HEIFGPU_SOLO_MAX_PICS moves the automatic
+// switch-over.
+int parse_mode_for(int requested, int n_pics) {
+    static const int env = [] {
+        const char *e = std::getenv("HEIFGPU_PARSE");
+        if (!e) return PARSE_AUTO;
+        return e[0] == 's' ? PARSE_SOLO : (e[0] == 'l' ? PARSE_LANES : PARSE_AUTO);
+    }();
+    static const int max_pics = [] {
+        const char *e = std::getenv("HEIFGPU_SOLO_MAX_PICS");
+        return e ? std::atoi(e) : 256;
+    }();
+    if (env != PARSE_AUTO) return env;
+    if (requested == PARSE_LANES || requested == PARSE_SOLO) return requested;
+    return n_pics <= max_pics ? PARSE_SOLO : PARSE_LANES;
+}
+
+// waves per solo workgroup: one per WPP row of the tallest picture, at most 16
+// (1024 threads); taller pictures wrap their rows round the waves
+int solo_waves_for(int lane_rows) { return lane_rows < 1 ? 1 : (lane_rows > kSoloMaxWaves ? kSoloMaxWaves : lane_rows); }
+
 #if defined(HG_HOST_EMU)
 // one wave at a time, one unit per live lane per pass, lanes in order
-void emu_parse(const BatchArgs &a) {
+void emu_parse_lanes(const BatchArgs &a) {
     const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : lanes_pics_per_wave(a.lane_rows, a.n_pics);
     const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
     const int waves = (n_slots + ppw - 1) / ppw;
@@ -1400,7 +1563,7 @@ void emu_parse(const BatchArgs &a) {
             const int slot = w * ppw + pl;
             const bool in = pl < ppw && slot < n_slots && (!a.parse_order || a.parse_order[slot] != ~0u);
             const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
-            const bool live = in && lane_init(lanes[l], pics[pl], lds[l], a, pic, row, pl * a.lane_rows);
+            const bool live = in && lane_init(lanes[l], pics[pl], lds[l], a, pic, row, pl * a.lane_rows, a.lane_rows);
             if (!live) lanes[l].st = U_DONE;
         }
         Env E{&a, lds.data(), prog, a.wpp_ring ? wctx.data() : nullptr, 0};
@@ -1442,6 +1605,67 @@ void emu_parse(const BatchArgs &a) {
             printf("wave %d: %ld passes, %.1f units per pass\n", w, passes, (double)units / passes);
     }
 }
+
+// solo mode: each picture's rows (waves) round-robin, one unit per ready wave
+// per round, with the GPU driver's window logic (SoloWin) per wave
+void emu_parse_solo(const BatchArgs &a) {
+    const int NW = a.solo_waves;
+    const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
+    uint64_t seq[15];
+    for (int i = 0; i < 15; ++i) seq[i] = sig_seq(i);
+    std::vector<LaneLds> lds((size_t)NW);
+    std::vector<Lane> lanes((size_t)NW);
+    std::vector<uint8_t> wctx((size_t)NW * CTX_PAD);
+    std::vector<uint32_t> wbuf((size_t)NW * 192);
+    std::vector<SoloWin> wins((size_t)NW);
+    LanePic P;
+    uint32_t prog[64];
+    for (int slot = 0; slot < n_slots; ++slot) {
+        const bool in = !a.parse_order || a.parse_order[slot] != ~0u;
+        if (!in) continue;
+        const int pic = a.pic0 + (a.parse_order ? (int)a.parse_order[slot] : slot);
+        for (int w = 0; w < NW; ++w) {
+            prog[w] = 0;
+            if (!lane_init(lanes[(size_t)w], P, lds[(size_t)w], a, pic, w, 0, NW)) lanes[(size_t)w].st = U_DONE;
+            wins[(size_t)w].w = &wbuf[(size_t)w * 192];
+            wins[(size_t)w].f = &wbuf[(size_t)w * 192 + 128];
+        }
+        const uint32_t lim = (P.bits_end + 64u) & ~3u;
+        Env E{&a, lds.data(), prog, wctx.data(), 0};
+        for (;;) {
+            bool any = false, progressed = false;
+            for (int w = 0; w < NW; ++w) {
+                Lane &L = lanes[(size_t)w];
+                if (L.st == U_DONE) continue;
+                any = true;
+                E.lane = w;
+                if (L.st == U_CTU && !ctu_ready(L, P, E)) continue;
+                progressed = true;
+                SoloWin &sw = wins[(size_t)w];
+                const uint32_t start = L.st == U_CTU ? substream_start(L, P, a) : ~0u;
+                if (start != ~0u) sw.restart(a.rbsp, start, lim, 0);
+                else sw.advance(a.rbsp, L.lb, lim, 0);
+                const EngSolo G{lds[(size_t)w].ctx, 0u, 0u, seq, a.rbsp, lim, sw.view()};
+                run_unit(L.st, L, lds[(size_t)w], P, E, G);
+            }
+            if (!any) break;
+            if (!progressed) {
+                for (int w = 0; w < NW; ++w)
+                    if (lanes[(size_t)w].st != U_DONE) {
+                        lanes[(size_t)w].status |= ST_SUBSTREAM_END;
+                        atomicOr(&a.status[P.pic], lanes[(size_t)w].status);
+                        lanes[(size_t)w].st = U_DONE;
+                    }
+                break;
+            }
+        }
+    }
+}
+
+void emu_parse(const BatchArgs &a) {
+    if (a.parse_mode == PARSE_SOLO) emu_parse_solo(a);
+    else emu_parse_lanes(a);
+}
 #else
 // LDS of one wave: LaneLds per used lane, LanePic per picture, progress words,
 // engine tables, and the WPP context staging when rows wrap
@@ -1482,7 +1706,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     LaneLds &ld = s_lds[lane < nl ? lane : 0];
     LanePic &P = s_pic[pl < ppw ? pl : 0];
     s_prog[lane] = 0;
-    const bool live = in && lane_init(L, P, ld, a, pic, row, pl * a.lane_rows);
+    const bool live = in && lane_init(L, P, ld, a, pic, row, pl * a.lane_rows, a.lane_rows);
     if (!live) L.st = U_DONE;
     __syncthreads();
     const Env E{&a, s_lds, s_prog, s_wctx, lane};
@@ -1531,9 +1755,100 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
 #endif
 }
 
+// Solo mode: one workgroup per picture, one wave per WPP row (rows beyond 16
+// wrap round the waves).  All 64 lanes of a wave run the same substream in
+// lockstep (identical state in every lane, so exec stays full: the window and
+// state-row registers read with v_readlane are never left stale in inactive
+// lanes by a copy the compiler placed inside a divergent region), and the
+// lanes differ only in the window refill, where each loads its own dword.  WPP
+// progress words and the row-to-row context copies are in the workgroup's
+// LDS, so the 2-CTU lag needs no memory traffic; waves waiting for the row
+// above sleep.
+inline size_t solo_lds_bytes(int nw, bool ring) {
+    return sizeof(LaneLds) * (size_t)nw + sizeof(LanePic) + 64 * sizeof(uint32_t) + 16 * sizeof(uint64_t) +
+           (ring ? (size_t)nw * CTX_PAD : 0);
+}
+
+__global__ void __launch_bounds__(64 * kSoloMaxWaves) k_parse_solo(BatchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int NW = a.solo_waves;
+    LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
+    LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + NW);
+    uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + 1);
+    uint64_t *s_seq = reinterpret_cast<uint64_t *>(s_prog + 64);
+    uint8_t *s_wctx = a.wpp_ring ? reinterpret_cast<uint8_t *>(s_seq + 16) : nullptr;
+    const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    if (threadIdx.x < 15) s_seq[threadIdx.x] = sig_seq((int)threadIdx.x);
+    if (threadIdx.x < 64) s_prog[threadIdx.x] = 0;
+    const uint64_t trow = state_row(lane);
+    const uint32_t tlo = (uint32_t)trow, thi = (uint32_t)(trow >> 32);
+    const int slot = (int)blockIdx.x;
+    const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
+    const bool in = slot < n_slots && (!a.parse_order || a.parse_order[slot] != ~0u);
+    const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
+    Lane L;
+    LaneLds &ld = s_lds[w < NW ? w : 0];
+    LanePic &P = s_pic[0];
+    const bool live = in && w < NW && lane_init(L, P, ld, a, pic, w, 0, NW);  // every lane alike
+    if (!live) L.st = U_DONE;
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(live ? 1 : 0)) return;
+    const Env E{&a, s_lds, s_prog, s_wctx, w};
+    const uint32_t lim = (P.bits_end + 64u) & ~3u;
+    SoloWin sw;
+    sw.r0 = sw.r1 = sw.f = 0;
+    sw.ck = 0;
+#if defined(HG_PARSE_PROF)
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
+    for (;;) {
+        // the wave's state (equal in every lane), made scalar
+        int st = L.st, run = st != U_DONE && (st != U_CTU || ctu_ready(L, P, E));
+        uint32_t start = run && st == U_CTU ? substream_start(L, P, a) : ~0u;
+        const uint32_t rd = L.lb;
+        st = __builtin_amdgcn_readfirstlane(st);
+        if (st == U_DONE) break;
+        if (!__builtin_amdgcn_readfirstlane(run)) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        start = (uint32_t)__builtin_amdgcn_readfirstlane((int)start);
+        if (start != ~0u) sw.restart(a.rbsp, start, lim, lane);
+        else sw.advance(a.rbsp, (uint32_t)__builtin_amdgcn_readfirstlane((int)rd), lim, lane);
+        // the rows above (contexts, SAO parameters, depth line) before their readers
+        if (st == U_CTU) HG_FENCE_ACQ();
+#if defined(HG_PARSE_PROF)
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        ++pf[7];
+#endif
+        {
+            const EngSolo G{ld.ctx, tlo, thi, s_seq, a.rbsp, lim, sw.view()};
+            run_unit(st, L, ld, P, E, G);
+        }
+#if defined(HG_PARSE_PROF)
+        pf[st <= U_CTU ? 2 : st <= U_TT ? 3 : st - 1] += __builtin_amdgcn_s_memtime() - t1;
+        ++pf[1];
+#endif
+    }
+#if defined(HG_PARSE_PROF)
+    pf[0] = __builtin_amdgcn_s_memtime() - t_start;
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[k], (unsigned long long)pf[k]);
+#endif
+}
+
 hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
     BatchArgs a = a0;
     if (a.lane_rows < 1 || a.lane_rows > 64) return hipErrorInvalidValue;
+    if (a.parse_mode == PARSE_SOLO) {
+        if (a.solo_waves < 1 || a.solo_waves > kSoloMaxWaves) return hipErrorInvalidValue;
+        const int n = a.parse_order ? a.n_slots : a.n_pics;
+        if (n <= 0) return hipSuccess;
+        hipLaunchKernelGGL(k_parse_solo, dim3(n), dim3(64 * a.solo_waves), solo_lds_bytes(a.solo_waves, a.wpp_ring != 0),
+                           s, a);
+        return hipGetLastError();
+    }
     // the dealing of parse_order fixed the pictures per wave (lanes_parse_order)
     const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : lanes_pics_per_wave(a.lane_rows, a.n_pics);
     a.parse_group = ppw;

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define HEIFGPU_ABI_VERSION 2
+#define HEIFGPU_ABI_VERSION 3
 
 enum {
     HEIFGPU_OK = 0,
@@ -88,7 +88,17 @@ typedef struct {
      * written.  0 or 1 = every tile.  Tiles are independent IDR pictures
      * (src/heic/decoder.rs:98-119 decodes them one by one). */
     uint32_t tile_stride, tile_offset;
+    /* CABAC parse mode: HEIFGPU_PARSE_AUTO picks by batch
+     * size; HEIFGPU_PARSE_LANES packs one substream per lane (throughput);
+     * HEIFGPU_PARSE_SOLO runs one substream per wavefront (latency of small
+     * batches). */
+    uint32_t parse_mode;
+    /* lanes mode: pictures per wavefront (0 = adaptive; larger values are
+     * capped at 64 / CTB rows) */
+    uint32_t pics_per_wave;
 } heifgpu_batch_opts;
+
+enum { HEIFGPU_PARSE_AUTO = 0, HEIFGPU_PARSE_LANES = 1, HEIFGPU_PARSE_SOLO = 2 };
 
 /* ---- host: demux + parameter sets + slice headers ------------------- */
 /* data is copied; the returned image owns its bytes. */
@@ -208,6 +218,11 @@ int heifgpu_image_tile_params(const heifgpu_image *img, uint32_t tile, heifgpu_t
  * counters written, or 0 for the product build (counters compiled out; the
  * `make prof` library has them). */
 int heifgpu_debug_counters(uint64_t *out, int n);
+/* The CABAC parse geometry a prepared batch launches: mode
+ * (HEIFGPU_PARSE_LANES / _SOLO), workgroups (waves in lanes mode, pictures in
+ * solo mode), pictures per wave (lanes) and waves per workgroup (solo). */
+int heifgpu_batch_parse_geometry(const heifgpu_batch *batch, uint32_t *mode, uint32_t *workgroups,
+                                 uint32_t *pics_per_wave, uint32_t *waves_per_workgroup);
 
 #ifdef __cplusplus
 }

@@ -29,11 +29,13 @@ def _run(exe, path, env_extra=None):
     return r.returncode, r.stdout + r.stderr
 
 
-# k_parse_lanes (one substream per lane) with its default geometry (adaptive:
-# one picture per wave for a single image), the full 64-lane packing of large
+# k_parse_solo (one substream per wave: the automatic choice for a single
+# image), k_parse_lanes (one substream per lane) with its adaptive geometry
+# (one picture per wave for a single image), the full 64-lane packing of large
 # batches (four 16-row pictures per wave), and batch (unsorted) wave order
-PARSERS = {"lanes": {}, "packed": {"HEIFGPU_PARSE_ADAPT": "0"}, "ppw1": {"HEIFGPU_LANES_PPW": "1"},
-           "order0": {"HEIFGPU_PARSE_ORDER": "0"}}
+LANES = {"HEIFGPU_PARSE": "lanes"}
+PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "lanes": LANES, "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0"},
+           "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1"}, "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
 
 
 @pytest.mark.parametrize("parser", list(PARSERS))
@@ -42,7 +44,7 @@ def test_emulated_kernels_match_oracle(emu_check, parser):
     assert rc == 0 and "EMU PARITY OK" in out, out[-2000:]
 
 
-@pytest.mark.parametrize("parser", ["lanes", "packed"])
+@pytest.mark.parametrize("parser", ["solo", "lanes", "packed"])
 def test_emulated_kernels_permuted_image(emu_check, tmp_path, halfmoonbay, parser):
     p = tmp_path / "perm.heic"
     p.write_bytes(permuted_heic(halfmoonbay, 42))
@@ -69,7 +71,7 @@ def _corrupt(data: bytes, mode: str) -> bytes:
     return bytes(d)
 
 
-@pytest.mark.parametrize("parser", ["lanes", "packed"])
+@pytest.mark.parametrize("parser", ["solo", "lanes", "packed"])
 @pytest.mark.parametrize("mode", ["random", "zeroed"])
 def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode, parser):
     """Corrupt slice data must end in status bits, never in a crash (the same

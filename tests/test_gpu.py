@@ -62,6 +62,7 @@ def planes_np(o):
 
 
 def test_halfmoonbay_bit_exact(H, oracle_halfmoonbay, halfmoonbay):
+    """Config 3 through the reference-mirror API (one image: solo parse)."""
     out = H.HeicDecoder.decode(halfmoonbay)
     y, cb, cr = planes_np(out)
     assert np.array_equal(y, oracle_halfmoonbay.y)
@@ -69,6 +70,70 @@ def test_halfmoonbay_bit_exact(H, oracle_halfmoonbay, halfmoonbay):
     assert np.array_equal(cr, oracle_halfmoonbay.cr)
     g = json.loads((GOLDEN / "halfmoonbay_planes.json").read_text())
     assert hashlib.sha256(out.y.cpu().numpy().tobytes()).hexdigest() == g["planes"]["y"]
+
+
+@pytest.mark.parametrize("parse,ppw,geom", [
+    ("solo", 0, {"mode": "solo", "workgroups": 48, "pics_per_wave": 1, "waves_per_workgroup": 16}),
+    ("lanes", 0, {"mode": "lanes", "workgroups": 48, "pics_per_wave": 1, "waves_per_workgroup": 1}),
+    ("lanes", 4, {"mode": "lanes", "workgroups": 12, "pics_per_wave": 4, "waves_per_workgroup": 1}),
+])
+def test_halfmoonbay_parse_modes(H, ctx, oracle_halfmoonbay, halfmoonbay, parse, ppw, geom):
+    """Config 3 in every parse geometry: solo (a workgroup of 16 waves per
+    tile, one WPP row per wave), lanes with one tile per wave (the adaptive
+    choice for one image) and lanes packed four tiles per wave."""
+    img = H.HeifImage.parse(halfmoonbay)
+    b = ctx.prepare([img], parse=parse, pics_per_wave=ppw)
+    assert b.parse_geometry() == geom
+    out = ctx.alloc_outputs([img])
+    b.decode_async(out)
+    assert b.status() == [0]
+    b.free()
+    for got, want in zip(planes_np(out[0]), (oracle_halfmoonbay.y, oracle_halfmoonbay.cb, oracle_halfmoonbay.cr)):
+        assert np.array_equal(got, want)
+
+
+def check_permuted(outs, seeds, oracle_tiles):
+    """Every image of a permuted batch, tile window by tile window against the
+    oracle's 48 tile decodes placed by the image's permutation (the per-tile
+    loop the batch replaces: /root/reference/src/heic/decoder.rs:114-119)."""
+    from heif_amd.synthetic import permutation
+
+    for s, o in zip(seeds, outs):
+        perm = permutation(48, s)
+        planes = [t.cpu().numpy() for t in (o.y, o.cb, o.cr)]
+        for k in range(48):
+            r, c = divmod(k, 8)
+            for ci, pl in enumerate(planes):
+                sh = 1 if ci else 0
+                ts = 512 >> sh
+                win = pl[ts * r:ts * (r + 1), ts * c:ts * (c + 1)]
+                ref = oracle_tiles[perm[k]][ci][:win.shape[0], :win.shape[1]]
+                assert np.array_equal(win, ref), (s, k, ci)
+
+
+@pytest.mark.parametrize("parse,geom", [
+    ("auto", {"mode": "lanes", "workgroups": 1536, "pics_per_wave": 4, "waves_per_workgroup": 1}),
+    ("solo", {"mode": "solo", "workgroups": 6144, "pics_per_wave": 1, "waves_per_workgroup": 16}),
+])
+def test_bench_shard_every_image(H, ctx, oracle_tiles, halfmoonbay, parse, geom):
+    """The headline configuration itself (bench.py, config 4 shard): 128
+    permuted 4032x3024 images = 6144 pictures.  The automatic choice packs four
+    16-row pictures per k_parse_lanes wave (1536 waves); solo runs 6144
+    16-wave workgroups.  Every image is checked, decoded twice back to back
+    (both parse-output sets of the pipeline)."""
+    from heif_amd.synthetic import permuted_heic
+
+    seeds = list(range(128))
+    imgs = H.HeifImage.parse_many([permuted_heic(halfmoonbay, s) for s in seeds], threads=8)
+    b = ctx.prepare(imgs, parse=parse)
+    assert b.parse_geometry() == geom
+    outs = [ctx.alloc_outputs(imgs) for _ in range(2)]
+    for o in outs:
+        b.decode_async(o)
+    assert not any(b.status())
+    b.free()
+    for o in outs:
+        check_permuted(o, seeds, oracle_tiles)
 
 
 def test_permuted_batch_row_parallel(H, ctx, oracle_tiles, halfmoonbay):
@@ -88,20 +153,19 @@ def test_permuted_batch_row_parallel(H, ctx, oracle_tiles, halfmoonbay):
 
 
 def test_large_batch_many_waves(H, ctx, oracle_tiles, halfmoonbay):
-    """22 images = 1056 pictures = 264 k_parse_lanes waves (more than one per CU),
-    size-sorted snake order across waves, every image checked."""
-    from heif_amd.synthetic import permutation, permuted_heic
+    """22 images = 1056 pictures: the adaptive lanes packing takes the fewest
+    pictures per wave that fit one wave per SIMD, 2 here (528 waves on the
+    1024 SIMDs), size-sorted snake order across waves, every image checked."""
+    from heif_amd.synthetic import permuted_heic
 
     seeds = list(range(100, 122))
     imgs = [H.HeifImage.parse(permuted_heic(halfmoonbay, s)) for s in seeds]
     outs = ctx.alloc_outputs(imgs)
     b = ctx.prepare(imgs)
+    assert b.parse_geometry() == {"mode": "lanes", "workgroups": 528, "pics_per_wave": 2, "waves_per_workgroup": 1}
     b.decode_async(outs)
     assert not any(b.status())
-    for s, o in zip(seeds, outs):
-        want = assemble(oracle_tiles, permutation(48, s))
-        for got, w in zip(planes_np(o), want):
-            assert np.array_equal(got, w), s
+    check_permuted(outs, seeds, oracle_tiles)
     b.free()
 
 

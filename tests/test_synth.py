@@ -148,15 +148,36 @@ def _assert_equal(got, img, tag):
         assert bad == 0, f"{tag} {c}: {bad} samples differ"
 
 
+@pytest.fixture(scope="module")
+def gctx(H):
+    c = H.DecodeContext(0)
+    yield c
+    c.close()
+
+
+def _decode(H, ctx, datas, parse, ppw=0):
+    imgs = [H.HeifImage.parse(d) for d in datas]
+    b = ctx.prepare(imgs, parse=parse, pics_per_wave=ppw)
+    outs = ctx.alloc_outputs(imgs)
+    b.decode_async(outs)
+    st = b.status()
+    b.free()
+    return outs, st
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("parse", ["solo", "lanes"])
 @pytest.mark.parametrize("name,over", CASES, ids=[c[0] for c in CASES])
-def test_gpu_synthetic_bit_exact(H, oracle_mod, name, over):
+def test_gpu_synthetic_bit_exact(H, gctx, oracle_mod, name, over, parse):
+    """Every tool / geometry case in both parse modes: k_parse_solo (one
+    substream per wave; rows beyond 16 wrap round the waves) and
+    k_parse_lanes (one substream per lane; rows beyond 64 wrap round the lanes)."""
     p = params(over)
     for seed in range(2):
         data = S.single_heic(p, seed=seed)
-        out = H.HeicDecoder.decode(data)
-        torch.cuda.synchronize()
-        _assert_equal(_planes(out), oracle_mod.decode_heic(data, with_checks=False), (name, seed))
+        outs, st = _decode(H, gctx, [data], parse)
+        assert st == [0], (name, seed)
+        _assert_equal(_planes(outs[0]), oracle_mod.decode_heic(data, with_checks=False), (name, seed))
 
 
 @pytest.mark.gpu
@@ -184,16 +205,17 @@ def test_gpu_mixed_geometry_batch(H, oracle_mod):
 
 
 @pytest.mark.gpu
-def test_gpu_mixed_wpp_ring_batch(H, oracle_mod, halfmoonbay):
+@pytest.mark.parametrize("parse", ["solo", "lanes"])
+def test_gpu_mixed_wpp_ring_batch(H, oracle_mod, halfmoonbay, parse):
     """One batch mixing a 48-tile WPP grid (halfmoonbay), a non-WPP 512x512
     single-substream picture (config 2) and a 68-row CTB-16 picture whose WPP
-    rows wrap round its 64 lanes: lanes per picture is the batch maximum (64),
-    and each picture keeps its own substream layout."""
+    rows wrap round its 64 lanes (16 waves in solo mode): lanes per picture is
+    the batch maximum, and each picture keeps its own substream layout."""
     datas = [halfmoonbay, S.single_heic(params(dict(width=512, height=512, wpp=0)), seed=11),
              S.single_heic(params(dict(width=64, height=1088, log2_ctb=4, log2_max_tb=4)), seed=12)]
     ctx = H.DecodeContext(0)
     imgs = [H.HeifImage.parse(d) for d in datas]
-    b = ctx.prepare(imgs)
+    b = ctx.prepare(imgs, parse=parse)
     outs = ctx.alloc_outputs(imgs)
     for _ in range(2):  # two pipelined decodes (alternate parse sets)
         b.decode_async(outs)
@@ -205,20 +227,18 @@ def test_gpu_mixed_wpp_ring_batch(H, oracle_mod, halfmoonbay):
 
 
 @pytest.mark.gpu
-def test_gpu_nowpp_batch_64_per_wave(H, oracle_mod):
-    """128 non-WPP pictures: one lane each, 64 pictures per k_parse_lanes wave."""
+@pytest.mark.parametrize("parse,ppw", [("lanes", 64), ("lanes", 0), ("solo", 0)])
+def test_gpu_nowpp_batch_64_per_wave(H, gctx, oracle_mod, parse, ppw):
+    """128 non-WPP pictures (one substream each).  ("lanes", 64): every
+    k_parse_lanes wave packs 64 pictures, one per lane (2 waves); ("lanes", 0):
+    the adaptive packing, which for 128 pictures is one picture per wave; solo:
+    one single-wave workgroup per picture.  Every picture checked."""
     p = params(dict(width=64, height=64, wpp=0))
     datas = [S.single_heic(p, seed=100 + k) for k in range(128)]
-    ctx = H.DecodeContext(0)
-    imgs = [H.HeifImage.parse(d) for d in datas]
-    b = ctx.prepare(imgs)
-    outs = ctx.alloc_outputs(imgs)
-    b.decode_async(outs)
-    assert not any(b.status())
-    for k in (0, 1, 63, 64, 127):
+    outs, st = _decode(H, gctx, datas, parse, ppw)
+    assert not any(st)
+    for k in range(128):
         _assert_equal(_planes(outs[k]), oracle_mod.decode_heic(datas[k], with_checks=False), k)
-    b.free()
-    ctx.close()
 
 
 @pytest.mark.gpu
@@ -233,7 +253,7 @@ def test_gpu_config5_8k_main10_grid(H, oracle_mod):
 
 
 # ------------------------------------------- kernels compiled for the host
-@pytest.mark.parametrize("parser", ["lanes", "ppw1"])
+@pytest.mark.parametrize("parser", ["solo", "lanes", "ppw1"])
 def test_emulated_kernels_on_synthetic_streams(tmp_path, parser):
     """The GPU kernels' source built for the host (HG_HOST_EMU, see
     test_emulation.py) decodes every synthetic case bit-exactly vs the oracle."""
@@ -244,7 +264,8 @@ def test_emulated_kernels_on_synthetic_streams(tmp_path, parser):
     csrc = pathlib.Path(__file__).resolve().parents[1] / "heif_amd" / "csrc"
     subprocess.run(["make", "-s", "-C", str(csrc), "emu-fast"], check=True, capture_output=True)
     exe = csrc / "build" / "emu_fast" / "emu_check"
-    env = dict(os.environ, **({"HEIFGPU_LANES_PPW": "1"} if parser == "ppw1" else {}))
+    env = dict(os.environ, HEIFGPU_PARSE="solo" if parser == "solo" else "lanes",
+               **({"HEIFGPU_LANES_PPW": "1"} if parser == "ppw1" else {}))
     for name, over in CASES:
         path = tmp_path / f"{name}.heic"
         path.write_bytes(S.single_heic(params(over), seed=1))
