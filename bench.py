@@ -133,6 +133,39 @@ def cpu_baseline(data: bytes, seconds: float, threads: int, label: str = "halfmo
     }
 
 
+def verify_images(outs, seeds, src, info, stride, offset, threads) -> int:
+    """Checks every given image bit-exactly against the oracle without
+    re-decoding whole images: image `seed` places tile perm_seed[k] of `src`
+    (the identity-order grid) at grid position k, so each of its tile windows
+    must equal the oracle's decode of that one tile of `src` (the per-tile
+    loop the batch replaces, /root/reference/src/heic/decoder.rs:114-119).
+    With a tile split only this rank's positions k % stride == offset are
+    checked.  Returns the number of images checked."""
+    import numpy as np
+
+    from heif_amd.synthetic import permutation
+    from oracle import oracle
+
+    tiles, (ho, hl) = oracle.list_tiles(src)
+    hvcc = src[ho:ho + hl]
+    tw, th = info.tile_width, info.tile_height
+    with cf.ThreadPoolExecutor(max(1, threads)) as ex:  # ctypes releases the GIL
+        ref = list(ex.map(lambda t: oracle.decode_tile(hvcc, src[t[0]:t[0] + t[1]], tw, th), tiles))
+    n, cols = info.num_tiles, info.grid_cols
+    for s, o in zip(seeds, outs):
+        perm = permutation(n, s)
+        planes = [t.cpu().numpy().astype(np.uint16) for t in (o.y, o.cb, o.cr) if t is not None]
+        for k in range(offset, n, stride):
+            r, c = divmod(k, cols)
+            for ci, pl in enumerate(planes):
+                sh = 1 if ci else 0
+                w, h = tw >> sh, th >> sh
+                win = pl[h * r:h * (r + 1), w * c:w * (c + 1)]
+                if not np.array_equal(win, ref[perm[k]][ci][:win.shape[0], :win.shape[1]]):
+                    raise SystemExit(f"image seed {s} tile {k} plane {ci}: GPU planes differ from the oracle")
+    return len(outs)
+
+
 def end_to_end(H, ctx, files, outs0, n_batches, threads, stream, info) -> dict:
     """Host parse + pinned upload + decode of n_batches batches of `files`
     (re-parsed every time), two device batches reloaded alternately so the
@@ -185,7 +218,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=["config4", "config5"], default="config4")
-    ap.add_argument("--verify", type=int, default=2, help="images checked bit-exact against the oracle (rank 0)")
+    ap.add_argument("--verify", type=int, default=-1,
+                    help="images checked bit-exact against the oracle on rank 0 (-1 = every image)")
     ap.add_argument("--split", choices=["images", "tiles"], default="images",
                     help="images: each rank its own shard (weak); tiles: every rank the same images, "
                          "tiles k %% world == rank (strong)")
@@ -237,7 +271,8 @@ def main():
     host_parse_ms_mt = (time.perf_counter() - t0) * 1e3 / len(files)
     info = images[0].info
     ctx = H.DecodeContext(local)
-    outs = ctx.alloc_outputs(images)
+    # a tile split's planes sit in one buffer: one IPC handle per rank for the gather to rank 0
+    outs, outbuf = ctx.alloc_outputs_contiguous(images) if tiles_split else (ctx.alloc_outputs(images), None)
     stride, offset = (world, rank) if tiles_split else (1, 0)
     t0 = time.perf_counter()
     batch = ctx.prepare(images, tile_stride=stride, tile_offset=offset, parse=args.parse, pics_per_wave=args.ppw)
@@ -283,6 +318,42 @@ def main():
     alone = ctx.stage_times()
     ctx.set_timing(False)
 
+    # Row e2 across processes (outside the timed region): the tile split's
+    # planes gathered to rank 0 over IPC + xGMI (heif_amd/tile_split.py).  In
+    # the image split (default), one image is decoded tile-split for this check.
+    gather = None
+    g_full, g_seeds = None, None
+    if world > 1:
+        from heif_amd.tile_split import DeviceBackend, gather_to_rank0
+
+        if tiles_split:
+            g_imgs, g_outs, g_buf, g_seeds = images, outs, outbuf, seeds
+        else:
+            g_seeds = [0]
+            g_imgs = [H.HeifImage.parse(files[0] if rank == 0 else permuted_heic(src, 0) if not c5 else
+                                        S.grid_heic(S.CONFIG5["out_w"], S.CONFIG5["out_h"], p5,
+                                                    pictures=[pool[j] for j in permutation(135, 0)]))]
+            gb = ctx.prepare(g_imgs, tile_stride=world, tile_offset=rank)
+            g_outs, g_buf = ctx.alloc_outputs_contiguous(g_imgs)
+            gb.decode_async(g_outs, stream.cuda_stream)
+            if any(gb.status(stream.cuda_stream)):
+                raise SystemExit(f"rank {rank}: tile-split decode status")
+            gb.free()
+        g_full = ctx.alloc_outputs(g_imgs) if rank == 0 else None
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        gather_to_rank0(DeviceBackend(H, ctx, stream), torch.distributed, g_outs, g_buf, g_full, rank, world)
+        g_ms = (time.perf_counter() - t0) * 1e3
+        if rank == 0:
+            g_bytes = sum(t.numel() * t.element_size() for o in g_full for t in (o.y, o.cb, o.cr) if t is not None)
+            gather = {"images": len(g_full), "ranks": world, "ms": round(g_ms, 3),
+                      "bytes": g_bytes * (world - 1) // world,
+                      "what": "each rank's tile subset (k % world == rank) gathered into rank 0's planes: handles "
+                              "exchanged with all_gather_object, peers mapped with heifgpu_ipc_open, one "
+                              "k_gather_tiles launch per image and rank reading over xGMI (ms includes the exchange "
+                              "and the closing barrier)"}
+
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = end_to_end(H, ctx, files, outs, args.e2e_batches, host_threads, stream, info)
@@ -290,23 +361,15 @@ def main():
     if rank == 0:
         verified = 0
         if args.verify:
-            import numpy as np
-            from oracle import oracle
-
-            for i in range(min(args.verify, len(files))):
-                ref = oracle.decode_heic(files[i], with_checks=False)
-                for c, (g, r) in enumerate(((outs[i].y, ref.y), (outs[i].cb, ref.cb), (outs[i].cr, ref.cr))):
-                    g = g.cpu().numpy().astype(np.uint16)
-                    if tiles_split:  # only this rank's tiles were decoded
-                        sub = 1 if c else 0
-                        tw, th = info.tile_width >> sub, info.tile_height >> sub
-                        for k in range(offset, info.num_tiles, stride):
-                            ty, tx = (k // info.grid_cols) * th, (k % info.grid_cols) * tw
-                            if not np.array_equal(g[ty:ty + th, tx:tx + tw], r[ty:ty + th, tx:tx + tw]):
-                                raise SystemExit(f"image {i} tile {k}: GPU planes differ from the oracle")
-                    elif not np.array_equal(g, r):
-                        raise SystemExit(f"image {i}: GPU planes differ from the oracle")
-                verified += 1
+            n_check = len(files) if args.verify < 0 else min(args.verify, len(files))
+            if tiles_split and g_full is not None:  # the gathered images, every tile
+                verified = verify_images(g_full[:n_check], g_seeds[:n_check], src, info, 1, 0, host_threads)
+            else:
+                verified = verify_images(outs[:n_check], seeds[:n_check], src, info, stride, offset, host_threads)
+            if gather is not None and not tiles_split:
+                gather["verified"] = verify_images(g_full, g_seeds, src, info, 1, 0, host_threads)
+            elif gather is not None:
+                gather["verified"] = verified
         px = info.width * info.height
         total_images = args.batch if tiles_split else args.batch * world
         value = total_images * px * args.steps / elapsed / 1e6  # every step decodes the whole batch
@@ -373,7 +436,7 @@ def main():
                         "the timed region includes the pipeline fill and drain; stage_ms_per_step are means over the "
                         "timed steps (overlap included), stage_ms_alone one decode with nothing beside it",
             "latency_ms_one_step": round(sum(alone), 3),
-            "pipeline_hbm_gbs": round(args.batch * algo_per_image / (elapsed / args.steps) / 1e9, 2),
+            "pipeline_hbm_gbs": round(launch_bytes / (elapsed / args.steps) / 1e9, 2),
             "host_parse_ms_per_image": round(host_parse_ms, 3),
             "host_parse_ms_per_image_mt": {"threads": host_threads, "ms": round(host_parse_ms_mt, 4)},
             "upload_s": round(upload_s, 3),
@@ -381,6 +444,8 @@ def main():
         }
         if e2e:
             line["e2e"] = e2e
+        if gather:
+            line["tile_split_gather"] = gather
         if not args.no_cpu_baseline:
             build = cpu_build
             threads = effective_cpus()

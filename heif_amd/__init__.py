@@ -24,7 +24,7 @@ from ._lib import HeifGpuError, UnsupportedError, lib
 
 __all__ = [
     "HeicDecoder", "HeifImage", "DecodeContext", "DeviceBatch", "DecodedImage", "RbspReader",
-    "HeifGpuError", "UnsupportedError",
+    "HeifGpuError", "UnsupportedError", "ipc_export", "ipc_open", "ipc_close",
 ]
 
 
@@ -133,6 +133,32 @@ class DecodeContext:
         except Exception:
             pass
 
+    def alloc_outputs_contiguous(self, images: Sequence[HeifImage]):
+        """Output planes of `images` carved from ONE device buffer (256-byte
+        aligned planes), so a single heifgpu_ipc_export handle covers all of
+        them; returns (outputs, buffer)."""
+        torch = self._torch
+        dev = torch.device("cuda", self.device)
+        shapes = []
+        total = 0
+        for im in images:
+            inf = im.info
+            dims = [(inf.height, inf.width)]
+            if inf.chroma_format_idc == 1:
+                dims += [((inf.height + 1) // 2, (inf.width + 1) // 2)] * 2
+            offs = []
+            for h, w in dims:
+                offs.append((total, h, w))
+                total += (h * w * inf.bytes_per_sample + 255) // 256 * 256
+            shapes.append((inf, offs))
+        buf = torch.empty(max(total, 256), dtype=torch.uint8, device=dev)
+        outs = []
+        for inf, offs in shapes:
+            dt = torch.uint8 if inf.bytes_per_sample == 1 else torch.int16
+            pl = [buf[o:o + h * w * inf.bytes_per_sample].view(dt).view(h, w) for o, h, w in offs]
+            outs.append(DecodedImage(pl[0], pl[1] if len(pl) > 1 else None, pl[2] if len(pl) > 1 else None, inf))
+        return outs, buf
+
     def alloc_outputs(self, images: Sequence[HeifImage]) -> List[DecodedImage]:
         torch = self._torch
         outs = []
@@ -194,6 +220,19 @@ class DecodeContext:
                                             DecodeContext.planes_of([src]), tile_stride, tile_offset,
                                             ctypes.c_void_p(stream)))
 
+    def gather_tiles_from(self, dst: DecodedImage, src_ptrs: Sequence[int], src_pitches: Sequence[int],
+                          tile_stride: int, tile_offset: int, stream: Optional[int] = None):
+        """gather_tiles from raw device pointers, e.g. another process's planes
+        mapped with ipc_open."""
+        if stream is None:
+            stream = self._torch.cuda.current_stream(self.device).cuda_stream
+        src = (_lib.Planes * 1)()
+        for c in range(3):
+            src[0].plane[c] = src_ptrs[c] if c < len(src_ptrs) else None
+            src[0].pitch[c] = src_pitches[c] if c < len(src_pitches) else 0
+        _lib.check(lib.heifgpu_gather_tiles(ctypes.byref(dst.info), DecodeContext.planes_of([dst]), src, tile_stride,
+                                            tile_offset, ctypes.c_void_p(stream)))
+
     def set_timing(self, enable: bool):
         _lib.check(lib.heifgpu_set_timing(self._h, 1 if enable else 0))
 
@@ -217,6 +256,27 @@ class DecodeContext:
         _lib.check(lib.heifgpu_ycbcr_to_rgb(self._h, ctypes.byref(inf), planes, ctypes.c_void_p(rgb.data_ptr()),
                                             rgb.stride(0), ctypes.c_void_p(stream)))
         return rgb
+
+
+def ipc_export(tensor) -> bytes:
+    """heifgpu_ipc_export of a device tensor's storage: 72 bytes another
+    process passes to ipc_open (e.g. through torch.distributed)."""
+    h = _lib.IpcHandle()
+    _lib.check(lib.heifgpu_ipc_export(ctypes.c_void_p(tensor.data_ptr()), ctypes.byref(h)))
+    return bytes(h)
+
+
+def ipc_open(device: int, blob: bytes) -> int:
+    """Maps another process's exported allocation on `device`; returns the
+    device address of the exported byte (close with ipc_close)."""
+    h = _lib.IpcHandle.from_buffer_copy(blob)
+    p = ctypes.c_void_p()
+    _lib.check(lib.heifgpu_ipc_open(device, ctypes.byref(h), ctypes.byref(p)))
+    return p.value
+
+
+def ipc_close(ptr: int) -> None:
+    _lib.check(lib.heifgpu_ipc_close(ctypes.c_void_p(ptr)))
 
 
 class DeviceBatch:

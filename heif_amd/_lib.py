@@ -115,6 +115,11 @@ class BatchOpts(ctypes.Structure):
                 ("parse_mode", ctypes.c_uint32), ("pics_per_wave", ctypes.c_uint32)]
 
 
+class IpcHandle(ctypes.Structure):
+    """heifgpu_ipc_handle: a device allocation exported to another process."""
+    _fields_ = [("handle", ctypes.c_uint8 * 64), ("offset", ctypes.c_uint64)]
+
+
 PARSE_AUTO, PARSE_LANES, PARSE_SOLO = 0, 1, 2
 PARSE_MODES = {"auto": PARSE_AUTO, "lanes": PARSE_LANES, "solo": PARSE_SOLO}
 
@@ -128,7 +133,8 @@ EXPORTS = (
     "heifgpu_read_se", "heifgpu_bins_truncated_rice", "heifgpu_bins_chroma_pred_mode",
     "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb", "heifgpu_image_tile_params", "heifgpu_debug_counters",
     "heifgpu_image_parse_item", "heifgpu_ycbcr_to_rgb", "heifgpu_batch_prepare_ex", "heifgpu_gather_tiles",
-    "heifgpu_image_parse_many", "heifgpu_batch_parse_geometry",
+    "heifgpu_image_parse_many", "heifgpu_batch_parse_geometry", "heifgpu_ipc_export", "heifgpu_ipc_open",
+    "heifgpu_ipc_close",
 )
 
 
@@ -194,6 +200,9 @@ def _load() -> ctypes.CDLL:
         "heifgpu_gather_tiles": (I32, [P(ImageInfo), P(Planes), P(Planes), U32, U32, VP]),
         "heifgpu_image_parse_many": (I32, [P(P(ctypes.c_uint8)), P(SZ), SZ, I32, P(VP), P(I32)]),
         "heifgpu_batch_parse_geometry": (I32, [VP, P(U32), P(U32), P(U32), P(U32)]),
+        "heifgpu_ipc_export": (I32, [VP, P(IpcHandle)]),
+        "heifgpu_ipc_open": (I32, [I32, P(IpcHandle), P(VP)]),
+        "heifgpu_ipc_close": (I32, [VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

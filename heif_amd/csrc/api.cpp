@@ -7,6 +7,7 @@
 #include <cstring>
 #include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -270,34 +271,89 @@ int heifgpu_gather_tiles(const heifgpu_image_info *info, const heifgpu_planes *d
     hipPointerAttribute_t ad{}, as{};
     HIP_TRY(hipPointerGetAttributes(&ad, dst->plane[0]));
     HIP_TRY(hipPointerGetAttributes(&as, src->plane[0]));
-    if (ad.device != as.device) {  // peer copy over xGMI
-        int cur = 0;
-        HIP_TRY(hipGetDevice(&cur));
-        HIP_TRY(hipSetDevice(ad.device));
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(ad.device));
+    if (ad.device != as.device) {  // a pointer of another device in this process: read it over xGMI
         const hipError_t e = hipDeviceEnablePeerAccess(as.device, 0);
         (void)hipGetLastError();
-        HIP_TRY(hipSetDevice(cur));
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIP_TRY(e);
-    }
-    const uint32_t W = info->width, H = info->height, bps = info->bytes_per_sample;
-    const uint32_t cols = std::max(1u, info->grid_cols), tw = info->tile_width ? info->tile_width : W,
-                   th = info->tile_height ? info->tile_height : H;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    for (uint32_t k = tile_offset; k < std::max(1u, info->num_tiles); k += tile_stride) {
-        const uint32_t x0 = (k % cols) * tw, y0 = (k / cols) * th;
-        if (x0 >= W || y0 >= H) continue;  // a tile wholly inside the crop
-        for (int c = 0; c < planes; ++c) {
-            const uint32_t sx = c ? 1 : 0;  // 4:2:0 chroma halves both axes
-            const uint32_t pw = (W + sx) >> sx, ph = (H + sx) >> sx;
-            const uint32_t x = x0 >> sx, y = y0 >> sx;
-            const uint32_t w = std::min(tw >> sx, pw - x), h = std::min(th >> sx, ph - y);
-            const size_t so = size_t(y) * size_t(src->pitch[c]) + size_t(x) * bps;
-            const size_t d0 = size_t(y) * size_t(dst->pitch[c]) + size_t(x) * bps;
-            HIP_TRY(hipMemcpy2DAsync(static_cast<uint8_t *>(dst->plane[c]) + d0, size_t(dst->pitch[c]),
-                                     static_cast<const uint8_t *>(src->plane[c]) + so, size_t(src->pitch[c]),
-                                     size_t(w) * bps, h, hipMemcpyDefault, s));
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+            (void)hipSetDevice(cur);
+            HIP_TRY(e);
         }
     }
+    GatherArgs g{};
+    for (int c = 0; c < 3; ++c) {
+        g.dst[c] = reinterpret_cast<uint64_t>(dst->plane[c]);
+        g.src[c] = reinterpret_cast<uint64_t>(src->plane[c]);
+        g.dpitch[c] = dst->pitch[c];
+        g.spitch[c] = src->pitch[c];
+    }
+    g.planes = planes;
+    g.bps = int32_t(info->bytes_per_sample);
+    g.W = int32_t(info->width);
+    g.H = int32_t(info->height);
+    g.cols = int32_t(std::max(1u, info->grid_cols));
+    g.tw = int32_t(info->tile_width ? info->tile_width : info->width);
+    g.th = int32_t(info->tile_height ? info->tile_height : info->height);
+    g.n_tiles = int32_t(std::max(1u, info->num_tiles));
+    g.stride = int32_t(tile_stride);
+    g.offset = int32_t(tile_offset);
+    const hipError_t e = launch_gather_tiles(g, static_cast<hipStream_t>(stream));
+    (void)hipSetDevice(cur);
+    HIP_TRY(e);
+    return HEIFGPU_OK;
+}
+
+namespace {
+std::mutex g_ipc_mu;
+std::vector<std::pair<void *, void *>> g_ipc_open;  // (pointer returned, mapping base)
+}  // namespace
+
+int heifgpu_ipc_export(const void *dev_ptr, heifgpu_ipc_handle *out) {
+    static_assert(sizeof(hipIpcMemHandle_t) == sizeof(out->handle), "hipIpcMemHandle_t is 64 bytes");
+    if (!dev_ptr || !out) return fail(HEIFGPU_E_INVALID, "null argument");
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    HIP_TRY(hipMemGetAddressRange(&base, &size, const_cast<void *>(dev_ptr)));
+    hipIpcMemHandle_t h;
+    HIP_TRY(hipIpcGetMemHandle(&h, base));
+    std::memcpy(out->handle, &h, sizeof(h));
+    out->offset = uint64_t(static_cast<const uint8_t *>(dev_ptr) - static_cast<const uint8_t *>(base));
+    return HEIFGPU_OK;
+}
+
+int heifgpu_ipc_open(int device, const heifgpu_ipc_handle *h, void **dev_ptr) {
+    if (!h || !dev_ptr) return fail(HEIFGPU_E_INVALID, "null argument");
+    *dev_ptr = nullptr;
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(device));
+    hipIpcMemHandle_t mh;
+    std::memcpy(&mh, h->handle, sizeof(mh));
+    void *base = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&base, mh, hipIpcMemLazyEnablePeerAccess);
+    (void)hipSetDevice(cur);
+    HIP_TRY(e);
+    *dev_ptr = static_cast<uint8_t *>(base) + h->offset;
+    std::lock_guard<std::mutex> lk(g_ipc_mu);
+    g_ipc_open.emplace_back(*dev_ptr, base);
+    return HEIFGPU_OK;
+}
+
+int heifgpu_ipc_close(void *dev_ptr) {
+    void *base = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_ipc_mu);
+        for (size_t i = 0; i < g_ipc_open.size(); ++i)
+            if (g_ipc_open[i].first == dev_ptr) {
+                base = g_ipc_open[i].second;
+                g_ipc_open.erase(g_ipc_open.begin() + long(i));
+                break;
+            }
+    }
+    if (!base) return fail(HEIFGPU_E_INVALID, "not a pointer returned by heifgpu_ipc_open");
+    HIP_TRY(hipIpcCloseMemHandle(base));
     return HEIFGPU_OK;
 }
 

@@ -282,7 +282,8 @@ void validate_sps(const SequenceParameterSet &s) {
         (s.pic_width_in_luma_samples & ((1 << min_cb) - 1)) || (s.pic_height_in_luma_samples & ((1 << min_cb) - 1)))
         throw HeifError("picture size is not a multiple of MinCbSizeY");
     if (s.pcm_enabled_flag &&
-        (s.log2_max_pcm > (ctb < 5 ? ctb : 5) || s.pcm_bit_depth_luma > 8 + s.bit_depth_luma_minus8 ||
+        (s.log2_max_pcm > (ctb < 5 ? ctb : 5) || s.log2_min_pcm < (min_cb < 5 ? min_cb : 5) ||
+         s.pcm_bit_depth_luma > 8 + s.bit_depth_luma_minus8 ||
          s.pcm_bit_depth_chroma > 8 + s.bit_depth_chroma_minus8))
         throw HeifError("PCM parameters out of range");
     if (s.bit_depth_luma_minus8 > 2 || s.bit_depth_chroma_minus8 > 2)

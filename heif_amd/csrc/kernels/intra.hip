@@ -392,6 +392,8 @@ template <typename Pel>
 __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch *L, const TuRec &tb, const TuRec &tr,
                                                                    const Win<Pel> &wb, const Win<Pel> &wr, int PW,
                                                                    int PH, int bd, int lane) {
+    // lanes 0-31 predict Cb and 32-63 Cr: the pairing needs a full 64-lane wave
+    static_assert(kWave == 64, "predict_pair splits a 64-lane wave into two halves");
     const int log2n = tb.log2, n = 1 << log2n, mode = tb.mode;
     const int x0 = tb.x, y0 = tb.y;
     const int h = lane >> 5, sl = lane & 31;

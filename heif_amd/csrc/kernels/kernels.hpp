@@ -69,6 +69,14 @@ struct ColorArgs {
     int32_t yoff, ys;        // luma offset (16 limited range / 0 full) and scale (16.16)
     int32_t cr_r, cb_g, cr_g, cb_b;  // H.273 chroma weights (16.16, limited range rescaled)
 };
+// k_gather_tiles (gather.hip): tile windows k % stride == offset of src → dst
+struct GatherArgs {
+    uint64_t dst[3], src[3];  // planes (device pointers; src may be a peer / IPC mapping)
+    int32_t dpitch[3], spitch[3];
+    int32_t planes, bps;      // 1 or 3 planes (4:0:0 / 4:2:0), bytes per sample
+    int32_t W, H;             // luma output size
+    int32_t tw, th, cols, n_tiles, stride, offset;
+};
 // H.273 coefficients for matrix_coefficients / video_full_range_flag, rounded to 16.16
 inline void color_coefs(uint32_t matrix, bool full, ColorArgs &c) {
     double kr = 0.299, kb = 0.114;  // BT.601 (5, 6, and the unspecified default)
@@ -134,6 +142,7 @@ void emu_sao_out(const BatchArgs &a);
 #else
 hipError_t launch_rbsp(const BatchArgs &a, hipStream_t s);
 hipError_t launch_ycbcr_rgb(const ColorArgs &c, int bytes_per_sample, hipStream_t s);
+hipError_t launch_gather_tiles(const GatherArgs &g, hipStream_t s);
 hipError_t launch_parse(const BatchArgs &a, hipStream_t s);
 hipError_t launch_transform(const BatchArgs &a, hipStream_t s);
 hipError_t launch_intra(const BatchArgs &a, hipStream_t s);

@@ -159,12 +159,32 @@ int heifgpu_decode_batch(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, siz
 
 /* Gather of a tile split: copies the visible windows of the grid tiles k with
  * k % tile_stride == tile_offset from `src` (planes decoded by a batch with
- * those options, possibly on another device) into `dst` (full-size planes),
- * with 2-D copies on `stream` (a stream of dst's device; peer copies over
- * xGMI when the devices differ, peer access enabled here).  `info` describes
- * the image (heifgpu_image_get_info). */
+ * those options) into `dst` (full-size planes) with one kernel launch on
+ * `stream`, a stream of dst's device.  src may live on another device: a
+ * pointer of this process (peer access is enabled here) or a peer process's
+ * planes mapped with heifgpu_ipc_open; the kernel reads them over xGMI.
+ * Ordering: the copy reads src when it runs on `stream`, so the caller must
+ * order `stream` after the decode that wrote src (synchronise that decode, or
+ * make `stream` wait for an event recorded after it; across processes, the
+ * owner synchronises before it signals the gathering process).  `info`
+ * describes the image (heifgpu_image_get_info). */
 int heifgpu_gather_tiles(const heifgpu_image_info *info, const heifgpu_planes *dst, const heifgpu_planes *src,
                          uint32_t tile_stride, uint32_t tile_offset, void *stream);
+
+/* Cross-process device memory (the tile split with one process per GPU):
+ * heifgpu_ipc_export describes the device allocation holding `dev_ptr` (a HIP
+ * IPC handle plus the pointer's offset in it); another process passes the
+ * 72 bytes (e.g. over torch.distributed) to heifgpu_ipc_open, which maps the
+ * allocation on `device` and returns the same byte's address there.
+ * heifgpu_ipc_close unmaps a pointer heifgpu_ipc_open returned.  The owner
+ * must keep the allocation alive until every importer has closed it. */
+typedef struct {
+    uint8_t handle[64];  /* hipIpcMemHandle_t */
+    uint64_t offset;     /* dev_ptr - allocation base */
+} heifgpu_ipc_handle;
+int heifgpu_ipc_export(const void *dev_ptr, heifgpu_ipc_handle *out);
+int heifgpu_ipc_open(int device, const heifgpu_ipc_handle *h, void **dev_ptr);
+int heifgpu_ipc_close(void *dev_ptr);
 
 /* ---- YCbCr -> RGB with the irot rotation (libheif's default output) -------
  * Converts one decoded image (planes as written by heifgpu_batch_decode,

@@ -74,7 +74,7 @@ def _ptl(w: BitWriter, profile: int):
 
 SPS_DEFAULTS = dict(chroma_format=1, width=128, height=96, conf=None, bit_depth=8, log2_min_cb_minus3=0,
                     log2_diff_max_min_cb=2, log2_min_tb_minus2=0, log2_diff_max_min_tb=3, depth_inter=0,
-                    depth_intra=1, sao=1)
+                    depth_intra=1, sao=1, pcm=None)
 
 
 def sps(**over) -> bytes:
@@ -111,7 +111,16 @@ def sps(**over) -> bytes:
     w.u(0, 1)  # scaling_list_enabled
     w.u(0, 1)  # amp
     w.u(p["sao"], 1)
-    w.u(0, 1)  # pcm
+    if p["pcm"] is None:
+        w.u(0, 1)  # pcm_enabled_flag
+    else:  # (bit depth luma, chroma, log2_min_pcm_cb_size_minus3, log2_diff_max_min_pcm_cb_size)
+        w.u(1, 1)
+        bdy, bdc, mn, df = p["pcm"]
+        w.u(bdy - 1, 4)
+        w.u(bdc - 1, 4)
+        w.ue(mn)
+        w.ue(df)
+        w.u(0, 1)  # pcm_loop_filter_disabled_flag
     w.ue(0)    # num_short_term_ref_pic_sets
     w.u(0, 1)
     w.u(0, 1)

@@ -131,9 +131,19 @@ def test_conformance_window_legal_crop_accepted():
     dict(width=100),                               # not a multiple of MinCbSize
     dict(width=0),
     dict(width=20000),                             # beyond the level 6.2 limit
+    dict(pcm=(8, 8, 0, 3)),                        # Log2MaxIpcmCbSizeY 6 > Min(CtbLog2SizeY, 5)
+    dict(log2_min_cb_minus3=1, log2_diff_max_min_cb=1, log2_diff_max_min_tb=2,
+         pcm=(8, 8, 0, 1)),                        # Log2MinIpcmCbSizeY 3 < Min(MinCbLog2SizeY 4, 5) (7.4.3.2)
+    dict(pcm=(9, 8, 0, 1)),                        # PCM luma bit depth above BitDepthY
 ])
 def test_sps_out_of_range_rejected(over):
     _assert_error(_with_sets(sps=W.sps(**over)))
+
+
+def test_valid_pcm_sps_accepted():
+    """PCM enabled with legal sizes parses (a PCM CU itself is reported per picture as unsupported)."""
+    d = _with_sets(sps=W.sps(log2_min_cb_minus3=1, log2_diff_max_min_cb=1, log2_diff_max_min_tb=2, pcm=(8, 8, 1, 0)))
+    assert H.HeifImage.parse(d).info.width == 128
 
 
 def test_bit_depth_above_10_is_unsupported():

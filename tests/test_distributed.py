@@ -4,6 +4,7 @@ and the timed region reduces with MAX over ranks."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -91,3 +92,149 @@ def test_tile_split_ranks_compose_the_image():
     tbs, failures = q.get()
     assert failures == 0
     assert tbs == 207654
+
+
+# ---------------------------------------------------------------- e2 gather
+class _Info:
+    width, height, tile_width, tile_height, grid_cols, num_tiles, chroma = 1000, 700, 256, 256, 4, 12, 1
+
+
+def _windows(k, c, info=_Info):
+    """Plane-c window of grid tile k (k_gather_tiles' geometry, gather.hip)."""
+    sh = 1 if c else 0
+    pw, ph = (info.width + sh) >> sh, (info.height + sh) >> sh
+    x0, y0 = ((k % info.grid_cols) * info.tile_width) >> sh, ((k // info.grid_cols) * info.tile_height) >> sh
+    if x0 >= pw or y0 >= ph:
+        return None
+    w, h = min(info.tile_width >> sh, pw - x0), min(info.tile_height >> sh, ph - y0)
+    return slice(y0, y0 + h), slice(x0, x0 + w)
+
+
+class _ShmBackend:
+    """CPU stand-in for tile_split.DeviceBackend: "device memory" is shared
+    memory, addresses are fake 64-bit integers (one region per mapping), so
+    the handle exchange, the per-rank base + offset arithmetic and the open /
+    close / barrier order run exactly as on the GPU; k_gather_tiles is the
+    numpy window copy above."""
+
+    def __init__(self, rank):
+        self.regions = {}  # base -> (SharedMemory, ndarray)
+        self.next = (rank + 1) << 40
+        self.opened = 0
+
+    def _map(self, shm):
+        base = self.next
+        self.next += 1 << 32
+        self.regions[base] = (shm, np.ndarray((shm.size,), np.uint8, shm.buf))
+        return base
+
+    def alloc(self, info=_Info):
+        from multiprocessing import shared_memory
+
+        dims = [(info.height, info.width)] + [((info.height + 1) // 2, (info.width + 1) // 2)] * 2
+        offs, total = [], 0
+        for h, w in dims:
+            offs.append((total, h, w))
+            total += (h * w + 255) // 256 * 256
+        shm = shared_memory.SharedMemory(create=True, size=total)
+        base = self._map(shm)
+        return [{"planes": [(base + o, w) for o, h, w in offs], "dims": dims}], (shm, base)
+
+    def view(self, ptr, pitch, h, w):
+        base = max(b for b in self.regions if b <= ptr)
+        arr = self.regions[base][1]
+        o = ptr - base
+        return arr[o:o + h * pitch].reshape(h, pitch)[:, :w]
+
+    def sync(self):
+        pass
+
+    def export(self, buf):
+        return buf[0].name.encode()
+
+    def open(self, blob):
+        from multiprocessing import shared_memory
+
+        self.opened += 1
+        return self._map(shared_memory.SharedMemory(name=blob.decode()))
+
+    def close(self, ptr):
+        shm, _ = self.regions.pop(ptr)
+        shm.close()
+
+    @staticmethod
+    def buffer_ptr(buf):
+        return buf[1]
+
+    @staticmethod
+    def planes(out):
+        return out["planes"]
+
+    def _copy(self, dst, src_pl, stride, offset):
+        for k in range(offset, _Info.num_tiles, stride):
+            for c, ((dp, dpitch), (sp, spitch), (h, w)) in enumerate(zip(dst["planes"], src_pl, dst["dims"])):
+                win = _windows(k, c)
+                if win is not None:
+                    self.view(dp, dpitch, h, w)[win] = self.view(sp, spitch, h, w)[win]
+
+    def gather_own(self, dst, src, stride, offset):
+        self._copy(dst, src["planes"], stride, offset)
+
+    def gather_from(self, dst, src_ptrs, pitches, stride, offset):
+        self._copy(dst, list(zip(src_ptrs, pitches)), stride, offset)
+
+
+def _pattern(k, c):
+    return (k * 7 + c * 3 + 1) & 0xFF
+
+
+def _gather_worker(rank, world, port, out):
+    from heif_amd.tile_split import gather_to_rank0
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    be = _ShmBackend(rank)
+    outs, buf = be.alloc()
+    # "decode" this rank's tiles k % world == rank; every other sample keeps a sentinel
+    for c, ((p, pitch), (h, w)) in enumerate(zip(outs[0]["planes"], outs[0]["dims"])):
+        v = be.view(p, pitch, h, w)
+        v[:] = 0xA5
+        for k in range(rank, _Info.num_tiles, world):
+            win = _windows(k, c)
+            if win is not None:
+                v[win] = _pattern(k, c)
+    full = None
+    if rank == 0:
+        full, fbuf = be.alloc()
+    gather_to_rank0(be, dist, outs, buf, full, rank, world)
+    if rank == 0:
+        bad = 0
+        for c, ((p, pitch), (h, w)) in enumerate(zip(full[0]["planes"], full[0]["dims"])):
+            v = be.view(p, pitch, h, w)
+            for k in range(_Info.num_tiles):
+                win = _windows(k, c)
+                if win is not None:
+                    bad += int((v[win] != _pattern(k, c)).sum())
+        out.put((bad, be.opened, len(be.regions)))
+        fbuf[0].close()
+        fbuf[0].unlink()
+    dist.barrier()
+    buf[0].close()
+    buf[0].unlink()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tile_split_gather_to_rank0_over_gloo(world):
+    """Row e2's cross-process gather (heif_amd/tile_split.py, used by bench.py
+    --split tiles and the multi-GPU bench check) on CPU: handles exchanged with
+    all_gather_object, rank 0 maps world - 1 peer buffers, copies every peer's
+    tile windows at the peer's own base + the shared plane offsets, unmaps them,
+    and the assembled planes hold every tile exactly once."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.start_processes(_gather_worker, args=(world, _free_port(), q), nprocs=world, join=True, start_method="spawn")
+    bad, opened, live = q.get()
+    assert bad == 0
+    assert opened == world - 1
+    assert live == 2  # rank 0's own two buffers; every peer mapping closed
