@@ -55,6 +55,9 @@ sys.path.insert(0, str(ROOT))
 
 SAMPLE = ROOT / "tests" / "golden" / "halfmoonbay.heic"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+ROUND = "r03"
+PROFILES = ROOT / "profiles" / ROUND
+BINS_PER_IMAGE = 15358022  # CABAC bins of one halfmoonbay image (oracle count; every permutation has the same)
 
 
 def dist_env():
@@ -381,15 +384,40 @@ def main():
         # algorithmic bytes of this rank's launch (its tile share in a split)
         launch_bytes = args.batch * algo_per_image * len(range(offset, info.num_tiles, stride)) // info.num_tiles
         achieved = launch_bytes / (parse_ms / 1e3) / 1e9
-        traffic = None
-        tfile = ROOT / "profiles" / "pmc_traffic.json"
-        if tfile.exists():
+        geom = batch.parse_geometry()
+        kname = "k_parse_solo" if geom["mode"] == "solo" else "k_parse_lanes"
+        # counter evidence of this round (profiles/<round>/, written by tools/pmc_*.sh on the same
+        # command): HBM bytes per launch (FETCH_SIZE / WRITE_SIZE passes) and the parse's SQ counters
+        traffic, issue = None, None
+        same_cfg = lambda j: (j.get("batch", j.get("batch_images")) == args.batch and not tiles_split and not c5
+                              and j.get("parse_mode", "lanes") == geom["mode"])
+        try:
+            tj = json.loads((PROFILES / "pmc_traffic.json").read_text())
+            if same_cfg(tj):
+                traffic = tj.get("k_parse_hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        bins = args.batch * BINS_PER_IMAGE if not c5 and not tiles_split else None
+        if bins:
+            issue = {"bins_per_launch": bins, "bins_per_s": round(bins / (parse_ms / 1e3), 1)}
             try:
-                tj = json.loads(tfile.read_text())
-                if tj.get("batch") == args.batch and tj.get("chunks", 1) == chunks and not tiles_split and not c5:
-                    traffic = tj.get("k_parse_hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+                pj = json.loads((PROFILES / f"parse_counters_{geom['mode']}.json").read_text())
+                if same_cfg(pj):
+                    pl, pw = pj["per_launch"], pj.get("per_wave", {})
+                    valu, salu = pl["SQ_INSTS_VALU"] / bins, pl["SQ_INSTS_SALU"] / bins
+                    issue.update({
+                        "wave_instr_per_bin": round((pl["SQ_INSTS_VALU"] + pl["SQ_INSTS_SALU"] + pl["SQ_INSTS_LDS"]
+                                                     + pl["SQ_INSTS_BRANCH"] + pl.get("SQ_INSTS_VMEM", 0)) / bins, 3),
+                        "valu_per_bin": round(valu, 3), "salu_per_bin": round(salu, 3),
+                        # one wave alone issues a VALU op every 4 cycles and an SALU op every cycle
+                        # (MI355X_MICROARCH.md); SQ_WAVE_CYCLES counts quad-cycles
+                        "issue_floor_frac": round((4 * pw["SQ_INSTS_VALU"] + pw["SQ_INSTS_SALU"])
+                                                  / (4 * pw["SQ_WAVE_CYCLES"]), 4),
+                        "wait_frac": round(pl["SQ_WAIT_ANY"] / pl["SQ_WAVE_CYCLES"], 4),
+                        "source": f"profiles/{ROUND}/parse_counters_{geom['mode']}.json",
+                    })
+            except (OSError, ValueError, KeyError, ZeroDivisionError):
+                pass
         line = {
             "metric": ("Mpixels/s decoded (bit-exact) on 7680x4320 Main-10 HEIC batch" if c5 else
                        "Mpixels/s decoded (bit-exact) on 4032x3024 HEIC batch"),
@@ -422,11 +450,14 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": traffic,
-                "kernel": "k_parse (CABAC, one WPP row per lane)" if os.environ.get("HEIFGPU_PARSE", "lanes")[:1] != "s"
-                          else "k_parse (CABAC, one picture per wave)",
+                "traffic_source": f"profiles/{ROUND}/pmc_traffic.json" if traffic else None,
+                "kernel": kname,
+                "parse_geometry": geom,
                 "kernel_ms_per_launch": round(parse_ms / chunks, 3),
                 "algorithmic_bytes_per_launch": launch_bytes // chunks,
                 "launches_per_step": chunks,
+                "binding": "per-bin CABAC dependency chain (issue / latency), not HBM: see `issue`",
+                "issue": issue,
             },
             "stage_ms_per_step": {k: round(v, 3) for k, v in zip(
                 ["parse", "transform", "intra", "deblock", "sao_out", "rbsp"], per_step)},

@@ -1,13 +1,14 @@
 #!/bin/bash
 # SQ counters of k_parse_lanes (one rocprofv3 --pmc pass per counter set,
 # each within the 8-SQ-counter limit), reduced to per-launch and per-bin
-# figures in gpurun_out/pmc_parse/parse_counters.json.
-# usage: tools/pmc_parse.sh [library-suffix]   (on the GPU box, repo root)
+# figures in gpurun_out/pmc_parse/parse_counters_<mode>.json.
+# usage: [PARSE=lanes|solo] tools/pmc_parse.sh [library-suffix]   (on the GPU box, repo root)
 V=$1
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 LIB=$R/heif_amd/libheifgpu${V:+_$V}.so
 OUT=$R/gpurun_out/pmc_parse${V:+_$V}
 BATCH=${PMC_BATCH:-128}
+MODE=${PARSE:-lanes}
 cd /tmp && export TMPDIR=/tmp
 mkdir -p "$OUT"
 i=0
@@ -16,11 +17,11 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_
            "SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_IFETCH"; do
     i=$((i + 1))
     HEIFGPU_LIBRARY=$LIB timeout -s KILL 300 rocprofv3 --pmc $set -d "$OUT/set$i" -o p --output-format csv -- \
-        python3 "$R/bench.py" --batch "$BATCH" --steps 1 --warmup 1 --no-cpu-baseline --verify 0 > "$OUT/set$i.log" 2>&1 || { [ $i -eq 3 ] || exit 1; }
+        python3 "$R/bench.py" --batch "$BATCH" --parse "$MODE" --steps 1 --warmup 1 --no-cpu-baseline --no-e2e --verify 0 > "$OUT/set$i.log" 2>&1 || { [ $i -eq 3 ] || exit 1; }
 done
-python3 - "$OUT" "$BATCH" <<'PY'
+python3 - "$OUT" "$BATCH" "$MODE" <<'PY'
 import csv, collections, glob, json, sys
-out, batch = sys.argv[1], int(sys.argv[2])
+out, batch, mode = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 acc = collections.defaultdict(float)
 disp = collections.defaultdict(set)
 for f in glob.glob(out + "/set*/**/p_counter_collection.csv", recursive=True):
@@ -31,7 +32,8 @@ for f in glob.glob(out + "/set*/**/p_counter_collection.csv", recursive=True):
 per_launch = {k: v / len(disp[k]) for k, v in sorted(acc.items())}
 bins = batch * 15358022  # bins per halfmoonbay image (oracle count)
 res = {
-    "kernel": "k_parse_lanes",
+    "kernel": "k_parse_" + mode,
+    "parse_mode": mode,
     "batch_images": batch,
     "bins_per_launch": bins,
     "per_launch": {k: round(v) for k, v in per_launch.items()},
@@ -41,6 +43,6 @@ res = {
 w = per_launch.get("SQ_WAVES")
 if w:
     res["per_wave"] = {k: round(v / w, 1) for k, v in per_launch.items()}
-json.dump(res, open(out + "/parse_counters.json", "w"), indent=1)
+json.dump(res, open(out + f"/parse_counters_{mode}.json", "w"), indent=1)
 print(json.dumps(res["per_bin"]))
 PY

@@ -49,13 +49,13 @@ def main():
     out = {
         "tag": tag,
         "batch": bench["config"]["images_per_gpu"],
+        "parse_mode": bench["roofline"].get("parse_geometry", {}).get("mode", "lanes"),
         "k_parse_hbm_bytes_per_launch": round(parse["hbm_bytes_corrected"]),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of "
                   "`bench.py --steps 1 --warmup 1`; bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
         "kernels": kernels,
     }
     (dst / "pmc_traffic.json").write_text(json.dumps(out, indent=2) + "\n")
-    (ROOT / "profiles" / "pmc_traffic.json").write_text(json.dumps(out, indent=2) + "\n")
     print(json.dumps(out, indent=2))
 
 
