@@ -194,7 +194,9 @@ class DecodeContext:
         in place; wait=False returns before the upload has finished (the next
         decode of the batch waits for it).  parse: "auto" (by batch size),
         "lanes" (one substream per lane, `pics_per_wave` pictures per wave, 0 =
-        adaptive) or "solo" (one substream per wave: small-batch latency)."""
+        adaptive), "solo" (one substream per wave, a picture's rows in one
+        workgroup) or "spread" (one substream per wave, one workgroup per row:
+        small-batch latency)."""
         arr = (ctypes.c_void_p * len(images))(*[im._h.value for im in images])
         opts = _lib.BatchOpts(tile_stride, tile_offset, _lib.PARSE_MODES[parse], pics_per_wave)
         if reuse is not None:
@@ -306,7 +308,7 @@ class DeviceBatch:
         """The CABAC parse launch of this batch (heifgpu_batch_parse_geometry)."""
         v = [ctypes.c_uint32() for _ in range(4)]
         _lib.check(lib.heifgpu_batch_parse_geometry(self._h, *[ctypes.byref(x) for x in v]))
-        mode = {_lib.PARSE_LANES: "lanes", _lib.PARSE_SOLO: "solo"}[v[0].value]
+        mode = {_lib.PARSE_LANES: "lanes", _lib.PARSE_SOLO: "solo", _lib.PARSE_SPREAD: "spread"}[v[0].value]
         return {"mode": mode, "workgroups": v[1].value, "pics_per_wave": v[2].value,
                 "waves_per_workgroup": v[3].value}
 

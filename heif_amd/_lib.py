@@ -120,8 +120,8 @@ class IpcHandle(ctypes.Structure):
     _fields_ = [("handle", ctypes.c_uint8 * 64), ("offset", ctypes.c_uint64)]
 
 
-PARSE_AUTO, PARSE_LANES, PARSE_SOLO = 0, 1, 2
-PARSE_MODES = {"auto": PARSE_AUTO, "lanes": PARSE_LANES, "solo": PARSE_SOLO}
+PARSE_AUTO, PARSE_LANES, PARSE_SOLO, PARSE_SPREAD = 0, 1, 2, 3
+PARSE_MODES = {"auto": PARSE_AUTO, "lanes": PARSE_LANES, "solo": PARSE_SOLO, "spread": PARSE_SPREAD}
 
 
 # every symbol include/heifgpu.h declares (checked by tests/test_abi.py)

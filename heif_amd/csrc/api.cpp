@@ -29,7 +29,9 @@ struct heifgpu_image {
 static_assert(sizeof(heifgpu_image_info) == 80, "heifgpu_image_info: 20 x uint32");
 static_assert(sizeof(heifgpu_planes) == 40, "heifgpu_planes: 3 pointers + 3 int32 (+ padding)");
 static_assert(sizeof(heifgpu_batch_opts) == 16, "heifgpu_batch_opts: 4 x uint32");
-static_assert(HEIFGPU_PARSE_AUTO == PARSE_AUTO && HEIFGPU_PARSE_LANES == PARSE_LANES && HEIFGPU_PARSE_SOLO == PARSE_SOLO,
+static_assert(sizeof(heifgpu_ipc_handle) == 72, "heifgpu_ipc_handle: 64-byte HIP handle + uint64 offset");
+static_assert(HEIFGPU_PARSE_AUTO == PARSE_AUTO && HEIFGPU_PARSE_LANES == PARSE_LANES && HEIFGPU_PARSE_SOLO == PARSE_SOLO &&
+                  HEIFGPU_PARSE_SPREAD == PARSE_SPREAD,
               "parse modes");
 static_assert(sizeof(heifgpu_tile_params) == 55 * 4 + 64 * 4, "heifgpu_tile_params: 55 int32 + 64 uint32");
 
@@ -179,7 +181,8 @@ struct heifgpu_batch {
     BatchArgs args{};
     DevBuf<uint8_t> bits, rbsp, sf, recon;
     DevBuf<PicDesc> pics;
-    DevBuf<uint32_t> subs, rsubs, porder;
+    DevBuf<uint32_t> subs, rsubs, porder, xprog;
+    DevBuf<uint8_t> xctx;
     DevBuf<SeqParams> seqs;
     DevBuf<OutImage> outs;
     ParseSet set[3];
@@ -491,7 +494,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     const uint32_t offset = opts ? opts->tile_offset : 0u;
     if (offset >= stride) return fail(HEIFGPU_E_INVALID, "tile_offset must be below tile_stride");
     const uint32_t mode_req = opts ? opts->parse_mode : 0u;
-    if (mode_req > HEIFGPU_PARSE_SOLO) return fail(HEIFGPU_E_INVALID, "parse_mode");
+    if (mode_req > HEIFGPU_PARSE_SPREAD) return fail(HEIFGPU_E_INVALID, "parse_mode");
     const int ppw_req = opts ? int(std::min<uint32_t>(opts->pics_per_wave, 64u)) : 0;
     if (*inout && (*inout)->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
     HIP_TRY(hipSetDevice(ctx->device));
@@ -539,8 +542,14 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     std::vector<uint32_t> order;
     const int mode = parse_mode_for(int(mode_req), int(hb.pics.size()));
     const int solo_waves = solo_waves_for(hb.lane_rows);
-    const int parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows,
-                                              mode == PARSE_SOLO ? 1 : ppw_req, order);
+    int parse_group = 1;
+    if (mode == PARSE_SPREAD) {
+        if (spread_parse_order(hb.pics.data(), int(hb.pics.size()), order) < 0)
+            return fail(HEIFGPU_E_UNSUPPORTED, "spread parse: over 2^20 pictures or 4096 substreams per picture");
+    } else {
+        parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows,
+                                        mode == PARSE_SOLO ? 1 : ppw_req, order);
+    }
     const bool grows = (order.size() > b->porder.cap || hb.bits_size > b->bits.cap || hb.pics.size() > b->pics.cap ||
                                      hb.subs.size() > b->subs.cap || hb.seqs.size() > b->seqs.cap ||
                                      hb.sf.size() > b->sf.cap || n > b->outs.cap || hb.recon_bytes > b->recon.cap ||
@@ -574,6 +583,10 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     }
     HIP_TRY(b->recon.alloc(hb.recon_bytes));
     HIP_TRY(b->porder.alloc(order.size()));
+    if (mode == PARSE_SPREAD) {  // per-row WPP progress words and context hand-off blocks
+        HIP_TRY(b->xprog.alloc(std::max<size_t>(hb.rows, 1)));
+        HIP_TRY(b->xctx.alloc(std::max<size_t>(hb.rows, 1) * CTX_PAD));
+    }
     // ---- one pinned staging image of every upload, copied asynchronously
     struct Seg {
         const void *src;
@@ -651,6 +664,8 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.lane_rows = hb.lane_rows;
     a.parse_mode = mode;
     a.solo_waves = solo_waves;
+    a.xprog = mode == PARSE_SPREAD ? b->xprog.p : nullptr;
+    a.xctx = mode == PARSE_SPREAD ? b->xctx.p : nullptr;
     // rows wrap round the lanes (waves) of a picture: the WPP context staging
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.total_rows = int(hb.rows);
@@ -780,9 +795,9 @@ int heifgpu_batch_parse_geometry(const heifgpu_batch *b, uint32_t *mode, uint32_
                                  uint32_t *pics_per_wave, uint32_t *waves_per_workgroup) {
     if (!b || !b->loaded) return fail(HEIFGPU_E_INVALID, "invalid batch");
     const BatchArgs &a = b->args;
-    const bool solo = a.parse_mode == PARSE_SOLO;
-    const uint32_t ppw = solo ? 1u : uint32_t(std::max(1, a.parse_group));
-    if (mode) *mode = solo ? HEIFGPU_PARSE_SOLO : HEIFGPU_PARSE_LANES;
+    const bool solo = a.parse_mode == PARSE_SOLO, lanes = a.parse_mode == PARSE_LANES;
+    const uint32_t ppw = lanes ? uint32_t(std::max(1, a.parse_group)) : 1u;
+    if (mode) *mode = uint32_t(a.parse_mode);
     if (workgroups) *workgroups = (uint32_t(a.n_slots) + ppw - 1) / ppw;
     if (pics_per_wave) *pics_per_wave = ppw;
     if (waves_per_workgroup) *waves_per_workgroup = solo ? uint32_t(a.solo_waves) : 1u;

@@ -13,6 +13,7 @@
 
 #include "../../../oracle/oracle.h"
 #include "../host/batch.hpp"
+#include "../kernels/cabac.hpp"
 #include "../kernels/kernels.hpp"
 
 namespace hg {
@@ -64,8 +65,11 @@ int main(int argc, char **argv) {
     std::vector<uint32_t> order;
     const int mode = parse_mode_for(PARSE_AUTO, int(hb.pics.size()));
     const int solo_waves = solo_waves_for(hb.lane_rows);
-    const int parse_group =
-        lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0, order);
+    int parse_group = 1;
+    if (mode == PARSE_SPREAD) spread_parse_order(hb.pics.data(), int(hb.pics.size()), order);
+    else parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0, order);
+    std::vector<uint32_t> xprog(hb.rows + 1);
+    std::vector<uint8_t> xctx((hb.rows + 1) * size_t(CTX_PAD));
     a.parse_order = order.data();
     a.n_slots = int(order.size());
     a.parse_group = parse_group;
@@ -88,6 +92,8 @@ int main(int argc, char **argv) {
     a.lane_rows = hb.lane_rows;
     a.parse_mode = mode;
     a.solo_waves = solo_waves;
+    a.xprog = xprog.data();
+    a.xctx = xctx.data();
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = bps;
@@ -100,7 +106,7 @@ int main(int argc, char **argv) {
         ntu += rc[2 * r];
         ncoef += rc[2 * r + 1];
     }
-    printf("parse mode: %s\n", mode == PARSE_SOLO ? "solo" : "lanes");
+    printf("parse mode: %s\n", mode == PARSE_SOLO ? "solo" : mode == PARSE_SPREAD ? "spread" : "lanes");
     printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);
     if (stages >= 2) emu_transform(a);
     if (stages >= 3) emu_intra(a);

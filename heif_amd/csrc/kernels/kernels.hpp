@@ -54,6 +54,8 @@ struct BatchArgs {
     int wpp_ring;              // some WPP picture has more CTB rows than lanes (its rows wrap round its lanes)
     int parse_mode;            // PARSE_LANES (k_parse_lanes) or PARSE_SOLO (k_parse_solo)
     int solo_waves;            // k_parse_solo waves per workgroup (solo_waves_for(lane_rows))
+    uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
+    uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
 };
 
 // k_ycbcr_rgb (color.hip): one decoded image → interleaved RGB8, rotated
@@ -94,7 +96,7 @@ inline void color_coefs(uint32_t matrix, bool full, ColorArgs &c) {
 }
 
 // parse modes (BatchArgs::parse_mode; heifgpu_batch_opts::parse_mode)
-enum : int { PARSE_AUTO = 0, PARSE_LANES = 1, PARSE_SOLO = 2 };
+enum : int { PARSE_AUTO = 0, PARSE_LANES = 1, PARSE_SOLO = 2, PARSE_SPREAD = 3 };
 constexpr int kSoloMaxWaves = 16;
 // host: BatchArgs::parse_order for a batch (size-balanced k_parse_lanes waves,
 // or for solo mode with ppw_force = 1 one picture per workgroup, heaviest
@@ -103,6 +105,8 @@ constexpr int kSoloMaxWaves = 16;
 int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order);
 // the parse mode a batch of n_pics pictures runs in (requested: PARSE_*)
 int parse_mode_for(int requested, int n_pics);
+// spread mode's wave slots (row << 20 | picture); -1 if the batch exceeds the encoding
+int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order);
 int solo_waves_for(int lane_rows);
 
 #if defined(HG_HOST_EMU)

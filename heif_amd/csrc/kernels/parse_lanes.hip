@@ -40,10 +40,16 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #if defined(HG_HOST_EMU)
 #include <cstdio>
+#endif
+
+#if !defined(HG_HOST_EMU)
+// v_writelane_b32 (this clang exposes no builtin for it): lane `lane` of `old` := src
+extern "C" __device__ int hg_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 #endif
 
 namespace hg {
@@ -156,11 +162,17 @@ struct Lane {
     uint64_t rc_csbf;  // coded_sub_block_flag, bit yS * 8 + xS
     uint32_t ntu, ncoef;
     uint32_t tu_row, coef_row;  // TuRec / Coef index of the current row's outputs
+    // solo mode on the GPU: the context states, byte i of the LDS layout at
+    // byte i & 3 of lane i >> 2 (35 lanes), read / written with v_readlane /
+    // v_writelane; the one field whose lanes differ
+    uint32_t cx;
 };
 
 // engine context of one lane (lanes mode: every lane its own substream)
 struct Eng {
     static constexpr bool kSolo = false;
+    static constexpr bool kSpread = false;
+    static constexpr bool kCtxReg = false;  // contexts in LDS (ctx)
     uint8_t *ctx;
     const uint64_t *tab;  // per pStateIdx: rangeTabLps[4] | transIdxLps << 32 | transIdxMps << 40 (LDS)
     const uint64_t *seq;  // sig_seq(scan, pattern): slot of every scan position of a sub-block (LDS)
@@ -187,15 +199,27 @@ struct Win {
 #else
 struct Win {
     uint32_t r0, r1;
+    // both registers read and the result selected: a select of the register
+    // (or of its address) becomes a dynamically indexed array in scratch
     __device__ __forceinline__ uint32_t get(uint32_t d) const {
         const int ln = __builtin_amdgcn_readfirstlane((int)(d & 63u));
-        const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)((d >> 6) & 1u));
-        return (uint32_t)__builtin_amdgcn_readlane((int)(k ? r1 : r0), ln);
+        const uint32_t v0 = (uint32_t)__builtin_amdgcn_readlane((int)r0, ln);
+        const uint32_t v1 = (uint32_t)__builtin_amdgcn_readlane((int)r1, ln);
+        return (d & 64u) ? v1 : v0;
     }
 };
 #endif
-struct EngSolo {
+template <bool Spread>
+struct EngSoloT {
     static constexpr bool kSolo = true;
+    // one wave per workgroup: the rows of a picture on different CUs, their
+    // WPP progress, context hand-off, SAO and depth lines in coherent global memory
+    static constexpr bool kSpread = Spread;
+#if defined(HG_HOST_EMU)
+    static constexpr bool kCtxReg = false;  // one lane per wave: contexts stay in the LDS block
+#else
+    static constexpr bool kCtxReg = true;   // contexts in Lane::cx
+#endif
     uint8_t *ctx;
     uint32_t tlo, thi;    // lane s: state_row(s) (GPU); unused under emulation
     const uint64_t *seq;
@@ -213,6 +237,35 @@ struct EngSolo {
     }
 #endif
 };
+using EngSolo = EngSoloT<false>;
+using EngSpread = EngSoloT<true>;
+
+#if !defined(HG_HOST_EMU)
+// Solo mode: the wave's substream state is equal in every lane; say so to the
+// compiler (v_readfirstlane), so the units keep it in SGPRs and branch on it
+// with s_cbranch instead of exec masks.
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int uni32(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
+}
+__device__ __forceinline__ void uni_state(Lane &L) {
+#define HG_U(f) L.f = uni32(L.f)
+    HG_U(range); HG_U(value); HG_U(k); HG_U(cn); HG_U(lb); HG_U(budget); HG_U(status); HG_U(st); HG_U(fl);
+    HG_U(row); HG_U(c); HG_U(ctbx); HG_U(ctby); HG_U(qx); HG_U(qy); HG_U(ql); HG_U(qd); HG_U(tx); HG_U(ty);
+    HG_U(tl); HG_U(td); HG_U(tcbf); HG_U(qp_prev_last); HG_U(qp_pred); HG_U(cu_qp_delta_val); HG_U(qpy_cur);
+    HG_U(qg_x); HG_U(qg_y); HG_U(cu_modes); HG_U(cu_chroma); HG_U(tb_t); HG_U(tb_n); HG_U(tb_cidx); HG_U(tb_x);
+    HG_U(tb_y); HG_U(tb_log2); HG_U(tb_mode); HG_U(tb_coef0); HG_U(rc_scan); HG_U(rc_last_sub); HG_U(rc_last_pos);
+    HG_U(rc_i); HG_U(rc_prev_c1); HG_U(ntu); HG_U(ncoef); HG_U(tu_row); HG_U(coef_row);
+#undef HG_U
+    L.cur = uni64(L.cur);
+    L.rc_csbf = uni64(L.rc_csbf);
+}
+#endif
+
+#if !defined(HG_SOLO_SLEEP)
+#define HG_SOLO_SLEEP 1
+#endif
 
 // driver side of a solo wave's RBSP window: chunks (64 dwords, 256 bytes) c
 // and c + 1 of the reader in the window, c + 2 staged (in flight)
@@ -239,8 +292,9 @@ struct SoloWin {
     }
     // the copy is the first use of the staged load: the compiler waits for it here
     __device__ __forceinline__ void commit(uint32_t chunk) {
-        if (chunk & 1u) r1 = f;
-        else r0 = f;
+        const bool odd = (chunk & 1u) != 0;  // both written: no address select
+        r1 = odd ? f : r1;
+        r0 = odd ? r0 : f;
     }
     __device__ __forceinline__ Win view() const { return Win{r0, r1}; }
 #endif
@@ -316,6 +370,26 @@ HG_HD inline void store_bytes(uint8_t *p, int n, uint64_t v) {
         for (int i = 0; i < n; ++i) p[i] = (uint8_t)(v >> (8 * (i & 7)));
     }
 }
+
+// Spread mode: words another CU reads (agent-scope atomics: sc1 accesses,
+// coherent across the XCDs' L2s without whole-cache write-backs), and the
+// wait that makes this wave's earlier such stores visible before a progress word
+#if defined(HG_HOST_EMU)
+template <class T>
+inline void store_agent(T *p, T v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+inline uint32_t load_agent(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+inline void stores_done() { std::atomic_thread_fence(std::memory_order_release); }
+#else
+template <class T>
+__device__ __forceinline__ void store_agent(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t load_agent(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// s_waitcnt vmcnt(0): every store of this wave has completed
+__device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0x0f70); }
+#endif
 
 HG_HD inline uint8_t load_byte_coherent(const uint8_t *p) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -395,7 +469,10 @@ HG_HD inline void q_refill(Lane &L, const Eng &G) {
     }
 }
 
-// value += 16 more look-ahead bits (k < 8 on entry, so k <= 23 and value < 2^32 after)
+// value += 16 more look-ahead bits (k < 8 on entry, so k <= 23 and value < 2^32 after).
+// (A/B r03: comparisons as sign masks with k <= 22 and v_bfi selects instead
+// of compares into VCC: parse 94 vs 91 ms at 128 images, 37.9 vs 36.1 ms for
+// one image in spread mode — the compares stay.)
 template <class EG>
 HG_HD inline void vfill(Lane &L, const EG &G) {
     if (L.cn < 16) {
@@ -436,14 +513,15 @@ HG_HD inline void engine_init(Lane &L, const EG &G, uint32_t start, uint32_t end
 }
 
 // ------------------------------------------------------------------ engine (9.3.4.3)
-// DecodeDecision (arithmetic.rs:97-144), branch-free: one LDS row per
-// pStateIdx gives rangeTabLps and both transitions; the renormalisation of
-// either path is a shift by clz and lowers k.
+// DecodeDecision (arithmetic.rs:97-144), branch-free: one row per pStateIdx
+// gives rangeTabLps and both transitions; the renormalisation of either path
+// is a shift by clz and lowers k.
 template <class EG>
 HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
     const uint32_t st = s >> 1, mps = s & 1u;
     const uint64_t row = G.row(st);
-    const uint32_t lps = ((uint32_t)row >> (((L.range >> 6) & 3u) << 3)) & 0xffu;
+    const uint32_t hi = (uint32_t)(row >> 32);  // transIdxLps | transIdxMps << 8
+    const uint32_t lps = ((uint32_t)row >> ((L.range >> 3) & 24u)) & 0xffu;
     const uint32_t rm = L.range - lps;
     const uint32_t sr = rm << L.k;
     const bool isl = L.value >= sr;
@@ -452,15 +530,49 @@ HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
     const int nb = __builtin_clz(rn) - 23;
     L.range = rn << nb;
     L.k -= nb;
-    const uint32_t nst = ((uint32_t)(row >> 32) >> (isl ? 0 : 8)) & 0xffu;
+    const uint32_t nst = (hi >> (isl ? 0 : 8)) & 0xffu;
     s = (nst << 1) | (mps ^ ((isl && st == 0) ? 1u : 0u));
     if (L.k < 8) vfill(L, G);
     return (int)(mps ^ (isl ? 1u : 0u));
 }
 
-// the same on context ci in LDS
+// context state ci: a byte of the LDS block, or (solo on the GPU) of Lane::cx
+template <class EG>
+HG_HD inline uint32_t ctx_ld(const Lane &L, const EG &G, int ci) {
+#if !defined(HG_HOST_EMU)
+    if constexpr (EG::kCtxReg) {
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)L.cx, ci >> 2);
+        return (w >> ((ci & 3) * 8)) & 0xffu;
+    }
+#endif
+    return G.ctx[ci];
+}
+template <class EG>
+HG_HD inline void ctx_st(Lane &L, const EG &G, int ci, uint32_t v) {
+#if !defined(HG_HOST_EMU)
+    if constexpr (EG::kCtxReg) {
+        const int sh = (ci & 3) * 8;
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)L.cx, ci >> 2);
+        L.cx = (uint32_t)hg_writelane((int)((w & ~(0xffu << sh)) | (v << sh)), ci >> 2, (int)L.cx);
+        return;
+    }
+#endif
+    G.ctx[ci] = (uint8_t)v;
+}
+
+// the same on context ci
 template <class EG>
 HG_HD inline int dec(Lane &L, const EG &G, int ci) {
+#if !defined(HG_HOST_EMU)
+    if constexpr (EG::kCtxReg) {  // one v_readlane serves the read and the write back
+        const int sh = (ci & 3) * 8;
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)L.cx, ci >> 2);
+        uint32_t s = (w >> sh) & 0xffu;
+        const int bin = dec_s(L, G, s);
+        L.cx = (uint32_t)hg_writelane((int)((w & ~(0xffu << sh)) | (s << sh)), ci >> 2, (int)L.cx);
+        return bin;
+    }
+#endif
     uint32_t s = G.ctx[ci];
     const int bin = dec_s(L, G, s);
     G.ctx[ci] = (uint8_t)s;
@@ -700,10 +812,12 @@ struct Env {
 };
 
 // WPP: the row above is two CTUs ahead of CTU L.c (or finished)
+template <class EG>
 HG_HD inline bool wpp_ready(const Lane &L, const LanePic &P, const Env &E) {
     if (!(L.fl & F_WPP) || L.row == 0) return true;
     const uint32_t need = (uint32_t)(L.row - 1) * (uint32_t)P.wctb + (uint32_t)(L.c + 2 < P.wctb ? L.c + 2 : P.wctb);
-    return prog_load(&E.prog[P.lane0 + (L.row - 1) % P.R]) >= need;
+    const uint32_t *pw = &E.prog[P.lane0 + (L.row - 1) % P.R];
+    return (EG::kSpread ? load_agent(pw) : prog_load(pw)) >= need;
 }
 
 // RBSP offset (absolute) at which a lane about to run U_CTU starts its
@@ -730,19 +844,36 @@ HG_HD inline void coef_push(Lane &L, const LanePic &P, uint32_t w) { P.coef_base
 // change while the row above is less than two CTUs ahead (WPP).
 template <class EG>
 HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const EG &G) {
-    if (!wpp_ready(L, P, E)) return;
+    if (!wpp_ready<EG>(L, P, E)) return;
     L.ctbx = L.c << P.log2ctb;
     L.ctby = L.row << P.log2ctb;
     if (L.c == 0 && ((L.fl & F_WPP) || L.row == 0)) {
         // substream start: contexts (init, or the WPP copy already in ld.ctx) + engine
-        if (L.row == 0 || P.wctb < 2 || !(L.fl & F_WPP)) {
+        if constexpr (EG::kCtxReg) {
+#if !defined(HG_HOST_EMU)
+            // every lane its dword of the contexts: initialised, or the row above's copy
+            const int ln = (int)__lane_id();
+            uint32_t w = 0;
+            if (L.row == 0 || P.wctb < 2 || !(L.fl & F_WPP)) {
+                for (int b = 0; b < 4; ++b) {
+                    const int i = 4 * ln + b;
+                    if (i < CTX_NUM) w |= (uint32_t)ctx_init_state(c_ctx_init_l[i], P.sliceQp) << (8 * b);
+                }
+            } else if (ln < CTX_PAD / 4) {
+                const uint8_t *src = (EG::kSpread || P.ring) ? E.wctx + (size_t)E.lane * CTX_PAD : ld.ctx;
+                const uint32_t *sw = reinterpret_cast<const uint32_t *>(src) + ln;
+                w = EG::kSpread ? load_agent(sw) : *sw;
+            }
+            L.cx = w;
+#endif
+        } else if (L.row == 0 || P.wctb < 2 || !(L.fl & F_WPP)) {
 #pragma nounroll
             for (int i = 0; i < CTX_NUM; ++i) ld.ctx[i] = ctx_init_state(c_ctx_init_l[i], P.sliceQp);
-        } else if (P.ring) {
+        } else if (EG::kSpread || P.ring) {
             const uint32_t *src = reinterpret_cast<const uint32_t *>(E.wctx + (size_t)E.lane * CTX_PAD);
             uint32_t *dst = reinterpret_cast<uint32_t *>(ld.ctx);
 #pragma nounroll
-            for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = src[k];
+            for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = EG::kSpread ? load_agent(src + k) : src[k];
         }
         engine_init(L, G, substream_start(L, P, *E.a), P.bits_end);
         if (L.row == 0) L.fl |= F_FIRST_QG;
@@ -790,7 +921,10 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
             }
         }
         uint32_t *dst = reinterpret_cast<uint32_t *>(P.gsao + (size_t)L.row * P.wctb + L.c);
-        for (int k = 0; k < 8; ++k) dst[k] = w[k];
+        for (int k = 0; k < 8; ++k) {
+            if constexpr (EG::kSpread) store_agent(dst + k, w[k]);
+            else dst[k] = w[k];
+        }
     }
     L.qx = L.ctbx, L.qy = L.ctby, L.ql = P.log2ctb, L.qd = 0;
     L.st = U_CQT;
@@ -1157,19 +1291,18 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         // cache: a 4x4 TB uses sigCtx 0..8 (ctxIdxMap, slots 0..8); larger TBs
         // use sigCtx 0 at the TB's DC (slot 0) and off + 0..2 (slots 1..3)
         const int cbase = CTX_SIG + (cidx ? 27 : 0);
-        const uint8_t *cb = G.ctx + cbase;
+        auto cb = [&](int i) { return ctx_ld(L, G, cbase + i); };
         uint64_t seq = G.seq[L.rc_scan * 5 + (l2 == 2 ? 4 : pcs)];  // slot per scan position
         uint32_t c0, c1 = 0, c2 = 0;
         int off = 0;
         if (l2 == 2) {
-            c0 = (uint32_t)cb[0] | ((uint32_t)cb[1] << 8) | ((uint32_t)cb[2] << 16) | ((uint32_t)cb[3] << 24);
-            c1 = (uint32_t)cb[4] | ((uint32_t)cb[5] << 8) | ((uint32_t)cb[6] << 16) | ((uint32_t)cb[7] << 24);
-            c2 = cb[8];
+            c0 = cb(0) | (cb(1) << 8) | (cb(2) << 16) | (cb(3) << 24);
+            c1 = cb(4) | (cb(5) << 8) | (cb(6) << 16) | (cb(7) << 24);
+            c2 = cb(8);
         } else {
             off = cidx == 0 ? ((xS | yS) ? 3 : 0) + (l2 == 3 ? (L.rc_scan == 0 ? 9 : 15) : 21) : (l2 == 3 ? 9 : 12);
             if ((xS | yS) == 0) seq &= ~0xfull;  // DC of the TB (scan position 0 of sub-block 0): sigCtx 0
-            c0 = (uint32_t)cb[0] | ((uint32_t)cb[off] << 8) | ((uint32_t)cb[off + 1] << 16) |
-                 ((uint32_t)cb[off + 2] << 24);
+            c0 = cb(0) | (cb(off) << 8) | (cb(off + 1) << 16) | (cb(off + 2) << 24);
         }
         for (int nn = nstart; nn >= 0; --nn) {
             if (nn > 0 || !infer_dc) {
@@ -1185,16 +1318,16 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
                 sig |= 1u;  // inferred DC of a coded sub-block
             }
         }
-        uint8_t *cw = G.ctx + cbase;
+        auto cw = [&](int i, uint32_t v) { ctx_st(L, G, cbase + i, v & 0xffu); };
         if (l2 == 2) {
-            for (int k = 0; k < 4; ++k) cw[k] = (uint8_t)(c0 >> (8 * k));
-            for (int k = 0; k < 4; ++k) cw[4 + k] = (uint8_t)(c1 >> (8 * k));
-            cw[8] = (uint8_t)c2;
+            for (int k = 0; k < 4; ++k) cw(k, c0 >> (8 * k));
+            for (int k = 0; k < 4; ++k) cw(4 + k, c1 >> (8 * k));
+            cw(8, c2);
         } else {
-            cw[0] = (uint8_t)c0;
-            cw[off] = (uint8_t)(c0 >> 8);
-            cw[off + 1] = (uint8_t)(c0 >> 16);
-            cw[off + 2] = (uint8_t)(c0 >> 24);
+            cw(0, c0);
+            cw(off, c0 >> 8);
+            cw(off + 1, c0 >> 16);
+            cw(off + 2, c0 >> 24);
         }
     }
     if (sig) {
@@ -1206,8 +1339,8 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         uint32_t g1 = 0, g2 = 0;
         // the ctxSet's four greater1 contexts (9.3.4.2.6) in one register
         const int gbase = CTX_GT1 + ctx_set * 4 + (cidx ? 16 : 0);
-        uint32_t gc = (uint32_t)G.ctx[gbase] | ((uint32_t)G.ctx[gbase + 1] << 8) | ((uint32_t)G.ctx[gbase + 2] << 16) |
-                      ((uint32_t)G.ctx[gbase + 3] << 24);
+        uint32_t gc = ctx_ld(L, G, gbase) | (ctx_ld(L, G, gbase + 1) << 8) | (ctx_ld(L, G, gbase + 2) << 16) |
+                      (ctx_ld(L, G, gbase + 3) << 24);
         const int first_sig = 31 - __builtin_clz(sig & (0u - sig));
         const int last_sig = msb32(sig);
         int num_g1 = 0, last_g1 = -1;
@@ -1226,7 +1359,7 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             if (c1 > 0) c1 = f ? 0 : c1 + 1;
         }
         L.rc_prev_c1 = c1;
-        for (int k = 0; k < 4; ++k) G.ctx[gbase + k] = (uint8_t)(gc >> (8 * k));
+        for (int k = 0; k < 4; ++k) ctx_st(L, G, gbase + k, (gc >> (8 * k)) & 0xffu);
         if (last_g1 >= 0 && dec(L, G, CTX_GT2 + ctx_set + (cidx ? 4 : 0))) g2 = 1u << last_g1;
         const bool sign_hidden = !(L.fl & F_BYPASS) && (last_sig - first_sig > 3);
         const bool hide = (P.flags & SP_SIGN_HIDING) && sign_hidden;
@@ -1305,23 +1438,46 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
         // 9.3.2.4 storage for the next row's substream: into its lane's block, or
         // its staging block when that lane may still be parsing an earlier row
         const int nl = P.lane0 + (L.row + 1) % P.R;
-        uint32_t *dst = reinterpret_cast<uint32_t *>(P.ring ? E.wctx + (size_t)nl * CTX_PAD : E.lds[nl].ctx);
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(ld.ctx);
+        uint32_t *dst =
+            reinterpret_cast<uint32_t *>((EG::kSpread || P.ring) ? E.wctx + (size_t)nl * CTX_PAD : E.lds[nl].ctx);
+        if constexpr (EG::kCtxReg) {
+#if !defined(HG_HOST_EMU)
+            const int ln = (int)__lane_id();  // every lane stores its dword
+            if (ln < CTX_PAD / 4) {
+                if constexpr (EG::kSpread) store_agent(dst + ln, L.cx);
+                else dst[ln] = L.cx;
+            }
+#endif
+        } else {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(ld.ctx);
 #pragma nounroll
-        for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = src[k];
+            for (int k = 0; k < CTX_PAD / 4; ++k) {
+                if constexpr (EG::kSpread) store_agent(dst + k, src[k]);
+                else dst[k] = src[k];
+            }
+        }
     }
     {  // bottom CtDepth of this CTB for the row below
         const int nb8 = 1 << (P.log2ctb - 3), col0 = L.ctbx >> 3;
         uint8_t *line = P.gdepth + (size_t)L.row * P.w8;
-        for (int k = 0; k < nb8 && col0 + k < P.w8; ++k) line[col0 + k] = ld.dA[k];
+        for (int k = 0; k < nb8 && col0 + k < P.w8; ++k) {
+            if constexpr (EG::kSpread) store_agent(line + col0 + k, ld.dA[k]);
+            else line[col0 + k] = ld.dA[k];
+        }
     }
     const bool last_in_pic = L.row == P.hctb - 1 && L.c == P.wctb - 1;
     if (term(L, G) != (last_in_pic ? 1 : 0)) L.status |= ST_SUBSTREAM_END;
     if (!last_in_pic && (L.fl & F_WPP) && L.c == P.wctb - 1 && !term(L, G)) L.status |= ST_SUBSTREAM_END;
     if (L.budget + L.k < 0) L.status |= ST_OVERRUN;  // read past the NAL unit
-    release_fence();
     ++L.c;
-    prog_store(&E.prog[E.lane], (L.fl & F_STOP) ? kProgDone : (uint32_t)L.row * (uint32_t)P.wctb + (uint32_t)L.c);
+    const uint32_t pv = (L.fl & F_STOP) ? kProgDone : (uint32_t)L.row * (uint32_t)P.wctb + (uint32_t)L.c;
+    if constexpr (EG::kSpread) {
+        stores_done();
+        store_agent(&E.prog[E.lane], pv);
+    } else {
+        release_fence();
+        prog_store(&E.prog[E.lane], pv);
+    }
     if (!(L.fl & F_STOP) && L.c < P.wctb) {
         L.st = U_CTU;
         return;
@@ -1360,7 +1516,8 @@ HG_HD inline void run_unit(int kind, Lane &L, LaneLds &ld, LanePic &P, const Env
 }
 
 // a lane in U_CTU can start its CTU (WPP: the row above is two CTUs ahead)
-HG_HD inline bool ctu_ready(const Lane &L, const LanePic &P, const Env &E) { return wpp_ready(L, P, E); }
+template <class EG = Eng>
+HG_HD inline bool ctu_ready(const Lane &L, const LanePic &P, const Env &E) { return wpp_ready<EG>(L, P, E); }
 
 // lane setup: picture constants, outputs, first state.  Returns false for an idle lane.
 // `cap` lanes (waves, solo mode) at most per picture.
@@ -1526,20 +1683,38 @@ int parse_mode_for(int requested, int n_pics) {
     static const int env = [] {
         const char *e = std::getenv("HEIFGPU_PARSE");
         if (!e) return PARSE_AUTO;
-        return e[0] == 's' ? PARSE_SOLO : (e[0] == 'l' ? PARSE_LANES : PARSE_AUTO);
+        const std::string v(e);
+        return v == "solo" ? PARSE_SOLO : v == "spread" ? PARSE_SPREAD : v == "lanes" ? PARSE_LANES : PARSE_AUTO;
     }();
     static const int max_pics = [] {
         const char *e = std::getenv("HEIFGPU_SOLO_MAX_PICS");
         return e ? std::atoi(e) : 256;
     }();
     if (env != PARSE_AUTO) return env;
-    if (requested == PARSE_LANES || requested == PARSE_SOLO) return requested;
+    if (requested == PARSE_LANES || requested == PARSE_SOLO || requested == PARSE_SPREAD) return requested;
     return n_pics <= max_pics ? PARSE_SOLO : PARSE_LANES;
 }
 
 // waves per solo workgroup: one per WPP row of the tallest picture, at most 16
 // (1024 threads); taller pictures wrap their rows round the waves
 int solo_waves_for(int lane_rows) { return lane_rows < 1 ? 1 : (lane_rows > kSoloMaxWaves ? kSoloMaxWaves : lane_rows); }
+
+// spread mode: one wave slot per substream, entry row << 20 | picture; the
+// pictures by payload size (heaviest first, so the longest WPP chains start
+// first), a picture's rows consecutive and in order (a row waits only for a
+// lower slot, which the in-order dispatch has already placed)
+int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order) {
+    std::vector<uint32_t> by_size((size_t)n);
+    for (int i = 0; i < n; ++i) by_size[(size_t)i] = (uint32_t)i;
+    std::stable_sort(by_size.begin(), by_size.end(),
+                     [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
+    order.clear();
+    for (uint32_t p : by_size) {
+        if (p >= (1u << 20) || pics[p].n_sub >= (1u << 12)) return -1;
+        for (uint32_t r = 0; r < pics[p].n_sub; ++r) order.push_back(p | (r << 20));
+    }
+    return 1;
+}
 
 #if defined(HG_HOST_EMU)
 // one wave at a time, one unit per live lane per pass, lanes in order
@@ -1608,8 +1783,10 @@ void emu_parse_lanes(const BatchArgs &a) {
 
 // solo mode: each picture's rows (waves) round-robin, one unit per ready wave
 // per round, with the GPU driver's window logic (SoloWin) per wave
+template <bool Spread>
 void emu_parse_solo(const BatchArgs &a) {
-    const int NW = a.solo_waves;
+    using EG = EngSoloT<Spread>;
+    const int NW = Spread ? a.max_rows : a.solo_waves;  // spread: every row of a picture its own wave
     const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
     uint64_t seq[15];
     for (int i = 0; i < 15; ++i) seq[i] = sig_seq(i);
@@ -1623,15 +1800,22 @@ void emu_parse_solo(const BatchArgs &a) {
     for (int slot = 0; slot < n_slots; ++slot) {
         const bool in = !a.parse_order || a.parse_order[slot] != ~0u;
         if (!in) continue;
-        const int pic = a.pic0 + (a.parse_order ? (int)a.parse_order[slot] : slot);
+        // spread: one entry per row (row << 20 | picture); the picture's row-0 entry runs all its rows here
+        const uint32_t ent = a.parse_order ? a.parse_order[slot] : (uint32_t)slot;
+        if (Spread && (ent >> 20) != 0) continue;
+        const int pic = a.pic0 + (int)(Spread ? (ent & 0xfffffu) : ent);
         for (int w = 0; w < NW; ++w) {
             prog[w] = 0;
-            if (!lane_init(lanes[(size_t)w], P, lds[(size_t)w], a, pic, w, 0, NW)) lanes[(size_t)w].st = U_DONE;
+            if (!lane_init(lanes[(size_t)w], P, lds[(size_t)w], a, pic, w, 0, Spread ? (1 << 20) : NW))
+                lanes[(size_t)w].st = U_DONE;
             wins[(size_t)w].w = &wbuf[(size_t)w * 192];
             wins[(size_t)w].f = &wbuf[(size_t)w * 192 + 128];
         }
         const uint32_t lim = (P.bits_end + 64u) & ~3u;
-        Env E{&a, lds.data(), prog, wctx.data(), 0};
+        if (Spread)
+            for (int w = 0; w < NW; ++w) a.xprog[P.row_off + (uint32_t)w < (uint32_t)a.total_rows ? P.row_off + w : 0] = 0;
+        Env E = Spread ? Env{&a, lds.data(), a.xprog + P.row_off, a.xctx + (size_t)P.row_off * CTX_PAD, 0}
+                       : Env{&a, lds.data(), prog, wctx.data(), 0};
         for (;;) {
             bool any = false, progressed = false;
             for (int w = 0; w < NW; ++w) {
@@ -1639,13 +1823,13 @@ void emu_parse_solo(const BatchArgs &a) {
                 if (L.st == U_DONE) continue;
                 any = true;
                 E.lane = w;
-                if (L.st == U_CTU && !ctu_ready(L, P, E)) continue;
+                if (L.st == U_CTU && !ctu_ready<EG>(L, P, E)) continue;
                 progressed = true;
                 SoloWin &sw = wins[(size_t)w];
                 const uint32_t start = L.st == U_CTU ? substream_start(L, P, a) : ~0u;
                 if (start != ~0u) sw.restart(a.rbsp, start, lim, 0);
                 else sw.advance(a.rbsp, L.lb, lim, 0);
-                const EngSolo G{lds[(size_t)w].ctx, 0u, 0u, seq, a.rbsp, lim, sw.view()};
+                const EG G{lds[(size_t)w].ctx, 0u, 0u, seq, a.rbsp, lim, sw.view()};
                 run_unit(L.st, L, lds[(size_t)w], P, E, G);
             }
             if (!any) break;
@@ -1663,7 +1847,8 @@ void emu_parse_solo(const BatchArgs &a) {
 }
 
 void emu_parse(const BatchArgs &a) {
-    if (a.parse_mode == PARSE_SOLO) emu_parse_solo(a);
+    if (a.parse_mode == PARSE_SOLO) emu_parse_solo<false>(a);
+    else if (a.parse_mode == PARSE_SPREAD) emu_parse_solo<true>(a);
     else emu_parse_lanes(a);
 }
 #else
@@ -1769,31 +1954,38 @@ inline size_t solo_lds_bytes(int nw, bool ring) {
            (ring ? (size_t)nw * CTX_PAD : 0);
 }
 
-__global__ void __launch_bounds__(64 * kSoloMaxWaves) k_parse_solo(BatchArgs a) {
+template <bool Spread>
+__global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo(BatchArgs a) {
+    using EG = EngSoloT<Spread>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int NW = a.solo_waves;
+    const int NW = Spread ? 1 : a.solo_waves;
     LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
     LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + NW);
     uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + 1);
     uint64_t *s_seq = reinterpret_cast<uint64_t *>(s_prog + 64);
     uint8_t *s_wctx = a.wpp_ring ? reinterpret_cast<uint8_t *>(s_seq + 16) : nullptr;
-    const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    // wave index made scalar: every value of the substream state derives from uniform inputs, so the
+    // compiler can keep the engine in SGPRs and branch with s_cbranch
+    const int w = Spread ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
     if (threadIdx.x < 15) s_seq[threadIdx.x] = sig_seq((int)threadIdx.x);
     if (threadIdx.x < 64) s_prog[threadIdx.x] = 0;
     const uint64_t trow = state_row(lane);
     const uint32_t tlo = (uint32_t)trow, thi = (uint32_t)(trow >> 32);
     const int slot = (int)blockIdx.x;
     const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
-    const bool in = slot < n_slots && (!a.parse_order || a.parse_order[slot] != ~0u);
-    const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
+    const uint32_t ent = slot < n_slots ? (a.parse_order ? a.parse_order[slot] : (uint32_t)slot) : ~0u;
+    const bool in = ent != ~0u;
+    // spread: entry = row << 20 | picture, one wave per WPP row
+    const int pic = a.pic0 + (int)(Spread ? (ent & 0xfffffu) : ent), row = Spread ? (int)(ent >> 20) : w;
     Lane L;
     LaneLds &ld = s_lds[w < NW ? w : 0];
     LanePic &P = s_pic[0];
-    const bool live = in && w < NW && lane_init(L, P, ld, a, pic, w, 0, NW);  // every lane alike
+    const bool live = in && w < NW && lane_init(L, P, ld, a, pic, row, 0, Spread ? (1 << 20) : NW);  // every lane alike
     if (!live) L.st = U_DONE;
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(live ? 1 : 0)) return;
-    const Env E{&a, s_lds, s_prog, s_wctx, w};
+    const Env E = Spread ? Env{&a, s_lds, a.xprog + P.row_off, a.xctx + (size_t)P.row_off * CTX_PAD, row}
+                         : Env{&a, s_lds, s_prog, s_wctx, w};
     const uint32_t lim = (P.bits_end + 64u) & ~3u;
     SoloWin sw;
     sw.r0 = sw.r1 = sw.f = 0;
@@ -1804,13 +1996,15 @@ __global__ void __launch_bounds__(64 * kSoloMaxWaves) k_parse_solo(BatchArgs a) 
 #endif
     for (;;) {
         // the wave's state (equal in every lane), made scalar
-        int st = L.st, run = st != U_DONE && (st != U_CTU || ctu_ready(L, P, E));
+        int st = L.st, run = st != U_DONE && (st != U_CTU || ctu_ready<EG>(L, P, E));
         uint32_t start = run && st == U_CTU ? substream_start(L, P, a) : ~0u;
         const uint32_t rd = L.lb;
         st = __builtin_amdgcn_readfirstlane(st);
         if (st == U_DONE) break;
         if (!__builtin_amdgcn_readfirstlane(run)) {
-            __builtin_amdgcn_s_sleep(1);
+            // the row above is not 2 CTUs ahead: sleep (~64 cycles a unit), so the
+            // busy waves on this SIMD keep the issue slots
+            __builtin_amdgcn_s_sleep(HG_SOLO_SLEEP);
             continue;
         }
         start = (uint32_t)__builtin_amdgcn_readfirstlane((int)start);
@@ -1823,7 +2017,10 @@ __global__ void __launch_bounds__(64 * kSoloMaxWaves) k_parse_solo(BatchArgs a) 
         ++pf[7];
 #endif
         {
-            const EngSolo G{ld.ctx, tlo, thi, s_seq, a.rbsp, lim, sw.view()};
+#if !defined(HG_SOLO_NO_UNI)
+            uni_state(L);
+#endif
+            const EG G{ld.ctx, tlo, thi, s_seq, a.rbsp, lim, sw.view()};
             run_unit(st, L, ld, P, E, G);
         }
 #if defined(HG_PARSE_PROF)
@@ -1845,8 +2042,17 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
         if (a.solo_waves < 1 || a.solo_waves > kSoloMaxWaves) return hipErrorInvalidValue;
         const int n = a.parse_order ? a.n_slots : a.n_pics;
         if (n <= 0) return hipSuccess;
-        hipLaunchKernelGGL(k_parse_solo, dim3(n), dim3(64 * a.solo_waves), solo_lds_bytes(a.solo_waves, a.wpp_ring != 0),
-                           s, a);
+        hipLaunchKernelGGL(k_parse_solo<false>, dim3(n), dim3(64 * a.solo_waves),
+                           solo_lds_bytes(a.solo_waves, a.wpp_ring != 0), s, a);
+        return hipGetLastError();
+    }
+    if (a.parse_mode == PARSE_SPREAD) {
+        if (!a.parse_order || !a.xprog || !a.xctx) return hipErrorInvalidValue;
+        if (a.n_slots <= 0) return hipSuccess;
+        // progress words start at 0 for every decode
+        hipError_t e = hipMemsetAsync(a.xprog, 0, (size_t)a.total_rows * sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_parse_solo<true>, dim3(a.n_slots), dim3(64), solo_lds_bytes(1, false), s, a);
         return hipGetLastError();
     }
     // the dealing of parse_order fixed the pictures per wave (lanes_parse_order)

@@ -90,15 +90,16 @@ typedef struct {
     uint32_t tile_stride, tile_offset;
     /* CABAC parse mode: HEIFGPU_PARSE_AUTO picks by batch
      * size; HEIFGPU_PARSE_LANES packs one substream per lane (throughput);
-     * HEIFGPU_PARSE_SOLO runs one substream per wavefront (latency of small
-     * batches). */
+     * HEIFGPU_PARSE_SOLO runs one substream per wavefront, a picture's rows in
+     * one workgroup; HEIFGPU_PARSE_SPREAD one substream per wavefront, every
+     * row its own workgroup (latency of small batches). */
     uint32_t parse_mode;
     /* lanes mode: pictures per wavefront (0 = adaptive; larger values are
      * capped at 64 / CTB rows) */
     uint32_t pics_per_wave;
 } heifgpu_batch_opts;
 
-enum { HEIFGPU_PARSE_AUTO = 0, HEIFGPU_PARSE_LANES = 1, HEIFGPU_PARSE_SOLO = 2 };
+enum { HEIFGPU_PARSE_AUTO = 0, HEIFGPU_PARSE_LANES = 1, HEIFGPU_PARSE_SOLO = 2, HEIFGPU_PARSE_SPREAD = 3 };
 
 /* ---- host: demux + parameter sets + slice headers ------------------- */
 /* data is copied; the returned image owns its bytes. */
@@ -239,8 +240,9 @@ int heifgpu_image_tile_params(const heifgpu_image *img, uint32_t tile, heifgpu_t
  * `make prof` library has them). */
 int heifgpu_debug_counters(uint64_t *out, int n);
 /* The CABAC parse geometry a prepared batch launches: mode
- * (HEIFGPU_PARSE_LANES / _SOLO), workgroups (waves in lanes mode, pictures in
- * solo mode), pictures per wave (lanes) and waves per workgroup (solo). */
+ * (HEIFGPU_PARSE_LANES / _SOLO / _SPREAD), workgroups (waves in lanes mode,
+ * pictures in solo mode, substreams in spread mode), pictures per wave (lanes)
+ * and waves per workgroup (solo). */
 int heifgpu_batch_parse_geometry(const heifgpu_batch *batch, uint32_t *mode, uint32_t *workgroups,
                                  uint32_t *pics_per_wave, uint32_t *waves_per_workgroup);
 

@@ -34,7 +34,7 @@ def _run(exe, path, env_extra=None):
 # (one picture per wave for a single image), the full 64-lane packing of large
 # batches (four 16-row pictures per wave), and batch (unsorted) wave order
 LANES = {"HEIFGPU_PARSE": "lanes"}
-PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "lanes": LANES, "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0"},
+PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "spread"}, "lanes": LANES, "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0"},
            "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1"}, "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
 
 
@@ -44,7 +44,7 @@ def test_emulated_kernels_match_oracle(emu_check, parser):
     assert rc == 0 and "EMU PARITY OK" in out, out[-2000:]
 
 
-@pytest.mark.parametrize("parser", ["solo", "lanes", "packed"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed"])
 def test_emulated_kernels_permuted_image(emu_check, tmp_path, halfmoonbay, parser):
     p = tmp_path / "perm.heic"
     p.write_bytes(permuted_heic(halfmoonbay, 42))
@@ -71,7 +71,7 @@ def _corrupt(data: bytes, mode: str) -> bytes:
     return bytes(d)
 
 
-@pytest.mark.parametrize("parser", ["solo", "lanes", "packed"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed"])
 @pytest.mark.parametrize("mode", ["random", "zeroed"])
 def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode, parser):
     """Corrupt slice data must end in status bits, never in a crash (the same

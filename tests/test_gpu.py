@@ -74,13 +74,15 @@ def test_halfmoonbay_bit_exact(H, oracle_halfmoonbay, halfmoonbay):
 
 @pytest.mark.parametrize("parse,ppw,geom", [
     ("solo", 0, {"mode": "solo", "workgroups": 48, "pics_per_wave": 1, "waves_per_workgroup": 16}),
+    ("spread", 0, {"mode": "spread", "workgroups": 768, "pics_per_wave": 1, "waves_per_workgroup": 1}),
     ("lanes", 0, {"mode": "lanes", "workgroups": 48, "pics_per_wave": 1, "waves_per_workgroup": 1}),
     ("lanes", 4, {"mode": "lanes", "workgroups": 12, "pics_per_wave": 4, "waves_per_workgroup": 1}),
 ])
 def test_halfmoonbay_parse_modes(H, ctx, oracle_halfmoonbay, halfmoonbay, parse, ppw, geom):
     """Config 3 in every parse geometry: solo (a workgroup of 16 waves per
-    tile, one WPP row per wave), lanes with one tile per wave (the adaptive
-    choice for one image) and lanes packed four tiles per wave."""
+    tile, one WPP row per wave), spread (one single-wave workgroup per WPP
+    row: 768), lanes with one tile per wave and lanes packed four tiles per
+    wave."""
     img = H.HeifImage.parse(halfmoonbay)
     b = ctx.prepare([img], parse=parse, pics_per_wave=ppw)
     assert b.parse_geometry() == geom
@@ -114,12 +116,13 @@ def check_permuted(outs, seeds, oracle_tiles):
 @pytest.mark.parametrize("parse,geom", [
     ("auto", {"mode": "lanes", "workgroups": 1536, "pics_per_wave": 4, "waves_per_workgroup": 1}),
     ("solo", {"mode": "solo", "workgroups": 6144, "pics_per_wave": 1, "waves_per_workgroup": 16}),
+    ("spread", {"mode": "spread", "workgroups": 98304, "pics_per_wave": 1, "waves_per_workgroup": 1}),
 ])
 def test_bench_shard_every_image(H, ctx, oracle_tiles, halfmoonbay, parse, geom):
     """The headline configuration itself (bench.py, config 4 shard): 128
     permuted 4032x3024 images = 6144 pictures.  The automatic choice packs four
     16-row pictures per k_parse_lanes wave (1536 waves); solo runs 6144
-    16-wave workgroups.  Every image is checked, decoded twice back to back
+    16-wave workgroups, spread 98,304 one-wave workgroups.  Every image is checked, decoded twice back to back
     (both parse-output sets of the pipeline)."""
     from heif_amd.synthetic import permuted_heic
 

@@ -22,6 +22,19 @@ def _free_port():
     return port
 
 
+def _log(rank, msg):
+    import sys
+    import time
+
+    print(f"[ipc rank {rank} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def _digest(a) -> str:
+    import hashlib
+
+    return hashlib.sha256(np.ascontiguousarray(a.astype(np.uint16)).tobytes()).hexdigest()
+
+
 def _worker(rank, world, port, path, q):
     import torch.distributed as dist
 
@@ -29,8 +42,10 @@ def _worker(rank, world, port, path, q):
     from heif_amd.tile_split import DeviceBackend, gather_to_rank0
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    _log(rank, "init")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
+    _log(rank, "decode")
     ctx = H.DecodeContext(0)
     img = H.HeifImage.parse(open(path, "rb").read())
     b = ctx.prepare([img], tile_stride=world, tile_offset=rank)
@@ -43,9 +58,11 @@ def _worker(rank, world, port, path, q):
     if full:
         for t in (full[0].y, full[0].cb, full[0].cr):
             t.fill_(0)
+    _log(rank, f"status {st}; gather")
     gather_to_rank0(DeviceBackend(H, ctx), dist, outs, buf, full, rank, world)
-    if rank == 0:
-        q.put((st, [t.cpu().numpy() for t in (full[0].y, full[0].cb, full[0].cr)]))
+    _log(rank, "gathered")
+    if rank == 0:  # digests only: a large object would block in the pipe until the parent joins
+        q.put((st, [_digest(t.cpu().numpy()) for t in (full[0].y, full[0].cb, full[0].cr)]))
     dist.barrier()
     ctx.close()
     dist.destroy_process_group()
@@ -63,7 +80,6 @@ def test_ipc_tile_split_gather(world, oracle_halfmoonbay):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     mp.start_processes(_worker, args=(world, _free_port(), path, q), nprocs=world, join=True, start_method="spawn")
-    st, planes = q.get()
+    st, digests = q.get()
     assert st == [0]
-    for got, want in zip(planes, (oracle_halfmoonbay.y, oracle_halfmoonbay.cb, oracle_halfmoonbay.cr)):
-        assert np.array_equal(got.astype(np.uint16), want)
+    assert digests == [_digest(p) for p in (oracle_halfmoonbay.y, oracle_halfmoonbay.cb, oracle_halfmoonbay.cr)]

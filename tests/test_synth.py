@@ -166,12 +166,14 @@ def _decode(H, ctx, datas, parse, ppw=0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("parse", ["solo", "lanes"])
+@pytest.mark.parametrize("parse", ["solo", "spread", "lanes"])
 @pytest.mark.parametrize("name,over", CASES, ids=[c[0] for c in CASES])
 def test_gpu_synthetic_bit_exact(H, gctx, oracle_mod, name, over, parse):
-    """Every tool / geometry case in both parse modes: k_parse_solo (one
-    substream per wave; rows beyond 16 wrap round the waves) and
-    k_parse_lanes (one substream per lane; rows beyond 64 wrap round the lanes)."""
+    """Every tool / geometry case in every parse mode: k_parse_solo<false>
+    (one substream per wave, a picture's rows in one workgroup; rows beyond 16
+    wrap round the waves), k_parse_solo<true> (spread: every row its own
+    workgroup, WPP through coherent global memory) and k_parse_lanes (one
+    substream per lane; rows beyond 64 wrap round the lanes)."""
     p = params(over)
     for seed in range(2):
         data = S.single_heic(p, seed=seed)
@@ -205,7 +207,7 @@ def test_gpu_mixed_geometry_batch(H, oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("parse", ["solo", "lanes"])
+@pytest.mark.parametrize("parse", ["solo", "spread", "lanes"])
 def test_gpu_mixed_wpp_ring_batch(H, oracle_mod, halfmoonbay, parse):
     """One batch mixing a 48-tile WPP grid (halfmoonbay), a non-WPP 512x512
     single-substream picture (config 2) and a 68-row CTB-16 picture whose WPP
@@ -227,7 +229,7 @@ def test_gpu_mixed_wpp_ring_batch(H, oracle_mod, halfmoonbay, parse):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("parse,ppw", [("lanes", 64), ("lanes", 0), ("solo", 0)])
+@pytest.mark.parametrize("parse,ppw", [("lanes", 64), ("lanes", 0), ("solo", 0), ("spread", 0)])
 def test_gpu_nowpp_batch_64_per_wave(H, gctx, oracle_mod, parse, ppw):
     """128 non-WPP pictures (one substream each).  ("lanes", 64): every
     k_parse_lanes wave packs 64 pictures, one per lane (2 waves); ("lanes", 0):
@@ -253,7 +255,7 @@ def test_gpu_config5_8k_main10_grid(H, oracle_mod):
 
 
 # ------------------------------------------- kernels compiled for the host
-@pytest.mark.parametrize("parser", ["solo", "lanes", "ppw1"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "ppw1"])
 def test_emulated_kernels_on_synthetic_streams(tmp_path, parser):
     """The GPU kernels' source built for the host (HG_HOST_EMU, see
     test_emulation.py) decodes every synthetic case bit-exactly vs the oracle."""
@@ -264,7 +266,7 @@ def test_emulated_kernels_on_synthetic_streams(tmp_path, parser):
     csrc = pathlib.Path(__file__).resolve().parents[1] / "heif_amd" / "csrc"
     subprocess.run(["make", "-s", "-C", str(csrc), "emu-fast"], check=True, capture_output=True)
     exe = csrc / "build" / "emu_fast" / "emu_check"
-    env = dict(os.environ, HEIFGPU_PARSE="solo" if parser == "solo" else "lanes",
+    env = dict(os.environ, HEIFGPU_PARSE=parser if parser in ("solo", "spread") else "lanes",
                **({"HEIFGPU_LANES_PPW": "1"} if parser == "ppw1" else {}))
     for name, over in CASES:
         path = tmp_path / f"{name}.heic"

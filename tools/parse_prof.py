@@ -1,11 +1,14 @@
 """k_parse_lanes cycle breakdown (tuning only).
 
-usage: HEIFGPU_LIBRARY=heif_amd/libheifgpu_prof.so python tools/parse_prof.py [n_images] [out.json]
+usage: HEIFGPU_LIBRARY=heif_amd/libheifgpu_prof.so python tools/parse_prof.py [n_images] [out.json] [auto|lanes|solo]
 
 Decodes a batch of permuted halfmoonbay images with the counter-instrumented
 library (`make -C heif_amd/csrc prof`) and prints per-wave averages of the
 k_parse_lanes counters (s_memtime cycles per unit kind, passes, lanes that
 ran a unit), i.e. the mean active lanes per unit execution and per pass.
+Solo mode (k_parse_solo, one substream per wave): "passes" and "units" both
+count units run; the cycles no unit kind accounts for are the WPP waits and
+the driver (window refill, dispatch).
 """
 import ctypes
 import json
@@ -28,11 +31,13 @@ BINS_PER_IMAGE = 15358022  # context + bypass + terminate bins of one halfmoonba
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    mode = sys.argv[3] if len(sys.argv) > 3 else "auto"
     src = (ROOT / "tests/golden/halfmoonbay.heic").read_bytes()
     imgs = [H.HeifImage.parse(permuted_heic(src, s)) for s in range(n)]
     ctx = H.DecodeContext(0)
     outs = ctx.alloc_outputs(imgs)
-    batch = ctx.prepare(imgs)
+    batch = ctx.prepare(imgs, parse=mode)
+    geom = batch.parse_geometry()
     ctx.set_timing(True)
     lib = _lib.lib
     buf = (ctypes.c_uint64 * 16)()
@@ -46,10 +51,10 @@ def main():
     parse_ms = ctx.stage_times()[0]
     lib.heifgpu_debug_counters(buf, 16)
     c = dict(zip(LANES, buf[:k]))
-    pics = sum(im.info.num_tiles for im in imgs)
-    waves = (pics + 3) // 4
+    waves = geom["workgroups"] * geom["waves_per_workgroup"]
     res = {
         "images": n,
+        "geometry": geom,
         "waves": waves,
         "parse_ms": round(parse_ms, 3),
         "per_wave": {name: round(c[name] / waves, 1) for name in LANES},
@@ -58,6 +63,7 @@ def main():
         "unit_cycle_share": {name: round(c[name] / max(c["cycles"], 1), 3)
                              for name in ("ctu", "tree", "tb", "sb", "ctu_end")},
         "bins_per_wave": round(n * BINS_PER_IMAGE / waves, 1),
+        "unaccounted_share": round(1 - sum(c[k] for k in ("ctu", "tree", "tb", "sb", "ctu_end")) / max(c["cycles"], 1), 3),
         "note": "s_memtime shader cycles of the instrumented build (+~11% over the product build)",
     }
     print(json.dumps(res))
