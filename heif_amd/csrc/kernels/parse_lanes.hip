@@ -1673,12 +1673,16 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
     return ppw;
 }
 
-// Parse mode of a batch.  Solo mode parses each substream on a wave of its own
-// (lane 0), which is far faster per substream than a lane of a packed wave
-// but leaves 63 lanes idle: it is the latency path of small batches, where
-// the packed waves cannot fill the SIMDs anyway.  HEIFGPU_PARSE=lanes|solo
-// forces a mode for every batch, HEIFGPU_SOLO_MAX_PICS moves the automatic
-// switch-over.
+// Parse mode of a batch.  Spread mode parses each substream on a wave of its
+// own (every lane alike, so one syntax unit at a time with nothing else in
+// the pass), one workgroup per substream so a picture's rows spread over CUs:
+// far faster per substream than a lane of a packed wave, but 64 lanes do one
+// substream's work, so it is the latency path of small batches, where packed
+// waves cannot fill the SIMDs anyway.  MI355X, halfmoonbay permutations
+// (tools/lat_modes.sh, profiles/r03/latency_modes.json): 1 image 37 vs 71 ms
+// parse, 16 images 70 vs 83 ms, 32 images 117 vs 91 ms; so batches up to 768
+// pictures (16 such images) take spread mode.  HEIFGPU_PARSE=lanes|solo|spread
+// forces a mode for every batch, HEIFGPU_SOLO_MAX_PICS moves the switch-over.
 int parse_mode_for(int requested, int n_pics) {
     static const int env = [] {
         const char *e = std::getenv("HEIFGPU_PARSE");
@@ -1688,11 +1692,11 @@ int parse_mode_for(int requested, int n_pics) {
     }();
     static const int max_pics = [] {
         const char *e = std::getenv("HEIFGPU_SOLO_MAX_PICS");
-        return e ? std::atoi(e) : 256;
+        return e ? std::atoi(e) : 768;
     }();
     if (env != PARSE_AUTO) return env;
     if (requested == PARSE_LANES || requested == PARSE_SOLO || requested == PARSE_SPREAD) return requested;
-    return n_pics <= max_pics ? PARSE_SOLO : PARSE_LANES;
+    return n_pics <= max_pics ? PARSE_SPREAD : PARSE_LANES;
 }
 
 // waves per solo workgroup: one per WPP row of the tallest picture, at most 16

@@ -62,7 +62,7 @@ def planes_np(o):
 
 
 def test_halfmoonbay_bit_exact(H, oracle_halfmoonbay, halfmoonbay):
-    """Config 3 through the reference-mirror API (one image: solo parse)."""
+    """Config 3 through the reference-mirror API (one image: spread parse)."""
     out = H.HeicDecoder.decode(halfmoonbay)
     y, cb, cr = planes_np(out)
     assert np.array_equal(y, oracle_halfmoonbay.y)

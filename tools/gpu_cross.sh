@@ -1,0 +1,8 @@
+#!/bin/bash
+# full GPU tests, then the spread/lanes crossover by batch size
+cd ${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?
+tail -3 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || exit $rc
+tools/lat_modes.sh "1 4 8 16 32" "spread lanes" 10
