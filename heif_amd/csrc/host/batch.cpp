@@ -1,5 +1,6 @@
 // batch.cpp — see batch.hpp.
 #include "batch.hpp"
+#include "../kernels/kernels.hpp"
 
 #include <algorithm>
 #include <cstdlib>
@@ -171,6 +172,33 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
         hb.pieces.clear();
     }
     return hb;
+}
+
+void parse_chain_cost(const PicDesc *pics, int n, const uint32_t *subs, const SeqParams *seqs, std::vector<float> &cost) {
+    cost.assign(size_t(n), 0.f);
+    std::vector<float> prev, cur;
+    for (int p = 0; p < n; ++p) {
+        const PicDesc &pd = pics[p];
+        const SeqParams &sq = seqs[pd.seq];
+        const int ctb = 1 << sq.log2_ctb, wctb = (sq.width + ctb - 1) / ctb;
+        const uint32_t *sb = subs + pd.sub_first;
+        if (pd.n_sub <= 1 || wctb < 1) {
+            cost[size_t(p)] = float(pd.bits_len);
+            continue;
+        }
+        prev.assign(size_t(wctb), 0.f);
+        cur.assign(size_t(wctb), 0.f);
+        for (uint32_t r = 0; r < pd.n_sub; ++r) {
+            const float t = float(sb[r + 1] - sb[r]) / float(wctb);
+            for (int c = 0; c < wctb; ++c) {
+                const float left = c ? cur[size_t(c - 1)] : 0.f;
+                const float up = r ? prev[size_t(std::min(c + 1, wctb - 1))] : 0.f;
+                cur[size_t(c)] = std::max(left, up) + t;
+            }
+            std::swap(prev, cur);
+        }
+        cost[size_t(p)] = prev[size_t(wctb - 1)];
+    }
 }
 
 }  // namespace hg

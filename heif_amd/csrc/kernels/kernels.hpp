@@ -102,7 +102,12 @@ constexpr int kSoloMaxWaves = 16;
 // or for solo mode with ppw_force = 1 one picture per workgroup, heaviest
 // first); returns the pictures per wave it dealt for (BatchArgs::parse_group).
 // ppw_force = 0: the adaptive choice.
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order);
+// cost (optional): per-picture parse cost to deal by (default: payload bytes)
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
+                      const float *cost = nullptr);
+// per-picture WPP critical path in payload bytes (the rows' bytes spread evenly
+// over their CTUs, row r's CTU c after row r-1's CTU c+1); non-WPP: all bytes
+void parse_chain_cost(const PicDesc *pics, int n, const uint32_t *subs, const SeqParams *seqs, std::vector<float> &cost);
 // the parse mode a batch of n_pics pictures runs in (requested: PARSE_*)
 int parse_mode_for(int requested, int n_pics);
 // spread mode's wave slots (row << 20 | picture); -1 if the batch exceeds the encoding

@@ -1639,7 +1639,8 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
 // W gets ranks w, 2W-1-w, 2W+w, 4W-1-w, ...): heavy beside light.  Empty
 // slots are ~0u.  HEIFGPU_PARSE_ORDER=0: batch order; HEIFGPU_PARSE_HEAVY
 // overrides the heavy count.
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order) {
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
+                      const float *cost) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
         return e ? std::atoi(e) : 1;
@@ -1658,8 +1659,11 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
     }
     std::vector<uint32_t> by_size((size_t)n);
     for (int i = 0; i < n; ++i) by_size[(size_t)i] = (uint32_t)i;
-    std::stable_sort(by_size.begin(), by_size.end(),
-                     [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
+    if (cost)
+        std::stable_sort(by_size.begin(), by_size.end(), [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
+    else
+        std::stable_sort(by_size.begin(), by_size.end(),
+                         [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
     int heavy = heavy_env >= 0 ? heavy_env : 0;
     heavy = ppw > 1 ? std::min(heavy, n) : 0;
     const int rest = n - heavy, W = (rest + ppw - 1) / ppw;
