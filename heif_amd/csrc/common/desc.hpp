@@ -23,6 +23,10 @@ enum : uint32_t {
     SP_PCM = 1u << 7,
     SP_PCM_LOOP_FILTER_DISABLED = 1u << 8,
     SP_SAO = 1u << 9,
+    // one HEVC tile of a tiled picture decoded as its own picture (batch.cpp),
+    // not the last tile: its substream ends in end_of_slice_segment_flag 0 and
+    // end_of_subset_one_bit 1 (7.3.8.1)
+    SP_SUBSET_END = 1u << 10,
 };
 
 // Per distinct SPS/PPS pair (derived values only; H.265 7.4.3.2 / 7.4.3.3).

@@ -76,7 +76,8 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
     if (tile_stride == 0) tile_stride = 1;
     if (tile_offset >= tile_stride) throw HeifError("tile_offset must be below tile_stride");
     HostBatch hb;
-    std::vector<std::vector<uint8_t>> seq_keys;
+    std::vector<std::vector<uint8_t>> seq_keys, sf_keys;  // SeqParams: PPS + picture geometry; ScalingFactor: PPS
+    std::vector<uint32_t> sf_offs;
     for (size_t i = 0; i < n; ++i) {
         const ParsedImage &im = *imgs[i];
         const SequenceParameterSet &s0 = im.params[0].sps;
@@ -90,79 +91,128 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
         for (size_t t = tile_offset; t < im.tiles.size(); t += tile_stride) {
             const TileJob &tj = im.tiles[t];
             const ParamSet &ps = im.params[size_t(tj.param)];
-            uint32_t seq;
-            auto it = std::find(seq_keys.begin(), seq_keys.end(), ps.key);
-            if (it == seq_keys.end()) {
-                seq = uint32_t(seq_keys.size());
-                seq_keys.push_back(ps.key);
-                uint32_t off = uint32_t(hb.sf.size());
-                hb.sf.resize(hb.sf.size() + kSfBlockBytes);
-                fill_scaling(ps, hb.sf.data() + off);
-                hb.seqs.push_back(make_seq(ps, off));
-            } else {
-                seq = uint32_t(it - seq_keys.begin());
+            // HEVC tiles (6.5.1) with no loop filter across their boundaries
+            // (heic_image.cpp) are independent pictures: each becomes a picture of
+            // the tile's size whose one substream is the tile's entry-point range,
+            // placed at the tile's offset in the cropped output.  Without tiles the
+            // loop runs once over the whole picture and all its substreams.
+            const bool tiled = ps.pps.tiles_enabled_flag;
+            const int pctb = 1 << ps.sps.log2_ctb_size;
+            const int ntc = int(ps.col_bd.size()) - 1, ntr = int(ps.row_bd.size()) - 1;
+            std::vector<uint32_t> starts{tj.sh.slice_data_raw_offset};
+            for (uint32_t e : tj.sh.entry_point_offset) starts.push_back(starts.back() + e);
+            starts.push_back(uint32_t(tj.payload_len));
+            for (int ht = 0; ht < (tiled ? ntc * ntr : 1); ++ht) {
+                SeqParams base = make_seq(ps, 0);
+                int vis_dx = 0, vis_dy = 0;  // output offset of the sub-picture's visible part
+                if (tiled) {
+                    const int tc = ht % ntc, tr = ht / ntc;
+                    const int x0 = ps.col_bd[size_t(tc)] * pctb, y0 = ps.row_bd[size_t(tr)] * pctb;
+                    const int x1 = std::min(ps.col_bd[size_t(tc) + 1] * pctb, base.width);
+                    const int y1 = std::min(ps.row_bd[size_t(tr) + 1] * pctb, base.height);
+                    // the picture's conformance window [conf_l, conf_l + out_w) clipped to the tile
+                    const int vx0 = std::max(x0, base.conf_l), vx1 = std::min(x1, base.conf_l + base.out_w);
+                    const int vy0 = std::max(y0, base.conf_t), vy1 = std::min(y1, base.conf_t + base.out_h);
+                    base.width = x1 - x0;
+                    base.height = y1 - y0;
+                    base.conf_l = vx0 - x0;
+                    base.conf_t = vy0 - y0;
+                    base.out_w = std::max(vx1 - vx0, 0);
+                    base.out_h = std::max(vy1 - vy0, 0);
+                    vis_dx = vx0 - ps.sps.conf_win_left;
+                    vis_dy = vy0 - ps.sps.conf_win_top;
+                    if (ht + 1 < ntc * ntr) base.flags |= SP_SUBSET_END;
+                }
+                std::vector<uint8_t> key = ps.key;
+                {
+                    const int32_t g[7] = {base.width, base.height, base.conf_l, base.conf_t, base.out_w, base.out_h,
+                                          int32_t(base.flags)};
+                    const uint8_t *gb = reinterpret_cast<const uint8_t *>(g);
+                    key.insert(key.end(), gb, gb + sizeof(g));
+                }
+                uint32_t seq;
+                auto it = std::find(seq_keys.begin(), seq_keys.end(), key);
+                if (it == seq_keys.end()) {
+                    seq = uint32_t(seq_keys.size());
+                    seq_keys.push_back(key);
+                    auto sf = std::find(sf_keys.begin(), sf_keys.end(), ps.key);  // one ScalingFactor block per PPS
+                    if (sf == sf_keys.end()) {
+                        sf_keys.push_back(ps.key);
+                        sf_offs.push_back(uint32_t(hb.sf.size()));
+                        hb.sf.resize(hb.sf.size() + kSfBlockBytes);
+                        fill_scaling(ps, hb.sf.data() + sf_offs.back());
+                        sf = sf_keys.end() - 1;
+                    }
+                    base.sf_off = sf_offs[size_t(sf - sf_keys.begin())];
+                    hb.seqs.push_back(base);
+                } else {
+                    seq = uint32_t(it - seq_keys.begin());
+                }
+                const SeqParams &sq = hb.seqs[seq];
+                const int ctb = 1 << sq.log2_ctb;
+                const int wctb = (sq.width + ctb - 1) / ctb, hctb = (sq.height + ctb - 1) / ctb;
+                const int w4 = (sq.width + 3) >> 2, h4 = (sq.height + 3) >> 2;
+                const uint64_t samples = uint64_t(sq.width) * sq.height * (sq.chroma_format ? 3 : 2) / 2;
+                PicDesc pd{};
+                pd.bits_off = hb.bits_size;
+                pd.sub_first = uint32_t(hb.subs.size());
+                if (tiled) {  // the tile's substream alone (it starts after a nonzero byte: no EP state carries in)
+                    const uint32_t r0 = starts[size_t(ht)], r1 = starts[size_t(ht) + 1];
+                    pd.bits_len = r1 - r0;
+                    pd.n_sub = 1;
+                    hb.pieces.push_back({tj.payload + r0, pd.bits_len, hb.bits_size});
+                    hb.subs.push_back(0);
+                } else {
+                    pd.bits_len = uint32_t(tj.payload_len);
+                    pd.n_sub = uint32_t(tj.sh.num_entry_point_offsets + 1);
+                    hb.pieces.push_back({tj.payload, tj.payload_len, hb.bits_size});
+                    for (size_t k = 0; k + 1 < starts.size(); ++k) hb.subs.push_back(starts[k]);
+                }
+                hb.subs.push_back(pd.bits_len);
+                hb.bits_size = (hb.bits_size + pd.bits_len + 63) & ~size_t(63);
+                if ((sq.flags & SP_WPP) && int(pd.n_sub) != hctb)
+                    throw HeifError("WPP picture without one entry point per CTB row");
+                pd.seq = seq;
+                pd.slice_qp = 26 + ps.pps.init_qp_minus26 + tj.sh.slice_qp_delta;
+                pd.cb_qp_off = tj.sh.slice_cb_qp_offset;
+                pd.cr_qp_off = tj.sh.slice_cr_qp_offset;
+                pd.sao_luma = tj.sh.slice_sao_luma_flag;
+                pd.sao_chroma = tj.sh.slice_sao_chroma_flag;
+                pd.dbk_disabled = tj.sh.slice_deblocking_filter_disabled_flag;
+                pd.beta_off = tj.sh.slice_beta_offset_div2;
+                pd.tc_off = tj.sh.slice_tc_offset_div2;
+                pd.image = uint32_t(i);
+                pd.out_x = int32_t((t % im.cols) * im.tile_width) + vis_dx;
+                pd.out_y = int32_t((t / im.cols) * im.tile_height) + vis_dy;
+                pd.recon_off = hb.recon_bytes;
+                hb.recon_bytes += (samples * uint64_t(hb.bps) + 255) & ~uint64_t(255);
+                pd.resid_off = hb.resid_elems;
+                hb.resid_elems += (samples + 127) & ~uint64_t(127);
+                pd.map_off = hb.map_bytes;
+                const int w8 = (sq.width + 7) >> 3;
+                hb.map_bytes += (uint64_t(2) * w4 * h4 + uint64_t(hctb) * w8 + 255) & ~uint64_t(255);
+                pd.sao_off = hb.sao_n;
+                hb.sao_n += uint64_t(wctb) * hctb;
+                pd.row_off = hb.rows;
+                hb.rows += uint32_t(hctb);
+                // worst case per CTB row: every 8x8 CU split into four 4x4 luma TBs + 2 chroma TBs
+                pd.tu_cap_row = uint32_t(wctb * (ctb / 8) * (ctb / 8) * 6 + 64);  // + staging trash slot / slack
+                pd.coef_cap_row = uint32_t(wctb * ctb * ctb * 3 / 2 + 64);  // + staging trash slot / slack
+                pd.tu_off = hb.tu_n;
+                hb.tu_n += uint64_t(pd.tu_cap_row) * hctb;
+                pd.coef_off = hb.coef_n;
+                hb.coef_n += uint64_t(pd.coef_cap_row) * hctb;
+                hb.pics.push_back(pd);
+                hb.pic_image.push_back(uint32_t(i));
+                hb.max_w = std::max(hb.max_w, sq.width);
+                hb.max_wctb = std::max(hb.max_wctb, wctb);
+                hb.max_rows = std::max(hb.max_rows, hctb);
+                hb.max_log2ctb = std::max(hb.max_log2ctb, int(sq.log2_ctb));
+                const bool wpp = (sq.flags & SP_WPP) != 0;
+                hb.lane_rows = std::max(hb.lane_rows, wpp ? std::min(hctb, max_lane_rows()) : 1);
+                if (wpp && hctb > max_lane_rows()) hb.wpp_ring = 1;
+                if (wpp) hb.max_wpp_rows = std::max(hb.max_wpp_rows, hctb);
             }
-            const SeqParams &sq = hb.seqs[seq];
-            const int ctb = 1 << sq.log2_ctb;
-            const int wctb = (sq.width + ctb - 1) / ctb, hctb = (sq.height + ctb - 1) / ctb;
-            const int w4 = (sq.width + 3) >> 2, h4 = (sq.height + 3) >> 2;
-            const uint64_t samples = uint64_t(sq.width) * sq.height * (sq.chroma_format ? 3 : 2) / 2;
-            PicDesc pd{};
-            pd.bits_off = hb.bits_size;
-            pd.bits_len = uint32_t(tj.payload_len);
-            hb.pieces.push_back({tj.payload, tj.payload_len, hb.bits_size});
-            hb.bits_size = (hb.bits_size + tj.payload_len + 63) & ~size_t(63);
-            pd.sub_first = uint32_t(hb.subs.size());
-            pd.n_sub = uint32_t(tj.sh.num_entry_point_offsets + 1);
-            uint32_t o = tj.sh.slice_data_raw_offset;
-            hb.subs.push_back(o);
-            for (uint32_t e : tj.sh.entry_point_offset) {
-                o += e;
-                hb.subs.push_back(o);
-            }
-            hb.subs.push_back(pd.bits_len);
-            if ((sq.flags & SP_WPP) && int(pd.n_sub) != hctb)
-                throw HeifError("WPP picture without one entry point per CTB row");
-            pd.seq = seq;
-            pd.slice_qp = 26 + ps.pps.init_qp_minus26 + tj.sh.slice_qp_delta;
-            pd.cb_qp_off = tj.sh.slice_cb_qp_offset;
-            pd.cr_qp_off = tj.sh.slice_cr_qp_offset;
-            pd.sao_luma = tj.sh.slice_sao_luma_flag;
-            pd.sao_chroma = tj.sh.slice_sao_chroma_flag;
-            pd.dbk_disabled = tj.sh.slice_deblocking_filter_disabled_flag;
-            pd.beta_off = tj.sh.slice_beta_offset_div2;
-            pd.tc_off = tj.sh.slice_tc_offset_div2;
-            pd.image = uint32_t(i);
-            pd.out_x = int32_t((t % im.cols) * im.tile_width);
-            pd.out_y = int32_t((t / im.cols) * im.tile_height);
-            pd.recon_off = hb.recon_bytes;
-            hb.recon_bytes += (samples * uint64_t(hb.bps) + 255) & ~uint64_t(255);
-            pd.resid_off = hb.resid_elems;
-            hb.resid_elems += (samples + 127) & ~uint64_t(127);
-            pd.map_off = hb.map_bytes;
-            const int w8 = (sq.width + 7) >> 3;
-            hb.map_bytes += (uint64_t(2) * w4 * h4 + uint64_t(hctb) * w8 + 255) & ~uint64_t(255);
-            pd.sao_off = hb.sao_n;
-            hb.sao_n += uint64_t(wctb) * hctb;
-            pd.row_off = hb.rows;
-            hb.rows += uint32_t(hctb);
-            // worst case per CTB row: every 8x8 CU split into four 4x4 luma TBs + 2 chroma TBs
-            pd.tu_cap_row = uint32_t(wctb * (ctb / 8) * (ctb / 8) * 6 + 64);  // + staging trash slot / slack
-            pd.coef_cap_row = uint32_t(wctb * ctb * ctb * 3 / 2 + 64);  // + staging trash slot / slack
-            pd.tu_off = hb.tu_n;
-            hb.tu_n += uint64_t(pd.tu_cap_row) * hctb;
-            pd.coef_off = hb.coef_n;
-            hb.coef_n += uint64_t(pd.coef_cap_row) * hctb;
-            hb.pics.push_back(pd);
-            hb.pic_image.push_back(uint32_t(i));
-            hb.max_w = std::max(hb.max_w, sq.width);
-            hb.max_wctb = std::max(hb.max_wctb, wctb);
-            hb.max_rows = std::max(hb.max_rows, hctb);
-            hb.max_log2ctb = std::max(hb.max_log2ctb, int(sq.log2_ctb));
-            const bool wpp = (sq.flags & SP_WPP) != 0;
-            hb.lane_rows = std::max(hb.lane_rows, wpp ? std::min(hctb, max_lane_rows()) : 1);
-            if (wpp && hctb > max_lane_rows()) hb.wpp_ring = 1;
-            if (wpp) hb.max_wpp_rows = std::max(hb.max_wpp_rows, hctb);
         }
     }
     hb.bits_size += 128;

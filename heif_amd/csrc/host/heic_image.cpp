@@ -18,7 +18,12 @@ void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p
     if (s.separate_colour_plane_flag) throw UnsupportedError("separate_colour_plane_flag");
     if (s.bit_depth_luma_minus8 != s.bit_depth_chroma_minus8) throw UnsupportedError("luma/chroma bit depth differ");
     if (s.range_extension_tools || p.range_extension_tools) throw UnsupportedError("range-extension coding tools");
-    if (p.tiles_enabled_flag) throw UnsupportedError("HEVC tiles inside a picture");
+    // HEVC tiles decode as independent sub-pictures (batch.cpp) when no loop
+    // filter crosses a tile boundary
+    if (p.tiles_enabled_flag && p.entropy_coding_sync_enabled_flag)
+        throw UnsupportedError("HEVC tiles together with WPP");
+    if (p.tiles_enabled_flag && p.loop_filter_across_tiles_enabled_flag)
+        throw UnsupportedError("HEVC tiles with loop_filter_across_tiles_enabled_flag");
     if (s.pic_width_in_luma_samples > 8192 || s.pic_height_in_luma_samples > 8192)
         throw UnsupportedError("picture larger than 8192");
     if (s.pic_width_in_luma_samples % (1 << s.log2_min_luma_coding_block_size) ||
@@ -117,6 +122,7 @@ ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id) {
             ps.sps = sequence_parameter_set_rbsp(nal_rbsp(cfg.sps[0]));
             ps.pps = picture_parameter_set_rbsp(nal_rbsp(cfg.pps[0]), ps.sps);
             check_supported(ps.sps, ps.pps);
+            tile_boundaries(ps.sps, ps.pps, ps.col_bd, ps.row_bd);
             param = int(img.params.size());
             img.params.push_back(std::move(ps));
             param_of_prop[hv->offset] = param;
@@ -152,6 +158,9 @@ ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id) {
         }
         if (!have_vcl) throw HeifError("tile item holds no VCL NAL unit");
         job.sh = slice_segment_header(job.payload, job.payload_len, job.nal, ps.sps, ps.pps);
+        const size_t ntiles = (ps.col_bd.size() - 1) * (ps.row_bd.size() - 1);
+        if (ps.pps.tiles_enabled_flag && size_t(job.sh.num_entry_point_offsets) + 1 != ntiles)
+            throw HeifError("tiled picture without one entry point per tile");
         img.tiles.push_back(std::move(job));
     }
     const SequenceParameterSet &s0 = img.params[0].sps;

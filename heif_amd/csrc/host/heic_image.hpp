@@ -13,6 +13,7 @@ struct ParamSet {
     VideoParameterSet vps;
     SequenceParameterSet sps;
     PictureParameterSet pps;
+    std::vector<int> col_bd, row_bd;  // HEVC tile boundaries in CTBs (one tile without tiles)
 };
 
 struct TileJob {

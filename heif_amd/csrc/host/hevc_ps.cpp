@@ -397,6 +397,10 @@ PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp,
     p.entropy_coding_sync_enabled_flag = r.read_flag();
     if (p.tiles_enabled_flag) {
         int nc = r.read_ue_max(19, "num_tile_columns_minus1") + 1, nr = r.read_ue_max(21, "num_tile_rows_minus1") + 1;
+        if (nc > sps.pic_width_in_ctbs_y() || nr > sps.pic_height_in_ctbs_y())
+            throw HeifError("more tile columns / rows than CTBs");
+        p.num_tile_columns = nc;
+        p.num_tile_rows = nr;
         p.uniform_spacing_flag = r.read_flag();
         if (!p.uniform_spacing_flag) {
             for (int i = 0; i < nc - 1; ++i) p.column_widths.push_back(int(r.read_ue()) + 1);
@@ -568,6 +572,24 @@ SliceSegmentHeader slice_segment_header_prefix(const uint8_t *payload, size_t le
     return h;
 }
 }  // namespace
+
+void tile_boundaries(const SequenceParameterSet &sps, const PictureParameterSet &pps, std::vector<int> &col_bd,
+                     std::vector<int> &row_bd) {
+    for (int pass = 0; pass < 2; ++pass) {
+        const int n = !pps.tiles_enabled_flag ? 1 : pass ? pps.num_tile_rows : pps.num_tile_columns;
+        const int tot = pass ? sps.pic_height_in_ctbs_y() : sps.pic_width_in_ctbs_y();
+        const std::vector<int> &ex = pass ? pps.row_heights : pps.column_widths;
+        std::vector<int> &bd = pass ? row_bd : col_bd;
+        bd.assign(size_t(n) + 1, 0);
+        for (int i = 0; i < n; ++i) {
+            const int sz = (!pps.tiles_enabled_flag || pps.uniform_spacing_flag)
+                               ? ((i + 1) * tot) / n - (i * tot) / n
+                               : (i + 1 < n ? ex[size_t(i)] : tot - bd[size_t(i)]);
+            if (sz <= 0 || bd[size_t(i)] + sz > tot) throw HeifError("tile sizes exceed the picture");
+            bd[size_t(i) + 1] = bd[size_t(i)] + sz;
+        }
+    }
+}
 
 HevcConfig parse_hvcc(const uint8_t *p, size_t n) {
     if (n < 23) throw HeifError("hvcC too short");

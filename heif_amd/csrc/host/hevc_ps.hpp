@@ -82,6 +82,7 @@ struct PictureParameterSet {
     int pps_cb_qp_offset = 0, pps_cr_qp_offset = 0;
     bool pps_slice_chroma_qp_offsets_present_flag = false;
     bool transquant_bypass_enabled_flag = false, tiles_enabled_flag = false, entropy_coding_sync_enabled_flag = false;
+    int num_tile_columns = 1, num_tile_rows = 1;
     std::vector<int> column_widths, row_heights;  // kept (reference drops them, :393-400)
     bool uniform_spacing_flag = true, loop_filter_across_tiles_enabled_flag = false;
     bool pps_loop_filter_across_slices_enabled_flag = false;
@@ -108,6 +109,12 @@ struct SliceSegmentHeader {  // grammar.rs:550-572 + entry points in raw bytes
     std::vector<uint32_t> entry_point_offset;  // offset_minus1 + 1, raw bytes
     uint32_t slice_data_raw_offset = 0;        // raw payload byte where slice_segment_data() starts
 };
+
+// 6.5.1 (6-3..6-6): tile column / row boundaries in CTBs, num + 1 entries
+// each ({0, PicWidthInCtbsY} without tiles).  Throws HeifError when explicit
+// sizes leave no CTB for the last column / row.
+void tile_boundaries(const SequenceParameterSet &sps, const PictureParameterSet &pps, std::vector<int> &col_bd,
+                     std::vector<int> &row_bd);
 
 VideoParameterSet video_parameter_set_rbsp(const std::vector<uint8_t> &rbsp);
 SequenceParameterSet sequence_parameter_set_rbsp(const std::vector<uint8_t> &rbsp);

@@ -1466,8 +1466,9 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
         }
     }
     const bool last_in_pic = L.row == P.hctb - 1 && L.c == P.wctb - 1;
-    if (term(L, G) != (last_in_pic ? 1 : 0)) L.status |= ST_SUBSTREAM_END;
-    if (!last_in_pic && (L.fl & F_WPP) && L.c == P.wctb - 1 && !term(L, G)) L.status |= ST_SUBSTREAM_END;
+    const bool eos = last_in_pic && !(P.flags & SP_SUBSET_END);  // end_of_slice_segment_flag = 1 here
+    if (term(L, G) != (eos ? 1 : 0)) L.status |= ST_SUBSTREAM_END;
+    if (!eos && (last_in_pic || ((L.fl & F_WPP) && L.c == P.wctb - 1)) && !term(L, G)) L.status |= ST_SUBSTREAM_END;
     if (L.budget + L.k < 0) L.status |= ST_OVERRUN;  // read past the NAL unit
     ++L.c;
     const uint32_t pv = (L.fl & F_STOP) ? kProgDone : (uint32_t)L.row * (uint32_t)P.wctb + (uint32_t)L.c;

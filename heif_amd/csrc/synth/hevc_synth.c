@@ -13,7 +13,7 @@
  * The result is a conforming bitstream whose reconstruction exercises every
  * intra mode, TU size, transform-skip / bypass / sign hiding / scaling list /
  * cu_qp_delta path at any bit depth, chroma format 4:0:0 or 4:2:0, CTB size
- * and picture size, with WPP substreams and entry points.
+ * and picture size, with WPP or tile substreams and entry points.
  *
  * Arithmetic coder: the standard low/range encoder with carry propagation
  * through buffered 0xff bytes (the inverse of 9.3.4.3), flushed at every
@@ -286,6 +286,7 @@ typedef struct {
     cabe_t c;
     int W, H, log2ctb, ctb, wctb, hctb, w4, h4, qpbdY;
     uint8_t *ipm, *depth;
+    int *ts2rs, *tile_rs; /* 6.5.1 tile scan; tile of each CTB by raster address */
     /* current CU */
     int cu_bypass, intra_split, max_trafo_depth, chroma_mode;
     int is_qp_coded;
@@ -294,6 +295,45 @@ typedef struct {
 static void set_map(pic_t *p, uint8_t *m, int x0, int y0, int n, uint8_t v) {
     for (int y = y0 >> 2; y < (y0 + n) >> 2 && y < p->h4; y++)
         for (int x = x0 >> 2; x < (x0 + n) >> 2 && x < p->w4; x++) m[y * p->w4 + x] = v;
+}
+
+static int tiles_on(const synth_params *P) { return P->tile_cols * P->tile_rows > 1; }
+
+/* the neighbour (xn,yn) of (x,y) lies in the same tile (availability 6.4.1; in
+ * the picture and earlier in decoding order is the caller's check) */
+static int same_tile(const pic_t *p, int x, int y, int xn, int yn) {
+    return p->tile_rs[(yn >> p->log2ctb) * p->wctb + (xn >> p->log2ctb)] ==
+           p->tile_rs[(y >> p->log2ctb) * p->wctb + (x >> p->log2ctb)];
+}
+
+/* 6.5.1 column / row boundaries (6-3..6-6) → CtbAddrTsToRs, TileId */
+static int tile_layout(pic_t *p) {
+    const synth_params *P = p->P;
+    int nc = tiles_on(P) ? P->tile_cols : 1, nr = tiles_on(P) ? P->tile_rows : 1;
+    int colBd[SYNTH_MAX_TILES + 1], rowBd[SYNTH_MAX_TILES + 1];
+    for (int pass = 0; pass < 2; pass++) {
+        int n = pass ? nr : nc, tot = pass ? p->hctb : p->wctb, *bd = pass ? rowBd : colBd;
+        const int32_t *ex = pass ? P->tile_row_h : P->tile_col_w;
+        bd[0] = 0;
+        for (int i = 0; i < n; i++) {
+            int sz = (!tiles_on(P) || P->tile_uniform) ? ((i + 1) * tot) / n - (i * tot) / n
+                                                       : (i + 1 < n ? ex[i] : tot - bd[i]);
+            if (sz <= 0) return -1;
+            bd[i + 1] = bd[i] + sz;
+        }
+    }
+    int nctb = p->wctb * p->hctb, ts = 0;
+    p->ts2rs = (int *)malloc(sizeof(int) * (size_t)nctb);
+    p->tile_rs = (int *)malloc(sizeof(int) * (size_t)nctb);
+    if (!p->ts2rs || !p->tile_rs) return -1;
+    for (int ty = 0; ty < nr; ty++)
+        for (int tx = 0; tx < nc; tx++)
+            for (int y = rowBd[ty]; y < rowBd[ty + 1]; y++)
+                for (int x = colBd[tx]; x < colBd[tx + 1]; x++) {
+                    p->ts2rs[ts++] = y * p->wctb + x;
+                    p->tile_rs[y * p->wctb + x] = ty * nc + tx;
+                }
+    return 0;
 }
 
 static int scan_idx_for(const pic_t *p, int log2n, int cIdx, int mode) {
@@ -517,7 +557,7 @@ static void mpm_list(pic_t *p, int xPb, int yPb, int l[3]) {
     int cand[2];
     for (int k = 0; k < 2; k++) {
         int xn = k == 0 ? xPb - 1 : xPb, yn = k == 0 ? yPb : yPb - 1;
-        if (xn < 0 || yn < 0) cand[k] = 1;
+        if (xn < 0 || yn < 0 || !same_tile(p, xPb, yPb, xn, yn)) cand[k] = 1;
         else if (k == 1 && yPb - 1 < ((yPb >> p->log2ctb) << p->log2ctb)) cand[k] = 1;
         else cand[k] = p->ipm[(yn >> 2) * p->w4 + (xn >> 2)];
     }
@@ -592,8 +632,10 @@ static void coding_quadtree(pic_t *p, int x0, int y0, int log2cb, int depth) {
     int n = 1 << log2cb, split;
     if (x0 + n <= p->W && y0 + n <= p->H && log2cb > P->log2_min_cb) {
         int cond = 0;
-        if (x0 > 0 && p->depth[(y0 >> 2) * p->w4 + ((x0 - 1) >> 2)] > depth) cond++;
-        if (y0 > 0 && p->depth[((y0 - 1) >> 2) * p->w4 + (x0 >> 2)] > depth) cond++;
+        if (x0 > 0 && same_tile(p, x0, y0, x0 - 1, y0) && p->depth[(y0 >> 2) * p->w4 + ((x0 - 1) >> 2)] > depth)
+            cond++;
+        if (y0 > 0 && same_tile(p, x0, y0, x0, y0 - 1) && p->depth[((y0 - 1) >> 2) * p->w4 + (x0 >> 2)] > depth)
+            cond++;
         split = pct(&p->rng, log2cb >= 5 ? 60 : 45);
         ce_bin(&p->c, C_SPLIT_CU + cond, split);
     } else {
@@ -615,12 +657,13 @@ static void coding_quadtree(pic_t *p, int x0, int y0, int log2cb, int depth) {
 static void sao_syntax(pic_t *p, int rx, int ry, int sao_l, int sao_c) {
     const synth_params *P = p->P;
     cabe_t *c = &p->c;
-    if (rx > 0) {
+    const int t = p->tile_rs[ry * p->wctb + rx];
+    if (rx > 0 && p->tile_rs[ry * p->wctb + rx - 1] == t) {
         int ml = pct(&p->rng, 25);
         ce_bin(c, C_SAO_MERGE, ml);
         if (ml) return;
     }
-    if (ry > 0) {
+    if (ry > 0 && p->tile_rs[(ry - 1) * p->wctb + rx] == t) {
         int mu = pct(&p->rng, 25);
         ce_bin(c, C_SAO_MERGE, mu);
         if (mu) return;
@@ -811,8 +854,18 @@ long synth_pps(const synth_params *P, uint8_t *out, size_t cap) {
     bw_bits(&w, 0, 1);
     bw_bits(&w, 0, 1);
     bw_bits(&w, P->tq_bypass ? 1 : 0, 1);
-    bw_bits(&w, 0, 1); /* tiles */
+    bw_bits(&w, tiles_on(P) ? 1 : 0, 1); /* tiles_enabled_flag */
     bw_bits(&w, P->wpp ? 1 : 0, 1); /* entropy_coding_sync */
+    if (tiles_on(P)) {
+        bw_ue(&w, (uint32_t)(P->tile_cols - 1));
+        bw_ue(&w, (uint32_t)(P->tile_rows - 1));
+        bw_bits(&w, P->tile_uniform ? 1 : 0, 1);
+        if (!P->tile_uniform) {
+            for (int i = 0; i + 1 < P->tile_cols; i++) bw_ue(&w, (uint32_t)(P->tile_col_w[i] - 1));
+            for (int i = 0; i + 1 < P->tile_rows; i++) bw_ue(&w, (uint32_t)(P->tile_row_h[i] - 1));
+        }
+        bw_bits(&w, P->tile_lf_across ? 1 : 0, 1);
+    }
     bw_bits(&w, 0, 1); /* loop filter across slices */
     bw_bits(&w, 1, 1); /* deblocking control present */
     bw_bits(&w, 0, 1);
@@ -844,6 +897,18 @@ int synth_check_params(const synth_params *P) {
     if (P->diff_cu_qp_delta_depth < 0 || P->diff_cu_qp_delta_depth > P->log2_ctb - P->log2_min_cb) return -1;
     if (P->density < 0 || P->density > 100) return -1;
     if (P->wpp != 0 && P->wpp != 1) return -1;
+    if (P->tile_cols < 0 || P->tile_rows < 0 || P->tile_cols > SYNTH_MAX_TILES || P->tile_rows > SYNTH_MAX_TILES)
+        return -1;
+    if (tiles_on(P)) {
+        int ctb = 1 << P->log2_ctb, wctb = (P->width + ctb - 1) / ctb, hctb = (P->height + ctb - 1) / ctb;
+        if (P->wpp || P->tile_cols < 1 || P->tile_rows < 1 || P->tile_cols > wctb || P->tile_rows > hctb) return -1;
+        if (!P->tile_uniform) {
+            int sw = 0, sh = 0;
+            for (int i = 0; i + 1 < P->tile_cols; i++) { if (P->tile_col_w[i] < 1) return -1; sw += P->tile_col_w[i]; }
+            for (int i = 0; i + 1 < P->tile_rows; i++) { if (P->tile_row_h[i] < 1) return -1; sh += P->tile_row_h[i]; }
+            if (sw >= wctb || sh >= hctb) return -1;
+        }
+    }
     return 0;
 }
 
@@ -866,8 +931,13 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
     p->qpbdY = 6 * (P->bit_depth - 8);
     p->ipm = (uint8_t *)calloc((size_t)p->w4 * p->h4, 1);
     p->depth = (uint8_t *)calloc((size_t)p->w4 * p->h4, 1);
-    bw_t *subs = (bw_t *)calloc((size_t)p->hctb, sizeof(bw_t));
-    if (!p->ipm || !p->depth || !subs) { free(p->ipm); free(p->depth); free(subs); return -1; }
+    const int nctb = p->wctb * p->hctb;
+    const int nsub = P->wpp ? p->hctb : tiles_on(P) ? P->tile_cols * P->tile_rows : 1;
+    bw_t *subs = (bw_t *)calloc((size_t)nsub, sizeof(bw_t));
+    if (!p->ipm || !p->depth || !subs || tile_layout(p)) {
+        free(p->ipm); free(p->depth); free(subs); free(p->ts2rs); free(p->tile_rs);
+        return -1;
+    }
     int slice_qp_delta = P->slice_qp_delta;
     int slice_qp = P->init_qp + slice_qp_delta;
     int sao_l = P->sao ? !pct(&p->rng, 10) : 0;
@@ -875,28 +945,33 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
     uint8_t wst[C_NUM], wmps[C_NUM];
     int saved = 0;
     ce_init_ctx(&p->c, slice_qp);
-    /* WPP: one substream per CTB row (9.3.1: contexts after CTU 1 of the row
-     * above, engine restarted at the entry point, end_of_subset_one_bit and
-     * byte_alignment at the row end).  Without WPP the slice is one substream:
-     * the engine and the contexts run on across rows (slice.rs:206-231). */
-    const int nsub = P->wpp ? p->hctb : 1;
-    for (int ry = 0; ry < p->hctb; ry++) {
-        if (P->wpp || ry == 0) ce_start(&p->c, &subs[P->wpp ? ry : 0]);
-        if (P->wpp && ry > 0) {
-            if (p->wctb > 1 && saved) { memcpy(p->c.st, wst, C_NUM); memcpy(p->c.mps, wmps, C_NUM); }
-            else ce_init_ctx(&p->c, slice_qp);
+    /* CTUs in tile scan (7.3.8.1).  WPP: one substream per CTB row (9.3.1:
+     * contexts after CTU 1 of the row above, engine restarted at the entry
+     * point).  Tiles: one substream per tile, contexts initialised at its first
+     * CTU.  Each substream but the last ends in end_of_subset_one_bit and
+     * byte_alignment().  Otherwise the slice is one substream: the engine and
+     * the contexts run on across rows (slice.rs:206-231). */
+    for (int ts = 0, sub = 0; ts < nctb; ts++) {
+        const int rs = p->ts2rs[ts], rx = rs % p->wctb, ry = rs / p->wctb;
+        const int tile_start = ts > 0 && p->tile_rs[rs] != p->tile_rs[p->ts2rs[ts - 1]];
+        if (ts == 0 || (P->wpp && rx == 0) || tile_start) {
+            ce_start(&p->c, &subs[sub]);
+            if (tile_start) ce_init_ctx(&p->c, slice_qp);
+            else if (ts > 0) { /* WPP row start */
+                if (p->wctb > 1 && saved) { memcpy(p->c.st, wst, C_NUM); memcpy(p->c.mps, wmps, C_NUM); }
+                else ce_init_ctx(&p->c, slice_qp);
+            }
         }
-        for (int rx = 0; rx < p->wctb; rx++) {
-            if (sao_l || sao_c) sao_syntax(p, rx, ry, sao_l, sao_c);
-            coding_quadtree(p, rx << p->log2ctb, ry << p->log2ctb, p->log2ctb, 0);
-            if (rx == 1) { memcpy(wst, p->c.st, C_NUM); memcpy(wmps, p->c.mps, C_NUM); saved = 1; }
-            int last = (rx == p->wctb - 1 && ry == p->hctb - 1);
-            ce_term(&p->c, last);
+        if (sao_l || sao_c) sao_syntax(p, rx, ry, sao_l, sao_c);
+        coding_quadtree(p, rx << p->log2ctb, ry << p->log2ctb, p->log2ctb, 0);
+        if (P->wpp && rx == 1) { memcpy(wst, p->c.st, C_NUM); memcpy(wmps, p->c.mps, C_NUM); saved = 1; }
+        const int last = ts == nctb - 1;
+        ce_term(&p->c, last); /* end_of_slice_segment_flag */
+        if (last || (P->wpp && rx == p->wctb - 1) || p->tile_rs[p->ts2rs[ts + 1]] != p->tile_rs[rs]) {
+            if (!last) ce_term(&p->c, 1); /* end_of_subset_one_bit */
+            ce_finish(&p->c);
+            bw_align1(&subs[sub++]); /* byte_alignment() / rbsp_slice_segment_trailing_bits() */
         }
-        if (!P->wpp && ry != p->hctb - 1) continue;
-        if (ry != p->hctb - 1) ce_term(&p->c, 1); /* end_of_subset_one_bit */
-        ce_finish(&p->c);
-        bw_align1(&subs[P->wpp ? ry : 0]); /* byte_alignment() / rbsp_slice_segment_trailing_bits() */
     }
     /* substreams with emulation prevention, to size the entry points */
     long ret = -1;
@@ -904,7 +979,7 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
     int err = 0;
     for (int r = 0; r < nsub; r++) { total += subs[r].n; err |= subs[r].err; }
     uint8_t *data = (uint8_t *)malloc(total * 3 / 2 + 16);
-    size_t *sub_len = (size_t *)calloc((size_t)p->hctb, sizeof(size_t));
+    size_t *sub_len = (size_t *)calloc((size_t)nsub, sizeof(size_t));
     if (data && sub_len && !err) {
         size_t o = 0;
         int z = 0; /* the slice header ends in a nonzero byte (its alignment bit) */
@@ -924,7 +999,7 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
             if (P->chroma_format) bw_bits(&w, (uint32_t)sao_c, 1);
         }
         bw_se(&w, slice_qp_delta);
-        if (P->wpp) { /* num_entry_point_offsets: present only with tiles or WPP (7.3.6.1) */
+        if (P->wpp || tiles_on(P)) { /* num_entry_point_offsets: present only with tiles or WPP (7.3.6.1) */
             bw_ue(&w, (uint32_t)(nsub - 1));
             if (nsub > 1) {
                 size_t mx = 1;
@@ -958,5 +1033,7 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
     free(subs);
     free(p->ipm);
     free(p->depth);
+    free(p->ts2rs);
+    free(p->tile_rs);
     return ret;
 }

@@ -8,6 +8,8 @@
 extern "C" {
 #endif
 
+#define SYNTH_MAX_TILES 8
+
 typedef struct {
     int32_t width, height;            /* pic_width/height_in_luma_samples (multiples of MinCbSize) */
     int32_t conf_right, conf_bottom;  /* conformance-window crop in luma samples (even for 4:2:0) */
@@ -21,6 +23,11 @@ typedef struct {
     int32_t density;                  /* sig_coeff_flag probability, percent */
     int32_t wpp;                      /* entropy_coding_sync_enabled_flag: 1 = one substream per CTB row
                                          with entry points, 0 = the whole slice in one substream */
+    /* HEVC tiles (tiles_enabled_flag when tile_cols * tile_rows > 1; needs wpp 0):
+     * uniform_spacing_flag, else column widths / row heights in CTBs for all
+     * but the last column / row; loop_filter_across_tiles_enabled_flag */
+    int32_t tile_cols, tile_rows, tile_uniform, tile_lf_across;
+    int32_t tile_col_w[SYNTH_MAX_TILES], tile_row_h[SYNTH_MAX_TILES];
 } synth_params;
 
 /* Each returns the NAL unit length (2-byte header included, emulation
@@ -29,7 +36,7 @@ typedef struct {
 long synth_vps(const synth_params *p, uint8_t *out, size_t cap);
 long synth_sps(const synth_params *p, uint8_t *out, size_t cap);
 long synth_pps(const synth_params *p, uint8_t *out, size_t cap);
-/* One IDR picture (a single I slice; WPP substreams + entry points when p->wpp). */
+/* One IDR picture (a single I slice; WPP or tile substreams + entry points). */
 long synth_picture(const synth_params *p, uint64_t seed, uint8_t *out, size_t cap);
 int synth_check_params(const synth_params *p);
 

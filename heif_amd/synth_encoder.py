@@ -30,7 +30,9 @@ class _Params(ctypes.Structure):
         "sign_hiding", "cu_qp_delta", "diff_cu_qp_delta_depth",
         "transform_skip", "tq_bypass", "scaling_list", "strong_intra",
         "init_qp", "slice_qp_delta", "cb_qp_offset", "cr_qp_offset",
-        "sao", "deblock_disabled", "beta_offset_div2", "tc_offset_div2", "density", "wpp")]
+        "sao", "deblock_disabled", "beta_offset_div2", "tc_offset_div2", "density", "wpp",
+        "tile_cols", "tile_rows", "tile_uniform", "tile_lf_across")] + [
+        ("tile_col_w", ctypes.c_int32 * 8), ("tile_row_h", ctypes.c_int32 * 8)]
 
 
 @dataclasses.dataclass
@@ -66,9 +68,22 @@ class SynthParams:
     tc_offset_div2: int = 0
     density: int = 35
     wpp: int = 1  # entropy_coding_sync_enabled_flag (0: one CABAC substream per picture, BASELINE config 2)
+    # HEVC tiles inside the picture (tiles_enabled_flag when tile_cols * tile_rows > 1; needs wpp=0)
+    tile_cols: int = 1
+    tile_rows: int = 1
+    tile_uniform: int = 1
+    tile_lf_across: int = 0          # loop_filter_across_tiles_enabled_flag
+    tile_col_w: Tuple[int, ...] = ()  # explicit widths / heights in CTBs (all but the last), tile_uniform=0
+    tile_row_h: Tuple[int, ...] = ()
 
     def _c(self) -> _Params:
-        return _Params(*[getattr(self, n) for n, _ in _Params._fields_])
+        c = _Params(*[getattr(self, n) for n, t in _Params._fields_ if t is ctypes.c_int32])
+        for name in ("tile_col_w", "tile_row_h"):
+            v = list(getattr(self, name))
+            if len(v) > 8:
+                raise ValueError(f"{name}: at most 8 entries")
+            getattr(c, name)[:len(v)] = v
+        return c
 
 
 def _load():
@@ -138,7 +153,8 @@ def hvcc(p: SynthParams, vps: bytes, sps: bytes, pps: bytes) -> bytes:
     # compatibility/constraint bytes can carry emulation prevention).
     ptl = _unescape(sps[2:])[1:13]
     rec = bytes([1]) + ptl[:1] + ptl[1:5] + ptl[5:11] + ptl[11:12]
-    rec += struct.pack(">H", 0xF000) + bytes([0xFC | (2 if p.wpp else 0)])  # min_spatial_segmentation, parallelism
+    par = 3 if p.wpp else 2 if p.tile_cols * p.tile_rows > 1 else 0  # parallelismType: 3 wavefront, 2 tiles
+    rec += struct.pack(">H", 0xF000) + bytes([0xFC | par])  # min_spatial_segmentation, parallelism
     rec += bytes([0xFC | p.chroma_format, 0xF8 | (p.bit_depth - 8), 0xF8 | (p.bit_depth - 8)])
     rec += struct.pack(">H", 0) + bytes([0x0F])                     # avgFrameRate, 1 layer, nested, 4-byte lengths
     arrays = b""

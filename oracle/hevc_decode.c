@@ -28,7 +28,10 @@
 #include <string.h>
 
 static __thread char g_err[256];
-static __thread int g_debug_flags; /* bit0: skip deblocking, bit1: skip SAO (bring-up only) */
+/* bit0: skip deblocking, bit1: skip SAO (bring-up only); bit2: a picture may
+ * end in end_of_slice_segment_flag 0 + end_of_subset_one_bit 1 — a tile cut
+ * out of a tiled picture as a stand-alone picture (tests/hevc_tiles.py) */
+static __thread int g_debug_flags;
 void oracle_set_debug_flags(int flags) { g_debug_flags = flags; }
 int oracle_fail(const char *msg) {
     snprintf(g_err, sizeof(g_err), "%s", msg);
@@ -426,14 +429,22 @@ static int parse_pps(const uint8_t *rbsp, size_t n, const hevc_sps *sps, hevc_pp
     p->transquant_bypass = (int)br_u(&b, 1);
     p->tiles = (int)br_u(&b, 1);
     p->wpp = (int)br_u(&b, 1);
+    p->tile_cols = p->tile_rows = p->tile_uniform = 1;
+    p->lf_across_tiles = 1;
     if (p->tiles) {
-        int nc = (int)br_ue(&b), nr = (int)br_ue(&b);
-        int uniform = (int)br_u(&b, 1);
-        if (!uniform) {
-            for (int i = 0; i < nc; i++) br_ue(&b);
-            for (int i = 0; i < nr; i++) br_ue(&b);
+        /* num_tile_columns/rows_minus1, uniform_spacing_flag, column_width /
+         * row_height_minus1[], loop_filter_across_tiles_enabled_flag
+         * (parameter_set_reader.rs:380-408) */
+        uint32_t nc = br_ue(&b) + 1, nr = br_ue(&b) + 1;
+        if (nc > HEVC_MAX_TILE_DIM || nr > HEVC_MAX_TILE_DIM || nc * nr < 2) return oracle_fail("tile count");
+        p->tile_cols = (int)nc;
+        p->tile_rows = (int)nr;
+        p->tile_uniform = (int)br_u(&b, 1);
+        if (!p->tile_uniform) {
+            for (int i = 0; i + 1 < p->tile_cols; i++) p->tile_col_w[i] = (int)br_ue(&b) + 1;
+            for (int i = 0; i + 1 < p->tile_rows; i++) p->tile_row_h[i] = (int)br_ue(&b) + 1;
         }
-        br_u(&b, 1);
+        p->lf_across_tiles = (int)br_u(&b, 1);
     }
     p->loop_filter_across_slices = (int)br_u(&b, 1);
     if (br_u(&b, 1)) {
@@ -714,6 +725,10 @@ typedef struct {
     /* QP state */
     int cu_qp_delta_val, is_cu_qp_delta_coded, qg_new, qg_x, qg_y, qp_prev_last, qp_pred, qpy_cur;
     int ctb_x, ctb_y, first_qg_in_ctb_row_pending, first_qg_in_slice;
+    /* 6.5.1 tiles: column / row boundaries in CTBs, CtbAddrRsToTs / TsToRs and
+     * the tile of each CTB by raster address (one tile when tiles is 0) */
+    int colBd[HEVC_MAX_TILE_DIM + 1], rowBd[HEVC_MAX_TILE_DIM + 1];
+    int *rs2ts, *ts2rs, *tile_rs;
     /* current CU */
     int cu_bypass, cu_intra_split, cu_max_trafo_depth, cu_chroma_mode_c;
 } pic_t;
@@ -723,10 +738,11 @@ typedef struct {
 #define F_NOFILT 4
 
 static int zscan_addr(const pic_t *p, int x, int y) {
-    /* MinTbAddrZs (6-10) for luma sample (x,y) */
+    /* MinTbAddrZs (6-10) for luma sample (x,y): CtbAddrRsToTs of its CTB, then
+     * the z-order inside the CTB */
     int tbx = x >> p->minTb, tby = y >> p->minTb;
     int sh = p->log2ctb - p->minTb;
-    int ctbAddr = (tbx >> sh) + (tby >> sh) * p->wctb;
+    int ctbAddr = p->rs2ts[(tbx >> sh) + (tby >> sh) * p->wctb];
     int v = ctbAddr << (sh * 2);
     for (int i = 0; i < sh; i++) {
         int m = 1 << i;
@@ -734,10 +750,56 @@ static int zscan_addr(const pic_t *p, int x, int y) {
     }
     return v;
 }
-/* 6.4.1 z-scan availability (single slice, no tiles) */
+/* tile of the CTB holding luma sample (x,y) (TileId by raster CTB address) */
+static int tile_at(const pic_t *p, int x, int y) {
+    return p->tile_rs[(y >> p->log2ctb) * p->wctb + (x >> p->log2ctb)];
+}
+/* 6.4.1 z-scan availability (single slice): outside the picture, later in
+ * decoding order or in another tile ⇒ unavailable */
 static int avail_zs(const pic_t *p, int xc, int yc, int xn, int yn) {
     if (xn < 0 || yn < 0 || xn >= p->W || yn >= p->H) return 0;
+    if (tile_at(p, xn, yn) != tile_at(p, xc, yc)) return 0;
     return zscan_addr(p, xn, yn) <= zscan_addr(p, xc, yc);
+}
+
+/* 6.5.1 (6-3..6-10): colBd / rowBd, CtbAddrRsToTs, CtbAddrTsToRs, TileId */
+static int tile_scan_init(pic_t *p) {
+    const hevc_pps *pp = p->pps;
+    int nc = pp->tiles ? pp->tile_cols : 1, nr = pp->tiles ? pp->tile_rows : 1;
+    int colW[HEVC_MAX_TILE_DIM], rowH[HEVC_MAX_TILE_DIM];
+    for (int pass = 0; pass < 2; pass++) {
+        int n = pass ? nr : nc, tot = pass ? p->hctb : p->wctb, *sz = pass ? rowH : colW;
+        const int *ex = pass ? pp->tile_row_h : pp->tile_col_w;
+        int used = 0;
+        for (int i = 0; i < n; i++) {
+            if (!pp->tiles || pp->tile_uniform) sz[i] = ((i + 1) * tot) / n - (i * tot) / n;
+            else sz[i] = i + 1 < n ? ex[i] : tot - used;
+            if (sz[i] <= 0) return oracle_fail("tile sizes exceed the picture");
+            used += sz[i];
+        }
+        int *bd = pass ? p->rowBd : p->colBd;
+        bd[0] = 0;
+        for (int i = 0; i < n; i++) bd[i + 1] = bd[i] + sz[i];
+    }
+    int nctb = p->wctb * p->hctb;
+    p->rs2ts = (int *)malloc(sizeof(int) * (size_t)nctb);
+    p->ts2rs = (int *)malloc(sizeof(int) * (size_t)nctb);
+    p->tile_rs = (int *)malloc(sizeof(int) * (size_t)nctb);
+    for (int rs = 0; rs < nctb; rs++) {
+        int tbX = rs % p->wctb, tbY = rs / p->wctb, tx = 0, ty = 0;
+        for (int i = 0; i < nc; i++)
+            if (tbX >= p->colBd[i]) tx = i;
+        for (int j = 0; j < nr; j++)
+            if (tbY >= p->rowBd[j]) ty = j;
+        int v = 0;
+        for (int i = 0; i < tx; i++) v += rowH[ty] * colW[i];
+        for (int j = 0; j < ty; j++) v += p->wctb * rowH[j];
+        v += (tbY - p->rowBd[ty]) * colW[tx] + tbX - p->colBd[tx];
+        p->rs2ts[rs] = v;
+        p->ts2rs[v] = rs;
+        p->tile_rs[rs] = ty * nc + tx;
+    }
+    return 0;
 }
 
 static void build_scaling(pic_t *p) {
@@ -1033,7 +1095,7 @@ static void update_qpy(pic_t *p) {
 static void derive_qp_pred(pic_t *p) {
     int prev;
     int first_in_ctb = (p->qg_x == p->ctb_x && p->qg_y == p->ctb_y);
-    if (p->first_qg_in_slice) {
+    if (p->first_qg_in_slice) { /* first QG in the slice or in a tile */
         prev = p->slice_qp;
         p->first_qg_in_slice = 0;
     } else if (p->pps->wpp && first_in_ctb && p->ctb_x == 0) {
@@ -1419,9 +1481,10 @@ static void parse_sao(pic_t *p, int rx, int ry) {
     cabac_t *c = &p->c;
     sao_ctb *s = &p->sao[ry * p->wctb + rx];
     memset(s, 0, sizeof(*s));
-    int ml = 0, mu = 0;
-    if (rx > 0) ml = dec_bin(c, CTX_SAO_MERGE);
-    if (ry > 0 && !ml) mu = dec_bin(c, CTX_SAO_MERGE);
+    int ml = 0, mu = 0, t = p->tile_rs[ry * p->wctb + rx];
+    /* merge candidates: left / above CTB in the same slice (always) and tile */
+    if (rx > 0 && p->tile_rs[ry * p->wctb + rx - 1] == t) ml = dec_bin(c, CTX_SAO_MERGE);
+    if (ry > 0 && !ml && p->tile_rs[(ry - 1) * p->wctb + rx] == t) mu = dec_bin(c, CTX_SAO_MERGE);
     if (ml) { *s = p->sao[ry * p->wctb + rx - 1]; return; }
     if (mu) { *s = p->sao[(ry - 1) * p->wctb + rx]; return; }
     int ncomp = p->chroma ? 3 : 1;
@@ -1561,6 +1624,13 @@ static void dbk_chroma_seg(pic_t *p, int cIdx, int xc, int yc, int vertical, int
     }
 }
 
+/* 8.7.2: filterEdgeFlag = 0 on a tile boundary when
+ * loop_filter_across_tiles_enabled_flag is 0 */
+static int tile_edge_off(const pic_t *p, int x, int y, int vertical) {
+    if (p->pps->lf_across_tiles) return 0;
+    return vertical ? tile_at(p, x - 1, y) != tile_at(p, x, y) : tile_at(p, x, y - 1) != tile_at(p, x, y);
+}
+
 static void deblock_picture(pic_t *p) {
     if (p->dbk_disabled) return;
     for (int dir = 0; dir < 2; dir++) {
@@ -1573,6 +1643,7 @@ static void deblock_picture(pic_t *p) {
                 if (!vertical && (x & 3)) continue;
                 int f = p->flg[(y >> 2) * p->w4 + (x >> 2)];
                 if (!(f & (vertical ? F_EDGE_V : F_EDGE_H))) continue;
+                if (tile_edge_off(p, x, y, vertical)) continue;
                 dbk_luma_seg(p, x, y, vertical);
             }
         if (p->chroma == 0) continue;
@@ -1586,6 +1657,7 @@ static void deblock_picture(pic_t *p) {
                     int xl = xc * p->sw, yl = yc * p->sh;
                     int f = p->flg[(yl >> 2) * p->w4 + (xl >> 2)];
                     if (!(f & (vertical ? F_EDGE_V : F_EDGE_H))) continue;
+                    if (tile_edge_off(p, xl, yl, vertical)) continue;
                     dbk_chroma_seg(p, ci, xc, yc, vertical, lines);
                 }
     }
@@ -1627,6 +1699,12 @@ static void sao_picture(pic_t *p, uint16_t *out[3], const int ops[3]) {
                             int bx = x + hpos[cl][1], by = y + vpos[cl][1];
                             if (ax < 0 || ay < 0 || ax >= PW || ay >= PH || bx < 0 || by < 0 || bx >= PW || by >= PH)
                                 continue;
+                            /* 8.7.3.2: a neighbour in another tile with
+                             * loop_filter_across_tiles_enabled_flag 0 ⇒ SaoOffsetVal 0 */
+                            if (!p->pps->lf_across_tiles) {
+                                int tc = tile_at(p, xl, yl);
+                                if (tile_at(p, ax * sw, ay * sh) != tc || tile_at(p, bx * sw, by * sh) != tc) continue;
+                            }
                             int a = in[ay * ps + ax], b = in[by * ps + bx];
                             int e = 2 + (v > a) - (v < a) + (v > b) - (v < b);
                             if (e == 0 || e == 1 || e == 2) e = (e == 2) ? 0 : e + 1;
@@ -1742,7 +1820,7 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
     if (nal_len < 3) return oracle_fail("short NAL");
     int nal_type = (nal[0] >> 1) & 63;
     if (s->range_ext_any || pp->range_ext_any) return oracle_fail("range extension tools not supported");
-    if (pp->tiles) return oracle_fail("HEVC tiles not supported");
+    if (pp->tiles && pp->wpp) return oracle_fail("HEVC tiles together with WPP not supported");
     if (s->chroma_format_idc == 2 || s->chroma_format_idc == 3) return oracle_fail("only 4:0:0 / 4:2:0");
     uint8_t *rbsp = (uint8_t *)malloc(nal_len);
     uint32_t *ep = (uint32_t *)malloc(sizeof(uint32_t) * (nal_len / 3 + 4));
@@ -1793,6 +1871,7 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
     p->qpy = (int8_t *)calloc((size_t)p->w4 * p->h4, 1);
     p->sao = (sao_ctb *)calloc((size_t)p->wctb * p->hctb, sizeof(sao_ctb));
     build_scaling(p);
+    if (tile_scan_init(p)) goto out;
     /* raw offset (within NAL payload after header) of slice data start */
     {
         size_t rb = h->data_bit >> 3;
@@ -1821,8 +1900,8 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
         p->first_qg_in_slice = 1;
         size_t sub_start_rbsp = h->data_bit >> 3;
         uint32_t sub_bins0 = 0;
-        for (;;) {
-            int rx = ctbAddr % p->wctb, ry = ctbAddr / p->wctb;
+        for (;;) { /* ctbAddr is CtbAddrInTs: tile scan (7.3.8.1) */
+            int rs = p->ts2rs[ctbAddr], rx = rs % p->wctb, ry = rs / p->wctb;
             p->ctb_x = rx << p->log2ctb;
             p->ctb_y = ry << p->log2ctb;
             if (p->sao_luma || p->sao_chroma) parse_sao(p, rx, ry);
@@ -1834,8 +1913,10 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
             }
             int end = dec_term(&p->c);
             ctbAddr++;
+            int cut_end = !end && ctbAddr == nctb && (g_debug_flags & 4);
             int row_end = pp->wpp && (ctbAddr % p->wctb) == 0;
-            if (end || row_end) {
+            int tile_end = pp->tiles && ctbAddr < nctb && p->tile_rs[p->ts2rs[ctbAddr]] != p->tile_rs[rs];
+            if (end || row_end || tile_end || cut_end) {
                 int ok = 1;
                 if (!end) ok = dec_term(&p->c); /* end_of_subset_one_bit */
                 /* the last consumed bit must be 1 and the rest of the byte 0 */
@@ -1867,14 +1948,23 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
                     if (ctbAddr != nctb) { oracle_fail("end_of_slice_segment before last CTU"); goto out; }
                     break;
                 }
+                if (cut_end) {
+                    if (!ok) { oracle_fail("end_of_subset_one_bit mismatch"); goto out; }
+                    break;
+                }
                 if (!ok) { oracle_fail("end_of_subset_one_bit mismatch"); goto out; }
                 /* byte_alignment + engine re-init at next substream */
                 p->c.b.bit = pos;
                 substream++;
                 sub_start_rbsp = pos >> 3;
                 sub_bins0 = p->c.bins;
-                /* sync: T = above-right CTB available ⇒ restore; else init */
-                if (p->wctb > 1 && p->wpp_saved) {
+                /* 9.3.1: a new tile starts with initialised contexts (and
+                 * qPY_PREV = SliceQpY, 8.6.1); WPP sync: T = above-right CTB
+                 * available ⇒ restore; else init */
+                if (tile_end) {
+                    cabac_init_ctx(&p->c, p->slice_qp);
+                    p->first_qg_in_slice = 1;
+                } else if (p->wctb > 1 && p->wpp_saved) {
                     memcpy(p->c.st, p->wpp_st, CTX_NUM);
                     memcpy(p->c.mps, p->wpp_mps, CTX_NUM);
                 } else {
@@ -1916,6 +2006,9 @@ out:
     free(p->flg);
     free(p->qpy);
     free(p->sao);
+    free(p->rs2ts);
+    free(p->ts2rs);
+    free(p->tile_rs);
     for (int a = 0; a < 4; a++)
         for (int m = 0; m < 6; m++) free(p->sf[a][m]);
     free(p);

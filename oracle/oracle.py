@@ -51,6 +51,7 @@ def _load():
     lib.oracle_read_meta.argtypes = [u8p, SZ, P(_Meta)]
     lib.oracle_decode_heic.argtypes = [u8p, SZ, P(_Image), P(_Check), I, P(I)]
     lib.oracle_image_free.argtypes = [P(_Image)]
+    lib.oracle_set_debug_flags.argtypes = [I]
     lib.oracle_last_error.restype = ctypes.c_char_p
     lib.oracle_remove_emulation_prevention.argtypes = [u8p, SZ, u8p]
     lib.oracle_remove_emulation_prevention.restype = SZ
@@ -101,13 +102,19 @@ class OracleImage:
     checks: list
 
 
-def decode_heic(data: bytes, with_checks: bool = True) -> OracleImage:
+def decode_heic(data: bytes, with_checks: bool = True, debug_flags: int = 0) -> OracleImage:
+    """debug_flags: oracle_set_debug_flags bits for this call (4: the picture
+    may end like a non-last tile, see tests/hevc_tiles.py)."""
     img = _Image()
     maxc = 1 << 16
     checks = (_Check * maxc)() if with_checks else None
     nchk = ctypes.c_int(0)
-    rc = lib.oracle_decode_heic(_buf(data), len(data), ctypes.byref(img), checks, maxc if with_checks else 0,
-                                ctypes.byref(nchk))
+    lib.oracle_set_debug_flags(debug_flags)
+    try:
+        rc = lib.oracle_decode_heic(_buf(data), len(data), ctypes.byref(img), checks, maxc if with_checks else 0,
+                                    ctypes.byref(nchk))
+    finally:
+        lib.oracle_set_debug_flags(0)
     if rc:
         raise OracleError(last_error())
     try:

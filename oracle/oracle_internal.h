@@ -53,6 +53,7 @@ uint8_t *heif_item_data(heif_file *f, heif_item *it, size_t *len);
 int heif_grid_tiles(heif_file *f, uint32_t grid_id, uint32_t *tiles, int max);
 
 /* ---- HEVC parameter sets (H.265 7.3.2.2 / 7.3.2.3) ---- */
+#define HEVC_MAX_TILE_DIM 64
 typedef struct {
     int chroma_format_idc, separate_colour_plane;
     int width, height;                 /* pic_width/height_in_luma_samples */
@@ -81,6 +82,10 @@ typedef struct {
     int cu_qp_delta, diff_cu_qp_delta_depth;
     int cb_qp_offset, cr_qp_offset, slice_chroma_qp_offsets_present;
     int transquant_bypass, tiles, wpp;
+    /* 7.4.3.3 tile layout: columns / rows (1 when tiles is 0), explicit sizes in
+     * CTBs when not uniform_spacing (the last one is implied) */
+    int tile_cols, tile_rows, tile_uniform, lf_across_tiles;
+    int tile_col_w[HEVC_MAX_TILE_DIM], tile_row_h[HEVC_MAX_TILE_DIM];
     int loop_filter_across_slices;
     int deblock_override_enabled, deblock_disabled, beta_offset_div2, tc_offset_div2;
     int scaling_list_present;

@@ -159,8 +159,19 @@ def pps(**over) -> bytes:
     w.u(0, 1)
     w.u(0, 1)
     w.u(0, 1)  # transquant bypass
-    w.u(0, 1)  # tiles
+    t = p.get("tiles")  # dict(cols, rows, uniform=1, col_w=(), row_h=(), across=0) or None
+    w.u(1 if t else 0, 1)  # tiles_enabled_flag
     w.u(p["wpp"], 1)
+    if t:
+        w.ue(t["cols"] - 1)
+        w.ue(t["rows"] - 1)
+        w.u(t.get("uniform", 1), 1)
+        if not t.get("uniform", 1):
+            for v in t["col_w"]:
+                w.ue(v - 1)
+            for v in t["row_h"]:
+                w.ue(v - 1)
+        w.u(t.get("across", 0), 1)
     w.u(0, 1)
     w.u(1, 1)  # deblocking control present
     w.u(0, 1)
