@@ -40,8 +40,8 @@ CASES = [
                                  tq_bypass=1, transform_skip=1, scaling_list=1, diff_cu_qp_delta_depth=2,
                                  max_th_depth_intra=3)),
     ("mono_1ctb_tiles", dict(chroma_format=0, tile_cols=4, tile_rows=3)),
-    ("dense_lowqp", dict(width=256, height=128, tile_cols=4, tile_rows=2, init_qp=22, slice_qp_delta=-30,
-                         density=80, beta_offset_div2=3, tc_offset_div2=-2)),
+    ("dense_lowqp_10b", dict(width=256, height=128, bit_depth=10, tile_cols=4, tile_rows=2, init_qp=22,
+                             slice_qp_delta=-30, density=80, beta_offset_div2=3, tc_offset_div2=-2)),
 ]
 
 
