@@ -926,9 +926,9 @@ int heifgpu_image_tile_params(const heifgpu_image *img, uint32_t tile, heifgpu_t
     const TileJob &t = pi.tiles[tile];
     const SequenceParameterSet &sps = pi.params[t.param].sps;
     const PictureParameterSet &pps = pi.params[t.param].pps;
-    const SliceSegmentHeader &sh = t.sh;
+    const SliceSegmentHeader &sh = t.segs[0].sh;  // the picture's first slice segment
     std::memset(o, 0, sizeof(*o));
-    o->nal_unit_type = t.nal.nal_unit_type();
+    o->nal_unit_type = t.segs[0].nal.nal_unit_type();
     o->slice_type = sh.slice_type;
     o->first_slice_segment_in_pic = sh.first_slice_segment_in_pic_flag;
     o->general_profile_idc = sps.general_profile_idc;
@@ -982,7 +982,7 @@ int heifgpu_image_tile_params(const heifgpu_image *img, uint32_t tile, heifgpu_t
     o->slice_qp_y = 26 + pps.init_qp_minus26 + sh.slice_qp_delta;
     o->num_entry_point_offsets = sh.num_entry_point_offsets;
     o->slice_data_raw_offset = int32_t(sh.slice_data_raw_offset);
-    o->payload_bytes = int32_t(t.payload_len);
+    o->payload_bytes = int32_t(t.segs[0].payload_len);
     for (size_t i = 0; i < sh.entry_point_offset.size() && i < 64; ++i) o->entry_point_offset[i] = sh.entry_point_offset[i];
     return HEIFGPU_OK;
 }

@@ -91,26 +91,49 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
         for (size_t t = tile_offset; t < im.tiles.size(); t += tile_stride) {
             const TileJob &tj = im.tiles[t];
             const ParamSet &ps = im.params[size_t(tj.param)];
-            // HEVC tiles (6.5.1) with no loop filter across their boundaries
-            // (heic_image.cpp) are independent pictures: each becomes a picture of
-            // the tile's size whose one substream is the tile's entry-point range,
-            // placed at the tile's offset in the cropped output.  Without tiles the
-            // loop runs once over the whole picture and all its substreams.
-            const bool tiled = ps.pps.tiles_enabled_flag;
+            // A coded picture decodes as one or more independent sub-pictures
+            // (heic_image.cpp accepts only layouts where nothing crosses their
+            // boundaries): an HEVC tile (6.5.1) with no loop filter across tiles
+            // becomes a picture of the tile's size whose one substream is the
+            // tile's entry-point range; a slice starting at a CTB row with no
+            // loop filter across slices becomes the band of rows it covers, with
+            // its own slice header values and substreams.  Each is placed at its
+            // offset in the cropped output.  Otherwise: one sub-picture, the
+            // whole picture with all its substreams.
+            struct Sub {
+                int x0, y0, x1, y1;  // CTBs
+                size_t seg;          // slice segment
+                int s0, s1;          // its substreams [s0, s1)
+                bool subset_end;     // ends in end_of_subset_one_bit (a tile other than the last)
+            };
+            std::vector<Sub> subs_of;
             const int pctb = 1 << ps.sps.log2_ctb_size;
-            const int ntc = int(ps.col_bd.size()) - 1, ntr = int(ps.row_bd.size()) - 1;
-            std::vector<uint32_t> starts{tj.sh.slice_data_raw_offset};
-            for (uint32_t e : tj.sh.entry_point_offset) starts.push_back(starts.back() + e);
-            starts.push_back(uint32_t(tj.payload_len));
-            for (int ht = 0; ht < (tiled ? ntc * ntr : 1); ++ht) {
+            const int pw = ps.sps.pic_width_in_ctbs_y(), ph = ps.sps.pic_height_in_ctbs_y();
+            if (ps.pps.tiles_enabled_flag) {
+                const int ntc = int(ps.col_bd.size()) - 1, ntr = int(ps.row_bd.size()) - 1;
+                for (int ht = 0; ht < ntc * ntr; ++ht) {
+                    const int tc = ht % ntc, tr = ht / ntc;
+                    subs_of.push_back({ps.col_bd[size_t(tc)], ps.row_bd[size_t(tr)], ps.col_bd[size_t(tc) + 1],
+                                       ps.row_bd[size_t(tr) + 1], 0, ht, ht + 1, ht + 1 < ntc * ntr});
+                }
+            } else {
+                for (size_t k = 0; k < tj.segs.size(); ++k) {
+                    const int r0 = int(tj.segs[k].sh.slice_segment_address) / pw;
+                    const int r1 = k + 1 < tj.segs.size() ? int(tj.segs[k + 1].sh.slice_segment_address) / pw : ph;
+                    subs_of.push_back({0, r0, pw, r1, k, 0, tj.segs[k].sh.num_entry_point_offsets + 1, false});
+                }
+            }
+            for (const Sub &su : subs_of) {
+                const SliceSeg &sg = tj.segs[su.seg];
+                std::vector<uint32_t> starts{sg.sh.slice_data_raw_offset};  // the segment's substreams
+                for (uint32_t e : sg.sh.entry_point_offset) starts.push_back(starts.back() + e);
+                starts.push_back(uint32_t(sg.payload_len));
                 SeqParams base = make_seq(ps, 0);
                 int vis_dx = 0, vis_dy = 0;  // output offset of the sub-picture's visible part
-                if (tiled) {
-                    const int tc = ht % ntc, tr = ht / ntc;
-                    const int x0 = ps.col_bd[size_t(tc)] * pctb, y0 = ps.row_bd[size_t(tr)] * pctb;
-                    const int x1 = std::min(ps.col_bd[size_t(tc) + 1] * pctb, base.width);
-                    const int y1 = std::min(ps.row_bd[size_t(tr) + 1] * pctb, base.height);
-                    // the picture's conformance window [conf_l, conf_l + out_w) clipped to the tile
+                if (subs_of.size() > 1) {
+                    const int x0 = su.x0 * pctb, y0 = su.y0 * pctb;
+                    const int x1 = std::min(su.x1 * pctb, base.width), y1 = std::min(su.y1 * pctb, base.height);
+                    // the picture's conformance window [conf_l, conf_l + out_w) clipped to the sub-picture
                     const int vx0 = std::max(x0, base.conf_l), vx1 = std::min(x1, base.conf_l + base.out_w);
                     const int vy0 = std::max(y0, base.conf_t), vy1 = std::min(y1, base.conf_t + base.out_h);
                     base.width = x1 - x0;
@@ -121,7 +144,7 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                     base.out_h = std::max(vy1 - vy0, 0);
                     vis_dx = vx0 - ps.sps.conf_win_left;
                     vis_dy = vy0 - ps.sps.conf_win_top;
-                    if (ht + 1 < ntc * ntr) base.flags |= SP_SUBSET_END;
+                    if (su.subset_end) base.flags |= SP_SUBSET_END;
                 }
                 std::vector<uint8_t> key = ps.key;
                 {
@@ -156,16 +179,17 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                 PicDesc pd{};
                 pd.bits_off = hb.bits_size;
                 pd.sub_first = uint32_t(hb.subs.size());
-                if (tiled) {  // the tile's substream alone (it starts after a nonzero byte: no EP state carries in)
-                    const uint32_t r0 = starts[size_t(ht)], r1 = starts[size_t(ht) + 1];
+                if (su.s0 > 0 || su.s1 + 1 < int(starts.size())) {
+                    // a substream range alone (it starts after a nonzero byte: no EP state carries in)
+                    const uint32_t r0 = starts[size_t(su.s0)], r1 = starts[size_t(su.s1)];
                     pd.bits_len = r1 - r0;
-                    pd.n_sub = 1;
-                    hb.pieces.push_back({tj.payload + r0, pd.bits_len, hb.bits_size});
-                    hb.subs.push_back(0);
-                } else {
-                    pd.bits_len = uint32_t(tj.payload_len);
-                    pd.n_sub = uint32_t(tj.sh.num_entry_point_offsets + 1);
-                    hb.pieces.push_back({tj.payload, tj.payload_len, hb.bits_size});
+                    pd.n_sub = uint32_t(su.s1 - su.s0);
+                    hb.pieces.push_back({sg.payload + r0, pd.bits_len, hb.bits_size});
+                    for (int k = su.s0; k < su.s1; ++k) hb.subs.push_back(starts[size_t(k)] - r0);
+                } else {  // the whole NAL payload (subs from the slice data start)
+                    pd.bits_len = uint32_t(sg.payload_len);
+                    pd.n_sub = uint32_t(sg.sh.num_entry_point_offsets + 1);
+                    hb.pieces.push_back({sg.payload, sg.payload_len, hb.bits_size});
                     for (size_t k = 0; k + 1 < starts.size(); ++k) hb.subs.push_back(starts[k]);
                 }
                 hb.subs.push_back(pd.bits_len);
@@ -173,14 +197,14 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                 if ((sq.flags & SP_WPP) && int(pd.n_sub) != hctb)
                     throw HeifError("WPP picture without one entry point per CTB row");
                 pd.seq = seq;
-                pd.slice_qp = 26 + ps.pps.init_qp_minus26 + tj.sh.slice_qp_delta;
-                pd.cb_qp_off = tj.sh.slice_cb_qp_offset;
-                pd.cr_qp_off = tj.sh.slice_cr_qp_offset;
-                pd.sao_luma = tj.sh.slice_sao_luma_flag;
-                pd.sao_chroma = tj.sh.slice_sao_chroma_flag;
-                pd.dbk_disabled = tj.sh.slice_deblocking_filter_disabled_flag;
-                pd.beta_off = tj.sh.slice_beta_offset_div2;
-                pd.tc_off = tj.sh.slice_tc_offset_div2;
+                pd.slice_qp = 26 + ps.pps.init_qp_minus26 + sg.sh.slice_qp_delta;
+                pd.cb_qp_off = sg.sh.slice_cb_qp_offset;
+                pd.cr_qp_off = sg.sh.slice_cr_qp_offset;
+                pd.sao_luma = sg.sh.slice_sao_luma_flag;
+                pd.sao_chroma = sg.sh.slice_sao_chroma_flag;
+                pd.dbk_disabled = sg.sh.slice_deblocking_filter_disabled_flag;
+                pd.beta_off = sg.sh.slice_beta_offset_div2;
+                pd.tc_off = sg.sh.slice_tc_offset_div2;
                 pd.image = uint32_t(i);
                 pd.out_x = int32_t((t % im.cols) * im.tile_width) + vis_dx;
                 pd.out_y = int32_t((t / im.cols) * im.tile_height) + vis_dy;

@@ -31,6 +31,41 @@ void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p
         throw HeifError("picture size not a multiple of MinCbSizeY");
 }
 
+// The slice segments of a picture: in order and covering it (7.4.7.1), and
+// each with one entry point per tile / WPP row.  The GPU path decodes several
+// slices as one sub-picture per slice (batch.cpp), so they must be
+// independent, start at a CTB row and keep the loop filters inside
+// (slice_loop_filter_across_slices_enabled_flag 0); HEVC tiles must come with
+// a single slice.
+void check_segments(const TileJob &job, const ParamSet &ps) {
+    const SequenceParameterSet &sps = ps.sps;
+    const PictureParameterSet &pps = ps.pps;
+    const uint32_t pw = uint32_t(sps.pic_width_in_ctbs_y());
+    for (size_t k = 0; k < job.segs.size(); ++k) {
+        const SliceSegmentHeader &sh = job.segs[k].sh;
+        if (sh.first_slice_segment_in_pic_flag != (k == 0)) throw HeifError("first_slice_segment_in_pic_flag out of order");
+        if (k > 0 && sh.slice_segment_address <= job.segs[k - 1].sh.slice_segment_address)
+            throw HeifError("slice segments out of order");
+        if (k == 0) continue;
+        if (sh.dependent_slice_segment_flag) throw UnsupportedError("dependent slice segments");
+        if (pps.tiles_enabled_flag) throw UnsupportedError("several slices together with HEVC tiles");
+        if (sh.slice_segment_address % pw) throw UnsupportedError("a slice starting inside a CTB row");
+        if (sh.slice_loop_filter_across_slices_enabled_flag)
+            throw UnsupportedError("slices with slice_loop_filter_across_slices_enabled_flag");
+    }
+    const size_t ntiles = (ps.col_bd.size() - 1) * (ps.row_bd.size() - 1);
+    if (pps.tiles_enabled_flag && size_t(job.segs[0].sh.num_entry_point_offsets) + 1 != ntiles)
+        throw HeifError("tiled picture without one entry point per tile");
+    if (pps.entropy_coding_sync_enabled_flag)
+        for (size_t k = 0; k < job.segs.size(); ++k) {
+            const uint32_t r0 = job.segs[k].sh.slice_segment_address / pw;
+            const uint32_t r1 = k + 1 < job.segs.size() ? job.segs[k + 1].sh.slice_segment_address / pw
+                                                        : uint32_t(sps.pic_height_in_ctbs_y());
+            if (uint32_t(job.segs[k].sh.num_entry_point_offsets) + 1 != r1 - r0)
+                throw HeifError("WPP slice without one entry point per CTB row");
+        }
+}
+
 }  // namespace
 
 ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id) {
@@ -131,13 +166,12 @@ ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id) {
         }
         const ParamSet &ps = img.params[size_t(param)];
         // read_item_nal_unit (decoder.rs:146-164), generalised: length-prefixed NAL units,
-        // exactly one VCL NAL (one slice segment per picture), non-VCL units skipped
+        // the VCL ones are the picture's slice segments in order, non-VCL units skipped
         const uint8_t *item = img.coded.data() + item_off[ti];
         const size_t item_len = item_off[ti + 1] - item_off[ti];
         img.coded_bytes += uint32_t(item_len);
         int lsz = cfg.length_size_minus_one + 1;
         size_t pos = 0;
-        bool have_vcl = false;
         TileJob job;
         job.param = param;
         while (pos < item_len) {
@@ -148,19 +182,17 @@ ParsedImage parse_heic(const uint8_t *data, size_t len, uint32_t item_id) {
             if (nl < 3 || nl > item_len - pos) throw HeifError("NAL unit length out of range");
             NalUnitHeader h{uint16_t((item[pos] << 8) | item[pos + 1])};
             if (h.nal_unit_type() < 32) {
-                if (have_vcl) throw UnsupportedError("more than one slice segment per picture");
-                have_vcl = true;
-                job.nal = h;
-                job.payload = item + pos + 2;
-                job.payload_len = nl - 2;
+                SliceSeg sg;
+                sg.nal = h;
+                sg.payload = item + pos + 2;
+                sg.payload_len = nl - 2;
+                sg.sh = slice_segment_header(sg.payload, sg.payload_len, sg.nal, ps.sps, ps.pps);
+                job.segs.push_back(sg);
             }
             pos += nl;
         }
-        if (!have_vcl) throw HeifError("tile item holds no VCL NAL unit");
-        job.sh = slice_segment_header(job.payload, job.payload_len, job.nal, ps.sps, ps.pps);
-        const size_t ntiles = (ps.col_bd.size() - 1) * (ps.row_bd.size() - 1);
-        if (ps.pps.tiles_enabled_flag && size_t(job.sh.num_entry_point_offsets) + 1 != ntiles)
-            throw HeifError("tiled picture without one entry point per tile");
+        if (job.segs.empty()) throw HeifError("tile item holds no VCL NAL unit");
+        check_segments(job, ps);
         img.tiles.push_back(std::move(job));
     }
     const SequenceParameterSet &s0 = img.params[0].sps;

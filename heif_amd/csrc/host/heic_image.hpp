@@ -16,12 +16,16 @@ struct ParamSet {
     std::vector<int> col_bd, row_bd;  // HEVC tile boundaries in CTBs (one tile without tiles)
 };
 
-struct TileJob {
+struct SliceSeg {
     // raw NAL payload after the 2-byte header (EP bytes kept): a view into ParsedImage::coded
     const uint8_t *payload = nullptr;
     size_t payload_len = 0;
     NalUnitHeader nal;
     SliceSegmentHeader sh;
+};
+
+struct TileJob {
+    std::vector<SliceSeg> segs;  // the coded picture's slice segments in decoding order (one or more)
     int param = 0;
 };
 

@@ -478,65 +478,73 @@ SliceSegmentHeader slice_segment_header_prefix(const uint8_t *payload, size_t le
     h.first_slice_segment_in_pic_flag = r.read_flag();
     if (t >= 16 && t <= 23) r.read_flag();  // no_output_of_prior_pics_flag
     h.slice_pic_parameter_set_id = r.read_ue_max(63, "slice_pic_parameter_set_id");
-    if (!h.first_slice_segment_in_pic_flag) throw HeifError("multi-slice pictures are not supported");
-    r.read_bits(pps.num_extra_slice_header_bits);
-    h.slice_type = r.read_ue_max(2, "slice_type");
-    if (h.slice_type != 2) throw HeifError("P/B slices are not supported (still images are intra)");
-    if (pps.output_flag_present_flag) r.read_flag();
-    if (sps.separate_colour_plane_flag) r.read_bits(2);
-    if (t != 19 && t != 20) {  // not IDR: POC + RPS (the reference skips these, slice.rs:85)
-        r.read_bits(sps.log2_max_pic_order_cnt_lsb);
-        if (!r.read_flag()) {
-            std::vector<int> nd = sps.st_rps_num_delta_pocs;
-            st_ref_pic_set(r, sps.num_short_term_ref_pic_sets, sps.num_short_term_ref_pic_sets, nd);
-        } else if (sps.num_short_term_ref_pic_sets > 1) {
-            r.read_bits(ceil_log2(sps.num_short_term_ref_pic_sets));
-        }
-        if (sps.long_term_ref_pics_present_flag) {
-            int nsps = sps.num_long_term_ref_pics_sps > 0 ? r.read_ue_max(uint32_t(sps.num_long_term_ref_pics_sps), "num_long_term_sps") : 0;
-            int npics = r.read_ue_max(32, "num_long_term_pics");
-            for (int i = 0; i < nsps + npics; ++i) {
-                if (i < nsps) {
-                    if (sps.num_long_term_ref_pics_sps > 1) r.read_bits(ceil_log2(sps.num_long_term_ref_pics_sps));
-                } else {
-                    r.read_bits(sps.log2_max_pic_order_cnt_lsb);
-                    r.read_flag();
+    if (!h.first_slice_segment_in_pic_flag) {
+        if (pps.dependent_slice_segments_enabled_flag) h.dependent_slice_segment_flag = r.read_flag();
+        const uint32_t nctb = uint32_t(sps.pic_width_in_ctbs_y()) * uint32_t(sps.pic_height_in_ctbs_y());
+        h.slice_segment_address = r.read_bits(ceil_log2(int(nctb)));
+        if (h.slice_segment_address >= nctb) throw HeifError("slice_segment_address out of range");
+    }
+    h.slice_loop_filter_across_slices_enabled_flag = pps.pps_loop_filter_across_slices_enabled_flag;
+    if (!h.dependent_slice_segment_flag) {  // a dependent segment carries only the address and entry points
+        r.read_bits(pps.num_extra_slice_header_bits);
+        h.slice_type = r.read_ue_max(2, "slice_type");
+        if (h.slice_type != 2) throw HeifError("P/B slices are not supported (still images are intra)");
+        if (pps.output_flag_present_flag) r.read_flag();
+        if (sps.separate_colour_plane_flag) r.read_bits(2);
+        if (t != 19 && t != 20) {  // not IDR: POC + RPS (the reference skips these, slice.rs:85)
+            r.read_bits(sps.log2_max_pic_order_cnt_lsb);
+            if (!r.read_flag()) {
+                std::vector<int> nd = sps.st_rps_num_delta_pocs;
+                st_ref_pic_set(r, sps.num_short_term_ref_pic_sets, sps.num_short_term_ref_pic_sets, nd);
+            } else if (sps.num_short_term_ref_pic_sets > 1) {
+                r.read_bits(ceil_log2(sps.num_short_term_ref_pic_sets));
+            }
+            if (sps.long_term_ref_pics_present_flag) {
+                int nsps = sps.num_long_term_ref_pics_sps > 0 ? r.read_ue_max(uint32_t(sps.num_long_term_ref_pics_sps), "num_long_term_sps") : 0;
+                int npics = r.read_ue_max(32, "num_long_term_pics");
+                for (int i = 0; i < nsps + npics; ++i) {
+                    if (i < nsps) {
+                        if (sps.num_long_term_ref_pics_sps > 1) r.read_bits(ceil_log2(sps.num_long_term_ref_pics_sps));
+                    } else {
+                        r.read_bits(sps.log2_max_pic_order_cnt_lsb);
+                        r.read_flag();
+                    }
+                    if (r.read_flag()) r.read_ue();
                 }
-                if (r.read_flag()) r.read_ue();
+            }
+            if (sps.sps_temporal_mvp_enabled_flag) r.read_flag();
+        }
+        if (sps.sample_adaptive_offset_enabled_flag) {
+            h.slice_sao_luma_flag = r.read_flag();
+            if (sps.chroma_array_type() != 0) h.slice_sao_chroma_flag = r.read_flag();
+        }
+        h.slice_qp_delta = r.read_se();
+        {  // 7.4.7.1: SliceQpY in [-QpBdOffsetY, +51]
+            const int qp = 26 + pps.init_qp_minus26 + h.slice_qp_delta;
+            if (qp < -6 * sps.bit_depth_luma_minus8 || qp > 51) throw HeifError("SliceQpY out of range");
+        }
+        if (pps.pps_slice_chroma_qp_offsets_present_flag) {
+            h.slice_cb_qp_offset = r.read_se_range(-12, 12, "slice_cb_qp_offset");
+            h.slice_cr_qp_offset = r.read_se_range(-12, 12, "slice_cr_qp_offset");
+            if (pps.pps_cb_qp_offset + h.slice_cb_qp_offset < -12 || pps.pps_cb_qp_offset + h.slice_cb_qp_offset > 12 ||
+                pps.pps_cr_qp_offset + h.slice_cr_qp_offset < -12 || pps.pps_cr_qp_offset + h.slice_cr_qp_offset > 12)
+                throw HeifError("chroma QP offsets out of range");
+        }
+        bool override_flag = pps.deblocking_filter_override_enabled_flag ? r.read_flag() : false;
+        h.slice_deblocking_filter_disabled_flag = pps.pps_deblocking_filter_disabled_flag;
+        h.slice_beta_offset_div2 = pps.pps_beta_offset_div2;
+        h.slice_tc_offset_div2 = pps.pps_tc_offset_div2;
+        if (override_flag) {
+            h.slice_deblocking_filter_disabled_flag = r.read_flag();
+            if (!h.slice_deblocking_filter_disabled_flag) {
+                h.slice_beta_offset_div2 = r.read_se_range(-6, 6, "slice_beta_offset_div2");
+                h.slice_tc_offset_div2 = r.read_se_range(-6, 6, "slice_tc_offset_div2");
             }
         }
-        if (sps.sps_temporal_mvp_enabled_flag) r.read_flag();
+        if (pps.pps_loop_filter_across_slices_enabled_flag &&
+            (h.slice_sao_luma_flag || h.slice_sao_chroma_flag || !h.slice_deblocking_filter_disabled_flag))
+            h.slice_loop_filter_across_slices_enabled_flag = r.read_flag();
     }
-    if (sps.sample_adaptive_offset_enabled_flag) {
-        h.slice_sao_luma_flag = r.read_flag();
-        if (sps.chroma_array_type() != 0) h.slice_sao_chroma_flag = r.read_flag();
-    }
-    h.slice_qp_delta = r.read_se();
-    {  // 7.4.7.1: SliceQpY in [-QpBdOffsetY, +51]
-        const int qp = 26 + pps.init_qp_minus26 + h.slice_qp_delta;
-        if (qp < -6 * sps.bit_depth_luma_minus8 || qp > 51) throw HeifError("SliceQpY out of range");
-    }
-    if (pps.pps_slice_chroma_qp_offsets_present_flag) {
-        h.slice_cb_qp_offset = r.read_se_range(-12, 12, "slice_cb_qp_offset");
-        h.slice_cr_qp_offset = r.read_se_range(-12, 12, "slice_cr_qp_offset");
-        if (pps.pps_cb_qp_offset + h.slice_cb_qp_offset < -12 || pps.pps_cb_qp_offset + h.slice_cb_qp_offset > 12 ||
-            pps.pps_cr_qp_offset + h.slice_cr_qp_offset < -12 || pps.pps_cr_qp_offset + h.slice_cr_qp_offset > 12)
-            throw HeifError("chroma QP offsets out of range");
-    }
-    bool override_flag = pps.deblocking_filter_override_enabled_flag ? r.read_flag() : false;
-    h.slice_deblocking_filter_disabled_flag = pps.pps_deblocking_filter_disabled_flag;
-    h.slice_beta_offset_div2 = pps.pps_beta_offset_div2;
-    h.slice_tc_offset_div2 = pps.pps_tc_offset_div2;
-    if (override_flag) {
-        h.slice_deblocking_filter_disabled_flag = r.read_flag();
-        if (!h.slice_deblocking_filter_disabled_flag) {
-            h.slice_beta_offset_div2 = r.read_se_range(-6, 6, "slice_beta_offset_div2");
-            h.slice_tc_offset_div2 = r.read_se_range(-6, 6, "slice_tc_offset_div2");
-        }
-    }
-    if (pps.pps_loop_filter_across_slices_enabled_flag &&
-        (h.slice_sao_luma_flag || h.slice_sao_chroma_flag || !h.slice_deblocking_filter_disabled_flag))
-        r.read_flag();
     if (pps.tiles_enabled_flag || pps.entropy_coding_sync_enabled_flag) {
         const int max_entries = sps.pic_height_in_ctbs_y() * (pps.tiles_enabled_flag ? sps.pic_width_in_ctbs_y() : 1);
         h.num_entry_point_offsets = r.read_ue_max(uint32_t(max_entries), "num_entry_point_offsets");

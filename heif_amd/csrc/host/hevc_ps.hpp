@@ -99,6 +99,9 @@ struct PictureParameterSet {
 
 struct SliceSegmentHeader {  // grammar.rs:550-572 + entry points in raw bytes
     bool first_slice_segment_in_pic_flag = true;
+    bool dependent_slice_segment_flag = false;
+    uint32_t slice_segment_address = 0;  // first CTB, raster scan
+    bool slice_loop_filter_across_slices_enabled_flag = false;
     int slice_pic_parameter_set_id = 0;
     int slice_type = 2;
     bool slice_sao_luma_flag = false, slice_sao_chroma_flag = false;
@@ -121,7 +124,10 @@ SequenceParameterSet sequence_parameter_set_rbsp(const std::vector<uint8_t> &rbs
 PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp, const SequenceParameterSet &sps);
 
 // Parses the I-slice header of a VCL NAL payload (raw bytes after the 2-byte
-// NAL header, EP bytes included) — slice.rs:44-204.
+// NAL header, EP bytes included) — slice.rs:44-204, which takes the first
+// segment of a picture only (slice.rs:61-64); a later segment's address and
+// dependent flag are read here too (a dependent segment's other fields are
+// its slice's, left at their defaults).
 SliceSegmentHeader slice_segment_header(const uint8_t *payload, size_t len, NalUnitHeader nal,
                                         const SequenceParameterSet &sps, const PictureParameterSet &pps);
 

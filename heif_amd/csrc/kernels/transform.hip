@@ -21,7 +21,10 @@ namespace hg {
 
 namespace {
 
-constexpr int kWaves = 4;
+#ifndef HG_XF_WAVES
+#define HG_XF_WAVES 4
+#endif
+constexpr int kWaves = HG_XF_WAVES;
 
 // transMatrix of 8.6.4.2 (32x32 DCT; smaller sizes use rows k * 32/n)
 struct TransMatrix {

@@ -287,6 +287,7 @@ typedef struct {
     int W, H, log2ctb, ctb, wctb, hctb, w4, h4, qpbdY;
     uint8_t *ipm, *depth;
     int *ts2rs, *tile_rs; /* 6.5.1 tile scan; tile of each CTB by raster address */
+    int *slice_rs;        /* slice of each CTB by raster address */
     /* current CU */
     int cu_bypass, intra_split, max_trafo_depth, chroma_mode;
     int is_qp_coded;
@@ -299,11 +300,11 @@ static void set_map(pic_t *p, uint8_t *m, int x0, int y0, int n, uint8_t v) {
 
 static int tiles_on(const synth_params *P) { return P->tile_cols * P->tile_rows > 1; }
 
-/* the neighbour (xn,yn) of (x,y) lies in the same tile (availability 6.4.1; in
- * the picture and earlier in decoding order is the caller's check) */
+/* the neighbour (xn,yn) of (x,y) lies in the same tile and slice (availability
+ * 6.4.1; in the picture and earlier in decoding order is the caller's check) */
 static int same_tile(const pic_t *p, int x, int y, int xn, int yn) {
-    return p->tile_rs[(yn >> p->log2ctb) * p->wctb + (xn >> p->log2ctb)] ==
-           p->tile_rs[(y >> p->log2ctb) * p->wctb + (x >> p->log2ctb)];
+    const int a = (yn >> p->log2ctb) * p->wctb + (xn >> p->log2ctb), b = (y >> p->log2ctb) * p->wctb + (x >> p->log2ctb);
+    return p->tile_rs[a] == p->tile_rs[b] && p->slice_rs[a] == p->slice_rs[b];
 }
 
 /* 6.5.1 column / row boundaries (6-3..6-6) → CtbAddrTsToRs, TileId */
@@ -657,13 +658,12 @@ static void coding_quadtree(pic_t *p, int x0, int y0, int log2cb, int depth) {
 static void sao_syntax(pic_t *p, int rx, int ry, int sao_l, int sao_c) {
     const synth_params *P = p->P;
     cabe_t *c = &p->c;
-    const int t = p->tile_rs[ry * p->wctb + rx];
-    if (rx > 0 && p->tile_rs[ry * p->wctb + rx - 1] == t) {
+    if (rx > 0 && same_tile(p, rx << p->log2ctb, ry << p->log2ctb, (rx - 1) << p->log2ctb, ry << p->log2ctb)) {
         int ml = pct(&p->rng, 25);
         ce_bin(c, C_SAO_MERGE, ml);
         if (ml) return;
     }
-    if (ry > 0 && p->tile_rs[(ry - 1) * p->wctb + rx] == t) {
+    if (ry > 0 && same_tile(p, rx << p->log2ctb, ry << p->log2ctb, rx << p->log2ctb, (ry - 1) << p->log2ctb)) {
         int mu = pct(&p->rng, 25);
         ce_bin(c, C_SAO_MERGE, mu);
         if (mu) return;
@@ -836,7 +836,7 @@ long synth_pps(const synth_params *P, uint8_t *out, size_t cap) {
     nal_header(&w, 34);
     bw_ue(&w, 0);
     bw_ue(&w, 0);
-    bw_bits(&w, 0, 1);
+    bw_bits(&w, P->slice_dependent ? 1 : 0, 1); /* dependent_slice_segments_enabled_flag */
     bw_bits(&w, 0, 1);
     bw_bits(&w, 0, 3);
     bw_bits(&w, P->sign_hiding ? 1 : 0, 1);
@@ -866,9 +866,9 @@ long synth_pps(const synth_params *P, uint8_t *out, size_t cap) {
         }
         bw_bits(&w, P->tile_lf_across ? 1 : 0, 1);
     }
-    bw_bits(&w, 0, 1); /* loop filter across slices */
+    bw_bits(&w, P->slice_lf_across ? 1 : 0, 1); /* pps_loop_filter_across_slices_enabled_flag */
     bw_bits(&w, 1, 1); /* deblocking control present */
-    bw_bits(&w, 0, 1);
+    bw_bits(&w, P->slice_dbk_vary ? 1 : 0, 1); /* deblocking_filter_override_enabled_flag */
     bw_bits(&w, P->deblock_disabled ? 1 : 0, 1);
     if (!P->deblock_disabled) {
         bw_se(&w, P->beta_offset_div2);
@@ -899,6 +899,9 @@ int synth_check_params(const synth_params *P) {
     if (P->wpp != 0 && P->wpp != 1) return -1;
     if (P->tile_cols < 0 || P->tile_rows < 0 || P->tile_cols > SYNTH_MAX_TILES || P->tile_rows > SYNTH_MAX_TILES)
         return -1;
+    if (P->slice_ctus < 0 || P->slice_dependent < 0 || P->slice_dependent > 2 || P->slice_lf_across < 0 ||
+        P->slice_lf_across > 2)
+        return -1;
     if (tiles_on(P)) {
         int ctb = 1 << P->log2_ctb, wctb = (P->width + ctb - 1) / ctb, hctb = (P->height + ctb - 1) / ctb;
         if (P->wpp || P->tile_cols < 1 || P->tile_rows < 1 || P->tile_cols > wctb || P->tile_rows > hctb) return -1;
@@ -912,7 +915,20 @@ int synth_check_params(const synth_params *P) {
     return 0;
 }
 
-long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t cap) {
+/* one slice segment of the picture being written */
+typedef struct {
+    int ts0, first_sub, nsub, dependent;
+    int qp_delta, sao_l, sao_c, dbk_override, dbk_disabled, beta, tc, lf_across;
+} seg_t;
+
+static int n_segments(const synth_params *P, int nctb) {
+    return P->slice_ctus > 0 ? (nctb + P->slice_ctus - 1) / P->slice_ctus : 1;
+}
+
+/* Writes the picture's slice segments: item = 0 one NAL unit (a single
+ * segment only), item = 1 every segment as a 4-byte-length-prefixed NAL unit
+ * (the layout of a HEIF item). */
+static long synth_impl(const synth_params *P, uint64_t seed, uint8_t *out, size_t cap, int item) {
     if (synth_check_params(P)) return -2;
     init_scans();
     pic_t pic;
@@ -929,111 +945,207 @@ long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t ca
     p->w4 = (p->W + 3) >> 2;
     p->h4 = (p->H + 3) >> 2;
     p->qpbdY = 6 * (P->bit_depth - 8);
+    const int nctb = p->wctb * p->hctb, nseg = n_segments(P, nctb);
+    if (!item && nseg > 1) return -2;
+    const int seg_ctus = P->slice_ctus > 0 ? P->slice_ctus : nctb;
     p->ipm = (uint8_t *)calloc((size_t)p->w4 * p->h4, 1);
     p->depth = (uint8_t *)calloc((size_t)p->w4 * p->h4, 1);
-    const int nctb = p->wctb * p->hctb;
-    const int nsub = P->wpp ? p->hctb : tiles_on(P) ? P->tile_cols * P->tile_rows : 1;
-    bw_t *subs = (bw_t *)calloc((size_t)nsub, sizeof(bw_t));
-    if (!p->ipm || !p->depth || !subs || tile_layout(p)) {
-        free(p->ipm); free(p->depth); free(subs); free(p->ts2rs); free(p->tile_rs);
+    p->slice_rs = (int *)calloc((size_t)nctb, sizeof(int));
+    bw_t *subs = (bw_t *)calloc((size_t)nctb + 1, sizeof(bw_t)); /* every substream holds a CTU at least */
+    seg_t *segs = (seg_t *)calloc((size_t)nseg, sizeof(seg_t));
+    if (!p->ipm || !p->depth || !p->slice_rs || !subs || !segs || tile_layout(p)) {
+        free(p->ipm); free(p->depth); free(p->slice_rs); free(subs); free(segs); free(p->ts2rs); free(p->tile_rs);
         return -1;
     }
-    int slice_qp_delta = P->slice_qp_delta;
-    int slice_qp = P->init_qp + slice_qp_delta;
+    int slice_qp = P->init_qp + P->slice_qp_delta;
     int sao_l = P->sao ? !pct(&p->rng, 10) : 0;
     int sao_c = (P->sao && P->chroma_format) ? !pct(&p->rng, 10) : 0;
-    uint8_t wst[C_NUM], wmps[C_NUM];
-    int saved = 0;
+    uint8_t wst[C_NUM], wmps[C_NUM], dst_[C_NUM], dmps[C_NUM];
+    int saved = 0, nsub = 0, cur_slice = -1;
+    seg_t *sg = NULL;
     ce_init_ctx(&p->c, slice_qp);
-    /* CTUs in tile scan (7.3.8.1).  WPP: one substream per CTB row (9.3.1:
-     * contexts after CTU 1 of the row above, engine restarted at the entry
-     * point).  Tiles: one substream per tile, contexts initialised at its first
-     * CTU.  Each substream but the last ends in end_of_subset_one_bit and
-     * byte_alignment().  Otherwise the slice is one substream: the engine and
-     * the contexts run on across rows (slice.rs:206-231). */
-    for (int ts = 0, sub = 0; ts < nctb; ts++) {
+    /* CTUs in tile scan (7.3.8.1), cut into slice segments of slice_ctus CTUs.
+     * A substream starts at a segment start, a WPP row start (9.3.1: contexts
+     * after CTU 1 of the row above when the above-right CTB is available, else
+     * initialised) or a tile start (initialised); a dependent segment starts
+     * from the previous segment's final contexts.  Each substream but a
+     * segment's last ends in end_of_subset_one_bit and byte_alignment();
+     * without WPP or tiles a segment is one substream whose engine and
+     * contexts run on across rows (slice.rs:206-231). */
+    for (int ts = 0; ts < nctb; ts++) {
         const int rs = p->ts2rs[ts], rx = rs % p->wctb, ry = rs / p->wctb;
         const int tile_start = ts > 0 && p->tile_rs[rs] != p->tile_rs[p->ts2rs[ts - 1]];
-        if (ts == 0 || (P->wpp && rx == 0) || tile_start) {
-            ce_start(&p->c, &subs[sub]);
-            if (tile_start) ce_init_ctx(&p->c, slice_qp);
-            else if (ts > 0) { /* WPP row start */
-                if (p->wctb > 1 && saved) { memcpy(p->c.st, wst, C_NUM); memcpy(p->c.mps, wmps, C_NUM); }
+        const int seg_start = ts % seg_ctus == 0;
+        if (seg_start) {
+            const int k = ts / seg_ctus;
+            sg = &segs[k];
+            sg->ts0 = ts;
+            sg->first_sub = nsub;
+            sg->dependent = k > 0 && (P->slice_dependent == 1 || (P->slice_dependent == 2 && (k & 1)));
+            if (!sg->dependent) {
+                ++cur_slice;
+                if (k > 0) { /* a new slice: its own QP, SAO flags, deblocking and filter-across flags */
+                    int q = P->init_qp + P->slice_qp_delta + (k * 7) % 5 - 2;
+                    q = q < -p->qpbdY ? -p->qpbdY : q > 51 ? 51 : q;
+                    slice_qp = q;
+                    sao_l = P->sao ? !pct(&p->rng, 20) : 0;
+                    sao_c = (P->sao && P->chroma_format) ? !pct(&p->rng, 20) : 0;
+                }
+                sg->qp_delta = slice_qp - P->init_qp;
+                sg->sao_l = sao_l;
+                sg->sao_c = sao_c;
+                sg->dbk_disabled = P->deblock_disabled;
+                sg->beta = P->beta_offset_div2;
+                sg->tc = P->tc_offset_div2;
+                if (P->slice_dbk_vary && k > 0) {
+                    sg->dbk_override = 1;
+                    sg->dbk_disabled = k % 3 == 2;
+                    sg->beta = k % 3 - 1;
+                    sg->tc = 1 - k % 3;
+                }
+                sg->lf_across = P->slice_lf_across == 1 || (P->slice_lf_across == 2 && !(cur_slice & 1));
+            } else {
+                *sg = segs[k - 1];
+                sg->ts0 = ts;
+                sg->first_sub = nsub;
+                sg->nsub = 0;
+                sg->dependent = 1;
+            }
+        }
+        p->slice_rs[rs] = cur_slice;
+        if (seg_start || (P->wpp && rx == 0) || tile_start) {
+            ce_start(&p->c, &subs[nsub]);
+            sg->nsub++;
+            if (ts == 0 || tile_start) {
+                ce_init_ctx(&p->c, slice_qp);
+            } else if (P->wpp && rx == 0) {
+                const int t_ok = saved && p->wctb > 1 && p->slice_rs[rs - p->wctb + 1] == cur_slice;
+                if (t_ok) { memcpy(p->c.st, wst, C_NUM); memcpy(p->c.mps, wmps, C_NUM); }
                 else ce_init_ctx(&p->c, slice_qp);
+            } else if (sg->dependent && seg_start) {
+                memcpy(p->c.st, dst_, C_NUM);
+                memcpy(p->c.mps, dmps, C_NUM);
+            } else {
+                ce_init_ctx(&p->c, slice_qp);
             }
         }
         if (sao_l || sao_c) sao_syntax(p, rx, ry, sao_l, sao_c);
         coding_quadtree(p, rx << p->log2ctb, ry << p->log2ctb, p->log2ctb, 0);
         if (P->wpp && rx == 1) { memcpy(wst, p->c.st, C_NUM); memcpy(wmps, p->c.mps, C_NUM); saved = 1; }
-        const int last = ts == nctb - 1;
-        ce_term(&p->c, last); /* end_of_slice_segment_flag */
-        if (last || (P->wpp && rx == p->wctb - 1) || p->tile_rs[p->ts2rs[ts + 1]] != p->tile_rs[rs]) {
-            if (!last) ce_term(&p->c, 1); /* end_of_subset_one_bit */
+        const int seg_end = ts == nctb - 1 || (ts + 1) % seg_ctus == 0;
+        ce_term(&p->c, seg_end); /* end_of_slice_segment_flag */
+        if (seg_end || (P->wpp && rx == p->wctb - 1) || p->tile_rs[p->ts2rs[ts + 1]] != p->tile_rs[rs]) {
+            if (!seg_end) ce_term(&p->c, 1); /* end_of_subset_one_bit */
             ce_finish(&p->c);
-            bw_align1(&subs[sub++]); /* byte_alignment() / rbsp_slice_segment_trailing_bits() */
+            bw_align1(&subs[nsub++]); /* byte_alignment() / rbsp_slice_segment_trailing_bits() */
+            if (seg_end) { memcpy(dst_, p->c.st, C_NUM); memcpy(dmps, p->c.mps, C_NUM); } /* 9.3.2.4 */
         }
     }
-    /* substreams with emulation prevention, to size the entry points */
+    /* NAL units: slice header + the segment's substreams with emulation
+     * prevention (the entry points are their sizes) */
     long ret = -1;
-    size_t total = 0;
-    int err = 0;
-    for (int r = 0; r < nsub; r++) { total += subs[r].n; err |= subs[r].err; }
-    uint8_t *data = (uint8_t *)malloc(total * 3 / 2 + 16);
-    size_t *sub_len = (size_t *)calloc((size_t)nsub, sizeof(size_t));
-    if (data && sub_len && !err) {
-        size_t o = 0;
+    size_t o = 0;
+    int err = 0, addr_bits = 0;
+    while ((1 << addr_bits) < nctb) addr_bits++;
+    for (int r = 0; r < nsub; r++) err |= subs[r].err;
+    for (int k = 0; k < nseg && !err; k++) {
+        seg_t *g = &segs[k];
+        size_t total = 0;
+        for (int r = 0; r < g->nsub; r++) total += subs[g->first_sub + r].n;
+        uint8_t *data = (uint8_t *)malloc(total * 3 / 2 + 16);
+        size_t *sub_len = (size_t *)calloc((size_t)g->nsub, sizeof(size_t));
+        if (!data || !sub_len) { free(data); free(sub_len); err = 1; break; }
+        size_t dn = 0;
         int z = 0; /* the slice header ends in a nonzero byte (its alignment bit) */
-        for (int r = 0; r < nsub; r++) {
-            size_t m = ep_insert(subs[r].d, subs[r].n, data + o, total * 3 / 2 + 16 - o, &z);
+        for (int r = 0; r < g->nsub; r++) {
+            const bw_t *b = &subs[g->first_sub + r];
+            size_t m = ep_insert(b->d, b->n, data + dn, total * 3 / 2 + 16 - dn, &z);
             sub_len[r] = m;
-            o += m;
+            dn += m;
         }
         bw_t w = {0};
         nal_header(&w, 19);
-        bw_bits(&w, 1, 1); /* first_slice_segment_in_pic_flag */
-        bw_bits(&w, 0, 1); /* no_output_of_prior_pics_flag */
+        bw_bits(&w, k == 0, 1); /* first_slice_segment_in_pic_flag */
+        bw_bits(&w, 0, 1);      /* no_output_of_prior_pics_flag */
         bw_ue(&w, 0);
-        bw_ue(&w, 2);      /* I slice */
-        if (P->sao) {
-            bw_bits(&w, (uint32_t)sao_l, 1);
-            if (P->chroma_format) bw_bits(&w, (uint32_t)sao_c, 1);
+        if (k > 0) {
+            if (P->slice_dependent) bw_bits(&w, (uint32_t)g->dependent, 1);
+            bw_bits(&w, (uint32_t)p->ts2rs[g->ts0], addr_bits); /* slice_segment_address (raster) */
         }
-        bw_se(&w, slice_qp_delta);
+        if (!g->dependent) {
+            bw_ue(&w, 2); /* I slice */
+            if (P->sao) {
+                bw_bits(&w, (uint32_t)g->sao_l, 1);
+                if (P->chroma_format) bw_bits(&w, (uint32_t)g->sao_c, 1);
+            }
+            bw_se(&w, g->qp_delta); /* slice_qp_delta: SliceQpY - (26 + init_qp_minus26) */
+            if (P->slice_dbk_vary) {
+                bw_bits(&w, (uint32_t)g->dbk_override, 1);
+                if (g->dbk_override) {
+                    bw_bits(&w, (uint32_t)g->dbk_disabled, 1);
+                    if (!g->dbk_disabled) { bw_se(&w, g->beta); bw_se(&w, g->tc); }
+                }
+            }
+            if (P->slice_lf_across && (g->sao_l || g->sao_c || !g->dbk_disabled))
+                bw_bits(&w, (uint32_t)g->lf_across, 1);
+        }
         if (P->wpp || tiles_on(P)) { /* num_entry_point_offsets: present only with tiles or WPP (7.3.6.1) */
-            bw_ue(&w, (uint32_t)(nsub - 1));
-            if (nsub > 1) {
+            bw_ue(&w, (uint32_t)(g->nsub - 1));
+            if (g->nsub > 1) {
                 size_t mx = 1;
-                for (int r = 0; r < nsub - 1; r++) mx = sub_len[r] > mx ? sub_len[r] : mx;
+                for (int r = 0; r < g->nsub - 1; r++) mx = sub_len[r] > mx ? sub_len[r] : mx;
                 int len = 1;
                 while (((size_t)1 << len) < mx) len++;
                 bw_ue(&w, (uint32_t)(len - 1));
-                for (int r = 0; r < nsub - 1; r++) bw_bits(&w, (uint32_t)(sub_len[r] - 1), len);
+                for (int r = 0; r < g->nsub - 1; r++) bw_bits(&w, (uint32_t)(sub_len[r] - 1), len);
             }
         }
         bw_align1(&w);
-        if (!w.err) {
-            uint8_t *hdr = (uint8_t *)malloc(w.n * 3 / 2 + 4);
-            size_t hm = hdr ? ep_insert(w.d + 2, w.n - 2, hdr, w.n * 3 / 2 + 4, NULL) : (size_t)-1;
-            if (hm != (size_t)-1 && 2 + hm + o <= cap) {
-                out[0] = w.d[0];
-                out[1] = w.d[1];
-                memcpy(out + 2, hdr, hm);
-                memcpy(out + 2 + hm, data, o);
-                ret = (long)(2 + hm + o);
-            } else if (hm != (size_t)-1) {
+        if (w.err) err = 1;
+        uint8_t *hdr = err ? NULL : (uint8_t *)malloc(w.n * 3 / 2 + 4);
+        size_t hm = hdr ? ep_insert(w.d + 2, w.n - 2, hdr, w.n * 3 / 2 + 4, NULL) : (size_t)-1;
+        if (hm == (size_t)-1) {
+            err = 1;
+        } else {
+            const size_t nl = 2 + hm + dn, pre = item ? 4 : 0;
+            if (o + pre + nl > cap) {
                 ret = -3; /* capacity */
+                err = 2;
+            } else {
+                if (item) {
+                    out[o] = (uint8_t)(nl >> 24);
+                    out[o + 1] = (uint8_t)(nl >> 16);
+                    out[o + 2] = (uint8_t)(nl >> 8);
+                    out[o + 3] = (uint8_t)nl;
+                }
+                out[o + pre] = w.d[0];
+                out[o + pre + 1] = w.d[1];
+                memcpy(out + o + pre + 2, hdr, hm);
+                memcpy(out + o + pre + 2 + hm, data, dn);
+                o += pre + nl;
             }
-            free(hdr);
         }
+        free(hdr);
         free(w.d);
+        free(data);
+        free(sub_len);
     }
-    free(data);
-    free(sub_len);
+    if (!err) ret = (long)o;
     for (int r = 0; r < nsub; r++) free(subs[r].d);
     free(subs);
+    free(segs);
     free(p->ipm);
     free(p->depth);
+    free(p->slice_rs);
     free(p->ts2rs);
     free(p->tile_rs);
     return ret;
+}
+
+long synth_picture(const synth_params *P, uint64_t seed, uint8_t *out, size_t cap) {
+    return synth_impl(P, seed, out, cap, 0);
+}
+
+long synth_picture_item(const synth_params *P, uint64_t seed, uint8_t *out, size_t cap) {
+    return synth_impl(P, seed, out, cap, 1);
 }

@@ -28,6 +28,14 @@ typedef struct {
      * but the last column / row; loop_filter_across_tiles_enabled_flag */
     int32_t tile_cols, tile_rows, tile_uniform, tile_lf_across;
     int32_t tile_col_w[SYNTH_MAX_TILES], tile_row_h[SYNTH_MAX_TILES];
+    /* slice segments of slice_ctus CTUs (tile scan; 0 = one segment).  A new
+     * slice k > 0 takes SliceQpY + (7k mod 5) - 2 and its own SAO flags;
+     * slice_dependent 1: every segment after the first is a dependent one,
+     * 2: odd-numbered segments are; slice_lf_across 0: no loop filtering across
+     * slices (pps flag 0), 1: across every slice boundary, 2: the even-numbered
+     * slices' flag is 1; slice_dbk_vary: slices k > 0 override the deblocking
+     * (disabled when k mod 3 = 2, beta k mod 3 - 1, tc 1 - k mod 3) */
+    int32_t slice_ctus, slice_dependent, slice_lf_across, slice_dbk_vary;
 } synth_params;
 
 /* Each returns the NAL unit length (2-byte header included, emulation
@@ -38,6 +46,9 @@ long synth_sps(const synth_params *p, uint8_t *out, size_t cap);
 long synth_pps(const synth_params *p, uint8_t *out, size_t cap);
 /* One IDR picture (a single I slice; WPP or tile substreams + entry points). */
 long synth_picture(const synth_params *p, uint64_t seed, uint8_t *out, size_t cap);
+/* The picture's slice segments as 4-byte-length-prefixed NAL units (a HEIF
+ * item's layout); synth_picture takes single-segment pictures only. */
+long synth_picture_item(const synth_params *p, uint64_t seed, uint8_t *out, size_t cap);
 int synth_check_params(const synth_params *p);
 
 #ifdef __cplusplus

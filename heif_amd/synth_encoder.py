@@ -32,7 +32,8 @@ class _Params(ctypes.Structure):
         "init_qp", "slice_qp_delta", "cb_qp_offset", "cr_qp_offset",
         "sao", "deblock_disabled", "beta_offset_div2", "tc_offset_div2", "density", "wpp",
         "tile_cols", "tile_rows", "tile_uniform", "tile_lf_across")] + [
-        ("tile_col_w", ctypes.c_int32 * 8), ("tile_row_h", ctypes.c_int32 * 8)]
+        ("tile_col_w", ctypes.c_int32 * 8), ("tile_row_h", ctypes.c_int32 * 8)] + [
+        (n, ctypes.c_int32) for n in ("slice_ctus", "slice_dependent", "slice_lf_across", "slice_dbk_vary")]
 
 
 @dataclasses.dataclass
@@ -76,8 +77,19 @@ class SynthParams:
     tile_col_w: Tuple[int, ...] = ()  # explicit widths / heights in CTBs (all but the last), tile_uniform=0
     tile_row_h: Tuple[int, ...] = ()
 
+    # slice segments (see hevc_synth.h): CTUs per segment (0 = one), dependent
+    # segments (1 all after the first, 2 odd-numbered), loop filter across
+    # slices (0 none, 1 all, 2 even-numbered slices), per-slice deblocking override
+    slice_ctus: int = 0
+    slice_dependent: int = 0
+    slice_lf_across: int = 0
+    slice_dbk_vary: int = 0
+
     def _c(self) -> _Params:
-        c = _Params(*[getattr(self, n) for n, t in _Params._fields_ if t is ctypes.c_int32])
+        c = _Params()
+        for n, t in _Params._fields_:
+            if t is ctypes.c_int32:
+                setattr(c, n, getattr(self, n))
         for name in ("tile_col_w", "tile_row_h"):
             v = list(getattr(self, name))
             if len(v) > 8:
@@ -95,8 +107,9 @@ def _load():
         for f in ("synth_vps", "synth_sps", "synth_pps"):
             getattr(lib, f).restype = ctypes.c_long
             getattr(lib, f).argtypes = [ctypes.POINTER(_Params), ctypes.c_void_p, ctypes.c_size_t]
-        lib.synth_picture.restype = ctypes.c_long
-        lib.synth_picture.argtypes = [ctypes.POINTER(_Params), ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t]
+        for f in ("synth_picture", "synth_picture_item"):
+            getattr(lib, f).restype = ctypes.c_long
+            getattr(lib, f).argtypes = [ctypes.POINTER(_Params), ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t]
         lib.synth_check_params.restype = ctypes.c_int
         lib.synth_check_params.argtypes = [ctypes.POINTER(_Params)]
         _lib = lib
@@ -118,11 +131,19 @@ def parameter_sets(p: SynthParams) -> Tuple[bytes, bytes, bytes]:
 
 
 def picture(p: SynthParams, seed: int) -> bytes:
-    """One IDR NAL unit (2-byte header included)."""
+    """One IDR NAL unit (2-byte header included); single-segment pictures."""
     lib = _load()
     # worst case: dense 32x32 blocks with long level tails
     cap = max(1 << 16, p.width * p.height * 8)
     return _call(lib.synth_picture, p, ctypes.c_uint64(seed), cap=cap)
+
+
+def picture_item(p: SynthParams, seed: int) -> bytes:
+    """The picture's slice segments as 4-byte-length-prefixed IDR NAL units
+    (a HEIF coded image item's payload)."""
+    lib = _load()
+    cap = max(1 << 16, p.width * p.height * 8)
+    return _call(lib.synth_picture_item, p, ctypes.c_uint64(seed), cap=cap)
 
 
 # ---------------------------------------------------------------- HEIF boxes
@@ -266,13 +287,15 @@ def grid_heic(out_w: int, out_h: int, p: SynthParams, seed: int = 0, pictures: O
     rows = -(-out_h // (p.height - p.conf_bottom))
     n = rows * cols
     if pictures is None:
-        pictures = [picture(p, (seed << 16) + k) for k in range(n)]
+        items_data = [picture_item(p, (seed << 16) + k) for k in range(n)]
+    else:
+        items_data = [_len_prefixed(pic) for pic in pictures]
     vps, sps, pps = parameter_sets(p)
     props = [hvcc(p, vps, sps, pps), _ispe(p.width - p.conf_right, p.height - p.conf_bottom), _ispe(out_w, out_h)]
     grid_id = 1
     items = [(grid_id, b"grid", struct.pack(">BBBBHH", 0, 0, rows - 1, cols - 1, out_w, out_h))]
     for k in range(n):
-        items.append((k + 2, b"hvc1", _len_prefixed(pictures[k])))
+        items.append((k + 2, b"hvc1", items_data[k]))
     assoc = [(grid_id, [3])] + [(k + 2, [1, 2]) for k in range(n)]
     iref = _fbox(b"iref", 0, 0, _box(b"dimg", struct.pack(">HH", grid_id, n) +
                                      b"".join(struct.pack(">H", k + 2) for k in range(n))))
@@ -286,7 +309,7 @@ def single_heic(p: SynthParams, seed: int = 0, layout: Optional[BoxLayout] = Non
     (robustness tests hand-craft out-of-range parameter sets)."""
     vps, sps, pps = param_sets or parameter_sets(p)
     props = [hvcc(p, vps, sps, pps), _ispe(p.width - p.conf_right, p.height - p.conf_bottom)]
-    items = [(1, b"hvc1", _len_prefixed(nal if nal is not None else picture(p, seed)))]
+    items = [(1, b"hvc1", _len_prefixed(nal) if nal is not None else picture_item(p, seed))]
     return _assemble(items, 1, props, [(1, [1, 2])], b"", b"", layout)
 
 

@@ -702,10 +702,16 @@ typedef struct {
     int off[3][5];
 } sao_ctb;
 
+/* per-slice values the loop filters need after parsing (7.4.7.1) */
+typedef struct {
+    int qp, sao_l, sao_c, dbk_disabled, beta, tc, cb_off, cr_off, lf_across;
+    int addr_rs; /* SliceAddrRs */
+} slice_par;
+
 typedef struct {
     const hevc_sps *sps;
     const hevc_pps *pps;
-    /* slice */
+    /* the slice being parsed */
     int slice_qp, sao_luma, sao_chroma, dbk_disabled, beta_off, tc_off, cb_qp_off, cr_qp_off;
     /* geometry */
     int W, H, log2ctb, ctb, wctb, hctb, minTb, minCb;
@@ -729,6 +735,10 @@ typedef struct {
      * the tile of each CTB by raster address (one tile when tiles is 0) */
     int colBd[HEVC_MAX_TILE_DIM + 1], rowBd[HEVC_MAX_TILE_DIM + 1];
     int *rs2ts, *ts2rs, *tile_rs;
+    /* slices: index of the slice holding each CTB (raster address), their values */
+    int *slice_rs;
+    slice_par *slices;
+    uint8_t ds_st[CTX_NUM], ds_mps[CTX_NUM]; /* 9.3.2.4 storage at a slice segment's end */
     /* current CU */
     int cu_bypass, cu_intra_split, cu_max_trafo_depth, cu_chroma_mode_c;
 } pic_t;
@@ -754,12 +764,17 @@ static int zscan_addr(const pic_t *p, int x, int y) {
 static int tile_at(const pic_t *p, int x, int y) {
     return p->tile_rs[(y >> p->log2ctb) * p->wctb + (x >> p->log2ctb)];
 }
-/* 6.4.1 z-scan availability (single slice): outside the picture, later in
- * decoding order or in another tile ⇒ unavailable */
+/* slice of the CTB holding luma sample (x,y) (-1: not decoded yet) */
+static int slice_at(const pic_t *p, int x, int y) {
+    return p->slice_rs[(y >> p->log2ctb) * p->wctb + (x >> p->log2ctb)];
+}
+/* 6.4.1 z-scan availability: outside the picture, later in decoding order,
+ * in another tile or in another slice ⇒ unavailable */
 static int avail_zs(const pic_t *p, int xc, int yc, int xn, int yn) {
     if (xn < 0 || yn < 0 || xn >= p->W || yn >= p->H) return 0;
     if (tile_at(p, xn, yn) != tile_at(p, xc, yc)) return 0;
-    return zscan_addr(p, xn, yn) <= zscan_addr(p, xc, yc);
+    if (zscan_addr(p, xn, yn) > zscan_addr(p, xc, yc)) return 0;
+    return slice_at(p, xn, yn) == slice_at(p, xc, yc);
 }
 
 /* 6.5.1 (6-3..6-10): colBd / rowBd, CtbAddrRsToTs, CtbAddrTsToRs, TileId */
@@ -1481,10 +1496,12 @@ static void parse_sao(pic_t *p, int rx, int ry) {
     cabac_t *c = &p->c;
     sao_ctb *s = &p->sao[ry * p->wctb + rx];
     memset(s, 0, sizeof(*s));
-    int ml = 0, mu = 0, t = p->tile_rs[ry * p->wctb + rx];
-    /* merge candidates: left / above CTB in the same slice (always) and tile */
-    if (rx > 0 && p->tile_rs[ry * p->wctb + rx - 1] == t) ml = dec_bin(c, CTX_SAO_MERGE);
-    if (ry > 0 && !ml && p->tile_rs[(ry - 1) * p->wctb + rx] == t) mu = dec_bin(c, CTX_SAO_MERGE);
+    const int cr = ry * p->wctb + rx, t = p->tile_rs[cr], sl = p->slice_rs[cr];
+    int ml = 0, mu = 0;
+    /* merge candidates: left / above CTB in the same slice and tile */
+    if (rx > 0 && p->tile_rs[cr - 1] == t && p->slice_rs[cr - 1] == sl) ml = dec_bin(c, CTX_SAO_MERGE);
+    if (ry > 0 && !ml && p->tile_rs[cr - p->wctb] == t && p->slice_rs[cr - p->wctb] == sl)
+        mu = dec_bin(c, CTX_SAO_MERGE);
     if (ml) { *s = p->sao[ry * p->wctb + rx - 1]; return; }
     if (mu) { *s = p->sao[(ry - 1) * p->wctb + rx]; return; }
     int ncomp = p->chroma ? 3 : 1;
@@ -1624,15 +1641,23 @@ static void dbk_chroma_seg(pic_t *p, int cIdx, int xc, int yc, int vertical, int
     }
 }
 
-/* 8.7.2: filterEdgeFlag = 0 on a tile boundary when
- * loop_filter_across_tiles_enabled_flag is 0 */
-static int tile_edge_off(const pic_t *p, int x, int y, int vertical) {
-    if (p->pps->lf_across_tiles) return 0;
-    return vertical ? tile_at(p, x - 1, y) != tile_at(p, x, y) : tile_at(p, x, y - 1) != tile_at(p, x, y);
+/* 8.7.2: the edge whose q0 sample is (x,y) is not filtered when q0's slice
+ * has slice_deblocking_filter_disabled_flag, or the edge is a tile boundary
+ * with loop_filter_across_tiles_enabled_flag 0, or a boundary with an earlier
+ * slice and q0's slice_loop_filter_across_slices_enabled_flag is 0.
+ * Otherwise the filter takes q0's slice_beta / tc offsets. */
+static int edge_off(pic_t *p, int x, int y, int vertical) {
+    const int xp = vertical ? x - 1 : x, yp = vertical ? y : y - 1;
+    const slice_par *sq = &p->slices[slice_at(p, x, y)];
+    if (sq->dbk_disabled) return 1;
+    if (!p->pps->lf_across_tiles && tile_at(p, xp, yp) != tile_at(p, x, y)) return 1;
+    if (!sq->lf_across && slice_at(p, xp, yp) != slice_at(p, x, y)) return 1;
+    p->beta_off = sq->beta;
+    p->tc_off = sq->tc;
+    return 0;
 }
 
 static void deblock_picture(pic_t *p) {
-    if (p->dbk_disabled) return;
     for (int dir = 0; dir < 2; dir++) {
         int vertical = dir == 0;
         /* luma: edges on the 8x8 grid, 4-line segments */
@@ -1643,7 +1668,7 @@ static void deblock_picture(pic_t *p) {
                 if (!vertical && (x & 3)) continue;
                 int f = p->flg[(y >> 2) * p->w4 + (x >> 2)];
                 if (!(f & (vertical ? F_EDGE_V : F_EDGE_H))) continue;
-                if (tile_edge_off(p, x, y, vertical)) continue;
+                if (edge_off(p, x, y, vertical)) continue;
                 dbk_luma_seg(p, x, y, vertical);
             }
         if (p->chroma == 0) continue;
@@ -1657,7 +1682,7 @@ static void deblock_picture(pic_t *p) {
                     int xl = xc * p->sw, yl = yc * p->sh;
                     int f = p->flg[(yl >> 2) * p->w4 + (xl >> 2)];
                     if (!(f & (vertical ? F_EDGE_V : F_EDGE_H))) continue;
-                    if (tile_edge_off(p, xl, yl, vertical)) continue;
+                    if (edge_off(p, xl, yl, vertical)) continue;
                     dbk_chroma_seg(p, ci, xc, yc, vertical, lines);
                 }
     }
@@ -1666,6 +1691,15 @@ static void deblock_picture(pic_t *p) {
 /* ===================================================================== */
 /* SAO — H.265 8.7.3                                                      */
 /* ===================================================================== */
+/* 8.7.3.2: SaoOffsetVal 0 when the neighbour (xn,yn) of (x,y) is in another
+ * slice whose boundary with it is not filtered across */
+static int sao_slice_off(const pic_t *p, int x, int y, int xn, int yn) {
+    const int sc = slice_at(p, x, y), sn = slice_at(p, xn, yn);
+    if (sc == sn) return 0;
+    const int later = zscan_addr(p, xn, yn) < zscan_addr(p, x, y) ? sc : sn;
+    return !p->slices[later].lf_across;
+}
+
 static void sao_picture(pic_t *p, uint16_t *out[3], const int ops[3]) {
     int ncomp = p->chroma ? 3 : 1;
     static const int hpos[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
@@ -1705,6 +1739,10 @@ static void sao_picture(pic_t *p, uint16_t *out[3], const int ops[3]) {
                                 int tc = tile_at(p, xl, yl);
                                 if (tile_at(p, ax * sw, ay * sh) != tc || tile_at(p, bx * sw, by * sh) != tc) continue;
                             }
+                            /* a neighbour in another slice: the flag of the later of the two slices (in
+                             * MinTbAddrZs order) decides */
+                            if (sao_slice_off(p, xl, yl, ax * sw, ay * sh) || sao_slice_off(p, xl, yl, bx * sw, by * sh))
+                                continue;
                             int a = in[ay * ps + ax], b = in[by * ps + bx];
                             int e = 2 + (v > a) - (v < a) + (v > b) - (v < b);
                             if (e == 0 || e == 1 || e == 2) e = (e == 2) ? 0 : e + 1;
@@ -1722,18 +1760,31 @@ static void sao_picture(pic_t *p, uint16_t *out[3], const int ops[3]) {
 /* Slice header + slice data                                              */
 /* ===================================================================== */
 typedef struct {
+    int first, dependent, address; /* first_slice_segment_in_pic_flag, dependent_slice_segment_flag,
+                                      slice_segment_address (raster) */
     int idr, slice_type, qp_delta, sao_l, sao_c, cb_off, cr_off;
-    int dbk_disabled, beta, tc;
+    int dbk_disabled, beta, tc, lf_across;
     int num_entry, entry[1024];
     size_t data_bit; /* RBSP bit offset of slice_segment_data() */
 } slice_hdr;
 
-static int parse_slice_header(br_t *b, int nal_type, const hevc_sps *s, const hevc_pps *pp, slice_hdr *h) {
+/* 7.3.6.1 slice_segment_header() — slice.rs:44-204 (which takes only the
+ * first segment: slice.rs:61-64); a dependent segment carries only the
+ * address and entry points, its other fields are the slice's (the caller
+ * copies them) */
+static int parse_slice_header(br_t *b, int nal_type, const hevc_sps *s, const hevc_pps *pp, int nctb, slice_hdr *h) {
     memset(h, 0, sizeof(*h));
-    int first = (int)br_u(b, 1);
+    h->first = (int)br_u(b, 1);
     if (nal_type >= 16 && nal_type <= 23) br_u(b, 1);
     br_ue(b);
-    if (!first) return oracle_fail("multi-slice pictures not supported");
+    if (!h->first) {
+        if (pp->dependent_slices) h->dependent = (int)br_u(b, 1);
+        int bits = 0;
+        while ((1 << bits) < nctb) bits++;
+        h->address = (int)br_u(b, bits);
+        if (h->address >= nctb) return oracle_fail("slice_segment_address out of range");
+    }
+    if (h->dependent) goto entry_points;
     br_u(b, pp->num_extra_bits);
     h->slice_type = (int)br_ue(b);
     if (h->slice_type != 2) return oracle_fail("only I slices are supported");
@@ -1787,7 +1838,9 @@ static int parse_slice_header(br_t *b, int nal_type, const hevc_sps *s, const he
         h->dbk_disabled = (int)br_u(b, 1);
         if (!h->dbk_disabled) { h->beta = br_se(b); h->tc = br_se(b); }
     }
-    if (pp->loop_filter_across_slices && (h->sao_l || h->sao_c || !h->dbk_disabled)) br_u(b, 1);
+    h->lf_across = pp->loop_filter_across_slices;
+    if (pp->loop_filter_across_slices && (h->sao_l || h->sao_c || !h->dbk_disabled)) h->lf_across = (int)br_u(b, 1);
+entry_points:
     if (pp->tiles || pp->wpp) {
         h->num_entry = (int)br_ue(b);
         if (h->num_entry > 1024) return oracle_fail("too many entry points");
@@ -1809,38 +1862,64 @@ static int parse_slice_header(br_t *b, int nal_type, const hevc_sps *s, const he
     return 0;
 }
 
-/* decode one picture (one IDR NAL unit payload incl. 2-byte header) */
-static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len, uint16_t *outp[3],
+/* rbsp byte offset → raw payload offset (ep[] holds the raw indices of the
+ * removed 0x03 bytes) */
+static size_t rbsp_to_raw(size_t rb, const uint32_t *ep, int nep) {
+    size_t r = 0, raw = 0;
+    int e = 0;
+    while (r < rb) {
+        if (e < nep && ep[e] == raw) { raw++; e++; continue; }
+        raw++;
+        r++;
+    }
+    while (e < nep && ep[e] == raw) { raw++; e++; }
+    return raw;
+}
+
+#define MAX_SEGMENTS 1024
+
+/* Decode one coded picture: the VCL NAL units (slice segments) of an item's
+ * length-prefixed NAL units, in order (heic/decoder.rs:146-164 takes the
+ * one NAL of a single-slice picture).  Each slice segment starts at its
+ * slice_segment_address and runs in tile scan until end_of_slice_segment_flag;
+ * contexts at a segment / substream start follow 9.3.1 (tile start: init;
+ * WPP row start: the stored row-above state if the above-right CTB is
+ * available, else init; dependent segment: the previous segment's end state;
+ * otherwise init). */
+static int decode_picture(const hevc_ps *ps, const uint8_t *item, size_t item_len, uint16_t *outp[3],
                           const int ops[3], int tile_index, oracle_substream_check *checks, int max_checks,
                           int *n_checks) {
     init_tables();
     init_transform();
     const hevc_sps *s = &ps->sps;
     const hevc_pps *pp = &ps->pps;
-    if (nal_len < 3) return oracle_fail("short NAL");
-    int nal_type = (nal[0] >> 1) & 63;
     if (s->range_ext_any || pp->range_ext_any) return oracle_fail("range extension tools not supported");
     if (pp->tiles && pp->wpp) return oracle_fail("HEVC tiles together with WPP not supported");
     if (s->chroma_format_idc == 2 || s->chroma_format_idc == 3) return oracle_fail("only 4:0:0 / 4:2:0");
-    uint8_t *rbsp = (uint8_t *)malloc(nal_len);
-    uint32_t *ep = (uint32_t *)malloc(sizeof(uint32_t) * (nal_len / 3 + 4));
-    int nep = 0;
-    size_t rn = ep_remove(nal + 2, nal_len - 2, rbsp, ep, &nep, (int)(nal_len / 3 + 4));
+    /* the VCL NAL units, 4-byte length prefixes */
+    const uint8_t *nals[MAX_SEGMENTS];
+    size_t nlen[MAX_SEGMENTS];
+    int nn = 0;
+    for (size_t pos = 0; pos < item_len;) {
+        if (item_len - pos < 4) return oracle_fail("truncated NAL length prefix");
+        size_t l = ((size_t)item[pos] << 24) | ((size_t)item[pos + 1] << 16) | ((size_t)item[pos + 2] << 8) | item[pos + 3];
+        pos += 4;
+        if (l < 3 || l > item_len - pos) return oracle_fail("NAL unit length out of range");
+        if (((item[pos] >> 1) & 63) < 32) {
+            if (nn == MAX_SEGMENTS) return oracle_fail("too many slice segments");
+            nals[nn] = item + pos;
+            nlen[nn++] = l;
+        }
+        pos += l;
+    }
+    if (!nn) return oracle_fail("no VCL NAL unit in the picture");
     pic_t *p = (pic_t *)calloc(1, sizeof(pic_t));
     int ret = -1;
     slice_hdr *h = (slice_hdr *)malloc(sizeof(slice_hdr));
-    br_t hb = {rbsp, rn, 0, 0};
-    if (parse_slice_header(&hb, nal_type, s, pp, h)) goto out;
+    uint8_t *rbsp = NULL;
+    uint32_t *ep = NULL;
     p->sps = s;
     p->pps = pp;
-    p->slice_qp = pp->init_qp + h->qp_delta;
-    p->sao_luma = h->sao_l;
-    p->sao_chroma = h->sao_c;
-    p->dbk_disabled = h->dbk_disabled;
-    p->beta_off = h->beta;
-    p->tc_off = h->tc;
-    p->cb_qp_off = h->cb_off;
-    p->cr_qp_off = h->cr_off;
     p->W = s->width;
     p->H = s->height;
     p->log2ctb = s->log2_ctb;
@@ -1865,45 +1944,96 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
         p->ps[ci] = w;
         p->pl[ci] = (uint16_t *)calloc((size_t)w * hh, sizeof(uint16_t));
     }
+    const int nctb = p->wctb * p->hctb;
     p->ipm = (uint8_t *)calloc((size_t)p->w4 * p->h4, 1);
     p->depth = (uint8_t *)calloc((size_t)p->w4 * p->h4, 1);
     p->flg = (uint8_t *)calloc((size_t)p->w4 * p->h4, 1);
     p->qpy = (int8_t *)calloc((size_t)p->w4 * p->h4, 1);
-    p->sao = (sao_ctb *)calloc((size_t)p->wctb * p->hctb, sizeof(sao_ctb));
+    p->sao = (sao_ctb *)calloc((size_t)nctb, sizeof(sao_ctb));
+    p->slice_rs = (int *)malloc(sizeof(int) * (size_t)nctb);
+    for (int i = 0; i < nctb; i++) p->slice_rs[i] = -1;
+    p->slices = (slice_par *)calloc((size_t)nn, sizeof(slice_par));
     build_scaling(p);
     if (tile_scan_init(p)) goto out;
-    /* raw offset (within NAL payload after header) of slice data start */
-    {
-        size_t rb = h->data_bit >> 3;
-        /* rbsp byte offset → raw payload offset (ep[] holds raw indices of removed 0x03) */
-        size_t raw = 0;
-        {
-            size_t r = 0;
-            int e = 0;
-            while (r < rb) {
-                if (e < nep && ep[e] == raw) { raw++; e++; continue; }
-                raw++;
-                r++;
-            }
-            while (e < nep && ep[e] == raw) { raw++; e++; }
+    int next_ts = 0, cur_slice = -1, any_sao = 0, substream = 0;
+    for (int k = 0; k < nn; k++) {
+        const uint8_t *nal = nals[k];
+        const size_t nal_len = nlen[k];
+        free(rbsp);
+        free(ep);
+        rbsp = (uint8_t *)malloc(nal_len);
+        ep = (uint32_t *)malloc(sizeof(uint32_t) * (nal_len / 3 + 4));
+        int nep = 0;
+        size_t rn = ep_remove(nal + 2, nal_len - 2, rbsp, ep, &nep, (int)(nal_len / 3 + 4));
+        br_t hb = {rbsp, rn, 0, 0};
+        if (parse_slice_header(&hb, (nal[0] >> 1) & 63, s, pp, nctb, h)) goto out;
+        if (h->first != (k == 0)) { oracle_fail("first_slice_segment_in_pic_flag out of order"); goto out; }
+        if (p->rs2ts[h->address] != next_ts) { oracle_fail("slice segments out of order or overlapping"); goto out; }
+        if (!h->dependent) {
+            slice_par *sl = &p->slices[++cur_slice];
+            sl->qp = pp->init_qp + h->qp_delta;
+            sl->sao_l = h->sao_l;
+            sl->sao_c = h->sao_c;
+            sl->dbk_disabled = h->dbk_disabled;
+            sl->beta = h->beta;
+            sl->tc = h->tc;
+            sl->cb_off = h->cb_off;
+            sl->cr_off = h->cr_off;
+            sl->lf_across = h->lf_across;
+            sl->addr_rs = h->address;
+            any_sao |= sl->sao_l || sl->sao_c;
+        } else if (cur_slice < 0) {
+            oracle_fail("dependent slice segment without a slice");
+            goto out;
         }
-        /* substream raw starts */
+        const slice_par *sl = &p->slices[cur_slice];
+        p->slice_qp = sl->qp;
+        p->sao_luma = sl->sao_l;
+        p->sao_chroma = sl->sao_c;
+        p->dbk_disabled = sl->dbk_disabled;
+        p->beta_off = sl->beta;
+        p->tc_off = sl->tc;
+        p->cb_qp_off = sl->cb_off;
+        p->cr_qp_off = sl->cr_off;
+        /* substream raw starts of this segment */
         size_t sub_raw[1025];
-        sub_raw[0] = raw;
+        sub_raw[0] = rbsp_to_raw(h->data_bit >> 3, ep, nep);
         for (int i = 0; i < h->num_entry; i++) sub_raw[i + 1] = sub_raw[i] + (size_t)h->entry[i];
         p->c.b.d = rbsp;
         p->c.b.n = rn;
         p->c.b.bit = h->data_bit;
-        int ctbAddr = 0, substream = 0, nctb = p->wctb * p->hctb;
-        cabac_init_ctx(&p->c, p->slice_qp);
-        if (cabac_init_engine(&p->c)) goto out;
-        p->first_qg_in_slice = 1;
+        int ctbAddr = next_ts, seg_sub = 0;
         size_t sub_start_rbsp = h->data_bit >> 3;
-        uint32_t sub_bins0 = 0;
+        uint32_t sub_bins0 = p->c.bins;
+        int sub_first = 1; /* the next CTU starts a substream */
         for (;;) { /* ctbAddr is CtbAddrInTs: tile scan (7.3.8.1) */
             int rs = p->ts2rs[ctbAddr], rx = rs % p->wctb, ry = rs / p->wctb;
             p->ctb_x = rx << p->log2ctb;
             p->ctb_y = ry << p->log2ctb;
+            p->slice_rs[rs] = cur_slice;
+            if (sub_first) {
+                /* 9.3.1 context variables at a substream start */
+                const int tile_start = ctbAddr == 0 || p->tile_rs[rs] != p->tile_rs[p->ts2rs[ctbAddr - 1]];
+                if (tile_start) {
+                    cabac_init_ctx(&p->c, p->slice_qp);
+                } else if (pp->wpp && rx == 0) {
+                    if (p->wpp_saved && avail_zs(p, p->ctb_x, p->ctb_y, p->ctb_x + p->ctb, p->ctb_y - p->ctb)) {
+                        memcpy(p->c.st, p->wpp_st, CTX_NUM);
+                        memcpy(p->c.mps, p->wpp_mps, CTX_NUM);
+                    } else {
+                        cabac_init_ctx(&p->c, p->slice_qp);
+                    }
+                } else if (h->dependent && ctbAddr == next_ts) {
+                    memcpy(p->c.st, p->ds_st, CTX_NUM);
+                    memcpy(p->c.mps, p->ds_mps, CTX_NUM);
+                } else {
+                    cabac_init_ctx(&p->c, p->slice_qp);
+                }
+                if (cabac_init_engine(&p->c)) goto out;
+                /* 8.6.1: qPY_PREV = SliceQpY at the first QG of a slice or a tile */
+                if (tile_start || (ctbAddr == next_ts && !h->dependent)) p->first_qg_in_slice = 1;
+                sub_first = 0;
+            }
             if (p->sao_luma || p->sao_chroma) parse_sao(p, rx, ry);
             if (coding_quadtree(p, p->ctb_x, p->ctb_y, p->log2ctb, 0)) goto out;
             if (pp->wpp && rx == 1) {
@@ -1929,52 +2059,37 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
                 if (checks && *n_checks < max_checks) {
                     oracle_substream_check *ck = &checks[(*n_checks)++];
                     ck->tile = (uint32_t)tile_index;
-                    ck->substream = (uint32_t)substream;
-                    /* rbsp → raw of this substream's start */
-                    size_t r = 0, rawp = 0;
-                    int e = 0;
-                    while (r < sub_start_rbsp) {
-                        if (e < nep && ep[e] == rawp) { rawp++; e++; continue; }
-                        rawp++;
-                        r++;
-                    }
-                    while (e < nep && ep[e] == rawp) { rawp++; e++; }
-                    ck->raw_start = (uint32_t)rawp;
-                    ck->raw_entry = substream <= h->num_entry ? (uint32_t)sub_raw[substream] : 0xffffffffu;
-                    ck->term_ok = (uint32_t)(ok && (end ? ctbAddr == nctb : 1));
+                    ck->substream = (uint32_t)substream; /* in the picture, over its segments */
+                    ck->raw_start = (uint32_t)rbsp_to_raw(sub_start_rbsp, ep, nep);
+                    ck->raw_entry = seg_sub <= h->num_entry ? (uint32_t)sub_raw[seg_sub] : 0xffffffffu;
+                    ck->term_ok = (uint32_t)(ok && (end ? (k + 1 < nn || ctbAddr == nctb) : 1));
                     ck->bins = p->c.bins - sub_bins0;
                 }
+                substream++;
                 if (end) {
-                    if (ctbAddr != nctb) { oracle_fail("end_of_slice_segment before last CTU"); goto out; }
-                    break;
-                }
-                if (cut_end) {
-                    if (!ok) { oracle_fail("end_of_subset_one_bit mismatch"); goto out; }
+                    if (k + 1 == nn && ctbAddr != nctb) { oracle_fail("end_of_slice_segment before last CTU"); goto out; }
+                    if (k + 1 < nn && ctbAddr == nctb) { oracle_fail("slice segments after the last CTU"); goto out; }
+                    if (seg_sub != h->num_entry) { oracle_fail("entry points do not match the substreams"); goto out; }
+                    if (pp->dependent_slices) { /* 9.3.2.4 storage for a following dependent segment */
+                        memcpy(p->ds_st, p->c.st, CTX_NUM);
+                        memcpy(p->ds_mps, p->c.mps, CTX_NUM);
+                    }
                     break;
                 }
                 if (!ok) { oracle_fail("end_of_subset_one_bit mismatch"); goto out; }
-                /* byte_alignment + engine re-init at next substream */
+                if (cut_end) break;
+                /* byte_alignment + engine re-init at the next substream */
                 p->c.b.bit = pos;
-                substream++;
+                seg_sub++;
                 sub_start_rbsp = pos >> 3;
                 sub_bins0 = p->c.bins;
-                /* 9.3.1: a new tile starts with initialised contexts (and
-                 * qPY_PREV = SliceQpY, 8.6.1); WPP sync: T = above-right CTB
-                 * available ⇒ restore; else init */
-                if (tile_end) {
-                    cabac_init_ctx(&p->c, p->slice_qp);
-                    p->first_qg_in_slice = 1;
-                } else if (p->wctb > 1 && p->wpp_saved) {
-                    memcpy(p->c.st, p->wpp_st, CTX_NUM);
-                    memcpy(p->c.mps, p->wpp_mps, CTX_NUM);
-                } else {
-                    cabac_init_ctx(&p->c, p->slice_qp);
-                }
-                if (cabac_init_engine(&p->c)) goto out;
+                sub_first = 1;
             }
             if (ctbAddr >= nctb) { oracle_fail("missing end_of_slice_segment_flag"); goto out; }
         }
+        next_ts = ctbAddr;
     }
+    if (next_ts != nctb && !(g_debug_flags & 4)) { oracle_fail("slice segments do not cover the picture"); goto out; }
     if (!(g_debug_flags & 1)) deblock_picture(p);
     {
         /* SAO into full-size temp, then crop into caller planes */
@@ -1983,7 +2098,7 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *nal, size_t nal_len,
         int nc = p->chroma ? 3 : 1;
         for (int ci = 0; ci < nc; ci++)
             full[ci] = (uint16_t *)malloc(sizeof(uint16_t) * (size_t)(ci ? p->cw * p->chh : p->W * p->H));
-        if ((p->sao_luma || p->sao_chroma) && !(g_debug_flags & 2)) sao_picture(p, full, fps);
+        if (any_sao && !(g_debug_flags & 2)) sao_picture(p, full, fps);
         else
             for (int ci = 0; ci < nc; ci++)
                 memcpy(full[ci], p->pl[ci], sizeof(uint16_t) * (size_t)(ci ? p->cw * p->chh : p->W * p->H));
@@ -2009,6 +2124,8 @@ out:
     free(p->rs2ts);
     free(p->ts2rs);
     free(p->tile_rs);
+    free(p->slice_rs);
+    free(p->slices);
     for (int a = 0; a < 4; a++)
         for (int m = 0; m < 6; m++) free(p->sf[a][m]);
     free(p);
@@ -2021,27 +2138,14 @@ out:
 /* ===================================================================== */
 /* Tile / HEIC entry points                                               */
 /* ===================================================================== */
-/* heic/decoder.rs:146-164: one NAL with 4-byte length prefix */
-static int tile_nal(const uint8_t *item, size_t len, const uint8_t **nal, size_t *nal_len) {
-    if (len < 6) return oracle_fail("tile item too short");
-    size_t l = ((size_t)item[0] << 24) | ((size_t)item[1] << 16) | ((size_t)item[2] << 8) | item[3];
-    if (l != len - 4) return oracle_fail("tile item must hold exactly one NAL unit");
-    *nal = item + 4;
-    *nal_len = l;
-    return 0;
-}
-
 int oracle_decode_tile(const uint8_t *hvcc, size_t hvcc_len, const uint8_t *item, size_t item_len, uint16_t *y,
                        int ypitch, uint16_t *cb, int cbpitch, uint16_t *cr, int crpitch) {
     hevc_ps ps;
     if (hevc_parse_hvcc(hvcc, hvcc_len, &ps)) return -1;
-    const uint8_t *nal = NULL;
-    size_t nl = 0;
-    if (tile_nal(item, item_len, &nal, &nl)) return -1;
     uint16_t *o[3] = {y, cb, cr};
     int op[3] = {ypitch, cbpitch, crpitch};
     int nchk = 0;
-    return decode_picture(&ps, nal, nl, o, op, 0, NULL, 0, &nchk);
+    return decode_picture(&ps, item, item_len, o, op, 0, NULL, 0, &nchk);
 }
 
 void oracle_image_free(oracle_image *img) {
@@ -2116,16 +2220,13 @@ int oracle_decode_heic(const uint8_t *data, size_t len, oracle_image *out, oracl
         size_t il;
         uint8_t *item = heif_item_data(f, it, &il);
         if (!item) goto free_grid;
-        const uint8_t *nal = NULL;
-        size_t nl = 0;
-        if (tile_nal(item, il, &nal, &nl)) { free(item); goto free_grid; }
         int r = t / cols, c = t % cols;
         uint16_t *o[3] = {0, 0, 0};
         for (int ci = 0; ci < np; ci++) {
             int x = c * tw / (ci ? sw : 1), y = r * th / (ci ? sh : 1);
             o[ci] = grid[ci] + (size_t)y * gp[ci] + x;
         }
-        int rc = decode_picture(&ps, nal, nl, o, gp, t, checks, max_checks, n_checks);
+        int rc = decode_picture(&ps, item, il, o, gp, t, checks, max_checks, n_checks);
         free(item);
         if (rc) goto free_grid;
     }

@@ -145,3 +145,81 @@ def assemble(p, subs: List[SubPicture], decode) -> Tuple:
             for dst, src in zip(c, (pcb, pcr)):
                 dst[s.y0 // 2:s.y0 // 2 + src.shape[0], s.x0 // 2:s.x0 // 2 + src.shape[1]] = src
     return y, c[0], c[1]
+
+
+def _nal_units(item: bytes) -> List[bytes]:
+    out, pos = [], 0
+    while pos < len(item):
+        n = int.from_bytes(item[pos:pos + 4], "big")
+        out.append(item[pos + 4:pos + 4 + n])
+        pos += 4 + n
+    return out
+
+
+def split_slices(p, item: bytes) -> List[SubPicture]:
+    """The slices of a picture written with p.slice_ctus a multiple of its
+    width in CTBs (every slice a band of CTB rows, all independent, no tiles)
+    as stand-alone pictures: each slice segment's header is rewritten without
+    its address (first_slice_segment_in_pic_flag = 1), every other field and
+    the slice data kept."""
+    ctb = 1 << p.log2_ctb
+    wctb, hctb = -(-p.width // ctb), -(-p.height // ctb)
+    assert p.slice_ctus % wctb == 0 and not p.slice_dependent and p.tile_cols * p.tile_rows == 1
+    nctb = wctb * hctb
+    abits = (nctb - 1).bit_length()
+    subs = []
+    for k, nal in enumerate(_nal_units(item)):
+        rbsp = _unescape(nal[2:])
+        r = _Reader(rbsp)
+        assert r.u(1) == (k == 0)
+        r.u(1)
+        assert r.ue() == 0
+        addr = r.u(abits) if k else 0
+        w = BitWriter()
+        w.u(1, 1)
+        w.u(0, 1)
+        w.ue(0)
+        # the rest of the header up to slice data: slice_type, SAO flags, QP delta,
+        # deblocking override, filter-across flag, entry points (hevc_synth.c's order)
+        slice_type = r.ue()
+        w.ue(slice_type)
+        sao = 0
+        if p.sao:
+            sao = r.u(1)
+            w.u(sao, 1)
+            if p.chroma_format:
+                c = r.u(1)
+                sao |= c
+                w.u(c, 1)
+        w.se(r.se())
+        dis = p.deblock_disabled
+        if p.slice_dbk_vary:
+            ov = r.u(1)
+            w.u(ov, 1)
+            if ov:
+                dis = r.u(1)
+                w.u(dis, 1)
+                if not dis:
+                    w.se(r.se())
+                    w.se(r.se())
+        if p.slice_lf_across and (sao or not dis):
+            w.u(r.u(1), 1)
+        if p.wpp:
+            n = r.ue()
+            w.ue(n)
+            if n:
+                ln = r.ue()
+                w.ue(ln)
+                for _ in range(n):
+                    w.u(r.u(ln + 1), ln + 1)
+        assert r.u(1) == 1
+        while r.pos & 7:
+            assert r.u(1) == 0
+        w.trailing()
+        hdr_raw = len(_ep(rbsp[:r.pos >> 3]))
+        y0 = addr // wctb * ctb
+        h = min(y0 + p.slice_ctus // wctb * ctb, p.height) - y0
+        last = y0 + h >= p.height
+        sp = dataclasses.replace(p, height=h, slice_ctus=0, conf_bottom=p.conf_bottom if last else 0)
+        subs.append(SubPicture(0, y0, sp, nal[:2] + _ep(w.bytes()) + nal[2 + hdr_raw:]))
+    return subs

@@ -1,0 +1,243 @@
+"""Pictures of several slice segments (the reference reads only the first
+segment of a picture: slice.rs:61-64 asserts first_slice_segment_in_pic_flag;
+its slice-header grammar, slice.rs:44-204, is the anchor for the fields).
+
+Oracle: spec-literal slices (oracle/hevc_decode.c decode_picture: segments in
+tile scan from slice_segment_address, 9.3.1 context initialisation /
+dependent-segment synchronisation, slice-bounded availability 6.4.1 and SAO
+merge 7.3.8.3, qPY_PREV restart 8.6.1, per-slice deblocking parameters and
+slice_loop_filter_across_slices_enabled_flag in 8.7.2 / 8.7.3).  Pinning: a
+picture whose slices are bands of CTB rows with no loop filter across them
+must equal its slices decoded as stand-alone pictures (tests/hevc_tiles.py
+rewrites each segment's header), and the single-slice decode is pinned by the
+reference's fixtures (test_oracle.py).  The generator and the oracle agreeing
+on every substream end (the per-substream checks) pins context selection
+for the other layouts (mid-row slices, dependent segments, slices with tiles).
+
+GPU: each slice of such a picture is decoded as its own picture
+(heif_amd/csrc/host/batch.cpp); dependent segments, slices starting inside a
+CTB row, loop filtering across slices and slices with HEVC tiles are
+HEIFGPU_E_UNSUPPORTED.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from hevc_tiles import _nal_units, assemble, split_slices
+
+S = pytest.importorskip("heif_amd.synth_encoder")
+
+# every layout the oracle decodes (128x96 / CTB 32 = 4 x 3 CTBs unless set)
+PARSE_CASES = [
+    ("rows_nowpp", dict(slice_ctus=4)),
+    ("rows_wpp", dict(slice_ctus=4, wpp=1)),
+    ("midrow_nowpp", dict(slice_ctus=5)),
+    ("midrow_wpp", dict(slice_ctus=5, wpp=1)),
+    ("dependent_nowpp", dict(slice_ctus=5, slice_dependent=1)),
+    ("dependent_alt_wpp", dict(slice_ctus=3, wpp=1, slice_dependent=2)),
+    ("across_mixed_dbk", dict(slice_ctus=3, wpp=1, slice_dependent=1, slice_lf_across=2, slice_dbk_vary=1)),
+    ("tiles_and_slices", dict(slice_ctus=3, tile_cols=2, tile_rows=2)),
+    ("tiles_slices_across", dict(slice_ctus=7, tile_cols=2, tile_rows=2, slice_dependent=2, slice_lf_across=2,
+                                 tile_lf_across=1)),
+    ("one_ctu_slices_10b", dict(slice_ctus=1, bit_depth=10, slice_dbk_vary=1)),
+]
+
+# bands of CTB rows, independent, nothing filtered across (the GPU's layouts)
+ROW_CASES = [
+    ("rows1_nowpp", dict(slice_ctus=4)),
+    ("rows2_wpp_dbk", dict(slice_ctus=8, wpp=1, slice_dbk_vary=1)),
+    ("crop_10b_wpp", dict(width=200, height=120, conf_right=6, conf_bottom=2, bit_depth=10, slice_ctus=7, wpp=1,
+                          slice_dbk_vary=1)),
+    ("ctb16_rows2", dict(log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2, slice_ctus=16)),
+    ("ctb64_partial_tools", dict(width=200, height=200, log2_ctb=6, bit_depth=10, slice_ctus=4, wpp=1,
+                                 tq_bypass=1, transform_skip=1, scaling_list=1, diff_cu_qp_delta_depth=2,
+                                 max_th_depth_intra=3)),
+    ("mono_rows", dict(chroma_format=0, slice_ctus=4, wpp=1)),
+]
+
+
+def params(over):
+    return S.SynthParams(**{**dict(width=128, height=96, wpp=0), **over})
+
+
+def checks_ok(img):
+    return all(c["term_ok"] and c["raw_start"] == c["raw_entry"] for c in img.checks)
+
+
+@pytest.mark.parametrize("name,over", PARSE_CASES, ids=[c[0] for c in PARSE_CASES])
+def test_oracle_decodes_slice_layouts(oracle_mod, name, over):
+    """Every segment's substreams end exactly at their entry points, with
+    end_of_slice_segment_flag on the segment's last CTU."""
+    p = params(over)
+    for seed in range(3):
+        item = S.picture_item(p, seed)
+        assert len(_nal_units(item)) > 1
+        img = oracle_mod.decode_heic(S.single_heic(p, seed=seed))
+        assert checks_ok(img), (name, seed)
+        assert img.y.shape == (p.height - p.conf_bottom, p.width - p.conf_right)
+
+
+def _split_decode(oracle_mod, p, item):
+    def dec(sp):
+        img = oracle_mod.decode_heic(S.single_heic(sp.params, nal=sp.nal))
+        assert checks_ok(img)
+        return img.y, img.cb, img.cr
+
+    return assemble(p, split_slices(p, item), dec)
+
+
+@pytest.mark.parametrize("name,over", ROW_CASES, ids=[c[0] for c in ROW_CASES])
+def test_oracle_slices_equal_standalone_slices(oracle_mod, name, over):
+    p = params(over)
+    for seed in range(3):
+        img = oracle_mod.decode_heic(S.single_heic(p, seed=seed))
+        want = _split_decode(oracle_mod, p, S.picture_item(p, seed))
+        for got, ref, c in zip((img.y, img.cb, img.cr), want, "YUV"):
+            if ref is None:
+                assert got is None
+                continue
+            assert got.shape == ref.shape, (name, seed, c)
+            assert int((got != ref).sum()) == 0, (name, seed, c)
+
+
+@pytest.mark.parametrize("across", [1, 2])
+def test_oracle_slices_loop_filter_across(oracle_mod, across):
+    """slice_loop_filter_across_slices_enabled_flag = 1 on every slice (1) or
+    on the even-numbered ones (2): the decode differs from the stand-alone
+    slices only within the loop filters' reach of a slice boundary whose lower
+    slice has the flag, and does differ there."""
+    base = dict(width=128, height=192, slice_ctus=4, wpp=1)  # 6 one-row slices
+    p0, p1 = params(base), params({**base, "slice_lf_across": across})
+    differs = 0
+    for seed in range(3):
+        img = oracle_mod.decode_heic(S.single_heic(p1, seed=seed))
+        assert checks_ok(img)
+        want = _split_decode(oracle_mod, p0, S.picture_item(p0, seed))
+        for got, ref, sub in zip((img.y, img.cb, img.cr), want, (1, 2, 2)):
+            near = np.zeros(ref.shape, bool)
+            reach = 4 if sub == 1 else 2
+            for k in range(1, 6):
+                if across == 2 and k % 2:
+                    continue  # odd-numbered slices keep their upper boundary unfiltered
+                e = k * 32 // sub
+                near[e - reach:e + reach, :] = True
+            diff = got != ref
+            assert not (diff & ~near).any(), seed
+            differs += int(diff.sum())
+    assert differs > 0
+
+
+def test_synth_writes_segments():
+    """slice_ctus splits the picture into segments of that many CTUs; a
+    single-NAL request for a multi-segment picture is refused."""
+    p = params(dict(slice_ctus=5))
+    assert len(_nal_units(S.picture_item(p, 0))) == 3
+    assert len(_nal_units(S.picture_item(params(dict()), 0))) == 1
+    with pytest.raises(ValueError):
+        S.picture(p, 0)
+
+
+@pytest.mark.parametrize("over,why", [
+    (dict(slice_ctus=5), "a slice starting inside a CTB row"),
+    (dict(slice_ctus=4, slice_lf_across=1), "slices with slice_loop_filter_across_slices_enabled_flag"),
+    (dict(slice_ctus=4, wpp=1, slice_dependent=1), "dependent slice segments"),
+    (dict(slice_ctus=8, tile_cols=2, tile_rows=1), "several slices together with HEVC tiles"),
+])
+def test_host_rejects_unsupported_slice_layouts(over, why):
+    import heif_amd as H
+
+    with pytest.raises(H.UnsupportedError, match=why):
+        H.HeifImage.parse(S.single_heic(params(over), seed=1))
+
+
+def test_host_rejects_segments_out_of_order():
+    import heif_amd as H
+    import struct
+
+    p = params(dict(slice_ctus=4))
+    nals = _nal_units(S.picture_item(p, 3))
+    swapped = b"".join(struct.pack(">I", len(n)) + n for n in (nals[1], nals[0], nals[2]))
+    data = S.single_heic(p, seed=3, nal=None)
+    good = S.picture_item(p, 3)
+    assert good in data
+    with pytest.raises(H.HeifGpuError) as e:
+        H.HeifImage.parse(data.replace(good, swapped))
+    assert not isinstance(e.value, H.UnsupportedError)
+
+
+# ------------------------------------------------------------ kernel emulation
+CSRC = os.path.join(os.path.dirname(__file__), "..", "heif_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def emu_check():
+    subprocess.run(["make", "-s", "-C", CSRC, "emu-fast"], check=True, capture_output=True)
+    return os.path.join(CSRC, "build", "emu_fast", "emu_check")
+
+
+@pytest.mark.parametrize("parse", ["lanes", "solo", "spread"])
+@pytest.mark.parametrize("name", ["rows2_wpp_dbk", "crop_10b_wpp", "ctb16_rows2"])
+def test_emulated_kernels_slices(emu_check, tmp_path, name, parse):
+    """The kernels' source compiled for the host decodes a picture of row
+    slices (one picture per slice) bit-exactly against the oracle."""
+    p = params(dict(ROW_CASES)[name])
+    path = tmp_path / "s.heic"
+    path.write_bytes(S.single_heic(p, seed=5))
+    r = subprocess.run([emu_check, str(path), "5"], capture_output=True, text=True, timeout=600,
+                       env={**os.environ, "HEIFGPU_PARSE": parse})
+    assert r.returncode == 0 and "EMU PARITY OK" in r.stdout + r.stderr, (r.stdout + r.stderr)[-2000:]
+
+
+# ------------------------------------------------------------------ GPU parity
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def H():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import heif_amd
+
+    return heif_amd
+
+
+def _planes(o):
+    return [None if t is None else t.cpu().numpy().astype(np.uint16) for t in (o.y, o.cb, o.cr)]
+
+
+def _assert_equal(got, img, tag):
+    for g, r, c in zip(got, (img.y, img.cb, img.cr), "YUV"):
+        if r is None:
+            assert g is None, tag
+            continue
+        assert g.shape == r.shape, (tag, c)
+        assert int((g != r).sum()) == 0, (tag, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parse", ["lanes", "solo", "spread"])
+def test_gpu_row_slices_bit_exact(H, oracle_mod, parse):
+    """Every row-slice case, two seeds each, one batch per format, checked
+    against the spec-literal oracle; plus a grid of sliced pictures batched
+    with a tiled one."""
+    ctx = H.DecodeContext(0)
+    for depth, chroma in ((8, 1), (10, 1), (8, 0)):
+        datas = []
+        for name, over in ROW_CASES:
+            p = params(over)
+            if (p.bit_depth, p.chroma_format) == (depth, chroma):
+                datas += [S.single_heic(p, seed=s) for s in (1, 2)]
+        if depth == 8 and chroma == 1:
+            datas.append(S.grid_heic(700, 500, params(dict(width=256, height=256, slice_ctus=16, wpp=1)), seed=4))
+            datas.append(S.single_heic(params(dict(width=256, height=128, tile_cols=2, tile_rows=2)), seed=4))
+        imgs = [H.HeifImage.parse(d) for d in datas]
+        b = ctx.prepare(imgs, parse=parse)
+        outs = ctx.alloc_outputs(imgs)
+        b.decode_async(outs)
+        assert not any(b.status()), (depth, chroma)
+        for k, (d, o) in enumerate(zip(datas, outs)):
+            _assert_equal(_planes(o), oracle_mod.decode_heic(d, with_checks=False), (depth, chroma, k))
+        b.free()
+    ctx.close()
