@@ -676,6 +676,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.xctx = mode == PARSE_SPREAD ? b->xctx.p : nullptr;
     // rows wrap round the lanes (waves) of a picture: the WPP context staging
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
+    a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = hb.bps;
     b->out_host.assign(n, OutImage{});

@@ -73,7 +73,19 @@ struct PicDesc {
     uint64_t coef_off;    // Coef index of row 0
     uint32_t row_off;     // index of row 0 in the per-row counters
     uint32_t tu_cap_row, coef_cap_row;
-    uint32_t pad;
+    uint32_t flags;       // PD_*
+    // A picture whose HEVC tiles / slices are filtered across their boundaries
+    // is decoded as sub-pictures (PD_CHILD: parse, transform and intra
+    // prediction only) put together into an assembly picture (PD_ASSEMBLY: no
+    // coded data; k_assemble copies its children's samples, QP / edge maps and
+    // SAO parameters in, then deblocking and SAO + output run on it whole).
+    int32_t org_x, org_y;     // PD_CHILD: luma position in its assembly
+    uint32_t child0, nchild;  // PD_ASSEMBLY: its children are pictures [child0, child0 + nchild)
+};
+
+enum : uint32_t {
+    PD_CHILD = 1u << 0,
+    PD_ASSEMBLY = 1u << 1,
 };
 
 struct OutImage {

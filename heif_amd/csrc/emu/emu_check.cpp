@@ -95,6 +95,7 @@ int main(int argc, char **argv) {
     a.xprog = xprog.data();
     a.xctx = xctx.data();
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
+    a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = bps;
     emu_rbsp(a);

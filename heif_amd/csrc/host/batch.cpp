@@ -62,6 +62,18 @@ int max_lane_rows() {
     return cap;
 }
 
+// a slice's header values of a picture
+void slice_values(PicDesc &pd, const ParamSet &ps, const SliceSegmentHeader &sh) {
+    pd.slice_qp = 26 + ps.pps.init_qp_minus26 + sh.slice_qp_delta;
+    pd.cb_qp_off = sh.slice_cb_qp_offset;
+    pd.cr_qp_off = sh.slice_cr_qp_offset;
+    pd.sao_luma = sh.slice_sao_luma_flag;
+    pd.sao_chroma = sh.slice_sao_chroma_flag;
+    pd.dbk_disabled = sh.slice_deblocking_filter_disabled_flag;
+    pd.beta_off = sh.slice_beta_offset_div2;
+    pd.tc_off = sh.slice_tc_offset_div2;
+}
+
 void fill_scaling(const ParamSet &ps, uint8_t *blk) {
     for (int sid = 0; sid < 4; ++sid) {
         int n = 4 << sid;
@@ -78,6 +90,66 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
     HostBatch hb;
     std::vector<std::vector<uint8_t>> seq_keys, sf_keys;  // SeqParams: PPS + picture geometry; ScalingFactor: PPS
     std::vector<uint32_t> sf_offs;
+    // SeqParams index of (PPS, picture geometry); one ScalingFactor block per PPS
+    auto seq_of = [&](const ParamSet &ps, SeqParams base) -> uint32_t {
+        std::vector<uint8_t> key = ps.key;
+        const int32_t g[7] = {base.width, base.height, base.conf_l, base.conf_t, base.out_w, base.out_h,
+                              int32_t(base.flags)};
+        const uint8_t *gb = reinterpret_cast<const uint8_t *>(g);
+        key.insert(key.end(), gb, gb + sizeof(g));
+        auto it = std::find(seq_keys.begin(), seq_keys.end(), key);
+        if (it != seq_keys.end()) return uint32_t(it - seq_keys.begin());
+        seq_keys.push_back(key);
+        auto sf = std::find(sf_keys.begin(), sf_keys.end(), ps.key);
+        if (sf == sf_keys.end()) {
+            sf_keys.push_back(ps.key);
+            sf_offs.push_back(uint32_t(hb.sf.size()));
+            hb.sf.resize(hb.sf.size() + kSfBlockBytes);
+            fill_scaling(ps, hb.sf.data() + sf_offs.back());
+            sf = sf_keys.end() - 1;
+        }
+        base.sf_off = sf_offs[size_t(sf - sf_keys.begin())];
+        hb.seqs.push_back(base);
+        return uint32_t(hb.seqs.size() - 1);
+    };
+    // the work arenas of a picture (coded: it is parsed and reconstructed; an
+    // assembly only holds samples, maps and SAO parameters), then the batch maxima
+    auto add_picture = [&](PicDesc &pd, bool coded) {
+        const SeqParams &sq = hb.seqs[pd.seq];
+        const int ctb = 1 << sq.log2_ctb;
+        const int wctb = (sq.width + ctb - 1) / ctb, hctb = (sq.height + ctb - 1) / ctb;
+        const int w4 = (sq.width + 3) >> 2, h4 = (sq.height + 3) >> 2, w8 = (sq.width + 7) >> 3;
+        const uint64_t samples = uint64_t(sq.width) * sq.height * (sq.chroma_format ? 3 : 2) / 2;
+        pd.recon_off = hb.recon_bytes;
+        hb.recon_bytes += (samples * uint64_t(hb.bps) + 255) & ~uint64_t(255);
+        pd.map_off = hb.map_bytes;
+        hb.map_bytes += (uint64_t(2) * w4 * h4 + uint64_t(hctb) * w8 + 255) & ~uint64_t(255);
+        pd.sao_off = hb.sao_n;
+        hb.sao_n += uint64_t(wctb) * hctb;
+        pd.resid_off = hb.resid_elems;
+        pd.row_off = hb.rows;
+        pd.tu_off = hb.tu_n;
+        pd.coef_off = hb.coef_n;
+        hb.pics.push_back(pd);
+        hb.pic_image.push_back(pd.image);
+        hb.max_w = std::max(hb.max_w, sq.width);
+        hb.max_wctb = std::max(hb.max_wctb, wctb);
+        hb.max_log2ctb = std::max(hb.max_log2ctb, int(sq.log2_ctb));
+        if (!coded) return;
+        PicDesc &p = hb.pics.back();
+        hb.resid_elems += (samples + 127) & ~uint64_t(127);
+        hb.rows += uint32_t(hctb);
+        // worst case per CTB row: every 8x8 CU split into four 4x4 luma TBs + 2 chroma TBs
+        p.tu_cap_row = uint32_t(wctb * (ctb / 8) * (ctb / 8) * 6 + 64);  // + staging trash slot / slack
+        p.coef_cap_row = uint32_t(wctb * ctb * ctb * 3 / 2 + 64);  // + staging trash slot / slack
+        hb.tu_n += uint64_t(p.tu_cap_row) * hctb;
+        hb.coef_n += uint64_t(p.coef_cap_row) * hctb;
+        hb.max_rows = std::max(hb.max_rows, hctb);
+        const bool wpp = (sq.flags & SP_WPP) != 0;
+        hb.lane_rows = std::max(hb.lane_rows, wpp ? std::min(hctb, max_lane_rows()) : 1);
+        if (wpp && hctb > max_lane_rows()) hb.wpp_ring = 1;
+        if (wpp) hb.max_wpp_rows = std::max(hb.max_wpp_rows, hctb);
+    };
     for (size_t i = 0; i < n; ++i) {
         const ParsedImage &im = *imgs[i];
         const SequenceParameterSet &s0 = im.params[0].sps;
@@ -123,6 +195,17 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                     subs_of.push_back({0, r0, pw, r1, k, 0, tj.segs[k].sh.num_entry_point_offsets + 1, false});
                 }
             }
+            // Loop filters across the sub-pictures' boundaries (tiles with
+            // loop_filter_across_tiles_enabled_flag, slices with
+            // slice_loop_filter_across_slices_enabled_flag; heic_image.cpp takes
+            // all-or-none): the sub-pictures are children of an assembly picture
+            // of the whole picture, which k_assemble puts together before the
+            // loop filters run on it (desc.hpp).
+            const bool assemble =
+                subs_of.size() > 1 && (ps.pps.tiles_enabled_flag ? ps.pps.loop_filter_across_tiles_enabled_flag
+                                                                 : tj.segs[1].sh.slice_loop_filter_across_slices_enabled_flag);
+            const uint32_t child0 = uint32_t(hb.pics.size());
+            const int32_t grid_x = int32_t((t % im.cols) * im.tile_width), grid_y = int32_t((t / im.cols) * im.tile_height);
             for (const Sub &su : subs_of) {
                 const SliceSeg &sg = tj.segs[su.seg];
                 std::vector<uint32_t> starts{sg.sh.slice_data_raw_offset};  // the segment's substreams
@@ -146,36 +229,8 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                     vis_dy = vy0 - ps.sps.conf_win_top;
                     if (su.subset_end) base.flags |= SP_SUBSET_END;
                 }
-                std::vector<uint8_t> key = ps.key;
-                {
-                    const int32_t g[7] = {base.width, base.height, base.conf_l, base.conf_t, base.out_w, base.out_h,
-                                          int32_t(base.flags)};
-                    const uint8_t *gb = reinterpret_cast<const uint8_t *>(g);
-                    key.insert(key.end(), gb, gb + sizeof(g));
-                }
-                uint32_t seq;
-                auto it = std::find(seq_keys.begin(), seq_keys.end(), key);
-                if (it == seq_keys.end()) {
-                    seq = uint32_t(seq_keys.size());
-                    seq_keys.push_back(key);
-                    auto sf = std::find(sf_keys.begin(), sf_keys.end(), ps.key);  // one ScalingFactor block per PPS
-                    if (sf == sf_keys.end()) {
-                        sf_keys.push_back(ps.key);
-                        sf_offs.push_back(uint32_t(hb.sf.size()));
-                        hb.sf.resize(hb.sf.size() + kSfBlockBytes);
-                        fill_scaling(ps, hb.sf.data() + sf_offs.back());
-                        sf = sf_keys.end() - 1;
-                    }
-                    base.sf_off = sf_offs[size_t(sf - sf_keys.begin())];
-                    hb.seqs.push_back(base);
-                } else {
-                    seq = uint32_t(it - seq_keys.begin());
-                }
+                const uint32_t seq = seq_of(ps, base);
                 const SeqParams &sq = hb.seqs[seq];
-                const int ctb = 1 << sq.log2_ctb;
-                const int wctb = (sq.width + ctb - 1) / ctb, hctb = (sq.height + ctb - 1) / ctb;
-                const int w4 = (sq.width + 3) >> 2, h4 = (sq.height + 3) >> 2;
-                const uint64_t samples = uint64_t(sq.width) * sq.height * (sq.chroma_format ? 3 : 2) / 2;
                 PicDesc pd{};
                 pd.bits_off = hb.bits_size;
                 pd.sub_first = uint32_t(hb.subs.size());
@@ -194,48 +249,40 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                 }
                 hb.subs.push_back(pd.bits_len);
                 hb.bits_size = (hb.bits_size + pd.bits_len + 63) & ~size_t(63);
+                const int hctb = (sq.height + (1 << sq.log2_ctb) - 1) >> sq.log2_ctb;
                 if ((sq.flags & SP_WPP) && int(pd.n_sub) != hctb)
                     throw HeifError("WPP picture without one entry point per CTB row");
                 pd.seq = seq;
-                pd.slice_qp = 26 + ps.pps.init_qp_minus26 + sg.sh.slice_qp_delta;
-                pd.cb_qp_off = sg.sh.slice_cb_qp_offset;
-                pd.cr_qp_off = sg.sh.slice_cr_qp_offset;
-                pd.sao_luma = sg.sh.slice_sao_luma_flag;
-                pd.sao_chroma = sg.sh.slice_sao_chroma_flag;
-                pd.dbk_disabled = sg.sh.slice_deblocking_filter_disabled_flag;
-                pd.beta_off = sg.sh.slice_beta_offset_div2;
-                pd.tc_off = sg.sh.slice_tc_offset_div2;
+                slice_values(pd, ps, sg.sh);
                 pd.image = uint32_t(i);
-                pd.out_x = int32_t((t % im.cols) * im.tile_width) + vis_dx;
-                pd.out_y = int32_t((t / im.cols) * im.tile_height) + vis_dy;
-                pd.recon_off = hb.recon_bytes;
-                hb.recon_bytes += (samples * uint64_t(hb.bps) + 255) & ~uint64_t(255);
-                pd.resid_off = hb.resid_elems;
-                hb.resid_elems += (samples + 127) & ~uint64_t(127);
-                pd.map_off = hb.map_bytes;
-                const int w8 = (sq.width + 7) >> 3;
-                hb.map_bytes += (uint64_t(2) * w4 * h4 + uint64_t(hctb) * w8 + 255) & ~uint64_t(255);
-                pd.sao_off = hb.sao_n;
-                hb.sao_n += uint64_t(wctb) * hctb;
-                pd.row_off = hb.rows;
-                hb.rows += uint32_t(hctb);
-                // worst case per CTB row: every 8x8 CU split into four 4x4 luma TBs + 2 chroma TBs
-                pd.tu_cap_row = uint32_t(wctb * (ctb / 8) * (ctb / 8) * 6 + 64);  // + staging trash slot / slack
-                pd.coef_cap_row = uint32_t(wctb * ctb * ctb * 3 / 2 + 64);  // + staging trash slot / slack
-                pd.tu_off = hb.tu_n;
-                hb.tu_n += uint64_t(pd.tu_cap_row) * hctb;
-                pd.coef_off = hb.coef_n;
-                hb.coef_n += uint64_t(pd.coef_cap_row) * hctb;
-                hb.pics.push_back(pd);
-                hb.pic_image.push_back(uint32_t(i));
-                hb.max_w = std::max(hb.max_w, sq.width);
-                hb.max_wctb = std::max(hb.max_wctb, wctb);
-                hb.max_rows = std::max(hb.max_rows, hctb);
-                hb.max_log2ctb = std::max(hb.max_log2ctb, int(sq.log2_ctb));
-                const bool wpp = (sq.flags & SP_WPP) != 0;
-                hb.lane_rows = std::max(hb.lane_rows, wpp ? std::min(hctb, max_lane_rows()) : 1);
-                if (wpp && hctb > max_lane_rows()) hb.wpp_ring = 1;
-                if (wpp) hb.max_wpp_rows = std::max(hb.max_wpp_rows, hctb);
+                pd.out_x = grid_x + vis_dx;
+                pd.out_y = grid_y + vis_dy;
+                if (assemble) {
+                    pd.flags |= PD_CHILD;
+                    pd.org_x = su.x0 * pctb;
+                    pd.org_y = su.y0 * pctb;
+                }
+                add_picture(pd, true);
+            }
+            if (assemble) {  // the whole picture: no coded data, loop filters and output
+                PicDesc pd{};
+                pd.seq = seq_of(ps, make_seq(ps, 0));
+                pd.bits_off = hb.bits_size;
+                pd.sub_first = uint32_t(hb.subs.size());
+                hb.subs.push_back(0);  // n_sub = 0: k_rbsp sees only the (empty) end entry
+                slice_values(pd, ps, tj.segs[0].sh);  // the deblocking values (all alike: heic_image.cpp)
+                for (const SliceSeg &sg : tj.segs) {
+                    pd.sao_luma |= sg.sh.slice_sao_luma_flag;
+                    pd.sao_chroma |= sg.sh.slice_sao_chroma_flag;
+                }
+                pd.image = uint32_t(i);
+                pd.out_x = grid_x;
+                pd.out_y = grid_y;
+                pd.flags = PD_ASSEMBLY;
+                pd.child0 = child0;
+                pd.nchild = uint32_t(subs_of.size());
+                add_picture(pd, false);
+                hb.has_assembly = true;
             }
         }
     }

@@ -30,6 +30,7 @@ struct HostBatch {
     int max_w = 0, max_wctb = 0, max_rows = 0, max_log2ctb = 4, bps = 0, chroma = -1;
     int lane_rows = 1, wpp_ring = 0;  // k_parse_lanes geometry (BatchArgs::lane_rows / wpp_ring)
     int max_wpp_rows = 0;             // CTB rows of the tallest WPP picture (k_parse_solo's context staging)
+    bool has_assembly = false;        // some picture is a PD_ASSEMBLY (BatchArgs::has_assembly)
 };
 
 // Throws HeifError / UnsupportedError.  Only grid tiles k (row-major) with

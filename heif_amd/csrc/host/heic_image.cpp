@@ -18,12 +18,9 @@ void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p
     if (s.separate_colour_plane_flag) throw UnsupportedError("separate_colour_plane_flag");
     if (s.bit_depth_luma_minus8 != s.bit_depth_chroma_minus8) throw UnsupportedError("luma/chroma bit depth differ");
     if (s.range_extension_tools || p.range_extension_tools) throw UnsupportedError("range-extension coding tools");
-    // HEVC tiles decode as independent sub-pictures (batch.cpp) when no loop
-    // filter crosses a tile boundary
+    // HEVC tiles decode as sub-pictures (batch.cpp)
     if (p.tiles_enabled_flag && p.entropy_coding_sync_enabled_flag)
         throw UnsupportedError("HEVC tiles together with WPP");
-    if (p.tiles_enabled_flag && p.loop_filter_across_tiles_enabled_flag)
-        throw UnsupportedError("HEVC tiles with loop_filter_across_tiles_enabled_flag");
     if (s.pic_width_in_luma_samples > 8192 || s.pic_height_in_luma_samples > 8192)
         throw UnsupportedError("picture larger than 8192");
     if (s.pic_width_in_luma_samples % (1 << s.log2_min_luma_coding_block_size) ||
@@ -34,9 +31,10 @@ void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p
 // The slice segments of a picture: in order and covering it (7.4.7.1), and
 // each with one entry point per tile / WPP row.  The GPU path decodes several
 // slices as one sub-picture per slice (batch.cpp), so they must be
-// independent, start at a CTB row and keep the loop filters inside
-// (slice_loop_filter_across_slices_enabled_flag 0); HEVC tiles must come with
-// a single slice.
+// independent and start at a CTB row; HEVC tiles must come with a single
+// slice.  Loop filtering across the slices' boundaries is either off for all
+// (independent sub-pictures) or on for all, with one set of deblocking values
+// (sub-pictures of an assembly filtered whole).
 void check_segments(const TileJob &job, const ParamSet &ps) {
     const SequenceParameterSet &sps = ps.sps;
     const PictureParameterSet &pps = ps.pps;
@@ -50,8 +48,15 @@ void check_segments(const TileJob &job, const ParamSet &ps) {
         if (sh.dependent_slice_segment_flag) throw UnsupportedError("dependent slice segments");
         if (pps.tiles_enabled_flag) throw UnsupportedError("several slices together with HEVC tiles");
         if (sh.slice_segment_address % pw) throw UnsupportedError("a slice starting inside a CTB row");
-        if (sh.slice_loop_filter_across_slices_enabled_flag)
-            throw UnsupportedError("slices with slice_loop_filter_across_slices_enabled_flag");
+        const SliceSegmentHeader &s1 = job.segs[1].sh;
+        if (sh.slice_loop_filter_across_slices_enabled_flag != s1.slice_loop_filter_across_slices_enabled_flag)
+            throw UnsupportedError("slices filtered across some slice boundaries only");
+        const SliceSegmentHeader &s0 = job.segs[0].sh;
+        if (s1.slice_loop_filter_across_slices_enabled_flag &&
+            (sh.slice_deblocking_filter_disabled_flag != s0.slice_deblocking_filter_disabled_flag ||
+             sh.slice_beta_offset_div2 != s0.slice_beta_offset_div2 ||
+             sh.slice_tc_offset_div2 != s0.slice_tc_offset_div2))
+            throw UnsupportedError("slices filtered across their boundaries with different deblocking values");
     }
     const size_t ntiles = (ps.col_bd.size() - 1) * (ps.row_bd.size() - 1);
     if (pps.tiles_enabled_flag && size_t(job.segs[0].sh.num_entry_point_offsets) + 1 != ntiles)

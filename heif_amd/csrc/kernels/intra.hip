@@ -526,6 +526,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
     const int pic = a.pic0 + blockIdx.x;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const PicDesc pd = a.pics[pic];
+    if (pd.flags & PD_ASSEMBLY) return;  // no coded data of its own (uniform: the whole workgroup leaves)
     const SeqParams sp = a.seqs[pd.seq];
     const int W = sp.width, H = sp.height, log2ctb = sp.log2_ctb;
     const int wctb = (W + (1 << log2ctb) - 1) >> log2ctb, hctb = (H + (1 << log2ctb) - 1) >> log2ctb;

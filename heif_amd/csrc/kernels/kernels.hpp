@@ -7,7 +7,8 @@
 //                   (slice.rs:206-256 + todo!()s)
 //   2. k_transform  dequant (8.6.2-3) + inverse DST/DCT (8.6.4) → residuals
 //   3. k_intra      intra prediction (8.4.4.2) + reconstruction (8.6.7)
-//   4. k_deblock    vertical then horizontal edges (8.7.2), in place
+//   4. k_deblock    vertical then horizontal edges (8.7.2), in place (after
+//                   k_assemble puts sub-picture assemblies together, if any)
 //   5. k_sao_out    SAO (8.7.3) + crop + grid placement into the caller's planes
 #pragma once
 #include "../common/desc.hpp"
@@ -56,6 +57,7 @@ struct BatchArgs {
     int solo_waves;            // k_parse_solo waves per workgroup (solo_waves_for(lane_rows))
     uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
+    int has_assembly;          // some picture is PD_ASSEMBLY (launch_deblock runs k_assemble first)
 };
 
 // k_ycbcr_rgb (color.hip): one decoded image → interleaved RGB8, rotated

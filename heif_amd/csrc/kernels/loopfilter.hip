@@ -90,12 +90,65 @@ __device__ void luma_segment(Pel *q, int sx, int sk, int qpP, int qpQ, bool nofp
 
 }  // namespace
 
+// Assembly pictures (PD_ASSEMBLY, see desc.hpp): each child's samples, QpY /
+// edge-flag maps and SAO parameters copied to its position in the assembly
+// (a child whose slice has SAO off wrote no parameters: zero them).  Runs
+// before deblocking; one workgroup row per picture, the others leave at once.
+template <typename Pel>
+__global__ void __launch_bounds__(256) k_assemble(BatchArgs a) {
+    const int pic = a.pic0 + blockIdx.y;
+    const PicDesc pd = a.pics[pic];
+    if (!(pd.flags & PD_ASSEMBLY)) return;
+    const SeqParams sp = a.seqs[pd.seq];
+    const int W = sp.width, H = sp.height, w4 = (W + 3) >> 2, h4 = (H + 3) >> 2;
+    const int wctb = (W + (1 << sp.log2_ctb) - 1) >> sp.log2_ctb;
+    const int cw = sp.chroma_format ? W >> 1 : 0, ch = sp.chroma_format ? H >> 1 : 0;
+    Pel *dY = reinterpret_cast<Pel *>(a.recon + pd.recon_off);
+    uint8_t *dmap = a.maps + pd.map_off;
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
+    for (uint32_t c = 0; c < pd.nchild; ++c) {
+        const PicDesc cd = a.pics[pd.child0 + c];
+        const SeqParams cs = a.seqs[cd.seq];
+        const int cW = cs.width, cH = cs.height, cw4 = (cW + 3) >> 2, ch4 = (cH + 3) >> 2;
+        const int ccw = cs.chroma_format ? cW >> 1 : 0, cch = cs.chroma_format ? cH >> 1 : 0;
+        const Pel *sY = reinterpret_cast<const Pel *>(a.recon + cd.recon_off);
+        // samples: Y then Cb, Cr (origins are CTB-aligned, so chroma at org / 2)
+        const int nl = cW * cH, nc = ccw * cch;
+        for (int t = tid; t < nl + 2 * nc; t += nth) {
+            if (t < nl) {
+                const int x = t % cW, y = t / cW;
+                dY[(size_t)(cd.org_y + y) * W + cd.org_x + x] = sY[t];
+            } else {
+                const int u = t - nl, k = u / nc, v = u % nc, x = v % ccw, y = v / ccw;
+                dY[(size_t)W * H + (size_t)k * cw * ch + (size_t)((cd.org_y >> 1) + y) * cw + (cd.org_x >> 1) + x] = sY[t];
+            }
+        }
+        // QpY and edge flags (4x4 units), then SAO parameters (CTBs)
+        const uint8_t *smap = a.maps + cd.map_off;
+        const int nm = cw4 * ch4;
+        for (int t = tid; t < 2 * nm; t += nth) {
+            const int k = t / nm, v = t % nm, x = v % cw4, y = v / cw4;
+            dmap[(size_t)k * w4 * h4 + (size_t)((cd.org_y >> 2) + y) * w4 + (cd.org_x >> 2) + x] = smap[t];
+        }
+        const int cwctb = (cW + (1 << cs.log2_ctb) - 1) >> cs.log2_ctb;
+        const int chctb = (cH + (1 << cs.log2_ctb) - 1) >> cs.log2_ctb;
+        const bool sao = cd.sao_luma || cd.sao_chroma;
+        for (int t = tid; t < cwctb * chctb * 8; t += nth) {
+            const int b = t >> 3, x = b % cwctb, y = b / cwctb;
+            uint32_t *dst = reinterpret_cast<uint32_t *>(
+                a.sao + pd.sao_off + (size_t)((cd.org_y >> sp.log2_ctb) + y) * wctb + (cd.org_x >> sp.log2_ctb) + x);
+            dst[t & 7] = sao ? reinterpret_cast<const uint32_t *>(a.sao + cd.sao_off + b)[t & 7] : 0u;
+        }
+    }
+    (void)h4;
+}
+
 // VERT: edges between columns (x-1 | x); otherwise between rows.
 template <typename Pel, bool VERT>
 __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
     const int pic = a.pic0 + blockIdx.y;
     const PicDesc pd = a.pics[pic];
-    if (pd.dbk_disabled) return;
+    if (pd.dbk_disabled || (pd.flags & PD_CHILD)) return;  // a child is filtered as part of its assembly
     const SeqParams sp = a.seqs[pd.seq];
     const int W = sp.width, H = sp.height;
     const int w4 = (W + 3) >> 2, h4 = (H + 3) >> 2;
@@ -199,6 +252,7 @@ template <typename Pel>
 __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
     const int pic = a.pic0 + blockIdx.y;
     const PicDesc pd = a.pics[pic];
+    if (pd.flags & PD_CHILD) return;  // output through its assembly
     const SeqParams sp = a.seqs[pd.seq];
     const OutImage oi = a.outs[pd.image];
     const int W = sp.width, H = sp.height, log2ctb = sp.log2_ctb;
@@ -264,6 +318,10 @@ __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
 
 #if defined(HG_HOST_EMU)
 void emu_deblock(const BatchArgs &a) {
+    if (a.has_assembly) {
+        if (a.bytes_per_sample == 1) emu_launch(k_assemble<uint8_t>, 1, a.n_pics, 1, a, true);
+        else emu_launch(k_assemble<uint16_t>, 1, a.n_pics, 1, a, true);
+    }
     if (a.bytes_per_sample == 1) {
         emu_launch(k_deblock<uint8_t, true>, 1, a.n_pics, 1, a, true);
         emu_launch(k_deblock<uint8_t, false>, 1, a.n_pics, 1, a, true);
@@ -279,6 +337,10 @@ void emu_sao_out(const BatchArgs &a) {
 #else
 hipError_t launch_deblock(const BatchArgs &a, hipStream_t s) {
     dim3 grid(64, a.n_pics), block(256);
+    if (a.has_assembly) {  // the assemblies' children are reconstructed: put them together first
+        if (a.bytes_per_sample == 1) hipLaunchKernelGGL(k_assemble<uint8_t>, grid, block, 0, s, a);
+        else hipLaunchKernelGGL(k_assemble<uint16_t>, grid, block, 0, s, a);
+    }
     if (a.bytes_per_sample == 1) {
         hipLaunchKernelGGL((k_deblock<uint8_t, true>), grid, block, 0, s, a);
         hipLaunchKernelGGL((k_deblock<uint8_t, false>), grid, block, 0, s, a);

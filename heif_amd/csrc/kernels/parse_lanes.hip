@@ -1525,6 +1525,7 @@ HG_HD inline bool ctu_ready(const Lane &L, const LanePic &P, const Env &E) { ret
 HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a, int pic, int row, int lane0,
                             int cap) {
     const PicDesc &pd = a.pics[pic];
+    if (pd.flags & PD_ASSEMBLY) return false;  // no coded data of its own
     const SeqParams &sp = a.seqs[pd.seq];
     const int log2ctb = sp.log2_ctb, ctb = 1 << log2ctb;
     const int hctb = (sp.height + ctb - 1) >> log2ctb;
@@ -1658,8 +1659,10 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
         order.resize((size_t)((n + ppw - 1) / ppw) * ppw, ~0u);
         return ppw;
     }
-    std::vector<uint32_t> by_size((size_t)n);
-    for (int i = 0; i < n; ++i) by_size[(size_t)i] = (uint32_t)i;
+    std::vector<uint32_t> by_size;  // assembly pictures have nothing to parse: no slot
+    for (int i = 0; i < n; ++i)
+        if (!(pics[i].flags & PD_ASSEMBLY)) by_size.push_back((uint32_t)i);
+    n = (int)by_size.size();
     if (cost)
         std::stable_sort(by_size.begin(), by_size.end(), [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
     else

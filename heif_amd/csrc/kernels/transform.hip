@@ -78,6 +78,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     __syncthreads();
     const int pic = a.pic0 + blockIdx.y, row = blockIdx.x;
     const PicDesc pd = a.pics[pic];
+    if (pd.flags & PD_ASSEMBLY) return;  // no coded data of its own
     const SeqParams sp = a.seqs[pd.seq];
     const int hctb = (sp.height + (1 << sp.log2_ctb) - 1) >> sp.log2_ctb;
     if (row >= hctb) return;

@@ -15,9 +15,11 @@ on every substream end (the per-substream checks) pins context selection
 for the other layouts (mid-row slices, dependent segments, slices with tiles).
 
 GPU: each slice of such a picture is decoded as its own picture
-(heif_amd/csrc/host/batch.cpp); dependent segments, slices starting inside a
-CTB row, loop filtering across slices and slices with HEVC tiles are
-HEIFGPU_E_UNSUPPORTED.
+(heif_amd/csrc/host/batch.cpp); when every slice is filtered across its
+upper boundary (one set of deblocking values) the slices are children of an
+assembly picture filtered whole (desc.hpp PD_ASSEMBLY).  Dependent segments,
+slices starting inside a CTB row, filtering across some slice boundaries only
+and slices with HEVC tiles are HEIFGPU_E_UNSUPPORTED.
 """
 import os
 import subprocess
@@ -141,7 +143,8 @@ def test_synth_writes_segments():
 
 @pytest.mark.parametrize("over,why", [
     (dict(slice_ctus=5), "a slice starting inside a CTB row"),
-    (dict(slice_ctus=4, slice_lf_across=1), "slices with slice_loop_filter_across_slices_enabled_flag"),
+    (dict(slice_ctus=4, slice_lf_across=2), "slices filtered across some slice boundaries only"),
+    (dict(slice_ctus=4, slice_lf_across=1, slice_dbk_vary=1), "with different deblocking values"),
     (dict(slice_ctus=4, wpp=1, slice_dependent=1), "dependent slice segments"),
     (dict(slice_ctus=8, tile_cols=2, tile_rows=1), "several slices together with HEVC tiles"),
 ])
@@ -178,11 +181,13 @@ def emu_check():
 
 
 @pytest.mark.parametrize("parse", ["lanes", "solo", "spread"])
-@pytest.mark.parametrize("name", ["rows2_wpp_dbk", "crop_10b_wpp", "ctb16_rows2"])
-def test_emulated_kernels_slices(emu_check, tmp_path, name, parse):
+@pytest.mark.parametrize("name,across", [("rows2_wpp_dbk", 0), ("crop_10b_wpp", 0), ("ctb16_rows2", 0),
+                                         ("ctb16_rows2", 1), ("mono_rows", 1)])
+def test_emulated_kernels_slices(emu_check, tmp_path, name, across, parse):
     """The kernels' source compiled for the host decodes a picture of row
-    slices (one picture per slice) bit-exactly against the oracle."""
-    p = params(dict(ROW_CASES)[name])
+    slices (one picture per slice; filtered across: children of an assembly)
+    bit-exactly against the oracle."""
+    p = params({**dict(ROW_CASES)[name], "slice_lf_across": across})
     path = tmp_path / "s.heic"
     path.write_bytes(S.single_heic(p, seed=5))
     r = subprocess.run([emu_check, str(path), "5"], capture_output=True, text=True, timeout=600,
@@ -219,16 +224,19 @@ def _assert_equal(got, img, tag):
 @pytest.mark.gpu
 @pytest.mark.parametrize("parse", ["lanes", "solo", "spread"])
 def test_gpu_row_slices_bit_exact(H, oracle_mod, parse):
-    """Every row-slice case, two seeds each, one batch per format, checked
-    against the spec-literal oracle; plus a grid of sliced pictures batched
-    with a tiled one."""
+    """Every row-slice case, with and without filtering across slices, two
+    seeds each, one batch per format, checked against the spec-literal
+    oracle; plus a grid of sliced pictures batched with a tiled one."""
     ctx = H.DecodeContext(0)
     for depth, chroma in ((8, 1), (10, 1), (8, 0)):
         datas = []
         for name, over in ROW_CASES:
-            p = params(over)
-            if (p.bit_depth, p.chroma_format) == (depth, chroma):
-                datas += [S.single_heic(p, seed=s) for s in (1, 2)]
+            for across in (0, 1):
+                p = params({**over, "slice_lf_across": across})
+                if across and p.slice_dbk_vary:
+                    continue  # different deblocking values per slice: unsupported when filtered across
+                if (p.bit_depth, p.chroma_format) == (depth, chroma):
+                    datas += [S.single_heic(p, seed=s) for s in (1, 2)]
         if depth == 8 and chroma == 1:
             datas.append(S.grid_heic(700, 500, params(dict(width=256, height=256, slice_ctus=16, wpp=1)), seed=4))
             datas.append(S.single_heic(params(dict(width=256, height=128, tile_cols=2, tile_rows=2)), seed=4))

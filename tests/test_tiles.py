@@ -13,8 +13,10 @@ the bitstream), and the untiled decode is pinned by the reference's fixtures
 filters' reach of a tile boundary.
 
 GPU: the host decodes a tiled picture as one picture per tile
-(heif_amd/csrc/host/batch.cpp) and rejects loop_filter_across_tiles = 1 and
-tiles together with WPP (HEIFGPU_E_UNSUPPORTED).
+(heif_amd/csrc/host/batch.cpp); with loop_filter_across_tiles = 1 the tiles
+are children of an assembly picture that k_assemble puts together before the
+loop filters run on it whole (desc.hpp PD_ASSEMBLY).  Tiles together with WPP
+are HEIFGPU_E_UNSUPPORTED.
 """
 import os
 import subprocess
@@ -132,21 +134,17 @@ def test_synth_tiled_stream_layout():
         S.picture(params(dict(tile_cols=2, tile_rows=1, tile_uniform=0, tile_col_w=(4,))), 0)
 
 
-def test_host_accepts_tiles_rejects_across_and_wpp(oracle_mod):
-    """Host parse: tiles without loop filtering across them are accepted;
-    loop_filter_across_tiles = 1 and tiles + WPP are valid streams outside
-    this path (UnsupportedError / HEIFGPU_E_UNSUPPORTED), which the oracle
-    still decodes (across) or also refuses (tiles + WPP)."""
+def test_host_accepts_tiles_rejects_tiles_with_wpp(oracle_mod):
+    """Host parse: tiles with and without loop filtering across them are
+    accepted; tiles + WPP is a valid stream outside this path
+    (UnsupportedError / HEIFGPU_E_UNSUPPORTED) which the oracle also refuses."""
     import heif_amd as H
     import ps_writer as W
 
     p = params(dict(tile_cols=2, tile_rows=2))
     inf = H.HeifImage.parse(S.single_heic(p, seed=1)).info
     assert (inf.width, inf.height) == (128, 96)
-    across = S.single_heic(params(dict(tile_cols=2, tile_rows=2), across=1), seed=1)
-    with pytest.raises(H.UnsupportedError):
-        H.HeifImage.parse(across)
-    oracle_mod.decode_heic(across)
+    H.HeifImage.parse(S.single_heic(params(dict(tile_cols=2, tile_rows=2), across=1), seed=1))
     vps, sps, _ = S.parameter_sets(p)
     pps = W.pps(wpp=1, tiles=dict(cols=2, rows=2))
     both = S.single_heic(p, param_sets=(vps, sps, pps), nal=S.picture(p, 1))
@@ -183,11 +181,13 @@ def emu_check():
 
 
 @pytest.mark.parametrize("parse", ["lanes", "solo", "spread"])
-@pytest.mark.parametrize("name", ["crop_4x3_explicit_10b", "ctb64_partial_tools", "mono_1ctb_tiles"])
-def test_emulated_kernels_tiled(emu_check, tmp_path, name, parse):
+@pytest.mark.parametrize("name,across", [("crop_4x3_explicit_10b", 0), ("ctb64_partial_tools", 0),
+                                         ("mono_1ctb_tiles", 0), ("crop_4x3_explicit_10b", 1), ("u2x2", 1)])
+def test_emulated_kernels_tiled(emu_check, tmp_path, name, across, parse):
     """The kernels' source compiled for the host decodes tiled pictures (one
-    picture per tile) bit-exactly against the spec-literal oracle."""
-    p = params(dict(CASES)[name])
+    picture per tile; with loop filtering across tiles, children of an
+    assembly) bit-exactly against the spec-literal oracle."""
+    p = params(dict(CASES)[name], across=across)
     path = tmp_path / "t.heic"
     path.write_bytes(S.single_heic(p, seed=7))
     r = subprocess.run([emu_check, str(path), "5"], capture_output=True, text=True, timeout=600,
@@ -224,16 +224,17 @@ def _assert_equal(got, img, tag):
 @pytest.mark.gpu
 @pytest.mark.parametrize("parse", ["lanes", "solo", "spread"])
 def test_gpu_tiled_pictures_bit_exact(H, oracle_mod, parse):
-    """Every tile case, two seeds each, in one batch per parse mode and format
-    (8-bit 4:2:0, 10-bit 4:2:0, 8-bit 4:0:0), checked against the
-    spec-literal oracle."""
+    """Every tile case, with and without loop filtering across tiles, two
+    seeds each, in one batch per parse mode and format (8-bit 4:2:0, 10-bit
+    4:2:0, 8-bit 4:0:0), checked against the spec-literal oracle."""
     ctx = H.DecodeContext(0)
     for depth, chroma in ((8, 1), (10, 1), (8, 0)):
         datas = []
         for name, over in CASES:
-            p = params(over)
-            if (p.bit_depth, p.chroma_format) == (depth, chroma):
-                datas += [S.single_heic(p, seed=s) for s in (1, 2)]
+            for across in (0, 1):  # loop_filter_across_tiles_enabled_flag (1: an assembly picture)
+                p = params(over, across=across)
+                if (p.bit_depth, p.chroma_format) == (depth, chroma):
+                    datas += [S.single_heic(p, seed=s) for s in (1, 2)]
         imgs = [H.HeifImage.parse(d) for d in datas]
         b = ctx.prepare(imgs, parse=parse)
         outs = ctx.alloc_outputs(imgs)
@@ -248,11 +249,12 @@ def test_gpu_tiled_pictures_bit_exact(H, oracle_mod, parse):
 @pytest.mark.gpu
 def test_gpu_tiled_grid_mixed_with_untiled(H, oracle_mod, halfmoonbay):
     """A HEIF grid whose grid tiles are themselves HEVC-tiled pictures (a 3x2
-    tile layout in each 512x256 picture), batched with halfmoonbay (WPP) and a
-    monochrome tiled picture's untiled twin: each picture keeps its own
-    substream layout; every image checked."""
+    tile layout in each 512x256 picture, filtered across tiles: six
+    assemblies), batched with halfmoonbay (WPP) and an untiled picture: each
+    picture keeps its own substream layout; every image checked, over two
+    pipelined decodes."""
     p = params(dict(width=512, height=256, tile_cols=3, tile_rows=2, tile_uniform=0, tile_col_w=(4, 6),
-                    tile_row_h=(3,)))
+                    tile_row_h=(3,)), across=1)
     grid = S.grid_heic(1000, 500, p, seed=9)
     plain = S.single_heic(params(dict(width=512, height=256)), seed=9)
     datas = [grid, halfmoonbay, plain]
