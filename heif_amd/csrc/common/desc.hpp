@@ -101,6 +101,7 @@ enum : uint8_t {
     TU_TSKIP = 1u << 3,
     TU_BYPASS = 1u << 4,
     TU_DST = 1u << 5,
+    TU_PCM = 1u << 6,     // pcm_sample(): the "coefficients" are the samples (BYPASS is set too)
 };
 
 // One transform block in decoding order (luma or chroma), written by the

@@ -372,6 +372,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             }
         }
         const int li = (ly0 + y) * w.cs + lx0 + x;
+        if (tu.flags & TU_PCM) pv = 0;  // the residual is the PCM sample itself
         if (cbf) pv += (n <= 8 && o == lane) ? r0 : w.res[(size_t)(y0 + y) * PW + x0 + x];
         pv = min(max(pv, 0), maxv);
         w.cur[li] = (Pel)pv;
@@ -407,6 +408,7 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     w.cx0 = wb.cx0;
     w.cy0 = wb.cy0;
     const bool cbf = ((h ? tr.flags : tb.flags) & TU_CBF) != 0;
+    const bool pcm = ((h ? tr.flags : tb.flags) & TU_PCM) != 0;
     const int bx0 = w.cx0 << 1, by0 = w.cy0 << 1, csl = w.cs << 1;
     const int ns = 4 * n + 1, nch = n == 8 ? 2 : 1;
     const int zc = zidx(((x0 << 1) - bx0) >> 2, ((y0 << 1) - by0) >> 2);
@@ -492,6 +494,7 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
                 const int p0 = *ang_ref(main_, side, inv, a + idx + 1);
                 pv = fact ? ((32 - fact) * p0 + fact * *ang_ref(main_, side, inv, a + idx + 2) + 16) >> 5 : p0;
             }
+            if (pcm) pv = 0;  // the residual is the PCM sample itself
             if (cbf) pv += it ? r1 : r0;
             pv = min(max(pv, 0), maxv);
             w.cur[(ly0 + y) * w.cs + lx0 + x] = (Pel)pv;

@@ -86,7 +86,7 @@ struct alignas(16) LaneLds {
 // picture constants and output pointers (LDS, one per picture of the wave)
 struct LanePic {
     int W, H, log2ctb, wctb, hctb, minCb, minTb, maxTb, maxDepthIntra, chroma;
-    int log2qg, bdY, bdC, qpbdY, qpbdC, pcmMin, pcmMax, cbOff, crOff, sliceQp;
+    int log2qg, bdY, bdC, qpbdY, qpbdC, pcmMin, pcmMax, pcmBdY, pcmBdC, cbOff, crOff, sliceQp;
     int w4, h4, w8, saoL, saoC;
     int R, lane0, ring;  // lanes of the picture, its first lane, rows wrap round the lanes (WPP rows > R)
     uint32_t flags, bits_off, bits_end, sub_first, row_off, tu_cap, coef_cap, pic;
@@ -124,6 +124,8 @@ enum : uint32_t {
     F_TB_CBF = 1u << 10,
     F_ANY_SB = 1u << 11,  // a sub-block of the TB had significant coefficients
     F_STOP = 1u << 12,
+    F_PCM = 1u << 13,     // the TB being recorded is a PCM block
+    F_REINIT = 1u << 14,  // solo modes: engine re-initialisation at byte L.reinit before the next unit
 };
 
 struct Lane {
@@ -166,6 +168,7 @@ struct Lane {
     // byte i & 3 of lane i >> 2 (35 lanes), read / written with v_readlane /
     // v_writelane; the one field whose lanes differ
     uint32_t cx;
+    uint32_t reinit;  // F_REINIT: RBSP byte (absolute) where the engine restarts after PCM samples
 };
 
 // engine context of one lane (lanes mode: every lane its own substream)
@@ -962,6 +965,76 @@ HG_HD inline void unit_cqt(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     L.st = U_CU;
 }
 
+HG_HD inline void cu_done(Lane &L, LaneLds &ld, LanePic &P);
+HG_HD inline void tu_emit(Lane &L, const LanePic &P);
+
+// pcm_flag = 1 (7.3.8.7 pcm_sample(); the reference parses the SPS PCM fields,
+// parameter_set_reader.rs:107-125): the decoder has consumed through the
+// codeword's final 1 bit, the samples start at the next byte boundary
+// (pcm_alignment_zero_bits).  They are recorded as bypass TBs (TU_PCM) whose
+// "coefficients" are the samples << (BitDepth - PcmBitDepth) in raster order:
+// k_transform copies them and k_intra adds them to a zero prediction.  The
+// engine restarts at the byte after them (9.3.2.5).  The CU counts as
+// INTRA_DC for later MPM derivations (8.4.2) and is one deblocking block,
+// unfiltered with pcm_loop_filter_disabled_flag.
+template <class EG>
+HG_HD inline void pcm_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
+    const int n = 1 << L.ql;
+    {
+        const int nb = n >> 2, by = (L.qy - L.ctby) >> 2, bx = (L.qx - L.ctbx) >> 2;
+        for (int k = 0; k < nb; ++k) {
+            ld.ipmL[by + k] = 1;
+            ld.ipmA[bx + k] = 1;
+        }
+    }
+    // bits consumed so far: 8 * end - budget - k (absolute RBSP bit position)
+    uint32_t bit = (uint32_t)(8 * (int32_t)P.bits_end - L.budget - L.k + 7) & ~7u;
+    L.fl = (L.fl | F_PCM | F_TB_CBF) & ~F_TS;
+    const int ncomp = P.chroma ? 3 : 1;
+    for (int c = 0; c < ncomp; ++c) {
+        const int l2 = c ? L.ql - 1 : L.ql, m = 1 << l2;
+        const int pbd = c ? P.pcmBdC : P.pcmBdY, sh = (c ? P.bdC : P.bdY) - pbd;
+        L.tb_cidx = c;
+        L.tb_x = c ? L.qx >> 1 : L.qx;
+        L.tb_y = c ? L.qy >> 1 : L.qy;
+        L.tb_log2 = l2;
+        L.tb_mode = 1;
+        L.tb_coef0 = L.ncoef;
+#pragma nounroll
+        for (int i = 0; i < m * m; ++i) {
+            const uint32_t b = bit >> 3;
+            const uint32_t w = ((uint32_t)G.rbsp[b] << 16) | ((uint32_t)G.rbsp[b + 1] << 8) | (uint32_t)G.rbsp[b + 2];
+            const uint32_t v = (w >> (24u - (bit & 7u) - (uint32_t)pbd)) & ((1u << pbd) - 1u);
+            bit += (uint32_t)pbd;
+            if (L.ncoef < P.coef_cap) coef_push(L, P, ((v << sh) << 16) | (uint32_t)i);
+            else L.status |= ST_CAPACITY;
+        }
+        tu_emit(L, P);
+    }
+    L.fl &= ~(F_PCM | F_TB_CBF);
+    {  // the CU's 4x4 blocks: one block for the deblocking edges
+        const int nb = n >> 2, gx0 = L.qx >> 2, gy0 = L.qy >> 2;
+        const int wx = gx0 + nb <= P.w4 ? nb : P.w4 - gx0, hy = gy0 + nb <= P.h4 ? nb : P.h4 - gy0;
+        const uint64_t nf = ((L.fl & F_BYPASS) || (P.flags & SP_PCM_LOOP_FILTER_DISABLED)) ? MF_NOFILT : 0;
+        const uint64_t rep = 0x0101010101010101ull;
+        for (int y = 0; y < hy; ++y) {
+            uint8_t *row = P.gflags + (size_t)(gy0 + y) * P.w4 + gx0;
+            const uint64_t h = (y == 0 ? (uint64_t)MF_EDGE_H : 0u) | nf;
+            store_bytes(row, wx, (rep * h) | (uint64_t)MF_EDGE_V);
+        }
+    }
+    const uint32_t next = bit >> 3;  // the samples end on a byte boundary
+    if (next > P.bits_end) L.status |= ST_OVERRUN;
+    if constexpr (EG::kSolo) {  // the driver moves the window first (run_unit re-initialises)
+        L.reinit = next;
+        L.lb = next >> 2;
+        L.fl |= F_REINIT;
+    } else {
+        engine_init(L, G, next, P.bits_end);
+    }
+    cu_done(L, ld, P);
+}
+
 // U_CU: coding_unit (7.3.8.5) up to its transform_tree
 template <class EG>
 HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
@@ -974,13 +1047,7 @@ HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     if ((P.flags & SP_TQ_BYPASS) && dec(L, G, CTX_TQ_BYPASS)) L.fl |= F_BYPASS;
     if (L.ql == P.minCb && !dec(L, G, CTX_PART_MODE)) L.fl |= F_NXN;
     const bool nxn = (L.fl & F_NXN) != 0;
-    if (!nxn && (P.flags & SP_PCM) && L.ql >= P.pcmMin && L.ql <= P.pcmMax && term(L, G)) {
-        // pcm_flag = 1: not supported on the GPU path
-        L.status |= ST_UNSUPPORTED;
-        L.fl |= F_STOP;
-        L.st = U_CTU_END;
-        return;
-    }
+    const bool pcm = !nxn && (P.flags & SP_PCM) && L.ql >= P.pcmMin && L.ql <= P.pcmMax && term(L, G);
     {  // CtDepth of the CU
         const int nd = 1 << (L.ql - 3);
         const int dy = (L.qy - L.ctby) >> 3, dx = (L.qx - L.ctbx) >> 3;
@@ -988,6 +1055,10 @@ HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             ld.dL[dy + k] = (uint8_t)L.qd;
             ld.dA[dx + k] = (uint8_t)L.qd;
         }
+    }
+    if (pcm) {
+        pcm_cu(L, ld, P, G);
+        return;
     }
     const int np = nxn ? 4 : 1;
     const int pb = nxn ? 1 << (L.ql - 1) : 1 << L.ql;
@@ -1107,6 +1178,7 @@ HG_HD inline void tu_emit(Lane &L, const LanePic &P) {
     if (L.fl & F_TB_CBF) f |= TU_CBF;
     if (L.fl & F_TS) f |= TU_TSKIP;
     if (L.fl & F_BYPASS) f |= TU_BYPASS;
+    if (L.fl & F_PCM) f |= TU_PCM | TU_BYPASS;
     if (L.tb_cidx == 0 && L.tb_log2 == 2) f |= TU_DST;
     if (L.ntu < P.tu_cap) {
         store_tu(P.tu_base + L.tu_row + L.ntu, (uint32_t)L.tb_x | ((uint32_t)L.tb_y << 16),
@@ -1117,6 +1189,8 @@ HG_HD inline void tu_emit(Lane &L, const LanePic &P) {
         L.status |= ST_CAPACITY;
     }
 }
+
+HG_HD inline void cu_done(Lane &L, LaneLds &ld, LanePic &P);
 
 // After a TB: its record, then the next TB of the TU, the next transform-tree
 // node, or (tree done) the CU's QpY and the next coding-quadtree node / CTU end.
@@ -1142,7 +1216,14 @@ HG_HD inline void tb_done(Lane &L, LaneLds &ld, LanePic &P) {
         ++L.tl;
         --L.td;
     }
-    {  // end of the CU: QpY for qPY_A/B and the 4x4 map (deblocking)
+    cu_done(L, ld, P);
+}
+
+// end of a CU: QpY for qPY_A/B and the 4x4 map (deblocking), then the next
+// coding-quadtree node in z-order (skipping children outside the picture) or
+// the CTU end
+HG_HD inline void cu_done(Lane &L, LaneLds &ld, LanePic &P) {
+    {
         const int n = 1 << L.ql, nd = n >> 3;
         const int dy = (L.qy - L.ctby) >> 3, dx = (L.qx - L.ctbx) >> 3;
         for (int k = 0; k < nd; ++k) {
@@ -1504,6 +1585,12 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
 // every L field a unit updates would then need a register per unit.
 template <class EG>
 HG_HD inline void run_unit(int kind, Lane &L, LaneLds &ld, LanePic &P, const Env &E, const EG &G) {
+    if constexpr (EG::kSolo) {
+        if (L.fl & F_REINIT) {  // after PCM samples: the driver has moved the window to L.reinit
+            engine_init(L, G, L.reinit, P.bits_end);
+            L.fl &= ~F_REINIT;
+        }
+    }
     switch (kind) {
     case U_SB: unit_sb(L, ld, P, G); break;
     case U_TB: unit_tb(L, ld, P, G); break;
@@ -1552,6 +1639,8 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
     P.qpbdC = 6 * (sp.bit_depth_c - 8);
     P.pcmMin = sp.log2_min_pcm;
     P.pcmMax = sp.log2_max_pcm;
+    P.pcmBdY = sp.pcm_bd_y;
+    P.pcmBdC = sp.pcm_bd_c;
     P.cbOff = sp.cb_qp_offset + pd.cb_qp_off;
     P.crOff = sp.cr_qp_offset + pd.cr_qp_off;
     P.sliceQp = pd.slice_qp;

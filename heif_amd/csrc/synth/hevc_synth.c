@@ -586,6 +586,21 @@ static void coding_unit(pic_t *p, int x0, int y0, int log2cb, int depth) {
         ce_bin(c, C_PART_MODE, !nxn);
     }
     set_map(p, p->depth, x0, y0, n, (uint8_t)depth);
+    if (!nxn && P->pcm && log2cb >= P->pcm_log2_min && log2cb <= P->pcm_log2_max) {
+        const int pcm = pct(&p->rng, P->pcm_pct);
+        ce_term(c, pcm); /* pcm_flag */
+        if (pcm) {       /* 7.3.8.7: flush + 1 + alignment zeros, raw samples, engine restart */
+            set_map(p, p->ipm, x0, y0, n, 1);
+            ce_finish(c);
+            bw_align1(c->w);
+            for (int ci = 0; ci < (P->chroma_format ? 3 : 1); ci++) {
+                const int ns = ci ? (n / 2) * (n / 2) : n * n, bd = ci ? P->pcm_bd_c : P->pcm_bd_y;
+                for (int k = 0; k < ns; k++) bw_bits(c->w, (uint32_t)rnd(&p->rng, 1 << bd), bd);
+            }
+            ce_start(c, c->w);
+            return;
+        }
+    }
     int np = nxn ? 4 : 1, pb = nxn ? n / 2 : n;
     int prev[4], mpm[4] = {0}, rem[4] = {0};
     for (int i = 0; i < np; i++) {
@@ -820,7 +835,14 @@ long synth_sps(const synth_params *P, uint8_t *out, size_t cap) {
     if (P->scaling_list) bw_bits(&w, 0, 1); /* default lists (Tables 7-5 / 7-6) */
     bw_bits(&w, 0, 1);                      /* amp */
     bw_bits(&w, P->sao ? 1 : 0, 1);
-    bw_bits(&w, 0, 1);                      /* pcm */
+    bw_bits(&w, P->pcm ? 1 : 0, 1); /* pcm_enabled_flag */
+    if (P->pcm) {
+        bw_bits(&w, (uint32_t)(P->pcm_bd_y - 1), 4);
+        bw_bits(&w, (uint32_t)(P->pcm_bd_c - 1), 4);
+        bw_ue(&w, (uint32_t)(P->pcm_log2_min - 3));
+        bw_ue(&w, (uint32_t)(P->pcm_log2_max - P->pcm_log2_min));
+        bw_bits(&w, P->pcm_lf_disabled ? 1 : 0, 1);
+    }
     bw_ue(&w, 0);
     bw_bits(&w, 0, 1);
     bw_bits(&w, 0, 1);
@@ -898,6 +920,11 @@ int synth_check_params(const synth_params *P) {
     if (P->density < 0 || P->density > 100) return -1;
     if (P->wpp != 0 && P->wpp != 1) return -1;
     if (P->tile_cols < 0 || P->tile_rows < 0 || P->tile_cols > SYNTH_MAX_TILES || P->tile_rows > SYNTH_MAX_TILES)
+        return -1;
+    if (P->pcm && (P->pcm_bd_y < 1 || P->pcm_bd_y > P->bit_depth || P->pcm_bd_c < 1 || P->pcm_bd_c > P->bit_depth ||
+                   P->pcm_log2_min < 3 || P->pcm_log2_min < P->log2_min_cb || P->pcm_log2_max > 5 ||
+                   P->pcm_log2_max > P->log2_ctb || P->pcm_log2_max < P->pcm_log2_min || P->pcm_pct < 0 ||
+                   P->pcm_pct > 100))
         return -1;
     if (P->slice_ctus < 0 || P->slice_dependent < 0 || P->slice_dependent > 2 || P->slice_lf_across < 0 ||
         P->slice_lf_across > 2)

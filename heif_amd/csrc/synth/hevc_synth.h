@@ -36,6 +36,10 @@ typedef struct {
      * slices' flag is 1; slice_dbk_vary: slices k > 0 override the deblocking
      * (disabled when k mod 3 = 2, beta k mod 3 - 1, tc 1 - k mod 3) */
     int32_t slice_ctus, slice_dependent, slice_lf_across, slice_dbk_vary;
+    /* PCM coding units: pcm_enabled_flag, PCM sample bit depths (1..bit_depth),
+     * CU sizes log2 [pcm_log2_min, pcm_log2_max] (3..5), pcm_loop_filter_disabled_flag,
+     * pcm_flag probability in percent for a CU that may take it */
+    int32_t pcm, pcm_bd_y, pcm_bd_c, pcm_log2_min, pcm_log2_max, pcm_lf_disabled, pcm_pct;
 } synth_params;
 
 /* Each returns the NAL unit length (2-byte header included, emulation

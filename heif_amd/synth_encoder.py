@@ -33,7 +33,9 @@ class _Params(ctypes.Structure):
         "sao", "deblock_disabled", "beta_offset_div2", "tc_offset_div2", "density", "wpp",
         "tile_cols", "tile_rows", "tile_uniform", "tile_lf_across")] + [
         ("tile_col_w", ctypes.c_int32 * 8), ("tile_row_h", ctypes.c_int32 * 8)] + [
-        (n, ctypes.c_int32) for n in ("slice_ctus", "slice_dependent", "slice_lf_across", "slice_dbk_vary")]
+        (n, ctypes.c_int32) for n in ("slice_ctus", "slice_dependent", "slice_lf_across", "slice_dbk_vary",
+                                      "pcm", "pcm_bd_y", "pcm_bd_c", "pcm_log2_min", "pcm_log2_max",
+                                      "pcm_lf_disabled", "pcm_pct")]
 
 
 @dataclasses.dataclass
@@ -84,6 +86,14 @@ class SynthParams:
     slice_dependent: int = 0
     slice_lf_across: int = 0
     slice_dbk_vary: int = 0
+    # PCM coding units (see hevc_synth.h): enable, sample bit depths, CU sizes, loop filter off, probability
+    pcm: int = 0
+    pcm_bd_y: int = 8
+    pcm_bd_c: int = 8
+    pcm_log2_min: int = 3
+    pcm_log2_max: int = 5
+    pcm_lf_disabled: int = 0
+    pcm_pct: int = 10
 
     def _c(self) -> _Params:
         c = _Params()

@@ -1411,6 +1411,43 @@ static int derive_luma_mode(pic_t *p, int xPb, int yPb, int prev, int mpm_idx, i
     return m;
 }
 
+/* 7.3.8.7 pcm_sample() of a CU with pcm_flag = 1 (the reference parses the SPS
+ * PCM fields, parameter_set_reader.rs:107-125, and stops at the CU): after the
+ * terminating bin the decoder has consumed through the codeword's final 1 bit;
+ * pcm_alignment_zero_bits up to a byte boundary, PcmBitDepth-bit samples
+ * (luma, then Cb, Cr), then 9.3.2.5 re-initialises the engine.  8.4.4.1:
+ * recSamples = pcm_sample << (BitDepth - PcmBitDepth); 8.4.2: a PCM neighbour
+ * counts as INTRA_DC; the CU is one block for deblocking, left unfiltered (and
+ * without SAO) when pcm_loop_filter_disabled_flag is 1. */
+static int pcm_cu(pic_t *p, int x0, int y0, int log2cb) {
+    cabac_t *c = &p->c;
+    const hevc_sps *s = p->sps;
+    const int n = 1 << log2cb;
+    set_map(p, p->ipm, x0, y0, n, 1);
+    while (c->b.bit & 7)
+        if (br_bit(&c->b)) return oracle_fail("pcm_alignment_zero_bit is 1");
+    for (int ci = 0; ci < (p->chroma ? 3 : 1); ci++) {
+        const int w = ci ? n / p->sw : n, h = ci ? n / p->sh : n;
+        const int xs = ci ? x0 / p->sw : x0, ys = ci ? y0 / p->sh : y0;
+        const int bd = ci ? p->bdC : p->bdY, pbd = ci ? s->pcm_bd_c : s->pcm_bd_y;
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++)
+                p->pl[ci][(size_t)(ys + y) * p->ps[ci] + xs + x] = (uint16_t)(br_u(&c->b, pbd) << (bd - pbd));
+    }
+    if (c->b.err) return oracle_fail("PCM samples overrun the slice data");
+    if (cabac_init_engine(c)) return -1;
+    for (int k = 0; k < n; k += 4) {
+        if (((y0 + k) >> 2) < p->h4) p->flg[((y0 + k) >> 2) * p->w4 + (x0 >> 2)] |= F_EDGE_V;
+        if (((x0 + k) >> 2) < p->w4) p->flg[(y0 >> 2) * p->w4 + ((x0 + k) >> 2)] |= F_EDGE_H;
+    }
+    set_map(p, (uint8_t *)p->qpy, x0, y0, n, (uint8_t)(int8_t)p->qpy_cur);
+    if (p->cu_bypass || s->pcm_loop_filter_disabled)
+        for (int y = y0 >> 2; y < (y0 + n) >> 2 && y < p->h4; y++)
+            for (int x = x0 >> 2; x < (x0 + n) >> 2 && x < p->w4; x++) p->flg[y * p->w4 + x] |= F_NOFILT;
+    p->qp_prev_last = p->qpy_cur;
+    return 0;
+}
+
 static int coding_unit(pic_t *p, int x0, int y0, int log2cb, int depth) {
     cabac_t *c = &p->c;
     const hevc_sps *s = p->sps;
@@ -1423,8 +1460,8 @@ static int coding_unit(pic_t *p, int x0, int y0, int log2cb, int depth) {
     if (nxn && log2cb == s->log2_min_tb) return oracle_fail("NxN at min TB size");
     int pcm = 0;
     if (!nxn && s->pcm && log2cb >= s->log2_min_pcm && log2cb <= s->log2_max_pcm) pcm = dec_term(c);
-    if (pcm) return oracle_fail("pcm_flag=1 not supported by the oracle");
     set_map(p, p->depth, x0, y0, n, (uint8_t)depth);
+    if (pcm) return pcm_cu(p, x0, y0, log2cb);
     int np = nxn ? 4 : 1, pb = nxn ? n / 2 : n;
     int prev[4], mpm[4] = {0}, rem[4] = {0};
     for (int i = 0; i < np; i++) prev[i] = dec_bin(c, CTX_PREV_INTRA);

@@ -141,7 +141,7 @@ def test_sps_out_of_range_rejected(over):
 
 
 def test_valid_pcm_sps_accepted():
-    """PCM enabled with legal sizes parses (a PCM CU itself is reported per picture as unsupported)."""
+    """PCM enabled with legal sizes parses (PCM CUs decode: tests/test_synth.py pcm_* cases)."""
     d = _with_sets(sps=W.sps(log2_min_cb_minus3=1, log2_diff_max_min_cb=1, log2_diff_max_min_tb=2, pcm=(8, 8, 1, 0)))
     assert H.HeifImage.parse(d).info.width == 128
 

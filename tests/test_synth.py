@@ -49,6 +49,15 @@ CASES = [
     # 132 CTBs wide x 70 rows: the row above a wrapped lane's next row is still
     # being parsed when its contexts are stored (the staging block)
     ("ring_wide_2112x1120", dict(width=2112, height=1120, log2_ctb=4, log2_max_tb=4, density=10)),
+    # PCM coding units (pcm_sample(): raw samples between two engine runs;
+    # parameter_set_reader.rs:107-125 parses the SPS fields): PCM bit depths
+    # below the coding bit depth, 8x8..32x32 CUs, loop filters off for them,
+    # 4:0:0, transquant bypass, every eligible CU PCM
+    ("pcm_8b", dict(pcm=1, pcm_pct=30)),
+    ("pcm_lowbd_nofilter_nowpp", dict(pcm=1, pcm_bd_y=5, pcm_bd_c=7, pcm_lf_disabled=1, pcm_pct=30, wpp=0)),
+    ("pcm_10b_16_32", dict(bit_depth=10, pcm=1, pcm_bd_y=9, pcm_bd_c=10, pcm_log2_min=4, pcm_log2_max=5, pcm_pct=40)),
+    ("pcm_mono_bypass", dict(chroma_format=0, pcm=1, pcm_pct=30, tq_bypass=1)),
+    ("pcm_all_ctb16", dict(pcm=1, pcm_pct=100, pcm_lf_disabled=1, log2_ctb=4, log2_max_tb=4, pcm_log2_max=4)),
 ]
 
 
