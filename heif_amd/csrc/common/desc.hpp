@@ -27,6 +27,19 @@ enum : uint32_t {
     // not the last tile: its substream ends in end_of_slice_segment_flag 0 and
     // end_of_subset_one_bit 1 (7.3.8.1)
     SP_SUBSET_END = 1u << 10,
+    // several slice segments in the picture, each starting at a CTB row: the
+    // substream table has one entry per CTB row (SUB_* flags below)
+    SP_ROW_SEGMENTS = 1u << 11,
+};
+
+// substream table entries (PicDesc::sub_first..): raw offset | flags.  With
+// SP_ROW_SEGMENTS, SUB_SEG_END marks a row whose last CTU ends a slice segment
+// (end_of_slice_segment_flag = 1), and SUB_CONTINUE a row of a picture without
+// WPP that starts no substream of its own (the segment's engine runs on).
+enum : uint32_t {
+    SUB_OFFSET = 0x3fffffffu,
+    SUB_CONTINUE = 1u << 30,
+    SUB_SEG_END = 1u << 31,
 };
 
 // Per distinct SPS/PPS pair (derived values only; H.265 7.4.3.2 / 7.4.3.3).

@@ -174,8 +174,8 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
             // whole picture with all its substreams.
             struct Sub {
                 int x0, y0, x1, y1;  // CTBs
-                size_t seg;          // slice segment
-                int s0, s1;          // its substreams [s0, s1)
+                size_t seg, nseg;    // slice segments [seg, seg + nseg): a slice and its dependent segments
+                int s0, s1;          // substreams [s0, s1) of a single segment
                 bool subset_end;     // ends in end_of_subset_one_bit (a tile other than the last)
             };
             std::vector<Sub> subs_of;
@@ -186,13 +186,16 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                 for (int ht = 0; ht < ntc * ntr; ++ht) {
                     const int tc = ht % ntc, tr = ht / ntc;
                     subs_of.push_back({ps.col_bd[size_t(tc)], ps.row_bd[size_t(tr)], ps.col_bd[size_t(tc) + 1],
-                                       ps.row_bd[size_t(tr) + 1], 0, ht, ht + 1, ht + 1 < ntc * ntr});
+                                       ps.row_bd[size_t(tr) + 1], 0, 1, ht, ht + 1, ht + 1 < ntc * ntr});
                 }
             } else {
-                for (size_t k = 0; k < tj.segs.size(); ++k) {
+                for (size_t k = 0; k < tj.segs.size();) {  // one sub-picture per slice
+                    size_t e = k + 1;
+                    while (e < tj.segs.size() && tj.segs[e].sh.dependent_slice_segment_flag) ++e;
                     const int r0 = int(tj.segs[k].sh.slice_segment_address) / pw;
-                    const int r1 = k + 1 < tj.segs.size() ? int(tj.segs[k + 1].sh.slice_segment_address) / pw : ph;
-                    subs_of.push_back({0, r0, pw, r1, k, 0, tj.segs[k].sh.num_entry_point_offsets + 1, false});
+                    const int r1 = e < tj.segs.size() ? int(tj.segs[e].sh.slice_segment_address) / pw : ph;
+                    subs_of.push_back({0, r0, pw, r1, k, e - k, 0, tj.segs[k].sh.num_entry_point_offsets + 1, false});
+                    k = e;
                 }
             }
             // Loop filters across the sub-pictures' boundaries (tiles with
@@ -203,7 +206,7 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
             // loop filters run on it (desc.hpp).
             const bool assemble =
                 subs_of.size() > 1 && (ps.pps.tiles_enabled_flag ? ps.pps.loop_filter_across_tiles_enabled_flag
-                                                                 : tj.segs[1].sh.slice_loop_filter_across_slices_enabled_flag);
+                                                                 : tj.segs[subs_of[1].seg].sh.slice_loop_filter_across_slices_enabled_flag);
             const uint32_t child0 = uint32_t(hb.pics.size());
             const int32_t grid_x = int32_t((t % im.cols) * im.tile_width), grid_y = int32_t((t / im.cols) * im.tile_height);
             for (const Sub &su : subs_of) {
@@ -213,6 +216,7 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                 starts.push_back(uint32_t(sg.payload_len));
                 SeqParams base = make_seq(ps, 0);
                 int vis_dx = 0, vis_dy = 0;  // output offset of the sub-picture's visible part
+                if (su.nseg > 1) base.flags |= SP_ROW_SEGMENTS;
                 if (subs_of.size() > 1) {
                     const int x0 = su.x0 * pctb, y0 = su.y0 * pctb;
                     const int x1 = std::min(su.x1 * pctb, base.width), y1 = std::min(su.y1 * pctb, base.height);
@@ -234,7 +238,35 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                 PicDesc pd{};
                 pd.bits_off = hb.bits_size;
                 pd.sub_first = uint32_t(hb.subs.size());
-                if (su.s0 > 0 || su.s1 + 1 < int(starts.size())) {
+                if (su.nseg > 1) {
+                    // a slice of several segments: their slice data back to back, one
+                    // substream-table entry per CTB row (SUB_* flags, desc.hpp)
+                    const bool wpp = ps.pps.entropy_coding_sync_enabled_flag;
+                    uint32_t off = 0;
+                    for (size_t j = su.seg; j < su.seg + su.nseg; ++j) {
+                        const SliceSeg &g = tj.segs[j];
+                        const uint32_t d0 = g.sh.slice_data_raw_offset;
+                        uint32_t d1 = uint32_t(g.payload_len);
+                        // cabac_zero_words (00 00 03 each) would leave zero bytes before the
+                        // next segment's data, where they could start an emulation-prevention pattern
+                        while (d1 >= d0 + 3 && g.payload[d1 - 1] == 3 && g.payload[d1 - 2] == 0 && g.payload[d1 - 3] == 0)
+                            d1 -= 3;
+                        hb.pieces.push_back({g.payload + d0, d1 - d0, hb.bits_size + off});
+                        const int r0 = int(g.sh.slice_segment_address) / pw;
+                        const int r1 = j + 1 < su.seg + su.nseg ? int(tj.segs[j + 1].sh.slice_segment_address) / pw
+                                                                : su.y1;
+                        uint32_t e = off;  // the row's substream start within the concatenation
+                        for (int r = r0; r < r1; ++r) {
+                            if (wpp && r > r0) e += g.sh.entry_point_offset[size_t(r - r0 - 1)];
+                            uint32_t v = (wpp || r == r0) ? e : (off | SUB_CONTINUE);
+                            if (r + 1 == r1 && j + 1 < su.seg + su.nseg) v |= SUB_SEG_END;
+                            hb.subs.push_back(v);
+                        }
+                        off += d1 - d0;
+                    }
+                    pd.bits_len = off;
+                    pd.n_sub = uint32_t(su.y1 - su.y0);
+                } else if (su.s0 > 0 || su.s1 + 1 < int(starts.size())) {
                     // a substream range alone (it starts after a nonzero byte: no EP state carries in)
                     const uint32_t r0 = starts[size_t(su.s0)], r1 = starts[size_t(su.s1)];
                     pd.bits_len = r1 - r0;
@@ -310,7 +342,7 @@ void parse_chain_cost(const PicDesc *pics, int n, const uint32_t *subs, const Se
         prev.assign(size_t(wctb), 0.f);
         cur.assign(size_t(wctb), 0.f);
         for (uint32_t r = 0; r < pd.n_sub; ++r) {
-            const float t = float(sb[r + 1] - sb[r]) / float(wctb);
+            const float t = float((sb[r + 1] & SUB_OFFSET) - (sb[r] & SUB_OFFSET)) / float(wctb);
             for (int c = 0; c < wctb; ++c) {
                 const float left = c ? cur[size_t(c - 1)] : 0.f;
                 const float up = r ? prev[size_t(std::min(c + 1, wctb - 1))] : 0.f;

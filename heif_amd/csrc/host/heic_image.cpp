@@ -29,13 +29,30 @@ void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p
 }
 
 // The slice segments of a picture: in order and covering it (7.4.7.1), and
-// each with one entry point per tile / WPP row.  The GPU path decodes several
-// slices as one sub-picture per slice (batch.cpp), so they must be
-// independent and start at a CTB row; HEVC tiles must come with a single
-// slice.  Loop filtering across the slices' boundaries is either off for all
-// (independent sub-pictures) or on for all, with one set of deblocking values
-// (sub-pictures of an assembly filtered whole).
-void check_segments(const TileJob &job, const ParamSet &ps) {
+// each with one entry point per tile / WPP row.  A dependent segment takes its
+// slice's header values (7.4.7.1), copied in here.  The GPU path decodes
+// several slices as one sub-picture per slice (batch.cpp), so every segment
+// must start at a CTB row (a slice's dependent segments are concatenated);
+// HEVC tiles must come with a single segment.  Loop filtering across the
+// slices' boundaries is either off for all (independent sub-pictures) or on
+// for all, with one set of deblocking values (sub-pictures of an assembly
+// filtered whole).
+void check_segments(TileJob &job, const ParamSet &ps) {
+    for (size_t k = 1; k < job.segs.size(); ++k) {
+        SliceSegmentHeader &sh = job.segs[k].sh;
+        if (!sh.dependent_slice_segment_flag) continue;
+        const SliceSegmentHeader &s = job.segs[k - 1].sh;  // (already inherited when dependent itself)
+        sh.slice_type = s.slice_type;
+        sh.slice_sao_luma_flag = s.slice_sao_luma_flag;
+        sh.slice_sao_chroma_flag = s.slice_sao_chroma_flag;
+        sh.slice_qp_delta = s.slice_qp_delta;
+        sh.slice_cb_qp_offset = s.slice_cb_qp_offset;
+        sh.slice_cr_qp_offset = s.slice_cr_qp_offset;
+        sh.slice_deblocking_filter_disabled_flag = s.slice_deblocking_filter_disabled_flag;
+        sh.slice_beta_offset_div2 = s.slice_beta_offset_div2;
+        sh.slice_tc_offset_div2 = s.slice_tc_offset_div2;
+        sh.slice_loop_filter_across_slices_enabled_flag = s.slice_loop_filter_across_slices_enabled_flag;
+    }
     const SequenceParameterSet &sps = ps.sps;
     const PictureParameterSet &pps = ps.pps;
     const uint32_t pw = uint32_t(sps.pic_width_in_ctbs_y());
@@ -45,10 +62,12 @@ void check_segments(const TileJob &job, const ParamSet &ps) {
         if (k > 0 && sh.slice_segment_address <= job.segs[k - 1].sh.slice_segment_address)
             throw HeifError("slice segments out of order");
         if (k == 0) continue;
-        if (sh.dependent_slice_segment_flag) throw UnsupportedError("dependent slice segments");
-        if (pps.tiles_enabled_flag) throw UnsupportedError("several slices together with HEVC tiles");
-        if (sh.slice_segment_address % pw) throw UnsupportedError("a slice starting inside a CTB row");
-        const SliceSegmentHeader &s1 = job.segs[1].sh;
+        if (pps.tiles_enabled_flag) throw UnsupportedError("several slice segments together with HEVC tiles");
+        if (sh.slice_segment_address % pw) throw UnsupportedError("a slice segment starting inside a CTB row");
+        if (sh.dependent_slice_segment_flag) continue;  // the loop-filter rules below are per slice
+        size_t second = 1;  // the second slice
+        while (job.segs[second].sh.dependent_slice_segment_flag) ++second;
+        const SliceSegmentHeader &s1 = job.segs[second].sh;
         if (sh.slice_loop_filter_across_slices_enabled_flag != s1.slice_loop_filter_across_slices_enabled_flag)
             throw UnsupportedError("slices filtered across some slice boundaries only");
         const SliceSegmentHeader &s0 = job.segs[0].sh;

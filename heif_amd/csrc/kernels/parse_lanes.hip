@@ -826,8 +826,13 @@ HG_HD inline bool wpp_ready(const Lane &L, const LanePic &P, const Env &E) {
 // RBSP offset (absolute) at which a lane about to run U_CTU starts its
 // substream (engine and context initialisation, unit_ctu), or ~0u
 HG_HD inline uint32_t substream_start(const Lane &L, const LanePic &P, const BatchArgs &a) {
-    if (L.c == 0 && ((L.fl & F_WPP) || L.row == 0))
-        return P.bits_off + a.rsubs[P.sub_first + ((L.fl & F_WPP) ? L.row : 0)];
+    if (L.c != 0) return ~0u;
+    if ((L.fl & F_WPP) || L.row == 0)
+        return P.bits_off + (a.rsubs[P.sub_first + ((L.fl & F_WPP) ? L.row : 0)] & SUB_OFFSET);
+    if (P.flags & SP_ROW_SEGMENTS) {  // no WPP: a dependent slice segment may start at this row
+        const uint32_t e = a.rsubs[P.sub_first + L.row];
+        if (!(e & SUB_CONTINUE)) return P.bits_off + (e & SUB_OFFSET);
+    }
     return ~0u;
 }
 
@@ -850,35 +855,44 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
     if (!wpp_ready<EG>(L, P, E)) return;
     L.ctbx = L.c << P.log2ctb;
     L.ctby = L.row << P.log2ctb;
-    if (L.c == 0 && ((L.fl & F_WPP) || L.row == 0)) {
-        // substream start: contexts (init, or the WPP copy already in ld.ctx) + engine
+    const uint32_t start = substream_start(L, P, *E.a);
+    if (start != ~0u) {
+        // substream start: contexts (init; the WPP copy already in ld.ctx; or, a
+        // dependent slice segment without WPP, the previous segment's final
+        // state, which the lane still holds: 9.3.2.4) + engine
+        const bool init = L.row == 0 || ((L.fl & F_WPP) && P.wctb < 2);
+        const bool wpp_copy = !init && (L.fl & F_WPP);
         if constexpr (EG::kCtxReg) {
 #if !defined(HG_HOST_EMU)
             // every lane its dword of the contexts: initialised, or the row above's copy
             const int ln = (int)__lane_id();
-            uint32_t w = 0;
-            if (L.row == 0 || P.wctb < 2 || !(L.fl & F_WPP)) {
+            uint32_t w = L.cx;
+            if (init) {
+                w = 0;
                 for (int b = 0; b < 4; ++b) {
                     const int i = 4 * ln + b;
                     if (i < CTX_NUM) w |= (uint32_t)ctx_init_state(c_ctx_init_l[i], P.sliceQp) << (8 * b);
                 }
-            } else if (ln < CTX_PAD / 4) {
-                const uint8_t *src = (EG::kSpread || P.ring) ? E.wctx + (size_t)E.lane * CTX_PAD : ld.ctx;
-                const uint32_t *sw = reinterpret_cast<const uint32_t *>(src) + ln;
-                w = EG::kSpread ? load_agent(sw) : *sw;
+            } else if (wpp_copy) {
+                w = 0;
+                if (ln < CTX_PAD / 4) {
+                    const uint8_t *src = (EG::kSpread || P.ring) ? E.wctx + (size_t)E.lane * CTX_PAD : ld.ctx;
+                    const uint32_t *sw = reinterpret_cast<const uint32_t *>(src) + ln;
+                    w = EG::kSpread ? load_agent(sw) : *sw;
+                }
             }
             L.cx = w;
 #endif
-        } else if (L.row == 0 || P.wctb < 2 || !(L.fl & F_WPP)) {
+        } else if (init) {
 #pragma nounroll
             for (int i = 0; i < CTX_NUM; ++i) ld.ctx[i] = ctx_init_state(c_ctx_init_l[i], P.sliceQp);
-        } else if (EG::kSpread || P.ring) {
+        } else if (wpp_copy && (EG::kSpread || P.ring)) {
             const uint32_t *src = reinterpret_cast<const uint32_t *>(E.wctx + (size_t)E.lane * CTX_PAD);
             uint32_t *dst = reinterpret_cast<uint32_t *>(ld.ctx);
 #pragma nounroll
             for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = EG::kSpread ? load_agent(src + k) : src[k];
         }
-        engine_init(L, G, substream_start(L, P, *E.a), P.bits_end);
+        engine_init(L, G, start, P.bits_end);
         if (L.row == 0) L.fl |= F_FIRST_QG;
     }
     if (P.saoL || P.saoC) {
@@ -1547,7 +1561,11 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
         }
     }
     const bool last_in_pic = L.row == P.hctb - 1 && L.c == P.wctb - 1;
-    const bool eos = last_in_pic && !(P.flags & SP_SUBSET_END);  // end_of_slice_segment_flag = 1 here
+    // end_of_slice_segment_flag = 1 at the picture's last CTU (unless a tile's
+    // substream goes on: SP_SUBSET_END) and at the end of a row that ends a slice segment
+    const bool seg_end = !last_in_pic && L.c == P.wctb - 1 && (P.flags & SP_ROW_SEGMENTS) &&
+                         (E.a->rsubs[P.sub_first + L.row] & SUB_SEG_END);
+    const bool eos = (last_in_pic && !(P.flags & SP_SUBSET_END)) || seg_end;
     if (term(L, G) != (eos ? 1 : 0)) L.status |= ST_SUBSTREAM_END;
     if (!eos && (last_in_pic || ((L.fl & F_WPP) && L.c == P.wctb - 1)) && !term(L, G)) L.status |= ST_SUBSTREAM_END;
     if (L.budget + L.k < 0) L.status |= ST_OVERRUN;  // read past the NAL unit

@@ -44,8 +44,8 @@ void emu_rbsp(const BatchArgs &a) {
         }
         removed_before[len] = r;
         for (uint32_t s = 0; s <= pd.n_sub; ++s) {
-            const uint32_t e = a.subs[pd.sub_first + s];
-            a.rsubs[pd.sub_first + s] = e < len ? e - removed_before[e] : len - r;
+            const uint32_t e = a.subs[pd.sub_first + s] & SUB_OFFSET, fl = a.subs[pd.sub_first + s] & ~SUB_OFFSET;
+            a.rsubs[pd.sub_first + s] = (e < len ? e - removed_before[e] : len - r) | fl;
         }
     }
 }
@@ -126,18 +126,21 @@ __global__ void __launch_bounds__(64) k_rbsp(BatchArgs a) {
         // entry points inside this step: lane t of the chunk holding e knows the removals before e
         for (uint32_t g = 0; g < nent; g += 64) {
             const uint32_t idx = g + (uint32_t)lane;
-            const uint32_t e = idx < nent ? subs[idx] : 0xffffffffu;
+            const uint32_t raw_e = idx < nent ? subs[idx] : 0xffffffffu;
+            const uint32_t e = raw_e & SUB_OFFSET;  // the flags ride along (SP_ROW_SEGMENTS)
             const bool here = e >= c0 && e < c0 + 1024u && e < len;
             const int t = here ? (int)((e - c0) >> 4) : 0;
             const uint32_t ext = (uint32_t)__shfl((int)ex, t, 64);
             const uint32_t mt = (uint32_t)__shfl((int)mask, t, 64);
-            if (here) rsubs[idx] = e - (run + ext + (uint32_t)__popc(mt & ((1u << ((e - c0) & 15u)) - 1u)));
+            if (here)
+                rsubs[idx] = (e - (run + ext + (uint32_t)__popc(mt & ((1u << ((e - c0) & 15u)) - 1u)))) |
+                             (raw_e & ~SUB_OFFSET);
         }
         run += (uint32_t)total;
     }
     // the RBSP length, and entries at or past the payload end (corrupt headers)
     for (uint32_t idx = (uint32_t)lane; idx < nent; idx += 64)
-        if (subs[idx] >= len) rsubs[idx] = len - run;
+        if ((subs[idx] & SUB_OFFSET) >= len) rsubs[idx] = (len - run) | (subs[idx] & ~SUB_OFFSET);
 }
 
 hipError_t launch_rbsp(const BatchArgs &a, hipStream_t s) {

@@ -15,11 +15,13 @@ on every substream end (the per-substream checks) pins context selection
 for the other layouts (mid-row slices, dependent segments, slices with tiles).
 
 GPU: each slice of such a picture is decoded as its own picture
-(heif_amd/csrc/host/batch.cpp); when every slice is filtered across its
-upper boundary (one set of deblocking values) the slices are children of an
-assembly picture filtered whole (desc.hpp PD_ASSEMBLY).  Dependent segments,
-slices starting inside a CTB row, filtering across some slice boundaries only
-and slices with HEVC tiles are HEIFGPU_E_UNSUPPORTED.
+(heif_amd/csrc/host/batch.cpp), its dependent segments back to back in it
+(SP_ROW_SEGMENTS: one substream-table entry per CTB row, flagged where a
+segment ends or, without WPP, where the engine runs on); when every slice is
+filtered across its upper boundary (one set of deblocking values) the slices
+are children of an assembly picture filtered whole (desc.hpp PD_ASSEMBLY).
+Segments starting inside a CTB row, filtering across some slice boundaries
+only and several segments with HEVC tiles are HEIFGPU_E_UNSUPPORTED.
 """
 import os
 import subprocess
@@ -57,6 +59,19 @@ ROW_CASES = [
                                  tq_bypass=1, transform_skip=1, scaling_list=1, diff_cu_qp_delta_depth=2,
                                  max_th_depth_intra=3)),
     ("mono_rows", dict(chroma_format=0, slice_ctus=4, wpp=1)),
+]
+
+# dependent slice segments starting at CTB rows (GPU: a slice's segments back
+# to back in one picture, one substream-table entry per row)
+DEP_CASES = [
+    ("dep_all_nowpp", dict(slice_ctus=4, slice_dependent=1)),
+    ("dep_all_wpp", dict(slice_ctus=4, slice_dependent=1, wpp=1)),
+    ("dep_alt_wpp", dict(slice_ctus=4, slice_dependent=2, wpp=1)),
+    ("dep_alt_nowpp_ctb16_pcm", dict(log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2, slice_ctus=8, slice_dependent=2,
+                                     pcm=1, pcm_pct=20, pcm_log2_max=4)),
+    ("dep_crop_10b_dbk", dict(width=200, height=120, conf_right=6, conf_bottom=2, bit_depth=10, slice_ctus=14,
+                              slice_dependent=1, wpp=1, slice_dbk_vary=1)),
+    ("dep_alt_across", dict(width=128, height=192, slice_ctus=4, slice_dependent=2, wpp=1, slice_lf_across=1)),
 ]
 
 
@@ -142,11 +157,11 @@ def test_synth_writes_segments():
 
 
 @pytest.mark.parametrize("over,why", [
-    (dict(slice_ctus=5), "a slice starting inside a CTB row"),
+    (dict(slice_ctus=5), "a slice segment starting inside a CTB row"),
+    (dict(slice_ctus=6, slice_dependent=1), "a slice segment starting inside a CTB row"),
     (dict(slice_ctus=4, slice_lf_across=2), "slices filtered across some slice boundaries only"),
     (dict(slice_ctus=4, slice_lf_across=1, slice_dbk_vary=1), "with different deblocking values"),
-    (dict(slice_ctus=4, wpp=1, slice_dependent=1), "dependent slice segments"),
-    (dict(slice_ctus=8, tile_cols=2, tile_rows=1), "several slices together with HEVC tiles"),
+    (dict(slice_ctus=8, tile_cols=2, tile_rows=1), "several slice segments together with HEVC tiles"),
 ])
 def test_host_rejects_unsupported_slice_layouts(over, why):
     import heif_amd as H
@@ -182,12 +197,14 @@ def emu_check():
 
 @pytest.mark.parametrize("parse", ["lanes", "solo", "spread"])
 @pytest.mark.parametrize("name,across", [("rows2_wpp_dbk", 0), ("crop_10b_wpp", 0), ("ctb16_rows2", 0),
-                                         ("ctb16_rows2", 1), ("mono_rows", 1)])
+                                         ("ctb16_rows2", 1), ("mono_rows", 1), ("dep_all_nowpp", 0),
+                                         ("dep_alt_wpp", 0), ("dep_alt_nowpp_ctb16_pcm", 0),
+                                         ("dep_alt_across", 1)])
 def test_emulated_kernels_slices(emu_check, tmp_path, name, across, parse):
     """The kernels' source compiled for the host decodes a picture of row
-    slices (one picture per slice; filtered across: children of an assembly)
-    bit-exactly against the oracle."""
-    p = params({**dict(ROW_CASES)[name], "slice_lf_across": across})
+    slices (one picture per slice, its dependent segments back to back;
+    filtered across: children of an assembly) bit-exactly against the oracle."""
+    p = params({**dict(ROW_CASES + DEP_CASES)[name], "slice_lf_across": across})
     path = tmp_path / "s.heic"
     path.write_bytes(S.single_heic(p, seed=5))
     r = subprocess.run([emu_check, str(path), "5"], capture_output=True, text=True, timeout=600,
@@ -230,7 +247,7 @@ def test_gpu_row_slices_bit_exact(H, oracle_mod, parse):
     ctx = H.DecodeContext(0)
     for depth, chroma in ((8, 1), (10, 1), (8, 0)):
         datas = []
-        for name, over in ROW_CASES:
+        for name, over in ROW_CASES + DEP_CASES:
             for across in (0, 1):
                 p = params({**over, "slice_lf_across": across})
                 if across and p.slice_dbk_vary:
