@@ -24,7 +24,7 @@ from ._lib import HeifGpuError, UnsupportedError, lib
 
 __all__ = [
     "HeicDecoder", "HeifImage", "DecodeContext", "DeviceBatch", "DecodedImage", "RbspReader",
-    "HeifGpuError", "UnsupportedError", "ipc_export", "ipc_open", "ipc_close",
+    "HeifGpuError", "UnsupportedError", "ipc_export", "ipc_open", "ipc_close", "chroma_dims",
 ]
 
 
@@ -102,6 +102,15 @@ class HeifImage:
             self._h = None
 
 
+def chroma_dims(info):
+    """(height, width) of an image's Cb / Cr planes: chroma_format_idc 1 (4:2:0)
+    halves both axes, 2 (4:2:2) the width, 3 (4:4:4) neither (Table 6-1), odd
+    sizes rounded up."""
+    sx = 1 if info.chroma_format_idc in (1, 2) else 0
+    sy = 1 if info.chroma_format_idc == 1 else 0
+    return (info.height + sy) >> sy, (info.width + sx) >> sx
+
+
 @dataclass
 class DecodedImage:
     y: "object"            # torch tensor on the device, (H, W)
@@ -144,8 +153,8 @@ class DecodeContext:
         for im in images:
             inf = im.info
             dims = [(inf.height, inf.width)]
-            if inf.chroma_format_idc == 1:
-                dims += [((inf.height + 1) // 2, (inf.width + 1) // 2)] * 2
+            if inf.chroma_format_idc:
+                dims += [chroma_dims(inf)] * 2
             offs = []
             for h, w in dims:
                 offs.append((total, h, w))
@@ -168,8 +177,8 @@ class DecodeContext:
             dev = torch.device("cuda", self.device)
             y = torch.empty((inf.height, inf.width), dtype=dt, device=dev)
             cb = cr = None
-            if inf.chroma_format_idc == 1:
-                ch, cw = (inf.height + 1) // 2, (inf.width + 1) // 2
+            if inf.chroma_format_idc:
+                ch, cw = chroma_dims(inf)
                 cb = torch.empty((ch, cw), dtype=dt, device=dev)
                 cr = torch.empty((ch, cw), dtype=dt, device=dev)
             outs.append(DecodedImage(y, cb, cr, inf))

@@ -267,7 +267,7 @@ int heifgpu_gather_tiles(const heifgpu_image_info *info, const heifgpu_planes *d
     if (!info || !dst || !src) return fail(HEIFGPU_E_INVALID, "null argument");
     if (tile_stride == 0) tile_stride = 1;
     if (tile_offset >= tile_stride) return fail(HEIFGPU_E_INVALID, "tile_offset must be below tile_stride");
-    if (info->chroma_format_idc > 1) return fail(HEIFGPU_E_UNSUPPORTED, "only 4:0:0 and 4:2:0");
+    if (info->chroma_format_idc > 3) return fail(HEIFGPU_E_INVALID, "chroma_format_idc");
     const int planes = info->chroma_format_idc ? 3 : 1;
     for (int c = 0; c < planes; ++c)
         if (!dst->plane[c] || !src->plane[c]) return fail(HEIFGPU_E_INVALID, "missing plane");
@@ -293,6 +293,8 @@ int heifgpu_gather_tiles(const heifgpu_image_info *info, const heifgpu_planes *d
         g.spitch[c] = src->pitch[c];
     }
     g.planes = planes;
+    g.sx = chroma_sx(int(info->chroma_format_idc));
+    g.sy = chroma_sy(int(info->chroma_format_idc));
     g.bps = int32_t(info->bytes_per_sample);
     g.W = int32_t(info->width);
     g.H = int32_t(info->height);
@@ -391,8 +393,8 @@ int heifgpu_image_get_info(const heifgpu_image *img, heifgpu_image_info *info) {
 int heifgpu_ycbcr_to_rgb(heifgpu_ctx *ctx, const heifgpu_image_info *info, const heifgpu_planes *in, void *rgb,
                          int32_t rgb_pitch, void *stream) {
     if (!ctx || !info || !in || !rgb || !in->plane[0]) return fail(HEIFGPU_E_INVALID, "invalid argument");
-    if (info->chroma_format_idc > 1) return fail(HEIFGPU_E_UNSUPPORTED, "only 4:0:0 and 4:2:0");
-    if (info->chroma_format_idc == 1 && (!in->plane[1] || !in->plane[2])) return fail(HEIFGPU_E_INVALID, "missing chroma plane");
+    if (info->chroma_format_idc > 3) return fail(HEIFGPU_E_INVALID, "chroma_format_idc");
+    if (info->chroma_format_idc && (!in->plane[1] || !in->plane[2])) return fail(HEIFGPU_E_INVALID, "missing chroma plane");
     if (info->bit_depth < 8 || info->bit_depth > 16) return fail(HEIFGPU_E_INVALID, "bit depth");
     HIP_TRY(hipSetDevice(ctx->device));
     ColorArgs c{};
@@ -408,7 +410,7 @@ int heifgpu_ycbcr_to_rgb(heifgpu_ctx *ctx, const heifgpu_image_info *info, const
     c.out_w = (c.rotation & 1) ? c.h : c.w;
     c.out_h = (c.rotation & 1) ? c.w : c.h;
     if (rgb_pitch < 3 * c.out_w) return fail(HEIFGPU_E_INVALID, "rgb_pitch smaller than 3 * output width");
-    c.chroma = info->chroma_format_idc ? 1 : 0;
+    c.chroma = int32_t(info->chroma_format_idc);
     c.shift = int32_t(info->bit_depth) - 8;
     color_coefs(info->matrix_coeffs, info->full_range != 0, c);
     HIP_TRY(launch_ycbcr_rgb(c, int(info->bytes_per_sample), static_cast<hipStream_t>(stream)));
@@ -679,6 +681,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = hb.bps;
+    a.chroma_format = hb.chroma;
     b->out_host.assign(n, OutImage{});
     if (fresh) *inout = fresh.release();
     return HEIFGPU_OK;

@@ -47,7 +47,7 @@ struct SeqParams {
     int32_t width, height;        // pic_width/height_in_luma_samples
     int32_t log2_ctb, log2_min_cb, log2_min_tb, log2_max_tb;
     int32_t max_th_depth_intra;
-    int32_t chroma_format;        // 0 (4:0:0) or 1 (4:2:0)
+    int32_t chroma_format;        // chroma_format_idc: 0 (4:0:0), 1 (4:2:0), 2 (4:2:2), 3 (4:4:4)
     int32_t bit_depth_y, bit_depth_c;
     uint32_t flags;
     int32_t diff_cu_qp_delta_depth;
@@ -58,6 +58,11 @@ struct SeqParams {
     uint32_t sf_off;              // byte offset of this set's ScalingFactor block
     int32_t pad[3];
 };
+
+// log2 SubWidthC / SubHeightC of a chroma_format_idc (Table 6-1): a W x H
+// picture's chroma planes are (W >> chroma_sx) x (H >> chroma_sy)
+constexpr int chroma_sx(int fmt) { return fmt == 1 || fmt == 2 ? 1 : 0; }
+constexpr int chroma_sy(int fmt) { return fmt == 1 ? 1 : 0; }
 
 // Scaling factor block layout (bytes, from sf_off): for sizeId 0..3 and
 // matrixId 0..5, n*n factors m[y*n+x] (n = 4<<sizeId), in this order.

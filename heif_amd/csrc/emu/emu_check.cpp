@@ -42,7 +42,8 @@ int main(int argc, char **argv) {
     std::vector<int16_t> resid(hb.resid_elems);
     std::vector<SaoParams> sao(hb.sao_n);
     const int W = int(im.out_width), H = int(im.out_height), bps = hb.bps;
-    const int CW = (W + 1) / 2, CH = (H + 1) / 2;
+    const int SX = chroma_sx(hb.chroma), SY = chroma_sy(hb.chroma);
+    const int CW = (W + (1 << SX) - 1) >> SX, CH = (H + (1 << SY) - 1) >> SY;
     constexpr uint8_t kSentinel = 0xa5;
     std::vector<uint8_t> oy(size_t(W) * H * bps, kSentinel), ocb(size_t(CW) * CH * bps, kSentinel),
         ocr(size_t(CW) * CH * bps, kSentinel);
@@ -98,6 +99,7 @@ int main(int argc, char **argv) {
     a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = bps;
+    a.chroma_format = hb.chroma;
     emu_rbsp(a);
     emu_parse(a);
     uint32_t st = 0;
@@ -121,14 +123,15 @@ int main(int argc, char **argv) {
         for (const PicDesc &pd : hb.pics) {
             const SeqParams &sp = hb.seqs[pd.seq];
             for (int c = 0; c < 3; ++c) {
-                int sub = c ? 1 : 0, PW = sp.width >> sub, PH = sp.height >> sub;
+                if (c && !sp.chroma_format) break;
+                const int sx = c ? SX : 0, sy = c ? SY : 0, PW = sp.width >> sx, PH = sp.height >> sy;
                 size_t off = c == 0 ? 0 : size_t(sp.width) * sp.height + size_t(c - 1) * PW * PH;
-                int vw = std::min(sp.out_w, W - pd.out_x) >> sub, vh = std::min(sp.out_h, H - pd.out_y) >> sub;
+                int vw = std::min(sp.out_w, W - pd.out_x) >> sx, vh = std::min(sp.out_h, H - pd.out_y) >> sy;
                 for (int y = 0; y < vh; ++y)
                     for (int x = 0; x < vw; ++x) {
-                        size_t src = (off + size_t(y + (sp.conf_t >> sub)) * PW + x + (sp.conf_l >> sub)) * bps;
+                        size_t src = (off + size_t(y + (sp.conf_t >> sy)) * PW + x + (sp.conf_l >> sx)) * bps;
                         uint8_t *dst = reinterpret_cast<uint8_t *>(out.plane[c]) +
-                                       size_t((pd.out_y >> sub) + y) * out.pitch[c] + size_t((pd.out_x >> sub) + x) * bps;
+                                       size_t((pd.out_y >> sy) + y) * out.pitch[c] + size_t((pd.out_x >> sx) + x) * bps;
                         memcpy(dst, recon.data() + pd.recon_off + src, size_t(bps));
                     }
             }
@@ -147,11 +150,11 @@ int main(int argc, char **argv) {
         int pw = int(ref.pw[c]), ph = int(ref.ph[c]);
         long bad = 0;
         int fx = -1, fy = -1;
-        const int s = c ? 1 : 0;
+        const int sx = c ? SX : 0, sy = c ? SY : 0;
         for (int y = 0; y < ph; ++y)
             for (int x = 0; x < pw; ++x) {
                 int gv = bps == 1 ? g[size_t(y) * pw + x] : reinterpret_cast<const uint16_t *>(g)[size_t(y) * pw + x];
-                const uint32_t tile = uint32_t((y << s) / int(im.tile_height)) * im.cols + uint32_t((x << s) / int(im.tile_width));
+                const uint32_t tile = uint32_t((y << sy) / int(im.tile_height)) * im.cols + uint32_t((x << sx) / int(im.tile_width));
                 const int want = tile % tstride == toff ? int(ref.plane[c][size_t(y) * pw + x])
                                                         : (bps == 1 ? kSentinel : kSentinel * 0x101);
                 if (gv != want) {
@@ -161,9 +164,8 @@ int main(int argc, char **argv) {
             }
         printf("%s: %ld mismatches", names[c], bad);
         if (bad) {
-            int sub = c ? 2 : 1;
-            printf(" first at (%d,%d) tile (%d,%d) emu %d ref %d", fx, fy, fy * sub / int(im.tile_height),
-                   fx * sub / int(im.tile_width),
+            printf(" first at (%d,%d) tile (%d,%d) emu %d ref %d", fx, fy, (fy << sy) / int(im.tile_height),
+                   (fx << sx) / int(im.tile_width),
                    bps == 1 ? g[size_t(fy) * pw + fx] : 0, ref.plane[c][size_t(fy) * pw + fx]);
         }
         printf("\n");

@@ -119,7 +119,9 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
         const int ctb = 1 << sq.log2_ctb;
         const int wctb = (sq.width + ctb - 1) / ctb, hctb = (sq.height + ctb - 1) / ctb;
         const int w4 = (sq.width + 3) >> 2, h4 = (sq.height + 3) >> 2, w8 = (sq.width + 7) >> 3;
-        const uint64_t samples = uint64_t(sq.width) * sq.height * (sq.chroma_format ? 3 : 2) / 2;
+        const int cf = sq.chroma_format;
+        const uint64_t samples = uint64_t(sq.width) * sq.height +
+                                 (cf ? 2 * uint64_t(sq.width >> chroma_sx(cf)) * uint64_t(sq.height >> chroma_sy(cf)) : 0);
         pd.recon_off = hb.recon_bytes;
         hb.recon_bytes += (samples * uint64_t(hb.bps) + 255) & ~uint64_t(255);
         pd.map_off = hb.map_bytes;
@@ -139,9 +141,13 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
         PicDesc &p = hb.pics.back();
         hb.resid_elems += (samples + 127) & ~uint64_t(127);
         hb.rows += uint32_t(hctb);
-        // worst case per CTB row: every 8x8 CU split into four 4x4 luma TBs + 2 chroma TBs
-        p.tu_cap_row = uint32_t(wctb * (ctb / 8) * (ctb / 8) * 6 + 64);  // + staging trash slot / slack
-        p.coef_cap_row = uint32_t(wctb * ctb * ctb * 3 / 2 + 64);  // + staging trash slot / slack
+        // worst case per CTB row: every 8x8 CU split into four 4x4 luma TBs and
+        // their chroma TBs (2 with 4:2:0, 4 with 4:2:2, 8 with 4:4:4); a
+        // coefficient (or PCM sample) per sample
+        const int tbs8 = cf == 3 ? 12 : (cf == 2 ? 8 : 6);
+        p.tu_cap_row = uint32_t(wctb * (ctb / 8) * (ctb / 8) * tbs8 + 64);  // + staging trash slot / slack
+        const int ctb_samples = ctb * ctb + (cf ? 2 * (ctb >> chroma_sx(cf)) * (ctb >> chroma_sy(cf)) : 0);
+        p.coef_cap_row = uint32_t(wctb * ctb_samples + 64);  // + staging trash slot / slack
         hb.tu_n += uint64_t(p.tu_cap_row) * hctb;
         hb.coef_n += uint64_t(p.coef_cap_row) * hctb;
         hb.max_rows = std::max(hb.max_rows, hctb);

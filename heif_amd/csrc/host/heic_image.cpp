@@ -14,7 +14,6 @@ std::vector<uint8_t> nal_rbsp(const std::vector<uint8_t> &nal) {
 }
 
 void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p) {
-    if (s.chroma_format_idc == 2 || s.chroma_format_idc == 3) throw UnsupportedError("only 4:0:0 and 4:2:0 are supported");
     if (s.separate_colour_plane_flag) throw UnsupportedError("separate_colour_plane_flag");
     if (s.bit_depth_luma_minus8 != s.bit_depth_chroma_minus8) throw UnsupportedError("luma/chroma bit depth differ");
     if (s.range_extension_tools || p.range_extension_tools) throw UnsupportedError("range-extension coding tools");

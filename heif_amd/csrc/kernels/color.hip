@@ -7,7 +7,7 @@
 // rescaled by 255/219 and 255/224) in 16-bit fixed point with the
 // coefficients rounded on the host (ColorCoefs), so a test can restate it
 // exactly.  irot rotates anticlockwise by 90 degrees per unit (ISO/IEC
-// 23008-12 6.5.10).  4:2:0 chroma is replicated (nearest sample).
+// 23008-12 6.5.10).  Subsampled chroma (4:2:0, 4:2:2) is replicated (nearest sample).
 //
 // Mapping: one thread per 4 output pixels along a row (12-byte store as
 // three dwords when the row is 4-byte aligned).  HBM-bound: 1.5 bytes read
@@ -42,8 +42,9 @@ __global__ void __launch_bounds__(256) k_ycbcr_rgb(ColorArgs c) {
                                                              + (size_t)x * sizeof(Pel))) >> c.shift;
         int cb = 0, cr = 0;
         if (c.chroma) {
-            const size_t o1 = (size_t)(y >> 1) * c.pitch[1] + (size_t)(x >> 1) * sizeof(Pel);
-            const size_t o2 = (size_t)(y >> 1) * c.pitch[2] + (size_t)(x >> 1) * sizeof(Pel);
+            const int xc = x >> chroma_sx(c.chroma), yc = y >> chroma_sy(c.chroma);
+            const size_t o1 = (size_t)yc * c.pitch[1] + (size_t)xc * sizeof(Pel);
+            const size_t o2 = (size_t)yc * c.pitch[2] + (size_t)xc * sizeof(Pel);
             cb = ((int)*reinterpret_cast<const Pel *>(reinterpret_cast<const uint8_t *>(Cb) + o1) >> c.shift) - 128;
             cr = ((int)*reinterpret_cast<const Pel *>(reinterpret_cast<const uint8_t *>(Cr) + o2) >> c.shift) - 128;
         }

@@ -22,11 +22,11 @@ __global__ void __launch_bounds__(256) k_gather_tiles(GatherArgs g) {
     const int c = (int)blockIdx.z;
     const int k = g.offset + (int)blockIdx.y * g.stride;
     if (c >= g.planes || k >= g.n_tiles) return;
-    const int sh = c ? 1 : 0;  // 4:2:0 chroma halves both axes
-    const int pw = (g.W + sh) >> sh, ph = (g.H + sh) >> sh;
-    const int x0 = ((k % g.cols) * g.tw) >> sh, y0 = ((k / g.cols) * g.th) >> sh;
+    const int sx = c ? g.sx : 0, sy = c ? g.sy : 0;  // chroma subsampling (log2)
+    const int pw = (g.W + (1 << sx) - 1) >> sx, ph = (g.H + (1 << sy) - 1) >> sy;
+    const int x0 = ((k % g.cols) * g.tw) >> sx, y0 = ((k / g.cols) * g.th) >> sy;
     if (x0 >= pw || y0 >= ph) return;  // a tile wholly inside the crop
-    const int w = min(g.tw >> sh, pw - x0), h = min(g.th >> sh, ph - y0);
+    const int w = min(g.tw >> sx, pw - x0), h = min(g.th >> sy, ph - y0);
     const int y = (int)blockIdx.x * 4 + (int)threadIdx.y;
     if (y >= h) return;
     const size_t wb = (size_t)w * (size_t)g.bps;

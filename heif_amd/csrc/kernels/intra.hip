@@ -47,7 +47,7 @@ struct alignas(16) IntraScratch {
 
 // Per-wave LDS block: scratch, then per component the CTU window.
 struct WinLayout {
-    int cs[3];                                   // component CTB size
+    int csx[3], csy[3];                          // component CTB width, height
     uint32_t cur[3], left[3], above[3], res[3];  // byte offsets in the block
     uint32_t bytes;                              // block size (16-aligned)
 };
@@ -62,15 +62,17 @@ WinLayout win_layout(int log2ctb, int chroma, int bps) {
     uint32_t o = (uint32_t)((sizeof(IntraScratch) + 15) & ~size_t(15));
     const int ncomp = chroma ? 3 : 1;
     for (int k = 0; k < 3; ++k) {
-        const int cs = k == 0 ? (1 << log2ctb) : (chroma ? (1 << log2ctb) >> 1 : 0);
-        L.cs[k] = cs;
+        const int cx = k == 0 ? (1 << log2ctb) : (chroma ? (1 << log2ctb) >> chroma_sx(chroma) : 0);
+        const int cy = k == 0 ? (1 << log2ctb) : (chroma ? (1 << log2ctb) >> chroma_sy(chroma) : 0);
+        L.csx[k] = cx;
+        L.csy[k] = cy;
         if (k >= ncomp) continue;
         L.cur[k] = o;
-        o += (uint32_t)(cs * cs * bps + 15) & ~15u;
+        o += (uint32_t)(cx * cy * bps + 15) & ~15u;
         L.left[k] = o;
-        o += (uint32_t)(cs * bps + 15) & ~15u;
+        o += (uint32_t)(cy * bps + 15) & ~15u;
         L.above[k] = o;
-        o += (uint32_t)((2 * cs + 1) * bps + 15) & ~15u;
+        o += (uint32_t)((2 * cx + 1) * bps + 15) & ~15u;
         // residuals are read from the k_transform planes, not staged here: half
         // the block, so twice the workgroups fit beside the next decode's k_parse
         L.res[k] = 0;
@@ -139,7 +141,8 @@ template <typename Pel>
 struct Win {
     Pel *cur, *left, *above;
     const int16_t *res;  // the component's residual plane (k_transform), pitch = plane width
-    int cs, cx0, cy0;    // CTB size and origin in component samples
+    int csx, csy;        // CTB width, height in component samples (4:2:2 chroma: csy = 2 csx)
+    int cx0, cy0;        // CTB origin in component samples
     // a decoded neighbour (xn, yn) in picture coordinates; only called for
     // available samples, which lie in the row above, the column to the left
     // or the current CTU
@@ -147,21 +150,22 @@ struct Win {
         const int lx = xn - cx0, ly = yn - cy0;
         if (ly < 0) return above[lx + 1];
         if (lx < 0) return left[ly];
-        return cur[ly * cs + lx];
+        return cur[ly * csx + lx];
     }
 };
 
 template <typename Pel>
 __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L, const TuRec &tu, const Win<Pel> &w,
                                                                  int PW, int PH, int cidx, int bd, bool strong,
-                                                                 int log2ctb, int min_tb, int wctb, int lane) {
+                                                                 int chroma, int lane) {
     const int log2n = tu.log2, n = 1 << log2n, mode = tu.mode;
     const int x0 = tu.x, y0 = tu.y;
-    const int sub = cidx ? 1 : 0;  // 4:2:0 chroma → luma = 2x
-    const int bx0 = w.cx0 << sub, by0 = w.cy0 << sub, csl = w.cs << sub;
+    // component → luma coordinates (6.4.1 takes luma locations)
+    const int subx = cidx ? chroma_sx(chroma) : 0, suby = cidx ? chroma_sy(chroma) : 0;
+    const int bx0 = w.cx0 << subx, by0 = w.cy0 << suby, csl = w.csx << subx;
     const int ns = 4 * n + 1;
     const bool cbf = (tu.flags & TU_CBF) != 0;
-    const int zc = zidx(((x0 << sub) - bx0) >> 2, ((y0 << sub) - by0) >> 2);
+    const int zc = zidx(((x0 << subx) - bx0) >> 2, ((y0 << suby) - by0) >> 2);
     // residual of a 4x4 / 8x8 TB (one sample per lane): loaded now, used after
     // the neighbour and filter phases, so the load latency hides behind them
     const int r0 = (cbf && n <= 8 && lane < n * n) ? w.res[(size_t)(y0 + (lane >> log2n)) * PW + x0 + (lane & (n - 1))] : 0;
@@ -184,7 +188,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
                 xn = x0 + s - 2 * n - 1;
                 yn = y0 - 1;
             }
-            sa[s] = xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(zc, xn << sub, yn << sub, bx0, by0, csl);
+            sa[s] = xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(zc, xn << subx, yn << suby, bx0, by0, csl);
             sv[s] = sa[s] ? w.fetch(xn, yn) : 0;
             any_av |= sa[s];
         }
@@ -217,7 +221,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             yn = y0 - 1;
         }
         const bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
-                        nb_avail(zc, xn << sub, yn << sub, bx0, by0, csl);
+                        nb_avail(zc, xn << subx, yn << suby, bx0, by0, csl);
         const int val = av ? w.fetch(xn, yn) : 0;
         const uint64_t msk = __ballot(av);
         int sl = lane;
@@ -252,7 +256,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             xn = x0 + s - 2 * n - 1;
             yn = y0 - 1;
         }
-        bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(zc, xn << sub, yn << sub, bx0, by0, csl);
+        bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(zc, xn << subx, yn << suby, bx0, by0, csl);
         val[k] = av ? w.fetch(xn, yn) : 0;
         msk[k] = __ballot(av);
     }
@@ -297,14 +301,14 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     }
 #endif
     wave_sync();
-    // 3. filtering (8.4.4.2.3), luma only for 4:2:0
+    // 3. filtering (8.4.4.2.3): luma, and chroma with 4:4:4
     const int16_t *lf = L->left, *tp = L->top;
-    if (cidx == 0 && mode != 1 && n != 4) {
+    if ((cidx == 0 || chroma == 3) && mode != 1 && n != 4) {
         const int dist = min(abs(mode - 26), abs(mode - 10));
         const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
         if (dist > thr) {
             const int c = L->left[0];
-            const bool bi = strong && n == 32 && abs(c + L->top[64] - 2 * L->top[32]) < (1 << (bd - 5)) &&
+            const bool bi = strong && cidx == 0 && n == 32 && abs(c + L->top[64] - 2 * L->top[32]) < (1 << (bd - 5)) &&
                             abs(c + L->left[64] - 2 * L->left[32]) < (1 << (bd - 5));
             for (int i = lane; i <= 2 * n; i += kWave) {
                 int a, b;
@@ -371,7 +375,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
                 if (mode == 10 && y == 0) pv = min(max(lf[1] + ((tp[1 + x] - tp[0]) >> 1), 0), maxv);
             }
         }
-        const int li = (ly0 + y) * w.cs + lx0 + x;
+        const int li = (ly0 + y) * w.csx + lx0 + x;
         if (tu.flags & TU_PCM) pv = 0;  // the residual is the PCM sample itself
         if (cbf) pv += (n <= 8 && o == lane) ? r0 : w.res[(size_t)(y0 + y) * PW + x0 + x];
         pv = min(max(pv, 0), maxv);
@@ -404,12 +408,13 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     w.left = h ? wr.left : wb.left;
     w.above = h ? wr.above : wb.above;
     w.res = h ? wr.res : wb.res;
-    w.cs = wb.cs;
+    w.csx = wb.csx;
+    w.csy = wb.csy;
     w.cx0 = wb.cx0;
     w.cy0 = wb.cy0;
     const bool cbf = ((h ? tr.flags : tb.flags) & TU_CBF) != 0;
     const bool pcm = ((h ? tr.flags : tb.flags) & TU_PCM) != 0;
-    const int bx0 = w.cx0 << 1, by0 = w.cy0 << 1, csl = w.cs << 1;
+    const int bx0 = w.cx0 << 1, by0 = w.cy0 << 1, csl = w.csx << 1;
     const int ns = 4 * n + 1, nch = n == 8 ? 2 : 1;
     const int zc = zidx(((x0 << 1) - bx0) >> 2, ((y0 << 1) - by0) >> 2);
     // residuals (sample sl and sl + 32 of this half), used after the neighbour phase
@@ -497,7 +502,7 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
             if (pcm) pv = 0;  // the residual is the PCM sample itself
             if (cbf) pv += it ? r1 : r0;
             pv = min(max(pv, 0), maxv);
-            w.cur[(ly0 + y) * w.cs + lx0 + x] = (Pel)pv;
+            w.cur[(ly0 + y) * w.csx + lx0 + x] = (Pel)pv;
         }
     }
     wave_sync();
@@ -534,7 +539,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
     const int W = sp.width, H = sp.height, log2ctb = sp.log2_ctb;
     const int wctb = (W + (1 << log2ctb) - 1) >> log2ctb, hctb = (H + (1 << log2ctb) - 1) >> log2ctb;
     const int chroma = sp.chroma_format;
-    const int cw = chroma ? W >> 1 : 0, ch = chroma ? H >> 1 : 0;
+    const int cw = chroma ? W >> chroma_sx(chroma) : 0, ch = chroma ? H >> chroma_sy(chroma) : 0;
     const int ncomp = chroma ? 3 : 1;
     Pel *planes[3];
     planes[0] = reinterpret_cast<Pel *>(a.recon + pd.recon_off);
@@ -553,7 +558,8 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
         win[k].left = reinterpret_cast<Pel *>(blk + lay.left[k]);
         win[k].above = reinterpret_cast<Pel *>(blk + lay.above[k]);
         win[k].res = resp[k];
-        win[k].cs = lay.cs[k];
+        win[k].csx = lay.csx[k];
+        win[k].csy = lay.csy[k];
     }
     progress[wave] = 0;  // every lane writes the same value
     __syncthreads();
@@ -595,23 +601,23 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                         if (k >= ncomp) break;
                         const Win<Pel> &w = win[k];
                         const int PW = k ? cw : W, PH = k ? ch : H;
-                        const int vw = min(w.cs, PW - w.cx0), vh = min(w.cs, PH - w.cy0);
-                        if (vw == w.cs && !(PW & 3) &&
+                        const int vw = min(w.csx, PW - w.cx0), vh = min(w.csy, PH - w.cy0);
+                        if (vw == w.csx && !(PW & 3) &&
                             !(reinterpret_cast<uintptr_t>(planes[k]) & (4 * sizeof(Pel) - 1))) {
                             // full-width CTU: four samples per lane, one 4- (8-) byte store
-                            const int lq = __builtin_ctz((unsigned)w.cs) - 2;
+                            const int lq = __builtin_ctz((unsigned)w.csx) - 2;
                             for (int o = lane; o < (vh << lq); o += kWave) {
                                 const int x = (o & ((1 << lq) - 1)) << 2, y = o >> lq;
                                 *reinterpret_cast<Quad<Pel> *>(planes[k] + (size_t)(w.cy0 + y) * PW + w.cx0 + x) =
-                                    *reinterpret_cast<const Quad<Pel> *>(w.cur + y * w.cs + x);
+                                    *reinterpret_cast<const Quad<Pel> *>(w.cur + y * w.csx + x);
                             }
                         } else {
                             for (int o = lane; o < vw * vh; o += kWave) {
                                 const int x = o % vw, y = o / vw;
-                                planes[k][(size_t)(w.cy0 + y) * PW + w.cx0 + x] = w.cur[y * w.cs + x];
+                                planes[k][(size_t)(w.cy0 + y) * PW + w.cx0 + x] = w.cur[y * w.csx + x];
                             }
                         }
-                        for (int y = lane; y < w.cs; y += kWave) w.left[y] = w.cur[y * w.cs + w.cs - 1];
+                        for (int y = lane; y < w.csy; y += kWave) w.left[y] = w.cur[y * w.csx + w.csx - 1];
                     }
                     wave_sync();
                     HG_FENCE_REL();
@@ -635,10 +641,10 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                     if (k >= ncomp) break;
                     Win<Pel> &w = win[k];
                     const int PW = k ? cw : W, PH = k ? ch : H;
-                    w.cx0 = c * w.cs;
-                    w.cy0 = r * w.cs;
+                    w.cx0 = c * w.csx;
+                    w.cy0 = r * w.csy;
                     const int yg = w.cy0 - 1;
-                    for (int i = lane; i <= 2 * w.cs; i += kWave) {
+                    for (int i = lane; i <= 2 * w.csx; i += kWave) {
                         const int xg = w.cx0 - 1 + i;
                         w.above[i] = (yg >= 0 && xg >= 0 && xg < PW) ? planes[k][(size_t)yg * PW + xg] : (Pel)0;
                     }
@@ -655,14 +661,15 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
             w.left = cidx == 0 ? win[0].left : (cidx == 1 ? win[1].left : win[2].left);
             w.above = cidx == 0 ? win[0].above : (cidx == 1 ? win[1].above : win[2].above);
             w.res = cidx == 0 ? win[0].res : (cidx == 1 ? win[1].res : win[2].res);
-            w.cs = cidx == 0 ? win[0].cs : (cidx == 1 ? win[1].cs : win[2].cs);
+            w.csx = cidx == 0 ? win[0].csx : (cidx == 1 ? win[1].csx : win[2].csx);
+            w.csy = cidx == 0 ? win[0].csy : (cidx == 1 ? win[1].csy : win[2].csy);
             w.cx0 = cidx == 0 ? win[0].cx0 : (cidx == 1 ? win[1].cx0 : win[2].cx0);
             w.cy0 = cidx == 0 ? win[0].cy0 : (cidx == 1 ? win[1].cy0 : win[2].cy0);
             const int PW = cidx ? cw : W, PH = cidx ? ch : H;
             // a TB must lie inside the picture and inside its CTU window
             if (tu.log2 < 2 || tu.log2 > 5 || tu.x + (1 << tu.log2) > PW || tu.y + (1 << tu.log2) > PH ||
-                tu.x < w.cx0 || tu.y < w.cy0 || tu.x + (1 << tu.log2) > w.cx0 + w.cs ||
-                tu.y + (1 << tu.log2) > w.cy0 + w.cs)
+                tu.x < w.cx0 || tu.y < w.cy0 || tu.x + (1 << tu.log2) > w.cx0 + w.csx ||
+                tu.y + (1 << tu.log2) > w.cy0 + w.csy)
                 continue;
 #if !defined(HG_HOST_EMU) && !defined(HG_INTRA_NO_PAIR)
             // a 4x4 / 8x8 Cb TB followed by its Cr TB (same TU; the next record of this 64-record block):
@@ -683,8 +690,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                 }
             }
 #endif
-            predict_tb<Pel>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, log2ctb,
-                            sp.log2_min_tb, wctb, lane);
+            predict_tb<Pel>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, chroma, lane);
         }
         HG_FENCE_REL();
         hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
@@ -706,12 +712,12 @@ static int intra_launch_waves(const BatchArgs &a) {
     }();
     int cap = forced > 0 ? forced : kResidentIntraWaves / (a.n_pics > 0 ? a.n_pics : 1);
     if (forced <= 0) cap = cap < 2 ? 2 : cap;
-    const int nw = intra_waves(a.max_log2ctb, 1, a.bytes_per_sample, a.max_rows);
+    const int nw = intra_waves(a.max_log2ctb, a.chroma_format, a.bytes_per_sample, a.max_rows);
     return cap < nw ? cap : nw;
 }
 
 static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
-    return 64 + (size_t)nw * win_layout(a.max_log2ctb, 1, a.bytes_per_sample).bytes;
+    return 64 + (size_t)nw * win_layout(a.max_log2ctb, a.chroma_format, a.bytes_per_sample).bytes;
 }
 
 #if defined(HG_HOST_EMU)

@@ -49,6 +49,7 @@ struct BatchArgs {
     int max_rows;              // CTB rows, batch max
     int total_rows;            // sum of CTB rows over pictures
     int bytes_per_sample;      // 1 or 2
+    int chroma_format;         // chroma_format_idc, shared by the batch's pictures
     int parse_group;           // k_parse_lanes pictures per wave (lanes_parse_order's choice; launch_parse otherwise)
     int max_log2ctb;           // largest CTB size in the batch (sizes k_intra's LDS)
     int lane_rows;             // k_parse_lanes lanes per picture: max over pictures of (WPP ? min(rows, 64) : 1)
@@ -69,7 +70,7 @@ struct ColorArgs {
     int32_t w, h;            // decoded (coded-orientation) size
     int32_t out_w, out_h;    // rotated size
     int32_t rotation;        // irot, anticlockwise 90-degree units
-    int32_t chroma, shift;   // chroma present; bit depth - 8
+    int32_t chroma, shift;   // chroma_format_idc (0: no chroma planes); bit depth - 8
     int32_t yoff, ys;        // luma offset (16 limited range / 0 full) and scale (16.16)
     int32_t cr_r, cb_g, cr_g, cb_b;  // H.273 chroma weights (16.16, limited range rescaled)
 };
@@ -77,7 +78,8 @@ struct ColorArgs {
 struct GatherArgs {
     uint64_t dst[3], src[3];  // planes (device pointers; src may be a peer / IPC mapping)
     int32_t dpitch[3], spitch[3];
-    int32_t planes, bps;      // 1 or 3 planes (4:0:0 / 4:2:0), bytes per sample
+    int32_t planes, bps;      // 1 or 3 planes, bytes per sample
+    int32_t sx, sy;           // log2 chroma subsampling (chroma_sx / chroma_sy)
     int32_t W, H;             // luma output size
     int32_t tw, th, cols, n_tiles, stride, offset;
 };

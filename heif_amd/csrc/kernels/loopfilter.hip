@@ -102,7 +102,8 @@ __global__ void __launch_bounds__(256) k_assemble(BatchArgs a) {
     const SeqParams sp = a.seqs[pd.seq];
     const int W = sp.width, H = sp.height, w4 = (W + 3) >> 2, h4 = (H + 3) >> 2;
     const int wctb = (W + (1 << sp.log2_ctb) - 1) >> sp.log2_ctb;
-    const int cw = sp.chroma_format ? W >> 1 : 0, ch = sp.chroma_format ? H >> 1 : 0;
+    const int sx = chroma_sx(sp.chroma_format), sy = chroma_sy(sp.chroma_format);
+    const int cw = sp.chroma_format ? W >> sx : 0, ch = sp.chroma_format ? H >> sy : 0;
     Pel *dY = reinterpret_cast<Pel *>(a.recon + pd.recon_off);
     uint8_t *dmap = a.maps + pd.map_off;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x, nth = gridDim.x * blockDim.x;
@@ -110,9 +111,9 @@ __global__ void __launch_bounds__(256) k_assemble(BatchArgs a) {
         const PicDesc cd = a.pics[pd.child0 + c];
         const SeqParams cs = a.seqs[cd.seq];
         const int cW = cs.width, cH = cs.height, cw4 = (cW + 3) >> 2, ch4 = (cH + 3) >> 2;
-        const int ccw = cs.chroma_format ? cW >> 1 : 0, cch = cs.chroma_format ? cH >> 1 : 0;
+        const int ccw = cs.chroma_format ? cW >> sx : 0, cch = cs.chroma_format ? cH >> sy : 0;
         const Pel *sY = reinterpret_cast<const Pel *>(a.recon + cd.recon_off);
-        // samples: Y then Cb, Cr (origins are CTB-aligned, so chroma at org / 2)
+        // samples: Y then Cb, Cr (origins are CTB-aligned, so chroma at org >> sx, sy)
         const int nl = cW * cH, nc = ccw * cch;
         for (int t = tid; t < nl + 2 * nc; t += nth) {
             if (t < nl) {
@@ -120,7 +121,7 @@ __global__ void __launch_bounds__(256) k_assemble(BatchArgs a) {
                 dY[(size_t)(cd.org_y + y) * W + cd.org_x + x] = sY[t];
             } else {
                 const int u = t - nl, k = u / nc, v = u % nc, x = v % ccw, y = v / ccw;
-                dY[(size_t)W * H + (size_t)k * cw * ch + (size_t)((cd.org_y >> 1) + y) * cw + (cd.org_x >> 1) + x] = sY[t];
+                dY[(size_t)W * H + (size_t)k * cw * ch + (size_t)((cd.org_y >> sy) + y) * cw + (cd.org_x >> sx) + x] = sY[t];
             }
         }
         // QpY and edge flags (4x4 units), then SAO parameters (CTBs)
@@ -155,13 +156,17 @@ __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
     const int8_t *qpy = reinterpret_cast<const int8_t *>(a.maps + pd.map_off);
     const uint8_t *flg = a.maps + pd.map_off + (size_t)w4 * h4;
     Pel *Y = reinterpret_cast<Pel *>(a.recon + pd.recon_off);
-    const int cw = sp.chroma_format ? W >> 1 : 0, ch = sp.chroma_format ? H >> 1 : 0;
+    const int sx = chroma_sx(sp.chroma_format), sy = chroma_sy(sp.chroma_format);
+    const int cw = sp.chroma_format ? W >> sx : 0, ch = sp.chroma_format ? H >> sy : 0;
     // luma segments
     const int ne_l = VERT ? (W - 1) >> 3 : (H - 1) >> 3;  // edges excluding the picture boundary
     const int ns_l = VERT ? H >> 2 : W >> 2;               // 4-sample segments along each edge
     const int nl = ne_l * ns_l;
+    // chroma: edges on the 8x8 chroma-sample grid, segments of the lines one
+    // 4-line luma segment covers (bS, QpY and flags come from that segment)
     const int ne_c = VERT ? (cw - 1) >> 3 : (ch - 1) >> 3;
-    const int ns_c = VERT ? ch >> 1 : cw >> 1;             // 2-sample chroma segments (= 4 luma)
+    const int lc = VERT ? 4 >> sy : 4 >> sx;
+    const int ns_c = VERT ? ch / lc : cw / lc;
     const int nc = sp.chroma_format ? ne_c * ns_c : 0;
     const int total = nl + 2 * nc;
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
@@ -187,12 +192,12 @@ __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
             int xc, yc;
             if (VERT) {
                 xc = 8 * (v % ne_c + 1);
-                yc = 2 * (v / ne_c);
+                yc = lc * (v / ne_c);
             } else {
-                xc = 2 * (v % ns_c);
+                xc = lc * (v % ns_c);
                 yc = 8 * (v / ns_c + 1);
             }
-            const int xl = xc << 1, yl = yc << 1;
+            const int xl = xc << sx, yl = yc << sy;
             const int fq = flg[(yl >> 2) * w4 + (xl >> 2)];
             if (!(fq & (VERT ? MF_EDGE_V : MF_EDGE_H))) continue;
             const int xlp = VERT ? xl - 1 : xl, ylp = VERT ? yl : yl - 1;
@@ -205,11 +210,11 @@ __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
             const int maxv = (1 << bd) - 1;
             Pel *C = Y + (size_t)W * H + (size_t)(cidx - 1) * cw * ch;
             Pel *q = C + (size_t)yc * cw + xc;
-            const int sx = VERT ? 1 : cw, sk = VERT ? cw : 1;
-            for (int k = 0; k < 2; ++k) {
-                const int p0 = q[k * sk - sx], p1 = q[k * sk - 2 * sx], q0 = q[k * sk], q1 = q[k * sk + sx];
+            const int sa = VERT ? 1 : cw, sk = VERT ? cw : 1;  // across / along the edge
+            for (int k = 0; k < lc; ++k) {
+                const int p0 = q[k * sk - sa], p1 = q[k * sk - 2 * sa], q0 = q[k * sk], q1 = q[k * sk + sa];
                 const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
-                if (!(fp & MF_NOFILT)) q[k * sk - sx] = (Pel)clip3(0, maxv, p0 + delta);
+                if (!(fp & MF_NOFILT)) q[k * sk - sa] = (Pel)clip3(0, maxv, p0 + delta);
                 if (!(fq & MF_NOFILT)) q[k * sk] = (Pel)clip3(0, maxv, q0 - delta);
             }
         }
@@ -218,13 +223,13 @@ __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
 
 // SAO (8.7.3) of one sample at picture position (xs, ys) of component cidx
 template <typename Pel>
-__device__ __forceinline__ int sao_sample(const Pel *P, int PW, int PH, int xs, int ys, int cidx, int sub,
-                                          const SaoParams *sao, int wctb, int log2ctb, const uint8_t *flg, int w4,
-                                          int bd) {
+__device__ __forceinline__ int sao_sample(const Pel *P, int PW, int PH, int xs, int ys, int cidx, int subx,
+                                          int suby, const SaoParams *sao, int wctb, int log2ctb, const uint8_t *flg,
+                                          int w4, int bd) {
     int v = P[(size_t)ys * PW + xs];
-    const SaoParams &s = sao[(ys >> (log2ctb - sub)) * wctb + (xs >> (log2ctb - sub))];
+    const SaoParams &s = sao[(ys >> (log2ctb - suby)) * wctb + (xs >> (log2ctb - subx))];
     const int type = s.type[cidx];
-    if (!type || (flg[((ys << sub) >> 2) * w4 + ((xs << sub) >> 2)] & MF_NOFILT)) return v;
+    if (!type || (flg[((ys << suby) >> 2) * w4 + ((xs << subx) >> 2)] & MF_NOFILT)) return v;
     int o = 0;
     if (type == 2) {
         const int cl = s.band_eo[cidx];
@@ -260,12 +265,14 @@ __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
     const int w4 = (W + 3) >> 2, h4 = (H + 3) >> 2;
     const uint8_t *flg = a.maps + pd.map_off + (size_t)w4 * h4;
     const Pel *Y = reinterpret_cast<const Pel *>(a.recon + pd.recon_off);
-    const int cw = sp.chroma_format ? W >> 1 : 0, ch = sp.chroma_format ? H >> 1 : 0;
+    const int sx = chroma_sx(sp.chroma_format), sy = chroma_sy(sp.chroma_format);
+    const int cw = sp.chroma_format ? W >> sx : 0, ch = sp.chroma_format ? H >> sy : 0;
     const SaoParams *sao = a.sao + pd.sao_off;
     // visible region of this picture in the output image (luma)
     const int vw = min(sp.out_w, oi.width - pd.out_x), vh = min(sp.out_h, oi.height - pd.out_y);
     if (vw <= 0 || vh <= 0) return;
-    const int vcw = sp.chroma_format ? (vw + 1) >> 1 : 0, vch = sp.chroma_format ? (vh + 1) >> 1 : 0;
+    const int vcw = sp.chroma_format ? (vw + (1 << sx) - 1) >> sx : 0;
+    const int vch = sp.chroma_format ? (vh + (1 << sy) - 1) >> sy : 0;
     const int qw = (vw + 3) >> 2, qcw = (vcw + 3) >> 2;  // quads per row
     const int nl = qw * vh, nc = qcw * vch;
     const int total = nl + 2 * nc;
@@ -281,12 +288,12 @@ __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
             q = (u % nc) % qcw;
             y = (u % nc) / qcw;
         }
-        const int sub = cidx ? 1 : 0;
+        const int subx = cidx ? sx : 0, suby = cidx ? sy : 0;
         const int PW = cidx ? cw : W, PH = cidx ? ch : H;
         const int vwc = cidx ? vcw : vw;
         const Pel *P = cidx == 0 ? Y : Y + (size_t)W * H + (size_t)(cidx - 1) * cw * ch;
         const int x0 = q * 4, n = min(4, vwc - x0);
-        const int ys = y + (sp.conf_t >> sub), xs0 = x0 + (sp.conf_l >> sub);  // picture coords
+        const int ys = y + (sp.conf_t >> suby), xs0 = x0 + (sp.conf_l >> subx);  // picture coords
         const bool on = pd.sao_luma || pd.sao_chroma;  // SaoTypeIdx is 0 for a component whose flag is off
         const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
         int v[4];
@@ -294,14 +301,14 @@ __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
         for (int j = 0; j < 4; ++j) {
             v[j] = 0;
             if (j < n)
-                v[j] = on ? sao_sample(P, PW, PH, xs0 + j, ys, cidx, sub, sao, wctb, log2ctb, flg, w4, bd)
+                v[j] = on ? sao_sample(P, PW, PH, xs0 + j, ys, cidx, subx, suby, sao, wctb, log2ctb, flg, w4, bd)
                           : (int)P[(size_t)ys * PW + xs0 + j];
         }
         // component fields by select: a lane-varying index into the OutImage copy made
         // the compiler keep it in LDS (12 KB per workgroup, 519 M bank-conflict cycles per launch)
         const uint64_t plane = cidx == 0 ? oi.plane[0] : (cidx == 1 ? oi.plane[1] : oi.plane[2]);
         const int pitch = cidx == 0 ? oi.pitch[0] : (cidx == 1 ? oi.pitch[1] : oi.pitch[2]);
-        const int ox = (pd.out_x >> sub) + x0, oy = (pd.out_y >> sub) + y;
+        const int ox = (pd.out_x >> subx) + x0, oy = (pd.out_y >> suby) + y;
         Pel *dst = reinterpret_cast<Pel *>(plane + (size_t)oy * pitch) + ox;
         if (n == 4 && (reinterpret_cast<uintptr_t>(dst) & (4 * sizeof(Pel) - 1)) == 0) {
             if (sizeof(Pel) == 1)

@@ -87,6 +87,7 @@ struct alignas(16) LaneLds {
 struct LanePic {
     int W, H, log2ctb, wctb, hctb, minCb, minTb, maxTb, maxDepthIntra, chroma;
     int log2qg, bdY, bdC, qpbdY, qpbdC, pcmMin, pcmMax, pcmBdY, pcmBdC, cbOff, crOff, sliceQp;
+    int subx, suby;  // log2 SubWidthC, SubHeightC (Table 6-1)
     int w4, h4, w8, saoL, saoC;
     int R, lane0, ring;  // lanes of the picture, its first lane, rows wrap round the lanes (WPP rows > R)
     uint32_t flags, bits_off, bits_end, sub_first, row_off, tu_cap, coef_cap, pic;
@@ -151,7 +152,7 @@ struct Lane {
     // coding quadtree / transform tree node
     int qx, qy, ql, qd;
     int tx, ty, tl, td;
-    uint32_t tcbf;  // cbf_cb | cbf_cr << 1 of the transform tree node at depth d, at bit 2d
+    uint32_t tcbf;  // cbf_cb | cbf_cr << 1 (| the 4:2:2 lower TBs' << 2, << 3) of the node at depth d, at bit 4d
     // quantization (8.6.1)
     int qp_prev_last, qp_pred, cu_qp_delta_val, qpy_cur, qg_x, qg_y;
     // coding unit: IntraPredModeY of PB k in byte k, IntraPredModeC
@@ -689,6 +690,14 @@ HG_HD inline int term(Lane &L, const EG &G) {
 }
 
 // ------------------------------------------------------------------ derivations
+// Table 8-3: IntraPredModeC of 4:2:2 from the 4:2:0-style derivation, 35 modes
+// packed four per word as bytes
+HG_HD inline int mode422(int m) {
+    constexpr uint32_t t[9] = {0x02020100u, 0x05030202u, 0x0b0a0807u, 0x12100f0du, 0x16151413u,
+                               0x18181717u, 0x1b1a1919u, 0x1d1c1c1bu, 0x001f1e1du};
+    return (int)((t[m >> 2] >> (8 * (m & 3))) & 0xffu);
+}
+
 HG_HD inline int chroma_qp_map(int qpi, int chroma) {
     if (chroma != 1) return qpi < 51 ? qpi : 51;
     if (qpi < 30) return qpi;
@@ -1004,13 +1013,16 @@ HG_HD inline void pcm_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     // bits consumed so far: 8 * end - budget - k (absolute RBSP bit position)
     uint32_t bit = (uint32_t)(8 * (int32_t)P.bits_end - L.budget - L.k + 7) & ~7u;
     L.fl = (L.fl | F_PCM | F_TB_CBF) & ~F_TS;
-    const int ncomp = P.chroma ? 3 : 1;
-    for (int c = 0; c < ncomp; ++c) {
-        const int l2 = c ? L.ql - 1 : L.ql, m = 1 << l2;
+    // luma, then Cb and Cr; a 4:2:2 chroma block (raster, m wide, 2m tall) is
+    // two stacked square TBs
+    const int ntb = P.chroma == 0 ? 1 : (P.chroma == 2 ? 5 : 3), nh = P.chroma == 2 ? 2 : 1;
+    for (int t = 0; t < ntb; ++t) {
+        const int c = t == 0 ? 0 : 1 + (t - 1) / nh, h = t == 0 ? 0 : (t - 1) % nh;
+        const int l2 = (c && P.chroma != 3) ? L.ql - 1 : L.ql, m = 1 << l2;
         const int pbd = c ? P.pcmBdC : P.pcmBdY, sh = (c ? P.bdC : P.bdY) - pbd;
         L.tb_cidx = c;
-        L.tb_x = c ? L.qx >> 1 : L.qx;
-        L.tb_y = c ? L.qy >> 1 : L.qy;
+        L.tb_x = c ? L.qx >> P.subx : L.qx;
+        L.tb_y = c ? (L.qy >> P.suby) + (h << l2) : L.qy;
         L.tb_log2 = l2;
         L.tb_mode = 1;
         L.tb_coef0 = L.ncoef;
@@ -1094,17 +1106,23 @@ HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         }
     }
     L.cu_modes = modes;
-    if (P.chroma) {
-        const int icpm = dec(L, G, CTX_CHROMA_MODE) ? (int)byp_bits(L, G, 2) : 4;
-        const int lm = modes & 0xff;
-        int cm;
-        if (icpm == 4) {
-            cm = lm;
-        } else {
-            cm = icpm == 0 ? 0 : (icpm == 1 ? 26 : (icpm == 2 ? 10 : 1));
-            if (cm == lm) cm = 34;
+    if (P.chroma) {  // intra_chroma_pred_mode: per PB with 4:4:4, else per CU; 8.4.3
+        const int nc = P.chroma == 3 ? np : 1;
+        int cms = 0;
+        for (int i = 0; i < nc; ++i) {
+            const int icpm = dec(L, G, CTX_CHROMA_MODE) ? (int)byp_bits(L, G, 2) : 4;
+            const int lm = (modes >> (8 * i)) & 0xff;
+            int cm;
+            if (icpm == 4) {
+                cm = lm;
+            } else {
+                cm = icpm == 0 ? 0 : (icpm == 1 ? 26 : (icpm == 2 ? 10 : 1));
+                if (cm == lm) cm = 34;
+            }
+            if (P.chroma == 2) cm = mode422(cm);
+            cms |= cm << (8 * i);
         }
-        L.cu_chroma = cm;
+        L.cu_chroma = nc == 1 ? cms * 0x01010101 : cms;  // byte k: PB k
     }
     L.tx = L.qx, L.ty = L.qy, L.tl = L.ql, L.td = 0, L.tcbf = 0;
     L.st = U_TT;
@@ -1122,23 +1140,30 @@ HG_HD inline void unit_tt(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             split = dec(L, G, CTX_SPLIT_TF + 5 - L.tl) != 0;
         else
             split = L.tl > P.maxTb || (nxn && L.td == 0);
-        uint32_t cbf = 0;  // cbf_cb | cbf_cr << 1
-        if (L.tl > 2 && P.chroma) {
-            const uint32_t pc = L.td == 0 ? 3u : (L.tcbf >> (2 * (L.td - 1))) & 3u;
-            if (pc & 1) cbf |= (uint32_t)dec(L, G, CTX_CBF_CHROMA + L.td);
-            if (pc & 2) cbf |= (uint32_t)dec(L, G, CTX_CBF_CHROMA + L.td) << 1;
+        uint32_t cbf = 0;  // cbf_cb | cbf_cr << 1, 4:2:2 lower TBs << 2 / << 3 (7.3.8.8)
+        if ((L.tl > 2 && P.chroma) || P.chroma == 3) {
+            const uint32_t pc = L.td == 0 ? 3u : (L.tcbf >> (4 * (L.td - 1))) & 3u;
+            const bool two = P.chroma == 2 && (!split || L.tl == 3);
+            if (pc & 1) {
+                cbf |= (uint32_t)dec(L, G, CTX_CBF_CHROMA + L.td);
+                if (two) cbf |= (uint32_t)dec(L, G, CTX_CBF_CHROMA + L.td) << 2;
+            }
+            if (pc & 2) {
+                cbf |= (uint32_t)dec(L, G, CTX_CBF_CHROMA + L.td) << 1;
+                if (two) cbf |= (uint32_t)dec(L, G, CTX_CBF_CHROMA + L.td) << 3;
+            }
         }
-        L.tcbf = (L.tcbf & ~(3u << (2 * L.td))) | (cbf << (2 * L.td));
+        L.tcbf = (L.tcbf & ~(15u << (4 * L.td))) | (cbf << (4 * L.td));
         if (!split) break;
         --L.tl;  // child 0
         ++L.td;
     }
-    const uint32_t cbf = (L.tcbf >> (2 * L.td)) & 3u;
-    L.fl = (L.fl & ~(F_CBF_L | F_CBF_CB | F_CBF_CR)) | ((cbf & 1) ? F_CBF_CB : 0u) | ((cbf & 2) ? F_CBF_CR : 0u);
+    const uint32_t cbf = (L.tcbf >> (4 * L.td)) & 15u;
+    L.fl &= ~F_CBF_L;
     if (dec(L, G, CTX_CBF_LUMA + (L.td == 0 ? 1 : 0))) L.fl |= F_CBF_L;
     // transform_unit
-    const bool chroma4 = P.chroma == 1 && L.tl == 2;
-    const uint32_t pc = L.td > 0 ? (L.tcbf >> (2 * (L.td - 1))) & 3u : 0u;  // parent's cbf_cb/cbf_cr
+    const bool chroma4 = (P.chroma == 1 || P.chroma == 2) && L.tl == 2;
+    const uint32_t pc = L.td > 0 ? (L.tcbf >> (4 * (L.td - 1))) & 15u : 0u;  // the parent's chroma cbfs
     const bool cbf_c = P.chroma == 0 ? false : (chroma4 ? pc != 0 : cbf != 0);
     if (((L.fl & F_CBF_L) || cbf_c) && (P.flags & SP_CU_QP_DELTA) && !(L.fl & F_DQP_CODED)) {
         int v = 0;  // cu_qp_delta_abs: TR prefix (cMax 5), EG0 suffix
@@ -1172,7 +1197,8 @@ HG_HD inline void unit_tt(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         }
     }
     const int blk = L.td == 0 ? 0 : (((L.tx >> L.tl) & 1) | (((L.ty >> L.tl) & 1) << 1));
-    L.tb_n = (P.chroma != 0 && (!chroma4 || blk == 3)) ? 3 : 1;
+    // luma, then Cb and Cr (two each with 4:2:2: upper, lower)
+    L.tb_n = (P.chroma != 0 && (!chroma4 || blk == 3)) ? (P.chroma == 2 ? 5 : 3) : 1;
     L.tb_t = 0;
     L.st = U_TB;
 }
@@ -1278,9 +1304,11 @@ HG_HD inline void cu_done(Lane &L, LaneLds &ld, LanePic &P) {
 template <class EG>
 HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     const int t = L.tb_t;
-    const bool chroma4 = P.chroma == 1 && L.tl == 2;
+    const bool chroma4 = (P.chroma == 1 || P.chroma == 2) && L.tl == 2;
+    const int nh = P.chroma == 2 ? 2 : 1;                     // chroma TBs per component
+    const int comp = t == 0 ? 0 : 1 + (t - 1) / nh, half = t == 0 ? 0 : (t - 1) % nh;
     bool cbf;
-    L.tb_cidx = t;
+    L.tb_cidx = comp;
     if (t == 0) {
         L.tb_x = L.tx;
         L.tb_y = L.ty;
@@ -1293,19 +1321,23 @@ HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         L.tb_mode = (L.cu_modes >> (8 * k)) & 0xff;
         cbf = (L.fl & F_CBF_L) != 0;
     } else if (!chroma4) {
-        L.tb_x = L.tx >> 1;
-        L.tb_y = L.ty >> 1;
-        L.tb_log2 = L.tl - 1;
-        L.tb_mode = L.cu_chroma;
-        cbf = (L.fl & (t == 1 ? F_CBF_CB : F_CBF_CR)) != 0;
-    } else {  // 4:2:0, 4x4 luma TBs: the chroma TBs of the 8x8 parent, after its 4th luma TB
+        L.tb_log2 = P.chroma == 3 ? L.tl : L.tl - 1;  // log2TrafoSizeC
+        L.tb_x = L.tx >> P.subx;
+        L.tb_y = (L.ty >> P.suby) + (half << L.tb_log2);
+        int k = 0;  // IntraPredModeC of the PB (4:4:4 NxN: four)
+        if (L.fl & F_NXN) {
+            const int hp = 1 << (L.ql - 1);
+            k = ((L.ty - L.qy) >= hp ? 2 : 0) + ((L.tx - L.qx) >= hp ? 1 : 0);
+        }
+        L.tb_mode = (L.cu_chroma >> (8 * k)) & 0xff;
+        cbf = ((L.tcbf >> (4 * L.td + (comp - 1) + 2 * half)) & 1u) != 0;
+    } else {  // 4:2:0 / 4:2:2, 4x4 luma TBs: the chroma TBs of the 8x8 parent, after its 4th luma TB
         const int s = 1 << (L.tl + 1);
         L.tb_x = (L.tx & ~(s - 1)) >> 1;
-        L.tb_y = (L.ty & ~(s - 1)) >> 1;
+        L.tb_y = ((L.ty & ~(s - 1)) >> P.suby) + 4 * half;
         L.tb_log2 = 2;
-        L.tb_mode = L.cu_chroma;
-        const uint32_t pc = (L.tcbf >> (2 * (L.td - 1))) & 3u;
-        cbf = ((pc >> (t - 1)) & 1u) != 0;
+        L.tb_mode = L.cu_chroma & 0xff;
+        cbf = ((L.tcbf >> (4 * (L.td - 1) + (comp - 1) + 2 * half)) & 1u) != 0;
     }
     L.fl = (L.fl & ~(F_TS | F_TB_CBF)) | (cbf ? F_TB_CBF : 0u);
     L.tb_coef0 = L.ncoef;
@@ -1314,7 +1346,7 @@ HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         return;
     }
     // residual_coding header (7.3.8.11)
-    const int l2 = L.tb_log2, n = 1 << l2, cidx = t;
+    const int l2 = L.tb_log2, n = 1 << l2, cidx = comp;
     if ((P.flags & SP_TRANSFORM_SKIP) && !(L.fl & F_BYPASS) && l2 == 2 && dec(L, G, CTX_TS_FLAG + (cidx ? 1 : 0)))
         L.fl |= F_TS;
     // last_sig_coeff_{x,y}_prefix (decoder.rs:109-130), suffixes
@@ -1334,7 +1366,7 @@ HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         ly = (1 << k) * (2 + (py & 1)) + (int)byp_bits(L, G, k);
     }
     int scan = 0;  // 7.4.9.11 scanIdx
-    if (l2 == 2 || (l2 == 3 && cidx == 0)) {
+    if (l2 == 2 || (l2 == 3 && (cidx == 0 || P.chroma == 3))) {
         if (L.tb_mode >= 6 && L.tb_mode <= 14) scan = 2;
         else if (L.tb_mode >= 22 && L.tb_mode <= 30) scan = 1;
     }
@@ -1650,6 +1682,8 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
     P.maxTb = sp.log2_max_tb;
     P.maxDepthIntra = sp.max_th_depth_intra;
     P.chroma = sp.chroma_format;
+    P.subx = (sp.chroma_format == 1 || sp.chroma_format == 2) ? 1 : 0;
+    P.suby = sp.chroma_format == 1 ? 1 : 0;
     P.log2qg = log2ctb - sp.diff_cu_qp_delta_depth;
     P.bdY = sp.bit_depth_y;
     P.bdC = sp.bit_depth_c;

@@ -87,7 +87,8 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     const TuRec *tus = a.tus + pd.tu_off + (uint64_t)row * pd.tu_cap_row;
     const Coef *coefs = a.coefs + pd.coef_off + (uint64_t)row * pd.coef_cap_row;
     const int W = sp.width, H = sp.height;
-    const int cw = sp.chroma_format ? W >> 1 : 0, ch = sp.chroma_format ? H >> 1 : 0;
+    const int cw = sp.chroma_format ? W >> chroma_sx(sp.chroma_format) : 0;
+    const int ch = sp.chroma_format ? H >> chroma_sy(sp.chroma_format) : 0;
     int16_t *res_plane[3] = {a.resid + pd.resid_off, a.resid + pd.resid_off + (size_t)W * H,
                              a.resid + pd.resid_off + (size_t)W * H + (size_t)cw * ch};
     const int pitch[3] = {W, cw, cw};

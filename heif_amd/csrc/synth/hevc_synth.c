@@ -289,7 +289,8 @@ typedef struct {
     int *ts2rs, *tile_rs; /* 6.5.1 tile scan; tile of each CTB by raster address */
     int *slice_rs;        /* slice of each CTB by raster address */
     /* current CU */
-    int cu_bypass, intra_split, max_trafo_depth, chroma_mode;
+    int cu_bypass, intra_split, max_trafo_depth;
+    int cu_x, cu_y, cu_pb, chroma_mode[4];  /* IntraPredModeC per PB (4:4:4 NxN: four) */
     int is_qp_coded;
 } pic_t;
 
@@ -338,8 +339,7 @@ static int tile_layout(pic_t *p) {
 }
 
 static int scan_idx_for(const pic_t *p, int log2n, int cIdx, int mode) {
-    (void)p;
-    if (log2n == 2 || (log2n == 3 && cIdx == 0)) {
+    if (log2n == 2 || (log2n == 3 && (cIdx == 0 || p->P->chroma_format == 3))) {
         if (mode >= 6 && mode <= 14) return 2;
         if (mode >= 22 && mode <= 30) return 1;
     }
@@ -501,7 +501,7 @@ static void residual_coding(pic_t *p, int log2n, int cIdx, int mode) {
 static void transform_unit(pic_t *p, int x0, int y0, int log2n, int blk, int cbf_l, int cbf_cb, int cbf_cr,
                            int pcb, int pcr) {
     const synth_params *P = p->P;
-    int chroma4 = log2n == 2;
+    int chroma4 = log2n == 2 && P->chroma_format != 3;
     int cbfChroma = P->chroma_format == 0 ? 0 : (chroma4 ? (pcb || pcr) : (cbf_cb || cbf_cr));
     if ((cbf_l || cbfChroma) && P->cu_qp_delta && !p->is_qp_coded) {
         int lim = 26 + p->qpbdY / 2;
@@ -516,13 +516,17 @@ static void transform_unit(pic_t *p, int x0, int y0, int log2n, int blk, int cbf
     int lmode = p->ipm[(y0 >> 2) * p->w4 + (x0 >> 2)];
     if (cbf_l) residual_coding(p, log2n, 0, lmode);
     if (P->chroma_format == 0) return;
-    if (!chroma4) {
-        if (cbf_cb) residual_coding(p, log2n - 1, 1, p->chroma_mode);
-        if (cbf_cr) residual_coding(p, log2n - 1, 2, p->chroma_mode);
-    } else if (blk == 3) {
-        if (pcb) residual_coding(p, 2, 1, p->chroma_mode);
-        if (pcr) residual_coding(p, 2, 2, p->chroma_mode);
-    }
+    /* chroma TBs (7.3.8.10): log2TrafoSizeC, two per component with 4:2:2
+     * (cbf bits 0 / 1); 4x4 luma TBs (not 4:4:4): the 8x8 parent's chroma */
+    const int k = ((y0 - p->cu_y) >= p->cu_pb ? 2 : 0) + ((x0 - p->cu_x) >= p->cu_pb ? 1 : 0);
+    const int cm = p->chroma_mode[P->chroma_format == 3 && p->intra_split ? k : 0];
+    const int l2c = chroma4 ? 2 : (P->chroma_format == 3 ? log2n : log2n - 1);
+    if (!chroma4 || blk == 3)
+        for (int ci = 1; ci < 3; ci++)
+            for (int h = 0; h < (P->chroma_format == 2 ? 2 : 1); h++) {
+                const int cbf = chroma4 ? (ci == 1 ? pcb : pcr) : (ci == 1 ? cbf_cb : cbf_cr);
+                if ((cbf >> h) & 1) residual_coding(p, l2c, ci, cm);
+            }
 }
 
 static void transform_tree(pic_t *p, int x0, int y0, int log2n, int depth, int blk, int pcb, int pcr) {
@@ -535,10 +539,20 @@ static void transform_tree(pic_t *p, int x0, int y0, int log2n, int depth, int b
     } else {
         split = (log2n > P->log2_max_tb || (p->intra_split && depth == 0));
     }
-    int cbf_cb = 0, cbf_cr = 0;
-    if (log2n > 2 && P->chroma_format != 0) {
-        if (depth == 0 || pcb) { cbf_cb = pct(&p->rng, 50); ce_bin(&p->c, C_CBF_CHROMA + depth, cbf_cb); }
-        if (depth == 0 || pcr) { cbf_cr = pct(&p->rng, 50); ce_bin(&p->c, C_CBF_CHROMA + depth, cbf_cr); }
+    int cbf_cb = 0, cbf_cr = 0;  /* bit 1: 4:2:2 lower chroma TB (coded when not split or 8x8) */
+    if ((log2n > 2 && P->chroma_format != 0) || P->chroma_format == 3) {
+        const int two = P->chroma_format == 2 && (!split || log2n == 3);
+        for (int ci = 0; ci < 2; ci++) {
+            if (!(depth == 0 || ((ci ? pcr : pcb) & 1))) continue;
+            int v = 0;
+            for (int h = 0; h < (two ? 2 : 1); h++) {
+                const int b = pct(&p->rng, 50);
+                ce_bin(&p->c, C_CBF_CHROMA + depth, b);
+                v |= b << h;
+            }
+            if (ci) cbf_cr = v;
+            else cbf_cb = v;
+        }
     }
     if (split) {
         int h = 1 << (log2n - 1);
@@ -594,7 +608,8 @@ static void coding_unit(pic_t *p, int x0, int y0, int log2cb, int depth) {
             ce_finish(c);
             bw_align1(c->w);
             for (int ci = 0; ci < (P->chroma_format ? 3 : 1); ci++) {
-                const int ns = ci ? (n / 2) * (n / 2) : n * n, bd = ci ? P->pcm_bd_c : P->pcm_bd_y;
+                const int sw = P->chroma_format == 3 ? 1 : 2, sh = P->chroma_format == 1 ? 2 : 1;
+                const int ns = ci ? (n / sw) * (n / sh) : n * n, bd = ci ? P->pcm_bd_c : P->pcm_bd_y;
                 for (int k = 0; k < ns; k++) bw_bits(c->w, (uint32_t)rnd(&p->rng, 1 << bd), bd);
             }
             ce_start(c, c->w);
@@ -630,13 +645,21 @@ static void coding_unit(pic_t *p, int x0, int y0, int log2cb, int depth) {
         }
         set_map(p, p->ipm, xPb, yPb, pb, (uint8_t)m);
     }
-    if (P->chroma_format != 0) {
+    /* intra_chroma_pred_mode per PB with 4:4:4, else per CU; 8.4.3 (Table 8-3 with 4:2:2) */
+    static const uint8_t k_mode422[35] = {0,  1,  2,  2,  2,  2,  3,  5,  7,  8,  10, 11, 13, 15, 16, 18, 19, 20,
+                                          21, 22, 23, 23, 24, 24, 25, 25, 26, 27, 27, 28, 28, 29, 29, 30, 31};
+    p->cu_x = x0;
+    p->cu_y = y0;
+    p->cu_pb = pb;
+    for (int i = 0; P->chroma_format != 0 && i < (P->chroma_format == 3 ? np : 1); i++) {
         int icpm = rnd(&p->rng, 5);
         ce_bin(c, C_CHROMA_MODE, icpm != 4);
         if (icpm != 4) ce_fl(c, (uint32_t)icpm, 2);
-        int lm = p->ipm[(y0 >> 2) * p->w4 + (x0 >> 2)];
+        const int xPb = x0 + (i & 1) * pb, yPb = y0 + (i >> 1) * pb;
+        int lm = p->ipm[(yPb >> 2) * p->w4 + (xPb >> 2)];
         static const int base[4] = {0, 26, 10, 1};
-        p->chroma_mode = icpm == 4 ? lm : (base[icpm] == lm ? 34 : base[icpm]);
+        const int cm = icpm == 4 ? lm : (base[icpm] == lm ? 34 : base[icpm]);
+        p->chroma_mode[i] = P->chroma_format == 2 ? k_mode422[cm] : cm;
     }
     p->intra_split = nxn;
     p->max_trafo_depth = P->max_th_depth_intra + nxn;
@@ -741,7 +764,7 @@ static size_t ep_insert(const uint8_t *in, size_t n, uint8_t *out, size_t cap, i
 }
 
 static int profile_idc(const synth_params *P) {
-    if (P->chroma_format == 0 || P->bit_depth > 10) return 4;
+    if (P->chroma_format != 1 || P->bit_depth > 10) return 4; /* format range extensions */
     return P->bit_depth > 8 ? 2 : 1;
 }
 
@@ -806,15 +829,16 @@ long synth_sps(const synth_params *P, uint8_t *out, size_t cap) {
     ptl(&w, P);
     bw_ue(&w, 0);
     bw_ue(&w, (uint32_t)P->chroma_format);
+    if (P->chroma_format == 3) bw_bits(&w, 0, 1); /* separate_colour_plane_flag */
     bw_ue(&w, (uint32_t)P->width);
     bw_ue(&w, (uint32_t)P->height);
-    int sub = P->chroma_format == 1 ? 2 : 1;
+    const int subw = (P->chroma_format == 1 || P->chroma_format == 2) ? 2 : 1, subh = P->chroma_format == 1 ? 2 : 1;
     if (P->conf_right || P->conf_bottom) {
         bw_bits(&w, 1, 1);
         bw_ue(&w, 0);
-        bw_ue(&w, (uint32_t)(P->conf_right / sub));
+        bw_ue(&w, (uint32_t)(P->conf_right / subw));
         bw_ue(&w, 0);
-        bw_ue(&w, (uint32_t)(P->conf_bottom / sub));
+        bw_ue(&w, (uint32_t)(P->conf_bottom / subh));
     } else {
         bw_bits(&w, 0, 1);
     }
@@ -906,7 +930,7 @@ long synth_pps(const synth_params *P, uint8_t *out, size_t cap) {
 }
 
 int synth_check_params(const synth_params *P) {
-    if (P->chroma_format != 0 && P->chroma_format != 1) return -1;
+    if (P->chroma_format < 0 || P->chroma_format > 3) return -1;
     if (P->bit_depth < 8 || P->bit_depth > 10) return -1;
     if (P->log2_min_cb < 3 || P->log2_ctb < 4 || P->log2_ctb > 6 || P->log2_min_cb > P->log2_ctb) return -1;
     if (P->log2_min_tb != 2 || P->log2_max_tb < P->log2_min_tb || P->log2_max_tb > 5 ||

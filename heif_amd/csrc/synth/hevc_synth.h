@@ -13,7 +13,7 @@ extern "C" {
 typedef struct {
     int32_t width, height;            /* pic_width/height_in_luma_samples (multiples of MinCbSize) */
     int32_t conf_right, conf_bottom;  /* conformance-window crop in luma samples (even for 4:2:0) */
-    int32_t chroma_format;            /* 0 = 4:0:0, 1 = 4:2:0 */
+    int32_t chroma_format;            /* chroma_format_idc: 0 = 4:0:0, 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4 */
     int32_t bit_depth;                /* 8..10, luma = chroma */
     int32_t log2_ctb, log2_min_cb, log2_min_tb, log2_max_tb, max_th_depth_intra;
     int32_t sign_hiding, cu_qp_delta, diff_cu_qp_delta_depth;

@@ -740,7 +740,9 @@ typedef struct {
     slice_par *slices;
     uint8_t ds_st[CTX_NUM], ds_mps[CTX_NUM]; /* 9.3.2.4 storage at a slice segment's end */
     /* current CU */
-    int cu_bypass, cu_intra_split, cu_max_trafo_depth, cu_chroma_mode_c;
+    int cu_bypass, cu_intra_split, cu_max_trafo_depth;
+    int cu_x, cu_y, cu_pb;        /* the CU and its prediction block size */
+    int cu_chroma_mode_c[4];      /* IntraPredModeC per PB (4:4:4 NxN: four; else PB 0) */
 } pic_t;
 
 #define F_EDGE_V 1
@@ -1307,13 +1309,17 @@ static int recon_tb(pic_t *p, int cIdx, int xTb, int yTb, int log2n, int mode, i
     return 0;
 }
 
-static int chroma_mode_of(pic_t *p, int x0, int y0) { (void)x0; (void)y0; return p->cu_chroma_mode_c; }
+/* IntraPredModeC of the PB holding luma location (x0, y0) */
+static int chroma_mode_of(pic_t *p, int x0, int y0) {
+    const int k = ((y0 - p->cu_y) >= p->cu_pb ? 2 : 0) + ((x0 - p->cu_x) >= p->cu_pb ? 1 : 0);
+    return p->cu_chroma_mode_c[p->chroma == 3 && p->cu_intra_split ? k : 0];
+}
 
 static int transform_unit(pic_t *p, int x0, int y0, int xB, int yB, int log2n, int depth, int blk, int cbf_l,
                           int cbf_cb, int cbf_cr, int pcb, int pcr) {
     (void)depth;
     int chroma4 = (p->chroma != 3 && log2n == 2);
-    int cbfChroma = p->chroma == 0 ? 0 : (chroma4 ? (pcb || pcr) : (cbf_cb || cbf_cr));
+    int cbfChroma = p->chroma == 0 ? 0 : (chroma4 ? (pcb || pcr) : (cbf_cb || cbf_cr));  /* either 4:2:2 flag */
     if (cbf_l || cbfChroma) {
         if (p->pps->cu_qp_delta && !p->is_cu_qp_delta_coded) {
             cabac_t *c = &p->c;
@@ -1340,13 +1346,19 @@ static int transform_unit(pic_t *p, int x0, int y0, int xB, int yB, int log2n, i
     if (recon_tb(p, 0, x0, y0, log2n, lmode, cbf_l, x0, y0)) return -1;
     if (p->chroma == 0) return 0;
     int cm = chroma_mode_of(p, x0, y0);
-    if (!chroma4) {
-        int l2c = log2n - 1;
-        if (recon_tb(p, 1, x0 / p->sw, y0 / p->sh, l2c, cm, cbf_cb, x0, y0)) return -1;
-        if (recon_tb(p, 2, x0 / p->sw, y0 / p->sh, l2c, cm, cbf_cr, x0, y0)) return -1;
-    } else if (blk == 3) {
-        if (recon_tb(p, 1, xB / p->sw, yB / p->sh, 2, cm, pcb, xB, yB)) return -1;
-        if (recon_tb(p, 2, xB / p->sw, yB / p->sh, 2, cm, pcr, xB, yB)) return -1;
+    /* the chroma TBs of the TU (7.3.8.10): log2TrafoSizeC, and for 4:2:2 a
+     * second TB below the first; with 4x4 luma TBs (not 4:4:4) the chroma of
+     * the 8x8 parent follows its 4th luma TB */
+    const int cx = chroma4 ? xB : x0, cy = chroma4 ? yB : y0;
+    const int l2c = chroma4 ? 2 : (p->chroma == 3 ? log2n : log2n - 1);
+    const int cb = chroma4 ? pcb : cbf_cb, cr = chroma4 ? pcr : cbf_cr;
+    if (!chroma4 || blk == 3) {
+        for (int ci = 1; ci < 3; ci++)
+            for (int h = 0; h < (p->chroma == 2 ? 2 : 1); h++) {
+                const int yc = cy / p->sh + (h << l2c);
+                if (recon_tb(p, ci, cx / p->sw, yc, l2c, cm, ((ci == 1 ? cb : cr) >> h) & 1, cx, yc * p->sh))
+                    return -1;
+            }
     }
     return 0;
 }
@@ -1361,10 +1373,19 @@ static int transform_tree(pic_t *p, int x0, int y0, int xB, int yB, int log2n, i
         split = dec_bin(c, CTX_SPLIT_TF + 5 - log2n);
     else
         split = (log2n > s->log2_max_tb || (p->cu_intra_split && depth == 0));
+    /* cbf_cb / cbf_cr: bit 0, and for 4:2:2 bit 1 of the lower chroma TB
+     * (coded when the node is not split or is 8x8: 7.3.8.8) */
     int cbf_cb = 0, cbf_cr = 0;
     if ((log2n > 2 && p->chroma != 0) || p->chroma == 3) {
-        if (depth == 0 || pcb) cbf_cb = dec_bin(c, CTX_CBF_CHROMA + depth);
-        if (depth == 0 || pcr) cbf_cr = dec_bin(c, CTX_CBF_CHROMA + depth);
+        const int two = p->chroma == 2 && (!split || log2n == 3);
+        if (depth == 0 || (pcb & 1)) {
+            cbf_cb = dec_bin(c, CTX_CBF_CHROMA + depth);
+            if (two) cbf_cb |= dec_bin(c, CTX_CBF_CHROMA + depth) << 1;
+        }
+        if (depth == 0 || (pcr & 1)) {
+            cbf_cr = dec_bin(c, CTX_CBF_CHROMA + depth);
+            if (two) cbf_cr |= dec_bin(c, CTX_CBF_CHROMA + depth) << 1;
+        }
     }
     if (split) {
         int h = 1 << (log2n - 1);
@@ -1472,9 +1493,18 @@ static int coding_unit(pic_t *p, int x0, int y0, int log2cb, int depth) {
         int m = derive_luma_mode(p, xPb, yPb, prev[i], mpm[i], rem[i]);
         set_map(p, p->ipm, xPb, yPb, pb, (uint8_t)m);
     }
-    if (p->chroma != 0) {
+    p->cu_x = x0;
+    p->cu_y = y0;
+    p->cu_pb = pb;
+    /* intra_chroma_pred_mode: one per PB with 4:4:4, else one per CU (7.3.8.5);
+     * 8.4.3 IntraPredModeC from it and the PB's luma mode, through Table 8-3
+     * with 4:2:2 */
+    static const uint8_t k_mode422[35] = {0,  1,  2,  2,  2,  2,  3,  5,  7,  8,  10, 11, 13, 15, 16, 18, 19, 20,
+                                          21, 22, 23, 23, 24, 24, 25, 25, 26, 27, 27, 28, 28, 29, 29, 30, 31};
+    for (int i = 0; p->chroma != 0 && i < (p->chroma == 3 ? np : 1); i++) {
         int icpm = dec_bin(c, CTX_CHROMA_MODE) ? bz_fl(bypass_src, c, 2) : 4;
-        int lm = p->ipm[(y0 >> 2) * p->w4 + (x0 >> 2)];
+        int xPb = x0 + (i & 1) * pb, yPb = y0 + (i >> 1) * pb;
+        int lm = p->ipm[(yPb >> 2) * p->w4 + (xPb >> 2)];
         int cm;
         if (icpm == 4) cm = lm;
         else {
@@ -1482,8 +1512,7 @@ static int coding_unit(pic_t *p, int x0, int y0, int log2cb, int depth) {
             cm = base[icpm];
             if (cm == lm) cm = 34;
         }
-        if (p->chroma == 2) return oracle_fail("4:2:2 not supported");
-        p->cu_chroma_mode_c = cm;
+        p->cu_chroma_mode_c[i] = p->chroma == 2 ? k_mode422[cm] : cm;
     }
     p->cu_intra_split = nxn;
     p->cu_max_trafo_depth = s->max_th_depth_intra + nxn;
@@ -1932,7 +1961,7 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *item, size_t item_le
     const hevc_pps *pp = &ps->pps;
     if (s->range_ext_any || pp->range_ext_any) return oracle_fail("range extension tools not supported");
     if (pp->tiles && pp->wpp) return oracle_fail("HEVC tiles together with WPP not supported");
-    if (s->chroma_format_idc == 2 || s->chroma_format_idc == 3) return oracle_fail("only 4:0:0 / 4:2:0");
+    if (s->separate_colour_plane) return oracle_fail("separate_colour_plane_flag not supported");
     /* the VCL NAL units, 4-byte length prefixes */
     const uint8_t *nals[MAX_SEGMENTS];
     size_t nlen[MAX_SEGMENTS];
@@ -1966,7 +1995,7 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *item, size_t item_le
     p->minTb = s->log2_min_tb;
     p->minCb = s->log2_min_cb;
     p->chroma = s->chroma_format_idc;
-    p->sw = p->chroma == 1 ? 2 : 1;
+    p->sw = (p->chroma == 1 || p->chroma == 2) ? 2 : 1; /* SubWidthC, SubHeightC (Table 6-1) */
     p->sh = p->chroma == 1 ? 2 : 1;
     p->cw = p->chroma ? p->W / p->sw : 0;
     p->chh = p->chroma ? p->H / p->sh : 0;
@@ -2238,7 +2267,7 @@ int oracle_decode_heic(const uint8_t *data, size_t len, oracle_image *out, oracl
     out->height = (uint32_t)oh;
     out->chroma_format_idc = (uint32_t)chroma;
     out->bit_depth = (uint32_t)ps.sps.bit_depth_y;
-    int sw = chroma == 1 ? 2 : 1, sh = chroma == 1 ? 2 : 1;
+    int sw = (chroma == 1 || chroma == 2) ? 2 : 1, sh = chroma == 1 ? 2 : 1; /* SubWidthC, SubHeightC */
     int np = chroma ? 3 : 1;
     for (int ci = 0; ci < np; ci++) {
         out->pw[ci] = (uint32_t)(ci ? (ow + sw - 1) / sw : ow);

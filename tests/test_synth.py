@@ -58,6 +58,24 @@ CASES = [
     ("pcm_10b_16_32", dict(bit_depth=10, pcm=1, pcm_bd_y=9, pcm_bd_c=10, pcm_log2_min=4, pcm_log2_max=5, pcm_pct=40)),
     ("pcm_mono_bypass", dict(chroma_format=0, pcm=1, pcm_pct=30, tq_bypass=1)),
     ("pcm_all_ctb16", dict(pcm=1, pcm_pct=100, pcm_lf_disabled=1, log2_ctb=4, log2_max_tb=4, pcm_log2_max=4)),
+    # 4:2:2 (two chroma TBs per component, stacked; Table 8-3 mode mapping) and
+    # 4:4:4 (chroma TBs the luma size, four chroma modes in an NxN CU, reference
+    # sample filtering, 32x32 chroma scaling factors); the reference's
+    # parameter_set_reader.rs reads chroma_format_idc 0..3
+    ("c422_8b", dict(chroma_format=2)),
+    ("c444_8b", dict(chroma_format=3)),
+    ("c422_10b_ctb64_tools", dict(chroma_format=2, bit_depth=10, log2_ctb=6, max_th_depth_intra=3, transform_skip=1,
+                                  tq_bypass=1, scaling_list=1, cb_qp_offset=-2, cr_qp_offset=3)),
+    ("c444_10b_ctb16_scaling", dict(chroma_format=3, bit_depth=10, log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2,
+                                    scaling_list=1, transform_skip=1)),
+    ("c444_ctb64_scaling32", dict(chroma_format=3, log2_ctb=6, max_th_depth_intra=3, scaling_list=1)),
+    ("c422_lowqp_dense_nowpp", dict(chroma_format=2, bit_depth=10, init_qp=22, slice_qp_delta=-33, density=80,
+                                    wpp=0)),
+    ("c444_lowqp_dense", dict(chroma_format=3, bit_depth=10, init_qp=22, slice_qp_delta=-33, density=80)),
+    ("c422_crop_200x120", dict(chroma_format=2, width=200, height=120, conf_right=6, conf_bottom=3)),
+    ("c444_crop_200x120", dict(chroma_format=3, width=200, height=120, conf_right=5, conf_bottom=3, bit_depth=9)),
+    ("c422_pcm_nowpp", dict(chroma_format=2, pcm=1, pcm_pct=30, pcm_bd_c=6, wpp=0)),
+    ("c444_pcm_nofilter", dict(chroma_format=3, pcm=1, pcm_pct=30, pcm_lf_disabled=1, pcm_log2_max=5)),
 ]
 
 
