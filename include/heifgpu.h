@@ -59,7 +59,8 @@ typedef struct heifgpu_batch heifgpu_batch; /* device-resident batch */
 
 typedef struct {
     uint32_t width, height;       /* output (grid-cropped) size, coded orientation */
-    uint32_t chroma_format_idc;   /* 0 = 4:0:0, 1 = 4:2:0 */
+    uint32_t chroma_format_idc;   /* 0 = 4:0:0, 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4 (Cb/Cr planes
+                                     ceil(w / SubWidthC) x ceil(h / SubHeightC)) */
     uint32_t bit_depth;           /* luma bit depth (chroma equal) */
     uint32_t bytes_per_sample;    /* 1 for 8-bit, 2 otherwise */
     uint32_t grid_rows, grid_cols;/* 1x1 for a single coded item */
@@ -194,8 +195,8 @@ int heifgpu_ipc_close(void *dev_ptr);
  * (device, caller-owned, rgb_pitch bytes per row), rotated anticlockwise by
  * info->rotation * 90 degrees: the output is height x width for rotation 1
  * and 3.  Matrix from info->matrix_coeffs (H.273: 1 BT.709, 9 BT.2020 NCL,
- * anything else BT.601), range from info->full_range, 4:2:0 chroma by sample
- * replication, samples above 8 bits rounded down to 8.  Fixed point: 16
+ * anything else BT.601), range from info->full_range, 4:2:0 / 4:2:2 chroma by
+ * sample replication, samples above 8 bits rounded down to 8.  Fixed point: 16
  * fractional bits, round half up, clip to 0..255.  Asynchronous on `stream`. */
 int heifgpu_ycbcr_to_rgb(heifgpu_ctx *ctx, const heifgpu_image_info *info, const heifgpu_planes *in, void *rgb,
                          int32_t rgb_pitch, void *stream);

@@ -137,13 +137,14 @@ def assemble(p, subs: List[SubPicture], decode) -> Tuple:
 
     W, H = p.width - p.conf_right, p.height - p.conf_bottom
     y = np.zeros((H, W), np.uint16)
-    c = [np.zeros((H // 2, W // 2), np.uint16) for _ in range(2)] if p.chroma_format else [None, None]
+    sx, sy = int(p.chroma_format in (1, 2)), int(p.chroma_format == 1)  # log2 SubWidthC, SubHeightC
+    c = [np.zeros(((H + sy) >> sy, (W + sx) >> sx), np.uint16) for _ in range(2)] if p.chroma_format else [None, None]
     for s in subs:
         py, pcb, pcr = decode(s)
         y[s.y0:s.y0 + py.shape[0], s.x0:s.x0 + py.shape[1]] = py
         if p.chroma_format:
             for dst, src in zip(c, (pcb, pcr)):
-                dst[s.y0 // 2:s.y0 // 2 + src.shape[0], s.x0 // 2:s.x0 // 2 + src.shape[1]] = src
+                dst[(s.y0 >> sy):(s.y0 >> sy) + src.shape[0], (s.x0 >> sx):(s.x0 >> sx) + src.shape[1]] = src
     return y, c[0], c[1]
 
 

@@ -2,7 +2,7 @@
 
 H.273 YCbCr -> R'G'B' with the coefficients rounded to 16.16 fixed point
 exactly as the library's color_coefs (heif_amd/csrc/kernels/kernels.hpp),
-4:2:0 chroma by replication, then the irot rotation (anticlockwise, 90
+subsampled chroma (4:2:0, 4:2:2) by replication, then the irot rotation (anticlockwise, 90
 degrees per unit; np.rot90 rotates anticlockwise).  The reference has no RGB
 path (it parses `irot` and stops), so this restatement is the checker:
 "parity unpinned" against libheif, which is not available here.
@@ -34,8 +34,10 @@ def ycbcr_to_rgb(y, cb, cr, matrix: int, full: bool, rotation: int, bit_depth: i
         Cb = Cr = np.zeros_like(Y)
     else:
         h, w = Y.shape
-        Cb = (cb.astype(np.int64) >> sh)[np.arange(h)[:, None] >> 1, np.arange(w)[None, :] >> 1] - 128
-        Cr = (cr.astype(np.int64) >> sh)[np.arange(h)[:, None] >> 1, np.arange(w)[None, :] >> 1] - 128
+        sy, sx = int(cb.shape[0] < h), int(cb.shape[1] < w)  # 4:2:0 / 4:2:2 / 4:4:4 from the plane shape
+        rows, cols = np.arange(h)[:, None] >> sy, np.arange(w)[None, :] >> sx
+        Cb = (cb.astype(np.int64) >> sh)[rows, cols] - 128
+        Cr = (cr.astype(np.int64) >> sh)[rows, cols] - 128
     yv = c["ys"] * (Y - c["yoff"])
     r = (yv + c["cr_r"] * Cr + 32768) >> 16
     g = (yv - c["cb_g"] * Cb - c["cr_g"] * Cr + 32768) >> 16

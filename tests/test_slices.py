@@ -59,6 +59,8 @@ ROW_CASES = [
                                  tq_bypass=1, transform_skip=1, scaling_list=1, diff_cu_qp_delta_depth=2,
                                  max_th_depth_intra=3)),
     ("mono_rows", dict(chroma_format=0, slice_ctus=4, wpp=1)),
+    ("c422_rows_wpp", dict(chroma_format=2, slice_ctus=4, wpp=1)),
+    ("c444_rows_10b", dict(chroma_format=3, bit_depth=10, slice_ctus=8)),
 ]
 
 # dependent slice segments starting at CTB rows (GPU: a slice's segments back
@@ -199,7 +201,7 @@ def emu_check():
 @pytest.mark.parametrize("name,across", [("rows2_wpp_dbk", 0), ("crop_10b_wpp", 0), ("ctb16_rows2", 0),
                                          ("ctb16_rows2", 1), ("mono_rows", 1), ("dep_all_nowpp", 0),
                                          ("dep_alt_wpp", 0), ("dep_alt_nowpp_ctb16_pcm", 0),
-                                         ("dep_alt_across", 1)])
+                                         ("dep_alt_across", 1), ("c422_rows_wpp", 1), ("c444_rows_10b", 0)])
 def test_emulated_kernels_slices(emu_check, tmp_path, name, across, parse):
     """The kernels' source compiled for the host decodes a picture of row
     slices (one picture per slice, its dependent segments back to back;
@@ -245,7 +247,7 @@ def test_gpu_row_slices_bit_exact(H, oracle_mod, parse):
     seeds each, one batch per format, checked against the spec-literal
     oracle; plus a grid of sliced pictures batched with a tiled one."""
     ctx = H.DecodeContext(0)
-    for depth, chroma in ((8, 1), (10, 1), (8, 0)):
+    for depth, chroma in ((8, 1), (10, 1), (8, 0), (8, 2), (10, 3)):
         datas = []
         for name, over in ROW_CASES + DEP_CASES:
             for across in (0, 1):

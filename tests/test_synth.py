@@ -210,6 +210,47 @@ def test_gpu_synthetic_bit_exact(H, gctx, oracle_mod, name, over, parse):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cf,bd", [(2, 8), (3, 10)])
+def test_gpu_chroma_format_grid_rgb_gather(H, oracle_mod, cf, bd):
+    """A 4:2:2 / 4:4:4 grid (cropped last row and column): bit-exact planes of
+    the Cb / Cr shapes chroma_dims gives, RGB exact against tests/rgb_ref.py,
+    and the tile split over two batches gathered (heifgpu_gather_tiles) back
+    into the same planes."""
+    import numpy as np
+    import torch
+
+    import rgb_ref
+
+    data = S.grid_heic(300, 200, params(dict(chroma_format=cf, bit_depth=bd)), seed=5)
+    ref = oracle_mod.decode_heic(data, with_checks=False)
+    ctx = H.DecodeContext(0)
+    img = H.HeifImage.parse(data)
+    assert img.info.chroma_format_idc == cf
+    out = ctx.alloc_outputs([img])[0]
+    assert tuple(out.cb.shape) == H.chroma_dims(img.info) == ref.cb.shape
+    b = ctx.prepare([img])
+    b.decode_async([out])
+    assert b.status() == [0]
+    _assert_equal(_planes(out), ref, ("grid", cf))
+    rgb = ctx.to_rgb(out).cpu().numpy()
+    want = rgb_ref.ycbcr_to_rgb(out.y.cpu().numpy(), out.cb.cpu().numpy(), out.cr.cpu().numpy(),
+                                img.info.matrix_coeffs, bool(img.info.full_range), img.info.rotation, bd)
+    assert np.array_equal(rgb, want)
+    dst = ctx.alloc_outputs([img])[0]
+    for t in (dst.y, dst.cb, dst.cr):
+        t.fill_(0)
+    for g in range(2):
+        part = ctx.alloc_outputs([img])[0]
+        bb = ctx.prepare([img], tile_stride=2, tile_offset=g)
+        bb.decode_async([part])
+        assert bb.status() == [0]
+        bb.free()
+        ctx.gather_tiles(dst, part, 2, g)
+    torch.cuda.synchronize()
+    _assert_equal(_planes(dst), ref, ("gather", cf))
+
+
+@pytest.mark.gpu
 def test_gpu_mixed_geometry_batch(H, oracle_mod):
     """One batch of 10-bit 4:2:0 grids whose tiles differ in size, CTB size and
     coding tools (one SeqParams per distinct SPS/PPS); a batch that mixes bit

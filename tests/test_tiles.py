@@ -44,6 +44,8 @@ CASES = [
     ("mono_1ctb_tiles", dict(chroma_format=0, tile_cols=4, tile_rows=3)),
     ("dense_lowqp_10b", dict(width=256, height=128, bit_depth=10, tile_cols=4, tile_rows=2, init_qp=22,
                              slice_qp_delta=-30, density=80, beta_offset_div2=3, tc_offset_div2=-2)),
+    ("c422_3x2", dict(chroma_format=2, tile_cols=3, tile_rows=2)),
+    ("c444_2x2_10b", dict(chroma_format=3, bit_depth=10, tile_cols=2, tile_rows=2, scaling_list=1)),
 ]
 
 
@@ -182,7 +184,8 @@ def emu_check():
 
 @pytest.mark.parametrize("parse", ["lanes", "solo", "spread"])
 @pytest.mark.parametrize("name,across", [("crop_4x3_explicit_10b", 0), ("ctb64_partial_tools", 0),
-                                         ("mono_1ctb_tiles", 0), ("crop_4x3_explicit_10b", 1), ("u2x2", 1)])
+                                         ("mono_1ctb_tiles", 0), ("crop_4x3_explicit_10b", 1), ("u2x2", 1),
+                                         ("c422_3x2", 1), ("c444_2x2_10b", 0)])
 def test_emulated_kernels_tiled(emu_check, tmp_path, name, across, parse):
     """The kernels' source compiled for the host decodes tiled pictures (one
     picture per tile; with loop filtering across tiles, children of an
@@ -226,9 +229,10 @@ def _assert_equal(got, img, tag):
 def test_gpu_tiled_pictures_bit_exact(H, oracle_mod, parse):
     """Every tile case, with and without loop filtering across tiles, two
     seeds each, in one batch per parse mode and format (8-bit 4:2:0, 10-bit
-    4:2:0, 8-bit 4:0:0), checked against the spec-literal oracle."""
+    4:2:0, 8-bit 4:0:0, 8-bit 4:2:2, 10-bit 4:4:4), checked against the
+    spec-literal oracle."""
     ctx = H.DecodeContext(0)
-    for depth, chroma in ((8, 1), (10, 1), (8, 0)):
+    for depth, chroma in ((8, 1), (10, 1), (8, 0), (8, 2), (10, 3)):
         datas = []
         for name, over in CASES:
             for across in (0, 1):  # loop_filter_across_tiles_enabled_flag (1: an assembly picture)
