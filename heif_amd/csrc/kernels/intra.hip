@@ -154,10 +154,11 @@ struct Win {
     }
 };
 
-template <typename Pel>
+template <typename Pel, int CF>
 __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L, const TuRec &tu, const Win<Pel> &w,
                                                                  int PW, int PH, int cidx, int bd, bool strong,
-                                                                 int chroma, int lane) {
+                                                                 int lane) {
+    constexpr int chroma = CF;
     const int log2n = tu.log2, n = 1 << log2n, mode = tu.mode;
     const int x0 = tu.x, y0 = tu.y;
     // component → luma coordinates (6.4.1 takes luma locations)
@@ -523,7 +524,9 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 #else
 #define HG_INTRA_ATTR
 #endif
-template <typename Pel>
+// CF: the batch's chroma_format_idc (a compile-time constant: the 4:2:0 build
+// carries no per-format arithmetic)
+template <typename Pel, int CF>
 __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArgs a) {
 #if defined(HG_HOST_EMU)
     unsigned char *smem = g_emu.smem;
@@ -538,7 +541,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
     const SeqParams sp = a.seqs[pd.seq];
     const int W = sp.width, H = sp.height, log2ctb = sp.log2_ctb;
     const int wctb = (W + (1 << log2ctb) - 1) >> log2ctb, hctb = (H + (1 << log2ctb) - 1) >> log2ctb;
-    const int chroma = sp.chroma_format;
+    constexpr int chroma = CF;  // = sp.chroma_format (launch_intra picks the instantiation)
     const int cw = chroma ? W >> chroma_sx(chroma) : 0, ch = chroma ? H >> chroma_sy(chroma) : 0;
     const int ncomp = chroma ? 3 : 1;
     Pel *planes[3];
@@ -690,7 +693,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                 }
             }
 #endif
-            predict_tb<Pel>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, chroma, lane);
+            predict_tb<Pel, CF>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, lane);
         }
         HG_FENCE_REL();
         hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
@@ -721,19 +724,37 @@ static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
 }
 
 #if defined(HG_HOST_EMU)
+template <int CF>
+static void emu_intra_cf(const BatchArgs &a, int nw) {
+    if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t, CF>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
+    else emu_launch(k_intra<uint16_t, CF>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
+}
 void emu_intra(const BatchArgs &a) {
     const int nw = intra_launch_waves(a);
-    if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
-    else emu_launch(k_intra<uint16_t>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
+    switch (a.chroma_format) {
+    case 0: emu_intra_cf<0>(a, nw); break;
+    case 2: emu_intra_cf<2>(a, nw); break;
+    case 3: emu_intra_cf<3>(a, nw); break;
+    default: emu_intra_cf<1>(a, nw); break;
+    }
 }
 #else
+template <int CF>
+static void launch_intra_cf(const BatchArgs &a, int nw, size_t lds, hipStream_t s) {
+    if (a.bytes_per_sample == 1)
+        hipLaunchKernelGGL((k_intra<uint8_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
+    else
+        hipLaunchKernelGGL((k_intra<uint16_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
+}
 hipError_t launch_intra(const BatchArgs &a, hipStream_t s) {
     const int nw = intra_launch_waves(a);
     const size_t lds = intra_lds_bytes(a, nw);
-    if (a.bytes_per_sample == 1)
-        hipLaunchKernelGGL(k_intra<uint8_t>, dim3(a.n_pics), dim3(nw * 64), lds, s, a);
-    else
-        hipLaunchKernelGGL(k_intra<uint16_t>, dim3(a.n_pics), dim3(nw * 64), lds, s, a);
+    switch (a.chroma_format) {
+    case 0: launch_intra_cf<0>(a, nw, lds, s); break;
+    case 2: launch_intra_cf<2>(a, nw, lds, s); break;
+    case 3: launch_intra_cf<3>(a, nw, lds, s); break;
+    default: launch_intra_cf<1>(a, nw, lds, s); break;
+    }
     return hipGetLastError();
 }
 #endif

@@ -1305,8 +1305,9 @@ template <class EG>
 HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     const int t = L.tb_t;
     const bool chroma4 = (P.chroma == 1 || P.chroma == 2) && L.tl == 2;
-    const int nh = P.chroma == 2 ? 2 : 1;                     // chroma TBs per component
-    const int comp = t == 0 ? 0 : 1 + (t - 1) / nh, half = t == 0 ? 0 : (t - 1) % nh;
+    // component and (4:2:2) upper / lower half of TB t: luma, Cb (, Cb lower), Cr (, Cr lower)
+    const bool c422 = P.chroma == 2;
+    const int comp = t == 0 ? 0 : (c422 ? 1 + ((t - 1) >> 1) : t), half = (c422 && t > 0) ? (t - 1) & 1 : 0;
     bool cbf;
     L.tb_cidx = comp;
     if (t == 0) {
@@ -1325,7 +1326,7 @@ HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         L.tb_x = L.tx >> P.subx;
         L.tb_y = (L.ty >> P.suby) + (half << L.tb_log2);
         int k = 0;  // IntraPredModeC of the PB (4:4:4 NxN: four)
-        if (L.fl & F_NXN) {
+        if (P.chroma == 3 && (L.fl & F_NXN)) {
             const int hp = 1 << (L.ql - 1);
             k = ((L.ty - L.qy) >= hp ? 2 : 0) + ((L.tx - L.qx) >= hp ? 1 : 0);
         }

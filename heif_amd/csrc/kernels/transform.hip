@@ -118,6 +118,8 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
 #if defined(HG_HOST_EMU)
             auto grp = group_tb;
 #else
+            // one record per lane: each `vl` loop below runs once per lane (vl == lane)
+            static_assert(kWave == 64, "the cached record assumes vl == lane");
             TuRec tu_c;
             const bool ok_c = group_tb(lane, tu_c);
             auto grp = [&](int, TuRec &tu) -> bool {
