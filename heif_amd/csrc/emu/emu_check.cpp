@@ -23,6 +23,7 @@ using namespace hg;
 
 int main(int argc, char **argv) {
     if (argc < 2) return 2;
+    setvbuf(stdout, nullptr, _IONBF, 0);  // every line out before a sanitizer abort
     int stages = argc > 2 ? atoi(argv[2]) : 5;
     const uint32_t tstride = argc > 4 ? uint32_t(atoi(argv[3])) : 1u, toff = argc > 4 ? uint32_t(atoi(argv[4])) : 0u;
     FILE *f = fopen(argv[1], "rb");
@@ -32,9 +33,16 @@ int main(int argc, char **argv) {
     std::vector<uint8_t> data(static_cast<size_t>(n), 0);
     if (fread(data.data(), 1, size_t(n), f) != size_t(n)) return 2;
     fclose(f);
-    ParsedImage im = parse_heic(data.data(), data.size());
-    const ParsedImage *ims[1] = {&im};
-    HostBatch hb = build_batch(ims, 1, tstride, toff);
+    ParsedImage im;
+    HostBatch hb;
+    try {  // the host's checks reject what the kernels never see (the API returns the error)
+        im = parse_heic(data.data(), data.size());
+        const ParsedImage *ims[1] = {&im};
+        hb = build_batch(ims, 1, tstride, toff);
+    } catch (const std::exception &e) {
+        printf("host rejected: %s\n", e.what());
+        return 3;
+    }
     std::vector<TuRec> tus(hb.tu_n);
     std::vector<Coef> coefs(hb.coef_n);
     std::vector<uint32_t> rc(2 * hb.rows), status(hb.pics.size());
@@ -108,6 +116,20 @@ int main(int argc, char **argv) {
     for (uint32_t r = 0; r < hb.rows; ++r) {
         ntu += rc[2 * r];
         ncoef += rc[2 * r + 1];
+    }
+    if (getenv("HG_EMU_DEBUG_MODES")) {  // tuning aid: TB records with an out-of-range mode
+        int shown = 0;
+        for (const PicDesc &pd : hb.pics)
+            for (uint32_t r = 0; r < (uint32_t)((hb.seqs[pd.seq].height + (1 << hb.seqs[pd.seq].log2_ctb) - 1) >> hb.seqs[pd.seq].log2_ctb); ++r) {
+                const uint32_t nt = rc[2 * (pd.row_off + r)];
+                for (uint32_t t = 0; t < nt && shown < 10; ++t) {
+                    const TuRec &tu = tus[pd.tu_off + (uint64_t)r * pd.tu_cap_row + t];
+                    if (tu.mode > 34) {
+                        printf("bad mode %d pic %u row %u t %u x %d y %d log2 %d flags 0x%x ctu %d\n", tu.mode, (unsigned)(&pd - hb.pics.data()), r, t, tu.x, tu.y, tu.log2, tu.flags, tu.ctu);
+                        ++shown;
+                    }
+                }
+            }
     }
     printf("parse mode: %s\n", mode == PARSE_SOLO ? "solo" : mode == PARSE_SPREAD ? "spread" : "lanes");
     printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);

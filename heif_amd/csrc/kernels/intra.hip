@@ -669,8 +669,9 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
             w.cx0 = cidx == 0 ? win[0].cx0 : (cidx == 1 ? win[1].cx0 : win[2].cx0);
             w.cy0 = cidx == 0 ? win[0].cy0 : (cidx == 1 ? win[1].cy0 : win[2].cy0);
             const int PW = cidx ? cw : W, PH = cidx ? ch : H;
-            // a TB must lie inside the picture and inside its CTU window
-            if (tu.log2 < 2 || tu.log2 > 5 || tu.x + (1 << tu.log2) > PW || tu.y + (1 << tu.log2) > PH ||
+            // a TB must lie inside the picture and inside its CTU window, with a mode
+            // of 8.4.2 (the parse keeps it so; the check keeps the tables in range)
+            if (tu.mode > 34 || tu.log2 < 2 || tu.log2 > 5 || tu.x + (1 << tu.log2) > PW || tu.y + (1 << tu.log2) > PH ||
                 tu.x < w.cx0 || tu.y < w.cy0 || tu.x + (1 << tu.log2) > w.cx0 + w.csx ||
                 tu.y + (1 << tu.log2) > w.cy0 + w.csy)
                 continue;

@@ -513,7 +513,13 @@ HG_HD inline void engine_init(Lane &L, const EG &G, uint32_t start, uint32_t end
     vfill(L, G);
     vfill(L, G);
     L.range = 510;
-    if ((L.value >> L.k) >= 510) L.status |= ST_CABAC_INIT;
+    if ((L.value >> L.k) >= 510) {
+        // ivlOffset 510 / 511 (9.3.2.5 forbids it): flagged, and clamped so that
+        // value < range << k holds and every later bin stays in range (a bypass
+        // run of n bins < 2^n, so no syntax element leaves its domain)
+        L.status |= ST_CABAC_INIT;
+        L.value = (509u << L.k) | ((1u << L.k) - 1u);
+    }
 }
 
 // ------------------------------------------------------------------ engine (9.3.4.3)
@@ -1028,7 +1034,9 @@ HG_HD inline void pcm_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         L.tb_coef0 = L.ncoef;
 #pragma nounroll
         for (int i = 0; i < m * m; ++i) {
-            const uint32_t b = bit >> 3;
+            // clamped to the substream's padded end: a truncated stream reads padding
+            // (and reports ST_OVERRUN below), never past the arena
+            const uint32_t b = (bit >> 3) < G.lim ? bit >> 3 : G.lim;
             const uint32_t w = ((uint32_t)G.rbsp[b] << 16) | ((uint32_t)G.rbsp[b + 1] << 8) | (uint32_t)G.rbsp[b + 2];
             const uint32_t v = (w >> (24u - (bit & 7u) - (uint32_t)pbd)) & ((1u << pbd) - 1u);
             bit += (uint32_t)pbd;
@@ -1181,6 +1189,13 @@ HG_HD inline void unit_tt(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             else v += (int)(((1u << ones) - 1u) + byp_bits(L, G, ones));
         }
         if (v && byp(L, G)) v = -v;
+        // 7.4.9.14: CuQpDeltaVal in [-(26 + QpBdOffsetY / 2), 25 + QpBdOffsetY / 2]
+        // (outside it, QpY and the scaling shift would leave their ranges)
+        const int vlo = -(26 + P.qpbdY / 2), vhi = 25 + P.qpbdY / 2;
+        if (v < vlo || v > vhi) {
+            L.status |= ST_SYNTAX;
+            v = v < vlo ? vlo : vhi;
+        }
         L.fl |= F_DQP_CODED;
         L.cu_qp_delta_val = v;
         update_qpy(L, P);

@@ -11,6 +11,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import bench
+from conftest import make_emu
 
 
 def _free_port():
@@ -83,7 +84,7 @@ def test_tile_split_ranks_compose_the_image():
     import subprocess
 
     root = pathlib.Path(__file__).resolve().parents[1]
-    subprocess.run(["make", "-s", "-C", str(root / "heif_amd" / "csrc"), "emu-fast"], check=True, capture_output=True)
+    make_emu("emu-fast")
     exe = str(root / "heif_amd" / "csrc" / "build" / "emu_fast" / "emu_check")
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()

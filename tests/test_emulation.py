@@ -10,6 +10,7 @@ import subprocess
 import pytest
 
 from heif_amd.synthetic import permuted_heic
+from conftest import make_emu
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 CSRC = ROOT / "heif_amd" / "csrc"
@@ -18,7 +19,7 @@ EXE = CSRC / "build" / "emu_fast" / "emu_check"
 
 @pytest.fixture(scope="module")
 def emu_check():
-    subprocess.run(["make", "-s", "-C", str(CSRC), "emu-fast"], check=True, capture_output=True)
+    make_emu("emu-fast")
     return EXE
 
 

@@ -30,6 +30,7 @@ import numpy as np
 import pytest
 
 from hevc_tiles import _nal_units, assemble, split_slices
+from conftest import make_emu
 
 S = pytest.importorskip("heif_amd.synth_encoder")
 
@@ -193,7 +194,7 @@ CSRC = os.path.join(os.path.dirname(__file__), "..", "heif_amd", "csrc")
 
 @pytest.fixture(scope="module")
 def emu_check():
-    subprocess.run(["make", "-s", "-C", CSRC, "emu-fast"], check=True, capture_output=True)
+    make_emu("emu-fast")
     return os.path.join(CSRC, "build", "emu_fast", "emu_check")
 
 

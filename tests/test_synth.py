@@ -15,7 +15,7 @@ import json
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, make_emu
 
 S = pytest.importorskip("heif_amd.synth_encoder")
 
@@ -332,7 +332,7 @@ def test_emulated_kernels_on_synthetic_streams(tmp_path, parser):
     import subprocess
 
     csrc = pathlib.Path(__file__).resolve().parents[1] / "heif_amd" / "csrc"
-    subprocess.run(["make", "-s", "-C", str(csrc), "emu-fast"], check=True, capture_output=True)
+    make_emu("emu-fast")
     exe = csrc / "build" / "emu_fast" / "emu_check"
     env = dict(os.environ, HEIFGPU_PARSE=parser if parser in ("solo", "spread") else "lanes",
                **({"HEIFGPU_LANES_PPW": "1"} if parser == "ppw1" else {}))
@@ -372,7 +372,7 @@ def test_emulated_kernels_survive_corrupt_synthetic(tmp_path, mode):
     import subprocess
 
     csrc = pathlib.Path(__file__).resolve().parents[1] / "heif_amd" / "csrc"
-    subprocess.run(["make", "-s", "-C", str(csrc), "emu-fast"], check=True, capture_output=True)
+    make_emu("emu-fast")
     path = tmp_path / f"{mode}.heic"
     path.write_bytes(_corrupt_synth(mode))
     r = subprocess.run([str(csrc / "build" / "emu_fast" / "emu_check"), str(path), "5"], capture_output=True,
