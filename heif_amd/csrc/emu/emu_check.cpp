@@ -108,6 +108,10 @@ int main(int argc, char **argv) {
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = bps;
     a.chroma_format = hb.chroma;
+    if (stages <= 0) {  // host only: container, parameter sets, slice headers, batch layout
+        printf("host ok: %zu pictures\n", hb.pics.size());
+        return 0;
+    }
     emu_rbsp(a);
     emu_parse(a);
     uint32_t st = 0;

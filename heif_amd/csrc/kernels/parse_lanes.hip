@@ -686,7 +686,13 @@ template <class EG>
 HG_HD inline int term(Lane &L, const EG &G) {
     L.range -= 2;
     const uint32_t sr = L.range << L.k;
-    if (L.value >= sr) return 1;
+    if (L.value >= sr) {
+        // 1 ends the engine's run (end of a segment / subset, pcm_flag: a new
+        // initialisation follows).  A corrupt stream may read on: keep
+        // value < range << k, so later bins stay in their domains
+        L.value = sr - 1u;
+        return 1;
+    }
     if (L.range < 256) {
         L.range <<= 1;
         L.k -= 1;
@@ -1130,7 +1136,7 @@ HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             if (P.chroma == 2) cm = mode422(cm);
             cms |= cm << (8 * i);
         }
-        L.cu_chroma = nc == 1 ? cms * 0x01010101 : cms;  // byte k: PB k
+        L.cu_chroma = nc == 1 ? (int)((uint32_t)cms * 0x01010101u) : cms;  // byte k: PB k
     }
     L.tx = L.qx, L.ty = L.qy, L.tl = L.ql, L.td = 0, L.tcbf = 0;
     L.st = U_TT;

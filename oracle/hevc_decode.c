@@ -1331,6 +1331,8 @@ static int transform_unit(pic_t *p, int x0, int y0, int xB, int yB, int log2n, i
                 v += s;
             }
             if (v && dec_bypass(c)) v = -v;
+            /* 7.4.9.14: CuQpDeltaVal in [-(26 + QpBdOffsetY / 2), 25 + QpBdOffsetY / 2] */
+            if (v < -(26 + p->qpbdY / 2) || v > 25 + p->qpbdY / 2) return oracle_fail("CuQpDeltaVal out of range");
             p->is_cu_qp_delta_coded = 1;
             p->cu_qp_delta_val = v;
             update_qpy(p);
@@ -2117,7 +2119,8 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *item, size_t item_le
                 if (!end) ok = dec_term(&p->c); /* end_of_subset_one_bit */
                 /* the last consumed bit must be 1 and the rest of the byte 0 */
                 size_t pos = p->c.b.bit;
-                if (pos == 0 || !((rbsp[(pos - 1) >> 3] >> (7 - ((pos - 1) & 7))) & 1)) ok = 0;
+                if (pos == 0 || ((pos - 1) >> 3) >= rn || !((rbsp[(pos - 1) >> 3] >> (7 - ((pos - 1) & 7))) & 1))
+                    ok = 0; /* (a reader past the end: a truncated substream) */
                 while (pos & 7) {
                     if ((pos >> 3) < rn && ((rbsp[pos >> 3] >> (7 - (pos & 7))) & 1)) ok = 0;
                     pos++;

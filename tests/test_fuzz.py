@@ -100,6 +100,42 @@ def test_asan_kernels_survive_corrupt_halfmoonbay(emu_asan, tmp_path, halfmoonba
     assert int(line.split()[2].rstrip(","), 16) != 0
 
 
+def _mutants(seed_name, data, n):
+    """n deterministic mutants of `data`: 1-8 bytes overwritten / flipped anywhere
+    (container boxes, parameter sets, slice headers or slice data)."""
+    out = []
+    for i in range(n):
+        rng = random.Random(1000 * i + sum(seed_name.encode()))
+        d = bytearray(data)
+        for _ in range(rng.choice([1, 2, 4, 8])):
+            k = rng.randrange(len(d))
+            op = rng.random()
+            if op < 0.6:
+                d[k] = rng.randrange(256)
+            elif op < 0.8:
+                d[k] ^= 1 << rng.randrange(8)
+            else:
+                d[k] = rng.choice([0, 0xFF, 0x7F, 0x80])
+        out.append(bytes(d))
+    return out
+
+
+@pytest.mark.parametrize("name", ["tiles_nowpp", "slices_dep_across", "pcm422_10b"])
+def test_asan_mutation_fuzz(emu_asan, tmp_path, name):
+    """Byte mutations of whole files (tools/fuzz_emu.py runs the long campaign):
+    the host rejects, or the kernels end with status bits or parity, and no
+    sanitizer reports anything.  The campaign found the ivlOffset, CuQpDeltaVal
+    and terminate-bin cases the parse now clamps."""
+    env = dict(os.environ, ASAN_OPTIONS="exitcode=99:detect_leaks=0", UBSAN_OPTIONS="halt_on_error=1:exitcode=98")
+    for k, d in enumerate(_mutants(name, S.single_heic(BASES[name], seed=3), 12)):
+        path = tmp_path / f"m{k}.heic"
+        path.write_bytes(d)
+        r = subprocess.run([emu_asan, str(path), "5"], capture_output=True, text=True, timeout=600, env=env)
+        out = r.stdout + r.stderr
+        assert "AddressSanitizer" not in out and "runtime error" not in out, (name, k, out[-3000:])
+        assert r.returncode in (0, 1, 3), (name, k, r.returncode, out[-2000:])
+
+
 # ------------------------------------------------------------------ GPU
 torch = pytest.importorskip("torch")
 
@@ -154,5 +190,44 @@ def test_gpu_corrupt_layouts_set_status(oracle_mod, parse):
         o = outs[-1]
         for g, r in zip((o.y, o.cb, o.cr), (ref.y, ref.cb, ref.cr)):
             assert np.array_equal(g.cpu().numpy().astype(np.uint16), r), (bd, cf)
+        b.free()
+    ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parse", ["lanes", "spread"])
+def test_gpu_mutation_fuzz(oracle_mod, parse):
+    """The mutants of test_asan_mutation_fuzz on the GPU, batched per format
+    with a clean image: no device fault, status bits or clean output for the
+    mutants, the clean image bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import heif_amd as H
+
+    ctx = H.DecodeContext(0)
+    for name in ("tiles_nowpp", "slices_dep_across", "pcm422_10b"):
+        clean = S.single_heic(BASES[name], seed=3)
+        cimg = H.HeifImage.parse(clean)
+        key = (cimg.info.bit_depth, cimg.info.chroma_format_idc)
+        imgs = []
+        for d in _mutants(name, clean, 12):
+            try:
+                im = H.HeifImage.parse(d)
+                if (im.info.bit_depth, im.info.chroma_format_idc) != key:
+                    continue
+                ctx.prepare([im], parse=parse).free()  # the batch layout is accepted on its own
+            except H.HeifGpuError:
+                continue
+            imgs.append(im)
+        imgs.append(cimg)
+        b = ctx.prepare(imgs, parse=parse)
+        outs = ctx.alloc_outputs(imgs)
+        b.decode_async(outs)
+        st = b.status()
+        assert st[-1] == 0, (name, st)
+        ref = oracle_mod.decode_heic(clean, with_checks=False)
+        o = outs[-1]
+        for g, r in zip((o.y, o.cb, o.cr), (ref.y, ref.cb, ref.cr)):
+            assert np.array_equal(g.cpu().numpy().astype(np.uint16), r), name
         b.free()
     ctx.close()
