@@ -33,6 +33,12 @@ static __thread char g_err[256];
  * out of a tiled picture as a stand-alone picture (tests/hevc_tiles.py) */
 static __thread int g_debug_flags;
 void oracle_set_debug_flags(int flags) { g_debug_flags = flags; }
+/* test coverage (debug flag 8): chroma TBs of 4:2:0 pictures by [log2 - 2][mode][cbf] */
+static __thread uint32_t g_chroma_tb_hist[2][35][2];
+void oracle_chroma_tb_hist(uint32_t *out, int reset) {
+    memcpy(out, g_chroma_tb_hist, sizeof(g_chroma_tb_hist));
+    if (reset) memset(g_chroma_tb_hist, 0, sizeof(g_chroma_tb_hist));
+}
 int oracle_fail(const char *msg) {
     snprintf(g_err, sizeof(g_err), "%s", msg);
     return -1;
@@ -1285,6 +1291,8 @@ static int residual_coding(pic_t *p, int x0, int y0, int log2n, int cIdx, int mo
 
 /* reconstruct one TB: predict + residual */
 static int recon_tb(pic_t *p, int cIdx, int xTb, int yTb, int log2n, int mode, int cbf, int x0l, int y0l) {
+    if ((g_debug_flags & 8) && cIdx && p->chroma == 1 && log2n <= 3 && mode >= 0 && mode < 35)
+        g_chroma_tb_hist[log2n - 2][mode][cbf ? 1 : 0]++;
     intra_predict(p, cIdx, xTb, yTb, log2n, mode);
     if (!cbf) return 0;
     int n = 1 << log2n;

@@ -113,8 +113,11 @@ int oracle_list_item_tiles(const uint8_t *data, size_t len, uint32_t item_id, ui
 uint32_t oracle_aux_item(const uint8_t *data, size_t len);
 
 const char *oracle_last_error(void);
-/* bring-up: bit0 skips deblocking, bit1 skips SAO (thread-local) */
+/* bring-up: bit0 skips deblocking, bit1 skips SAO, bit2 lets a picture end
+ * like a non-last tile, bit3 counts 4:2:0 chroma TBs (thread-local) */
 void oracle_set_debug_flags(int flags);
+/* the bit3 counts: out[2][35][2] = [log2 - 2][IntraPredModeC][cbf] */
+void oracle_chroma_tb_hist(uint32_t *out, int reset);
 
 #ifdef __cplusplus
 }

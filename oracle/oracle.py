@@ -52,6 +52,7 @@ def _load():
     lib.oracle_decode_heic.argtypes = [u8p, SZ, P(_Image), P(_Check), I, P(I)]
     lib.oracle_image_free.argtypes = [P(_Image)]
     lib.oracle_set_debug_flags.argtypes = [I]
+    lib.oracle_chroma_tb_hist.argtypes = [P(ctypes.c_uint32), I]
     lib.oracle_last_error.restype = ctypes.c_char_p
     lib.oracle_remove_emulation_prevention.argtypes = [u8p, SZ, u8p]
     lib.oracle_remove_emulation_prevention.restype = SZ
@@ -159,3 +160,10 @@ def decode_tile(hvcc: bytes, item: bytes, width: int, height: int):
     if rc:
         raise OracleError(last_error())
     return y, cb, cr
+
+
+def chroma_tb_hist(reset: bool = True) -> np.ndarray:
+    """Counts of 4:2:0 chroma TBs decoded with debug flag 8, [log2 - 2][mode][cbf]."""
+    out = (ctypes.c_uint32 * (2 * 35 * 2))()
+    lib.oracle_chroma_tb_hist(out, 1 if reset else 0)
+    return np.frombuffer(bytes(out), np.uint32).reshape(2, 35, 2).copy()

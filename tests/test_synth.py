@@ -100,6 +100,23 @@ def test_oracle_decodes_synthetic_streams(oracle_mod, name, over):
         assert int(img.y.max()) < (1 << p.bit_depth)
 
 
+def test_gpu_cases_cover_every_chroma_pair(oracle_mod):
+    """The 4:2:0 cases test_gpu_synthetic_bit_exact decodes (seeds 0 and 1)
+    hold 4x4 and 8x8 chroma TBs of every IntraPredModeC, with and without
+    coefficients: k_intra's GPU-only Cb+Cr pair path (predict_pair, which the
+    host emulation does not build) is pinned bit-exact on all 140 kinds."""
+    tot = np.zeros((2, 35, 2), np.int64)
+    for name, over in CASES:
+        p = params(over)
+        if p.chroma_format != 1:
+            continue
+        for seed in range(2):
+            oracle_mod.chroma_tb_hist(True)
+            oracle_mod.decode_heic(S.single_heic(p, seed=seed), with_checks=False, debug_flags=8)
+            tot += oracle_mod.chroma_tb_hist(True)
+    assert (tot > 0).all(), np.argwhere(tot == 0)[:10]
+
+
 def test_generator_is_deterministic():
     p = params(dict(bit_depth=10))
     assert S.picture(p, 3) == S.picture(p, 3)
