@@ -61,6 +61,11 @@ __constant__ uint8_t c_ctx_init_l[CTX_NUM] = {HG_CTX_INIT_VALUES};
 // s_memtime cycles per wave: [0] kernel, [1] passes, [2..6] unit kinds CTU, tree (CQT+CU+TT), TB, SB,
 // CTU_END; [7] units run (lanes x unit executions) (tuning build only; heifgpu_debug_counters slots 8..15)
 __device__ uint64_t g_prof_lanes[8];
+// solo / spread: per CTU (index (global CTB row) * 128 + column) s_memrealtime of
+// the first time its wave wanted to start it, the start of its U_CTU unit and
+// the end of its U_CTU_END unit (heifgpu_debug_counters slots 8 on)
+constexpr int kCtuTimeCap = 1 << 17;
+__device__ uint64_t g_ctu_t[kCtuTimeCap][3];
 #endif
 
 namespace {
@@ -2168,10 +2173,20 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
 #if defined(HG_PARSE_PROF)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    int want_seen = -1;  // the CTU whose want time is recorded
 #endif
     for (;;) {
         // the wave's state (equal in every lane), made scalar
         int st = L.st, run = st != U_DONE && (st != U_CTU || ctu_ready<EG>(L, P, E));
+#if defined(HG_PARSE_PROF)
+        const int tix = (P.row_off + L.row) * 128 + L.c;
+        if (st == U_CTU && L.c < 128 && tix < kCtuTimeCap) {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();  // chip-wide 100 MHz clock
+            if (want_seen != tix && lane == 0) g_ctu_t[tix][0] = now;
+            want_seen = tix;
+            if (run && lane == 0) g_ctu_t[tix][1] = now;
+        }
+#endif
         uint32_t start = run && st == U_CTU ? substream_start(L, P, a) : ~0u;
         const uint32_t rd = L.lb;
         st = __builtin_amdgcn_readfirstlane(st);
@@ -2196,7 +2211,13 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
             uni_state(L);
 #endif
             const EG G{ld.ctx, tlo, thi, s_seq, a.rbsp, lim, sw.view()};
+#if defined(HG_PARSE_PROF)
+            const int eix = (P.row_off + L.row) * 128 + L.c;
+#endif
             run_unit(st, L, ld, P, E, G);
+#if defined(HG_PARSE_PROF)
+            if (st == U_CTU_END && eix < kCtuTimeCap && lane == 0) g_ctu_t[eix][2] = __builtin_amdgcn_s_memrealtime();
+#endif
         }
 #if defined(HG_PARSE_PROF)
         pf[st <= U_CTU ? 2 : st <= U_TT ? 3 : st - 1] += __builtin_amdgcn_s_memtime() - t1;
@@ -2253,7 +2274,13 @@ extern "C" int heifgpu_debug_counters(uint64_t *out, int n) {
     const uint64_t zero[8] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_prof_lanes), zero, sizeof(zero)) != hipSuccess) return -1;
     for (int k = 0; k < n && k < 8; ++k) out[k] = tmp[k];
-    return 8;
+    if (n <= 8) return 8;
+    // slots 8 on: the per-CTU times (3 per CTU), then zeroed
+    const size_t m = std::min((size_t)(n - 8), (size_t)hg::kCtuTimeCap * 3);
+    if (hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(hg::g_ctu_t), m * sizeof(uint64_t)) != hipSuccess) return -1;
+    std::vector<uint64_t> z((size_t)hg::kCtuTimeCap * 3, 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_ctu_t), z.data(), z.size() * sizeof(uint64_t)) != hipSuccess) return -1;
+    return (int)(8 + m);
 #else
     (void)out;
     (void)n;
