@@ -70,11 +70,16 @@ __device__ uint64_t g_ctu_t[kCtuTimeCap][3];
 
 namespace {
 
-// engine row of pStateIdx st (Eng::tab): rangeTabLps[st][0..3], transIdxLps, transIdxMps
+// engine row of pStateIdx st (Eng::tab): rangeTabLps[st][0..3], then the
+// next context byte (pStateIdx << 1 | valMps) to XOR with valMps after an LPS
+// (transIdxLps << 1, | 1 at pStateIdx 0 where valMps flips) and after an MPS
+// (transIdxMps << 1)
 HG_HD inline uint64_t state_row(int st) {
     uint64_t r = 0;
     for (int q = 0; q < 4; ++q) r |= (uint64_t)c_lps_l[(st << 2) | q] << (8 * q);
-    return r | ((uint64_t)c_trans_l[st] << 32) | ((uint64_t)(st < 62 ? st + 1 : st) << 40);
+    const uint64_t lps_next = ((uint64_t)c_trans_l[st] << 1) | (st == 0 ? 1u : 0u);
+    const uint64_t mps_next = (uint64_t)(st < 62 ? st + 1 : st) << 1;
+    return r | (lps_next << 32) | (mps_next << 40);
 }
 
 constexpr uint32_t kProgDone = 0x7fffffffu;
@@ -535,7 +540,7 @@ template <class EG>
 HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
     const uint32_t st = s >> 1, mps = s & 1u;
     const uint64_t row = G.row(st);
-    const uint32_t hi = (uint32_t)(row >> 32);  // transIdxLps | transIdxMps << 8
+    const uint32_t hi = (uint32_t)(row >> 32);  // next byte after an LPS | after an MPS << 8
     const uint32_t lps = ((uint32_t)row >> ((L.range >> 3) & 24u)) & 0xffu;
     const uint32_t rm = L.range - lps;
     const uint32_t sr = rm << L.k;
@@ -545,8 +550,7 @@ HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
     const int nb = __builtin_clz(rn) - 23;
     L.range = rn << nb;
     L.k -= nb;
-    const uint32_t nst = (hi >> (isl ? 0 : 8)) & 0xffu;
-    s = (nst << 1) | (mps ^ ((isl && st == 0) ? 1u : 0u));
+    s = ((hi >> (isl ? 0 : 8)) & 0xffu) ^ mps;
     if (L.k < 8) vfill(L, G);
     return (int)(mps ^ (isl ? 1u : 0u));
 }
