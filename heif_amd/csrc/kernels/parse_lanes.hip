@@ -1462,18 +1462,41 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             if ((xS | yS) == 0) seq &= ~0xfull;  // DC of the TB (scan position 0 of sub-block 0): sigCtx 0
             c0 = cb(0) | (cb(off) << 8) | (cb(off + 1) << 16) | (cb(off + 2) << 24);
         }
-        for (int nn = nstart; nn >= 0; --nn) {
-            if (nn > 0 || !infer_dc) {
-                const int slot = (int)((seq >> (4 * nn)) & 15u);
-                uint32_t cs = cache_get(c0, c1, c2, slot);
-                const int bin = dec_s(L, G, cs);
-                cache_put(c0, c1, c2, slot, cs);
-                if (bin) {
-                    sig |= 1u << nn;
-                    infer_dc = false;
+        if constexpr (EG::kSolo) {
+            // scalar engine: slots 0..7 as one 64-bit word (a shift reads or
+            // writes a slot), slot 8 apart
+            uint64_t cc = (uint64_t)c0 | ((uint64_t)c1 << 32);
+            for (int nn = nstart; nn >= 0; --nn) {
+                if (nn > 0 || !infer_dc) {
+                    const uint32_t slot = (uint32_t)(seq >> (4 * nn)) & 15u, sh = (slot & 7u) * 8u;
+                    uint32_t cs = slot < 8u ? (uint32_t)(cc >> sh) & 0xffu : c2;
+                    const int bin = dec_s(L, G, cs);
+                    if (slot < 8u) cc = (cc & ~(0xffull << sh)) | ((uint64_t)cs << sh);
+                    else c2 = cs;
+                    if (bin) {
+                        sig |= 1u << nn;
+                        infer_dc = false;
+                    }
+                } else {
+                    sig |= 1u;  // inferred DC of a coded sub-block
                 }
-            } else {
-                sig |= 1u;  // inferred DC of a coded sub-block
+            }
+            c0 = (uint32_t)cc;
+            c1 = (uint32_t)(cc >> 32);
+        } else {
+            for (int nn = nstart; nn >= 0; --nn) {
+                if (nn > 0 || !infer_dc) {
+                    const int slot = (int)((seq >> (4 * nn)) & 15u);
+                    uint32_t cs = cache_get(c0, c1, c2, slot);
+                    const int bin = dec_s(L, G, cs);
+                    cache_put(c0, c1, c2, slot, cs);
+                    if (bin) {
+                        sig |= 1u << nn;
+                        infer_dc = false;
+                    }
+                } else {
+                    sig |= 1u;  // inferred DC of a coded sub-block
+                }
             }
         }
         auto cw = [&](int i, uint32_t v) { ctx_st(L, G, cbase + i, v & 0xffu); };
