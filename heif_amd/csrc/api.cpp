@@ -160,8 +160,7 @@ struct ParseSet {
     DevBuf<uint32_t> row_counts, status;
     DevBuf<uint8_t> maps;
     DevBuf<SaoParams> sao;
-    DevBuf<int16_t> resid;  // k_transform -> k_intra (TBs needing 16 bits)
-    DevBuf<int8_t> resid8;  // the same, TBs whose residuals fit 8 bits (TU_RES8)
+    DevBuf<int16_t> resid;  // k_transform -> k_intra
     hipEvent_t parsed = nullptr, transformed = nullptr, recon_done = nullptr;
     bool pending = false;  // recon_done recorded and not yet waited for by a parse
     ~ParseSet() {
@@ -182,8 +181,8 @@ struct heifgpu_batch {
     BatchArgs args{};
     DevBuf<uint8_t> bits, rbsp, sf, recon;
     DevBuf<PicDesc> pics;
-    DevBuf<uint32_t> subs, rsubs, porder, xprog, iprog;
-    DevBuf<uint8_t> xctx, iline;
+    DevBuf<uint32_t> subs, rsubs, porder, xprog;
+    DevBuf<uint8_t> xctx;
     DevBuf<SeqParams> seqs;
     DevBuf<OutImage> outs;
     ParseSet set[3];
@@ -590,7 +589,6 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         HIP_TRY(ps.sao.alloc(hb.sao_n));
         HIP_TRY(ps.status.alloc(hb.pics.size()));
         HIP_TRY(ps.resid.alloc(hb.resid_elems));
-        HIP_TRY(ps.resid8.alloc(hb.resid_elems));
         HIP_TRY(hipMemsetAsync(ps.status.p, 0, hb.pics.size() * sizeof(uint32_t), ctx->upload));
     }
     HIP_TRY(b->recon.alloc(hb.recon_bytes));
@@ -598,13 +596,6 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     if (mode == PARSE_SPREAD) {  // per-row WPP progress words and context hand-off blocks
         HIP_TRY(b->xprog.alloc(std::max<size_t>(hb.rows, 1)));
         HIP_TRY(b->xctx.alloc(std::max<size_t>(hb.rows, 1) * CTX_PAD));
-    }
-    // k_intra spread mode (a single-wave workgroup per CTB row) for batches of
-    // few rows: per-row progress words and bottom sample lines
-    const bool intra_spread = hb.rows > 0 && intra_spread_for(int(hb.rows));
-    if (intra_spread) {
-        HIP_TRY(b->iprog.alloc(hb.rows));
-        HIP_TRY(b->iline.alloc(size_t(hb.rows) * intra_line_stride(hb.max_w, hb.chroma, hb.bps)));
     }
     // ---- one pinned staging image of every upload, copied asynchronously
     struct Seg {
@@ -685,8 +676,6 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.solo_waves = solo_waves;
     a.xprog = mode == PARSE_SPREAD ? b->xprog.p : nullptr;
     a.xctx = mode == PARSE_SPREAD ? b->xctx.p : nullptr;
-    a.iprog = intra_spread ? b->iprog.p : nullptr;
-    a.iline = intra_spread ? b->iline.p : nullptr;
     // rows wrap round the lanes (waves) of a picture: the WPP context staging
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
@@ -744,7 +733,6 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     a.sao = ps.sao.p;
     a.status = ps.status.p;
     a.resid = ps.resid.p;
-    a.resid8 = ps.resid8.p;
     // bring-up knob: HEIFGPU_STAGES=k launches only the first k stages (in order, on the caller's stream)
     static const int max_stages = [] {
         const char *e = std::getenv("HEIFGPU_STAGES");

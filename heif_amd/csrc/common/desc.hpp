@@ -64,34 +64,6 @@ struct SeqParams {
 constexpr int chroma_sx(int fmt) { return fmt == 1 || fmt == 2 ? 1 : 0; }
 constexpr int chroma_sy(int fmt) { return fmt == 1 ? 1 : 0; }
 
-// k_transform -> k_intra residual layout (the int16 and int8 arenas alike): per
-// picture, per CTU in raster order, per component a square region whose side is
-// the larger of the component's CTB width and height; in it the 4x4 blocks in
-// z-order, and a TB's n*n samples contiguous (raster order) from 16 x the
-// z-index of its first block.  A TB is aligned to its size, so its blocks are
-// one z-range: each TB is written and read back as one contiguous run.
-constexpr int resid_side_log2(int log2ctb, int fmt) {  // chroma region side
-    return log2ctb - (chroma_sx(fmt) < chroma_sy(fmt) ? chroma_sx(fmt) : chroma_sy(fmt));
-}
-constexpr uint32_t resid_ctu_elems(int log2ctb, int fmt) {
-    return (1u << (2 * log2ctb)) + (fmt ? 2u << (2 * resid_side_log2(log2ctb, fmt)) : 0u);
-}
-constexpr uint32_t zorder4(uint32_t bx, uint32_t by) {  // bx, by < 16: bits interleaved
-    bx = (bx | (bx << 2)) & 0x33u;
-    bx = (bx | (bx << 1)) & 0x55u;
-    by = (by | (by << 2)) & 0x33u;
-    by = (by | (by << 1)) & 0x55u;
-    return bx | (by << 1);
-}
-// element offset (from the picture's resid_off) of the TB of component cidx at (x, y)
-constexpr uint64_t resid_tb_off(int log2ctb, int wctb, int fmt, int cidx, int x, int y) {
-    const int lx2 = log2ctb - (cidx ? chroma_sx(fmt) : 0), ly2 = log2ctb - (cidx ? chroma_sy(fmt) : 0);
-    const int cx = x >> lx2, cy = y >> ly2;
-    const uint32_t rl = 1u << (2 * log2ctb), rc = fmt ? 1u << (2 * resid_side_log2(log2ctb, fmt)) : 0u;
-    const uint64_t base = (uint64_t)(uint32_t)(cy * wctb + cx) * (rl + 2u * rc) + (cidx ? rl + (uint32_t)(cidx - 1) * rc : 0u);
-    return base + 16u * zorder4((uint32_t)(x - (cx << lx2)) >> 2, (uint32_t)(y - (cy << ly2)) >> 2);
-}
-
 // Scaling factor block layout (bytes, from sf_off): for sizeId 0..3 and
 // matrixId 0..5, n*n factors m[y*n+x] (n = 4<<sizeId), in this order.
 constexpr uint32_t sf_size_offset(int size_id) {
@@ -112,7 +84,7 @@ struct PicDesc {
     int32_t out_x, out_y; // luma position of the cropped picture in the output image
     // work-arena offsets
     uint64_t recon_off;   // bytes: Y (width*height samples), then Cb, Cr
-    uint64_t resid_off;   // residual elements (int16 planes and int8 planes alike): same layout as recon
+    uint64_t resid_off;   // int16 elements: same layout as recon
     uint64_t map_off;     // bytes: qpy[w4*h4], flags[w4*h4], then bottom CtDepth per CTB row [hctb][w8]
     uint64_t sao_off;     // SaoParams index of CTB 0
     uint64_t tu_off;      // TuRec index of row 0 (row r at tu_off + r*tu_cap_row)
@@ -148,7 +120,6 @@ enum : uint8_t {
     TU_BYPASS = 1u << 4,
     TU_DST = 1u << 5,
     TU_PCM = 1u << 6,     // pcm_sample(): the "coefficients" are the samples (BYPASS is set too)
-    TU_RES8 = 1u << 7,    // set by k_transform: the TB's residuals all fit int8 and are in the int8 planes
 };
 
 // One transform block in decoding order (luma or chroma), written by the

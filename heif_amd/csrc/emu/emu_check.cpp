@@ -48,7 +48,6 @@ int main(int argc, char **argv) {
     std::vector<uint32_t> rc(2 * hb.rows), status(hb.pics.size());
     std::vector<uint8_t> recon(hb.recon_bytes), maps(hb.map_bytes);
     std::vector<int16_t> resid(hb.resid_elems);
-    std::vector<int8_t> resid8(hb.resid_elems);
     std::vector<SaoParams> sao(hb.sao_n);
     const int W = int(im.out_width), H = int(im.out_height), bps = hb.bps;
     const int SX = chroma_sx(hb.chroma), SY = chroma_sy(hb.chroma);
@@ -91,7 +90,6 @@ int main(int argc, char **argv) {
     a.row_counts = rc.data();
     a.recon = recon.data();
     a.resid = resid.data();
-    a.resid8 = resid8.data();
     a.maps = maps.data();
     a.sao = sao.data();
     a.status = status.data();
@@ -105,11 +103,6 @@ int main(int argc, char **argv) {
     a.solo_waves = solo_waves;
     a.xprog = xprog.data();
     a.xctx = xctx.data();
-    const bool intra_spread = hb.rows > 0 && intra_spread_for(int(hb.rows));
-    std::vector<uint32_t> iprog(hb.rows + 1);
-    std::vector<uint8_t> iline((hb.rows + 1) * intra_line_stride(hb.max_w, hb.chroma < 0 ? 0 : hb.chroma, bps));
-    a.iprog = intra_spread ? iprog.data() : nullptr;
-    a.iline = intra_spread ? iline.data() : nullptr;
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);

@@ -139,7 +139,7 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
         hb.max_log2ctb = std::max(hb.max_log2ctb, int(sq.log2_ctb));
         if (!coded) return;
         PicDesc &p = hb.pics.back();
-        hb.resid_elems += (uint64_t(wctb) * hctb * resid_ctu_elems(sq.log2_ctb, cf) + 127) & ~uint64_t(127);
+        hb.resid_elems += (samples + 127) & ~uint64_t(127);
         hb.rows += uint32_t(hctb);
         // worst case per CTB row: every 8x8 CU split into four 4x4 luma TBs and
         // their chroma TBs (2 with 4:2:0, 4 with 4:2:2, 8 with 4:4:4); a

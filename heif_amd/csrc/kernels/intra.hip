@@ -29,7 +29,6 @@ namespace {
 constexpr int kMaxWaves = 16;
 constexpr int kResidentIntraWaves = 4096;  // ~16 per CU: enough pictures in flight to hide TB latency
 constexpr size_t kIntraLdsBudget = 128 * 1024;
-constexpr int kIntraSpreadRows = 1024;  // spread mode up to one CTB row per SIMD (256 CUs x 4)
 
 __constant__ int8_t c_angle[35] = {0, 0, 32, 26, 21, 17, 13, 9, 5, 2, 0, -2, -5, -9, -13, -17, -21, -26,
                                    -32, -26, -21, -17, -13, -9, -5, -2, 0, 2, 5, 9, 13, 17, 21, 26, 32};
@@ -141,8 +140,7 @@ using Quad = typename QuadT<Pel>::type;
 template <typename Pel>
 struct Win {
     Pel *cur, *left, *above;
-    const int16_t *res;  // the current TB's residuals (k_transform, resid_tb_off): n*n contiguous,
-    const int8_t *res8;  // 16 bits, or 8 for a TB with TU_RES8
+    const int16_t *res;  // the component's residual plane (k_transform), pitch = plane width
     int csx, csy;        // CTB width, height in component samples (4:2:2 chroma: csy = 2 csx)
     int cx0, cy0;        // CTB origin in component samples
     // a decoded neighbour (xn, yn) in picture coordinates; only called for
@@ -171,14 +169,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     const int zc = zidx(((x0 << subx) - bx0) >> 2, ((y0 << suby) - by0) >> 2);
     // residual of a 4x4 / 8x8 TB (one sample per lane): loaded now, used after
     // the neighbour and filter phases, so the load latency hides behind them
-    // the TB's width is wave-uniform: one scalar branch picks the load
-    const bool r8 = (HG_UNI((int)tu.flags) & TU_RES8) != 0;
-    auto resid = [&](int x, int y) -> int {
-        const int o = (y << log2n) + x;
-        if (r8) return (int)w.res8[o];
-        return (int)w.res[o];
-    };
-    const int r0 = (cbf && n <= 8 && lane < n * n) ? resid(lane & (n - 1), lane >> log2n) : 0;
+    const int r0 = (cbf && n <= 8 && lane < n * n) ? w.res[(size_t)(y0 + (lane >> log2n)) * PW + x0 + (lane & (n - 1))] : 0;
     // 1. gather neighbours in search order (8.4.4.2.2): s < 2n left column bottom-up,
     //    s == 2n corner, s > 2n top row left-to-right
 #if defined(HG_HOST_EMU)
@@ -387,7 +378,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         }
         const int li = (ly0 + y) * w.csx + lx0 + x;
         if (tu.flags & TU_PCM) pv = 0;  // the residual is the PCM sample itself
-        if (cbf) pv += (n <= 8 && o == lane) ? r0 : resid(x, y);
+        if (cbf) pv += (n <= 8 && o == lane) ? r0 : w.res[(size_t)(y0 + y) * PW + x0 + x];
         pv = min(max(pv, 0), maxv);
         w.cur[li] = (Pel)pv;
     }
@@ -418,30 +409,19 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     w.left = h ? wr.left : wb.left;
     w.above = h ? wr.above : wb.above;
     w.res = h ? wr.res : wb.res;
-    w.res8 = h ? wr.res8 : wb.res8;
     w.csx = wb.csx;
     w.csy = wb.csy;
     w.cx0 = wb.cx0;
     w.cy0 = wb.cy0;
     const bool cbf = ((h ? tr.flags : tb.flags) & TU_CBF) != 0;
     const bool pcm = ((h ? tr.flags : tb.flags) & TU_PCM) != 0;
-    // Cb and Cr stored at the same width (the usual case): a uniform branch
-    const bool r8b = (HG_UNI((int)tb.flags) & TU_RES8) != 0, r8r = (HG_UNI((int)tr.flags) & TU_RES8) != 0;
-    const bool r8 = h ? r8r : r8b;
     const int bx0 = w.cx0 << 1, by0 = w.cy0 << 1, csl = w.csx << 1;
     const int ns = 4 * n + 1, nch = n == 8 ? 2 : 1;
     const int zc = zidx(((x0 << 1) - bx0) >> 2, ((y0 << 1) - by0) >> 2);
     // residuals (sample sl and sl + 32 of this half), used after the neighbour phase
     int r0 = 0, r1 = 0;
-    auto resid = [&](int o) -> int {
-        if (r8b == r8r) {
-            if (r8b) return (int)w.res8[o];
-            return (int)w.res[o];
-        }
-        return r8 ? (int)w.res8[o] : (int)w.res[o];
-    };
-    if (cbf && sl < n * n) r0 = resid(sl);
-    if (cbf && sl + 32 < n * n) r1 = resid(sl + 32);
+    if (cbf && sl < n * n) r0 = w.res[(size_t)(y0 + (sl >> log2n)) * PW + x0 + (sl & (n - 1))];
+    if (cbf && sl + 32 < n * n) r1 = w.res[(size_t)(y0 + ((sl + 32) >> log2n)) * PW + x0 + ((sl + 32) & (n - 1))];
     int16_t *left = L->left + 33 * h, *top = L->top + 33 * h;
     // 1. neighbours in search order (8.4.4.2.2), chunk k = search positions sl + 32 k
     int val[2] = {0, 0};
@@ -545,21 +525,16 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 #define HG_INTRA_ATTR
 #endif
 // CF: the batch's chroma_format_idc (a compile-time constant: the 4:2:0 build
-// carries no per-format arithmetic).
-// Spread (small batches, BatchArgs::iline set): one single-wave workgroup per
-// CTB row (grid rows x pictures, so row r - 1 is dispatched before row r), each
-// wave alone on its SIMD instead of a picture's rows sharing one CU.  A row's
-// progress word and its bottom sample line (the row below's above neighbours)
-// go through global memory with agent-scope accesses, the line before the word.
-template <typename Pel, int CF, bool Spread>
-__global__ void __launch_bounds__(Spread ? 64 : kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArgs a) {
+// carries no per-format arithmetic)
+template <typename Pel, int CF>
+__global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArgs a) {
 #if defined(HG_HOST_EMU)
     unsigned char *smem = g_emu.smem;
 #else
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #endif
-    const int nw = Spread ? 1 : (int)HG_UNI(blockDim.x >> 6);
-    const int pic = a.pic0 + (Spread ? (int)blockIdx.y : (int)blockIdx.x);
+    const int nw = (int)HG_UNI(blockDim.x >> 6);
+    const int pic = a.pic0 + blockIdx.x;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const PicDesc pd = a.pics[pic];
     if (pd.flags & PD_ASSEMBLY) return;  // no coded data of its own (uniform: the whole workgroup leaves)
@@ -573,8 +548,8 @@ __global__ void __launch_bounds__(Spread ? 64 : kMaxWaves * 64) HG_INTRA_ATTR k_
     planes[0] = reinterpret_cast<Pel *>(a.recon + pd.recon_off);
     planes[1] = planes[0] + (size_t)W * H;
     planes[2] = planes[1] + (size_t)cw * ch;
-    const int16_t *res16 = a.resid + pd.resid_off;  // + resid_tb_off of each TB
-    const int8_t *res8 = a.resid8 + pd.resid_off;
+    const int16_t *resp[3] = {a.resid + pd.resid_off, a.resid + pd.resid_off + (size_t)W * H,
+                              a.resid + pd.resid_off + (size_t)W * H + (size_t)cw * ch};
     const bool strong = (sp.flags & SP_STRONG_INTRA) != 0;
     const WinLayout lay = win_layout(log2ctb, chroma, (int)sizeof(Pel));
     uint32_t *progress = reinterpret_cast<uint32_t *>(smem);  // [nw], 64 B reserved
@@ -585,8 +560,7 @@ __global__ void __launch_bounds__(Spread ? 64 : kMaxWaves * 64) HG_INTRA_ATTR k_
         win[k].cur = reinterpret_cast<Pel *>(blk + lay.cur[k]);
         win[k].left = reinterpret_cast<Pel *>(blk + lay.left[k]);
         win[k].above = reinterpret_cast<Pel *>(blk + lay.above[k]);
-        win[k].res = res16;
-        win[k].res8 = res8;
+        win[k].res = resp[k];
         win[k].csx = lay.csx[k];
         win[k].csy = lay.csy[k];
     }
@@ -594,16 +568,7 @@ __global__ void __launch_bounds__(Spread ? 64 : kMaxWaves * 64) HG_INTRA_ATTR k_
     __syncthreads();
     const uint32_t stride = (uint32_t)wctb + 1;
     const int prev_wave = (wave + nw - 1) % nw;
-    // spread: this picture's row progress words and lines; the components' parts of a line
-    uint32_t *gprog = Spread ? a.iprog + pd.row_off : nullptr;
-    const size_t lstride = intra_line_stride(a.max_width, CF, (int)sizeof(Pel));
-    uint8_t *glines = Spread ? a.iline + (size_t)pd.row_off * lstride : nullptr;
-    const size_t lpart0 = intra_line_part(a.max_width, CF, (int)sizeof(Pel), 0);
-    const size_t lpartc = intra_line_part(a.max_width, CF, (int)sizeof(Pel), 1);
-    auto line_of = [&](int row, int k) {
-        return reinterpret_cast<uint32_t *>(glines + (size_t)row * lstride + (k == 0 ? 0 : lpart0 + (size_t)(k - 1) * lpartc));
-    };
-    for (int r = Spread ? (int)blockIdx.x : wave; r < hctb; r += Spread ? hctb : nw) {
+    for (int r = wave; r < hctb; r += nw) {
         const uint32_t ntu = a.row_counts[2 * (pd.row_off + r)];
         const TuRec *tus = a.tus + pd.tu_off + (uint64_t)r * pd.tu_cap_row;
         int cur = -1;
@@ -656,31 +621,16 @@ __global__ void __launch_bounds__(Spread ? 64 : kMaxWaves * 64) HG_INTRA_ATTR k_
                             }
                         }
                         for (int y = lane; y < w.csy; y += kWave) w.left[y] = w.cur[y * w.csx + w.csx - 1];
-                        if (Spread && r + 1 < hctb) {
-                            // the CTU's bottom sample row for the row below (full height: a row follows)
-                            const uint32_t *src = reinterpret_cast<const uint32_t *>(w.cur + (w.csy - 1) * w.csx);
-                            uint32_t *dst = line_of(r, k) + ((size_t)w.cx0 * sizeof(Pel) >> 2);
-                            const int nwd = (int)((vw * (int)sizeof(Pel) + 3) >> 2);
-                            for (int i = lane; i < nwd; i += kWave) hg_store_agent(dst + i, src[i]);
-                        }
                     }
                     wave_sync();
-                    if constexpr (Spread) {
-                        hg_stores_done();  // the line before the word that lets the row below read it
-                        if (lane == 0) hg_store_agent(&gprog[r], (uint32_t)cur + 1u);
-                    } else {
-                        HG_FENCE_REL();
-                        hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)cur + 1u);
-                    }
+                    HG_FENCE_REL();
+                    hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)cur + 1u);
                 }
                 if (c >= wctb) break;
                 cur = c;
                 if (r > 0) {
-                    const uint32_t need = Spread ? (uint32_t)min(c + 2, wctb)
-                                                 : (uint32_t)(r - 1) * stride + (uint32_t)min(c + 2, wctb);
-                    for (uint32_t spin = 0;
-                         (uint32_t)HG_UNI(Spread ? hg_load_agent(&gprog[r - 1]) : hg_atomic_load(&progress[prev_wave])) < need;
-                         ++spin) {
+                    const uint32_t need = (uint32_t)(r - 1) * stride + (uint32_t)min(c + 2, wctb);
+                    for (uint32_t spin = 0; (uint32_t)HG_UNI(hg_atomic_load(&progress[prev_wave])) < need; ++spin) {
                         if (spin > (1u << 24)) {  // bounded: never hang the device
                             if (lane == 0) atomicOr(&a.status[pic], ST_SUBSTREAM_END);
                             break;
@@ -699,17 +649,7 @@ __global__ void __launch_bounds__(Spread ? 64 : kMaxWaves * 64) HG_INTRA_ATTR k_
                     const int yg = w.cy0 - 1;
                     for (int i = lane; i <= 2 * w.csx; i += kWave) {
                         const int xg = w.cx0 - 1 + i;
-                        Pel v = 0;
-                        if (yg >= 0 && xg >= 0 && xg < PW) {
-                            if constexpr (Spread) {  // the row above's line (its CTUs up to c + 1 are in)
-                                const uint32_t b = (uint32_t)xg * (uint32_t)sizeof(Pel);
-                                const uint32_t wd = hg_load_agent(line_of(r - 1, k) + (b >> 2));
-                                v = (Pel)(wd >> (8 * (b & 3)));
-                            } else {
-                                v = planes[k][(size_t)yg * PW + xg];
-                            }
-                        }
-                        w.above[i] = v;
+                        w.above[i] = (yg >= 0 && xg >= 0 && xg < PW) ? planes[k][(size_t)yg * PW + xg] : (Pel)0;
                     }
                     (void)PH;
                 }
@@ -723,6 +663,7 @@ __global__ void __launch_bounds__(Spread ? 64 : kMaxWaves * 64) HG_INTRA_ATTR k_
             w.cur = cidx == 0 ? win[0].cur : (cidx == 1 ? win[1].cur : win[2].cur);
             w.left = cidx == 0 ? win[0].left : (cidx == 1 ? win[1].left : win[2].left);
             w.above = cidx == 0 ? win[0].above : (cidx == 1 ? win[1].above : win[2].above);
+            w.res = cidx == 0 ? win[0].res : (cidx == 1 ? win[1].res : win[2].res);
             w.csx = cidx == 0 ? win[0].csx : (cidx == 1 ? win[1].csx : win[2].csx);
             w.csy = cidx == 0 ? win[0].csy : (cidx == 1 ? win[1].csy : win[2].csy);
             w.cx0 = cidx == 0 ? win[0].cx0 : (cidx == 1 ? win[1].cx0 : win[2].cx0);
@@ -732,7 +673,7 @@ __global__ void __launch_bounds__(Spread ? 64 : kMaxWaves * 64) HG_INTRA_ATTR k_
             // of 8.4.2 (the parse keeps it so; the check keeps the tables in range)
             if (tu.mode > 34 || tu.log2 < 2 || tu.log2 > 5 || tu.x + (1 << tu.log2) > PW || tu.y + (1 << tu.log2) > PH ||
                 tu.x < w.cx0 || tu.y < w.cy0 || tu.x + (1 << tu.log2) > w.cx0 + w.csx ||
-                tu.y + (1 << tu.log2) > w.cy0 + w.csy || ((tu.x | tu.y) & ((1 << tu.log2) - 1)))
+                tu.y + (1 << tu.log2) > w.cy0 + w.csy)
                 continue;
 #if !defined(HG_HOST_EMU) && !defined(HG_INTRA_NO_PAIR)
             // a 4x4 / 8x8 Cb TB followed by its Cr TB (same TU; the next record of this 64-record block):
@@ -747,42 +688,17 @@ __global__ void __launch_bounds__(Spread ? 64 : kMaxWaves * 64) HG_INTRA_ATTR k_
                 __builtin_memcpy(&tr, &r, sizeof(tr));
                 if ((tr.flags & TU_CIDX_MASK) == 2 && tr.x == tu.x && tr.y == tu.y && tr.log2 == tu.log2 &&
                     tr.mode == tu.mode && tr.ctu == tu.ctu) {
-                    Win<Pel> wb = win[1], wr = win[2];
-                    const uint64_t ob = resid_tb_off(log2ctb, wctb, CF, 1, tu.x, tu.y);
-                    const uint64_t orr = resid_tb_off(log2ctb, wctb, CF, 2, tr.x, tr.y);
-                    wb.res = res16 + ob;
-                    wb.res8 = res8 + ob;
-                    wr.res = res16 + orr;
-                    wr.res8 = res8 + orr;
-                    predict_pair<Pel>(S, tu, tr, wb, wr, PW, PH, sp.bit_depth_c, lane);
+                    predict_pair<Pel>(S, tu, tr, win[1], win[2], PW, PH, sp.bit_depth_c, lane);
                     ++t;
                     continue;
                 }
             }
 #endif
-            {
-                const uint64_t ro = resid_tb_off(log2ctb, wctb, CF, cidx, tu.x, tu.y);
-                w.res = res16 + ro;
-                w.res8 = res8 + ro;
-            }
             predict_tb<Pel, CF>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, lane);
         }
-        if constexpr (Spread) {
-            if (lane == 0) hg_store_agent(&gprog[r], (uint32_t)wctb);
-        } else {
-            HG_FENCE_REL();
-            hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
-        }
+        HG_FENCE_REL();
+        hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
     }
-}
-
-bool intra_spread_for(int rows) {
-    static const int forced = [] {
-        const char *e = std::getenv("HEIFGPU_INTRA_SPREAD");
-        return e ? std::atoi(e) : -1;
-    }();
-    if (forced >= 0) return forced != 0;
-    return rows <= kIntraSpreadRows;
 }
 
 static int intra_launch_waves(const BatchArgs &a) {
@@ -811,16 +727,8 @@ static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
 #if defined(HG_HOST_EMU)
 template <int CF>
 static void emu_intra_cf(const BatchArgs &a, int nw) {
-    if (a.iline) {  // spread: blocks run one at a time in grid order, so row r - 1 is done before row r starts
-        std::fill(a.iprog, a.iprog + a.total_rows, 0u);
-        if (a.bytes_per_sample == 1)
-            emu_launch(k_intra<uint8_t, CF, true>, a.max_rows, a.n_pics, 1, a, false, intra_lds_bytes(a, 1));
-        else
-            emu_launch(k_intra<uint16_t, CF, true>, a.max_rows, a.n_pics, 1, a, false, intra_lds_bytes(a, 1));
-        return;
-    }
-    if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t, CF, false>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
-    else emu_launch(k_intra<uint16_t, CF, false>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
+    if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t, CF>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
+    else emu_launch(k_intra<uint16_t, CF>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
 }
 void emu_intra(const BatchArgs &a) {
     const int nw = intra_launch_waves(a);
@@ -834,27 +742,14 @@ void emu_intra(const BatchArgs &a) {
 #else
 template <int CF>
 static void launch_intra_cf(const BatchArgs &a, int nw, size_t lds, hipStream_t s) {
-    if (a.iline) {
-        const dim3 grid(a.max_rows, a.n_pics);
-        if (a.bytes_per_sample == 1)
-            hipLaunchKernelGGL((k_intra<uint8_t, CF, true>), grid, dim3(64), intra_lds_bytes(a, 1), s, a);
-        else
-            hipLaunchKernelGGL((k_intra<uint16_t, CF, true>), grid, dim3(64), intra_lds_bytes(a, 1), s, a);
-        return;
-    }
     if (a.bytes_per_sample == 1)
-        hipLaunchKernelGGL((k_intra<uint8_t, CF, false>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
+        hipLaunchKernelGGL((k_intra<uint8_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
     else
-        hipLaunchKernelGGL((k_intra<uint16_t, CF, false>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
+        hipLaunchKernelGGL((k_intra<uint16_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
 }
 hipError_t launch_intra(const BatchArgs &a, hipStream_t s) {
     const int nw = intra_launch_waves(a);
     const size_t lds = intra_lds_bytes(a, nw);
-    if (a.iline) {
-        if (!a.iprog || a.total_rows <= 0) return hipErrorInvalidValue;
-        const hipError_t e = hipMemsetAsync(a.iprog, 0, (size_t)a.total_rows * sizeof(uint32_t), s);
-        if (e != hipSuccess) return e;
-    }
     switch (a.chroma_format) {
     case 0: launch_intra_cf<0>(a, nw, lds, s); break;
     case 2: launch_intra_cf<2>(a, nw, lds, s); break;

@@ -38,8 +38,7 @@ struct BatchArgs {
     Coef *coefs;
     uint32_t *row_counts;      // [row] = {ntu, ncoef}
     uint8_t *recon;            // sample arena (uint8 or uint16 samples)
-    int16_t *resid;            // k_transform → k_intra: residuals of TBs that need 16 bits
-    int8_t *resid8;            // the same planes at 8 bits, for TBs whose residuals all fit (TU_RES8)
+    int16_t *resid;
     uint8_t *maps;
     SaoParams *sao;
     uint32_t *status;          // per picture
@@ -60,24 +59,7 @@ struct BatchArgs {
     uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
     int has_assembly;          // some picture is PD_ASSEMBLY (launch_deblock runs k_assemble first)
-    // k_intra spread mode (small batches): one single-wave workgroup per CTB row;
-    // null: one workgroup per picture.  Per row (total_rows): CTUs finished, and
-    // the bottom sample line of the row (intra_line_stride bytes) for the row below
-    uint32_t *iprog;
-    uint8_t *iline;
 };
-
-// bytes of one k_intra spread-mode line: luma then Cb, Cr, each 4-byte aligned
-constexpr size_t intra_line_part(int max_width, int fmt, int bps, int cidx) {
-    const int w = cidx ? (fmt ? max_width >> chroma_sx(fmt) : 0) : max_width;
-    return ((size_t)w * (size_t)bps + 3) & ~size_t(3);
-}
-constexpr size_t intra_line_stride(int max_width, int fmt, int bps) {
-    return intra_line_part(max_width, fmt, bps, 0) + 2 * intra_line_part(max_width, fmt, bps, 1);
-}
-// host: whether a batch of `rows` CTB rows reconstructs in k_intra's spread
-// mode (HEIFGPU_INTRA_SPREAD=0/1 forces it; default: up to about one row per SIMD)
-bool intra_spread_for(int rows);
 
 // k_ycbcr_rgb (color.hip): one decoded image → interleaved RGB8, rotated
 struct ColorArgs {

@@ -70,7 +70,6 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     // VGPRs 34 -> 70 and measured 14.6 -> 18.6 ms.)
     HG_BLOCK_SHARED int16_t tile[kWaves][2][32 * 32];
     HG_BLOCK_SHARED int32_t extent[kWaves][2];  // last nonzero row / column of d
-    HG_BLOCK_SHARED int32_t wide[kWaves][4];    // per TB of the round: a residual outside int8
     HG_BLOCK_SHARED int8_t s_tm[32 * 32];
     HG_BLOCK_SHARED int8_t s_dst[16];
     // every wave fills the tables (same values; the host emulation runs one lane per wave)
@@ -85,19 +84,13 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     if (row >= hctb) return;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t ntu = a.row_counts[2 * (pd.row_off + row)];
-    TuRec *tus = a.tus + pd.tu_off + (uint64_t)row * pd.tu_cap_row;
+    const TuRec *tus = a.tus + pd.tu_off + (uint64_t)row * pd.tu_cap_row;
     const Coef *coefs = a.coefs + pd.coef_off + (uint64_t)row * pd.coef_cap_row;
     const int W = sp.width, H = sp.height;
     const int cw = sp.chroma_format ? W >> chroma_sx(sp.chroma_format) : 0;
     const int ch = sp.chroma_format ? H >> chroma_sy(sp.chroma_format) : 0;
-    // residuals of a TB go to the int16 arena, or (TU_RES8, set here) to the int8
-    // arena when every value fits, as one contiguous run (resid_tb_off)
-    int16_t *res16 = a.resid + pd.resid_off;
-    int8_t *res8 = a.resid8 + pd.resid_off;
-    const int wctb = (W + (1 << sp.log2_ctb) - 1) >> sp.log2_ctb;
-    auto tb_off = [&](const TuRec &tu) {
-        return resid_tb_off(sp.log2_ctb, wctb, sp.chroma_format, tu.flags & TU_CIDX_MASK, tu.x, tu.y);
-    };
+    int16_t *res_plane[3] = {a.resid + pd.resid_off, a.resid + pd.resid_off + (size_t)W * H,
+                             a.resid + pd.resid_off + (size_t)W * H + (size_t)cw * ch};
     const int pitch[3] = {W, cw, cw};
     const bool scaling = (sp.flags & SP_SCALING_LIST) != 0;
     int16_t *d = tile[wave][0];
@@ -118,7 +111,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                 tu = tus[(uint32_t)wave + kWaves * jq];
                 const int cidx = tu.flags & TU_CIDX_MASK;
                 return (tu.flags & TU_CBF) && tu.log2 == 2 && cidx <= 2 && tu.x + 4 <= pitch[cidx] &&
-                       tu.y + 4 <= (cidx ? ch : H) && !((tu.x | tu.y) & 3);
+                       tu.y + 4 <= (cidx ? ch : H);
             };
             // the lane's record, loaded once per round (each phase below would
             // otherwise re-load it after the wave syncs)
@@ -134,10 +127,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                 return ok_c;
             };
 #endif
-            for (int vl = lane; vl < 64; vl += kWave) {
-                d[vl] = 0;
-                if (vl < 4) wide[wave][vl] = 0;
-            }
+            for (int vl = lane; vl < 64; vl += kWave) d[vl] = 0;
             wave_sync();
             for (int vl = lane; vl < 64; vl += kWave) {
                 TuRec tu;
@@ -192,23 +182,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                         s += (int32_t)(dst_tr ? s_dst[k * 4 + x] : s_tm[(k * 8) * 32 + x]) * gq[y * 4 + k];
                     r = (int)((s + (1 << (bd2 - 1))) >> bd2);
                 }
-                // the lane's own d entry is free now (bypass / transform skip read it above)
-                r = clip16(r);
-                d[vl] = (int16_t)r;
-                if (r < -128 || r > 127) wide[wave][vl >> 4] = 1;
-            }
-            wave_sync();
-            // the residual store, 8 or 16 bits per TB, and the TB's TU_RES8
-            for (int vl = lane; vl < 64; vl += kWave) {
-                TuRec tu;
-                if (!grp(vl, tu)) continue;
-                const size_t o = tb_off(tu) + (size_t)(vl & 15);
-                const bool w16 = wide[wave][vl >> 4] != 0;
-                if (w16) res16[o] = d[vl];
-                else res8[o] = (int8_t)d[vl];
-                if ((vl & 15) == 0)
-                    tus[(uint32_t)wave + kWaves * (j + (uint32_t)(vl >> 4))].flags =
-                        (uint8_t)((tu.flags & ~TU_RES8) | (w16 ? 0 : TU_RES8));
+                res_plane[cidx][(size_t)(tu.y + y) * pitch[cidx] + tu.x + x] = (int16_t)clip16(r);
             }
             wave_sync();
         }
@@ -222,14 +196,11 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         const int cidx = tu.flags & TU_CIDX_MASK;
         const int log2n = tu.log2, n = 1 << log2n;
         if (log2n < 2 || log2n > 5 || cidx > 2 || tu.x + n > pitch[cidx] || tu.y + n > (cidx ? ch : H)) continue;
-        // aligned to its size and inside one CTB: its residual run stays in the CTU's region
-        if (((tu.x | tu.y) & (n - 1)) || log2n > sp.log2_ctb - (cidx ? max(chroma_sx(sp.chroma_format), chroma_sy(sp.chroma_format)) : 0))
-            continue;
         const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
         const bool bypass = (tu.flags & TU_BYPASS) != 0, ts = (tu.flags & TU_TSKIP) != 0;
         // 1. zero the tile, scatter d[y][x] (scaled unless bypass)
         for (int i = lane; i < n * n / 2; i += kWave) reinterpret_cast<int32_t *>(d)[i] = 0;
-        if (lane == 0) extent[wave][0] = extent[wave][1] = wide[wave][0] = 0;
+        if (lane == 0) extent[wave][0] = extent[wave][1] = 0;
         wave_sync();
         const int qp = tu.qp;
         const int bd_shift = bd + log2n - 5;
@@ -258,32 +229,16 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         wave_sync();
         const int rows = extent[wave][0] + 1, cols = extent[wave][1] + 1;  // d is zero beyond these
         const int bd2 = 20 - bd;
-        const size_t base = tb_off(tu);
-        int16_t *dst = res16 + base;
-        int8_t *dst8 = res8 + base;
-        // the TB's residuals, now in d, to the int8 or int16 planes (TU_RES8 when all fit)
-        auto store_tb = [&]() {
-            const bool w16 = wide[wave][0] != 0;
-            for (int i = lane; i < n * n; i += kWave) {
-                if (w16) dst[i] = d[i];
-                else dst8[i] = (int8_t)d[i];
-            }
-            if (lane == 0) tus[t].flags = (uint8_t)((tu.flags & ~TU_RES8) | (w16 ? 0 : TU_RES8));
-            wave_sync();
-        };
+        int16_t *dst = res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x;
         if (bypass || ts) {
             // bypass: r = TransCoeffLevel; transform skip: r = (d << tsShift) then >> bdShift
-            // (in place: each entry is read and rewritten by the same lane)
             const int ts_shift = 5 + log2n;
             for (int i = lane; i < n * n; i += kWave) {
                 int r = d[i];
                 if (!bypass) r = (r * (1 << ts_shift) + (1 << (bd2 - 1))) >> bd2;
-                r = clip16(r);
-                d[i] = (int16_t)r;
-                if (r < -128 || r > 127) wide[wave][0] = 1;
+                dst[(i >> log2n) * pitch[cidx] + (i & (n - 1))] = (int16_t)clip16(r);
             }
             wave_sync();
-            store_tb();
             continue;
         }
         const bool dst_tr = (tu.flags & TU_DST) != 0;
@@ -291,13 +246,8 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         if (!dst_tr && rows == 1 && cols == 1) {
             // DC only: both stages are constant (transMatrix[0][*] = 64)
             const int g0 = clip16(((int64_t)64 * d[0] + 64) >> 7);
-            const int r = clip16(((int64_t)64 * g0 + (1 << (bd2 - 1))) >> bd2);
-            const bool w16 = r < -128 || r > 127;
-            for (int i = lane; i < n * n; i += kWave) {
-                if (w16) dst[i] = (int16_t)r;
-                else dst8[i] = (int8_t)r;
-            }
-            if (lane == 0) tus[t].flags = (uint8_t)((tu.flags & ~TU_RES8) | (w16 ? 0 : TU_RES8));
+            const int16_t r = (int16_t)clip16(((int64_t)64 * g0 + (1 << (bd2 - 1))) >> bd2);
+            for (int i = lane; i < n * n; i += kWave) dst[(i >> log2n) * pitch[cidx] + (i & (n - 1))] = r;
             wave_sync();
             continue;
         }
@@ -327,13 +277,9 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
             } else {
                 for (int j = 0; j < cols; ++j) s += (int32_t)s_tm[(j * kstep) * 32 + x] * g[y * n + j];
             }
-            // d is free since the column pass: the TB's residuals go there first
-            const int r = clip16((s + (1 << (bd2 - 1))) >> bd2);
-            d[o] = (int16_t)r;
-            if (r < -128 || r > 127) wide[wave][0] = 1;
+            dst[y * pitch[cidx] + x] = (int16_t)clip16((s + (1 << (bd2 - 1))) >> bd2);
         }
         wave_sync();
-        store_tb();
     }
 }
 

@@ -70,10 +70,6 @@ inline void hg_atomic_store(T *p, T v) {
     __atomic_store_n(p, v, __ATOMIC_RELEASE);
 }
 inline void atomicOr(uint32_t *p, uint32_t v) { __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
-// words another CU reads (see the GPU versions below)
-inline void hg_store_agent(uint32_t *p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
-inline uint32_t hg_load_agent(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
-inline void hg_stores_done() { std::atomic_thread_fence(std::memory_order_release); }
 inline void atomicMax(int32_t *p, int32_t v) {
     int32_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);
     while (cur < v && !__atomic_compare_exchange_n(p, &cur, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
@@ -110,14 +106,4 @@ template <class T>
 __device__ __forceinline__ void hg_atomic_store(T *p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Words another CU (possibly on another XCD) reads: agent-scope accesses
-// (sc1: coherent across the XCDs' L2s without whole-cache write-backs), and the
-// wait that completes this wave's earlier such stores before a progress word.
-__device__ __forceinline__ void hg_store_agent(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t hg_load_agent(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void hg_stores_done() { __builtin_amdgcn_s_waitcnt(0x0f70); }  // vmcnt(0)
 #endif

@@ -35,12 +35,8 @@ def _run(exe, path, env_extra=None):
 # (one picture per wave for a single image), the full 64-lane packing of large
 # batches (four 16-row pictures per wave), and batch (unsorted) wave order
 LANES = {"HEIFGPU_PARSE": "lanes"}
-# k_intra: a single image reconstructs in spread mode (a workgroup per CTB
-# row) by default; "packed" and "ppw1" force the batch mode (a workgroup per picture)
-WG_INTRA = {"HEIFGPU_INTRA_SPREAD": "0"}
-PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "spread"}, "lanes": LANES,
-           "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0", **WG_INTRA},
-           "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1", **WG_INTRA}, "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
+PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "spread"}, "lanes": LANES, "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0"},
+           "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1"}, "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
 
 
 @pytest.mark.parametrize("parser", list(PARSERS))
