@@ -60,7 +60,7 @@ __constant__ uint8_t c_ctx_init_l[CTX_NUM] = {HG_CTX_INIT_VALUES};
 #if defined(HG_PARSE_PROF) && !defined(HG_HOST_EMU)
 // s_memtime cycles per wave: [0] kernel, [1] passes, [2..6] unit kinds CTU, tree (CQT+CU+TT), TB, SB,
 // CTU_END; [7] units run (lanes x unit executions) (tuning build only; heifgpu_debug_counters slots 8..15)
-__device__ uint64_t g_prof_lanes[8];
+__device__ uint64_t g_prof_lanes[16];  // 8 used; 16 in the prof-sb build
 // solo / spread: per CTU (index (global CTB row) * 128 + column) s_memrealtime of
 // the first time its wave wanted to start it, the start of its U_CTU unit and
 // the end of its U_CTU_END unit (heifgpu_debug_counters slots 8 on)
@@ -180,7 +180,22 @@ struct Lane {
     // v_writelane; the one field whose lanes differ
     uint32_t cx;
     uint32_t reinit;  // F_REINIT: RBSP byte (absolute) where the engine restarts after PCM samples
+#if defined(HG_PARSE_PROF_SB)
+    // solo tuning build: s_memtime cycles of unit_sb's phases (header, sig loop,
+    // greater1/2, signs + levels + coefficient stores) and sig bins / coefficients
+    uint64_t psb[6];
+#endif
 };
+#if defined(HG_PARSE_PROF_SB) && !defined(HG_HOST_EMU)
+#define HG_SB_T(L, i, t0)                                      \
+    do {                                                       \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
+        (L).psb[i] += t_ - (t0);                               \
+        (t0) = t_;                                             \
+    } while (0)
+#else
+#define HG_SB_T(L, i, t0) ((void)0)
+#endif
 
 // engine context of one lane (lanes mode: every lane its own substream)
 struct Eng {
@@ -287,10 +302,10 @@ struct SoloWin {
 #if defined(HG_HOST_EMU)
     uint32_t *w, *f;  // [128], [64]
     void load(const uint8_t *rbsp, uint32_t chunk, uint32_t lim, int) {
-        for (int l = 0; l < 64; ++l) {
+        for (int l = 0; l < 64; ++l) {  // big-endian words (as the GPU window holds them)
             const uint32_t o = std::min((chunk * 64u + (uint32_t)l) * 4u, lim);
-            f[l] = (uint32_t)rbsp[o] | ((uint32_t)rbsp[o + 1] << 8) | ((uint32_t)rbsp[o + 2] << 16) |
-                   ((uint32_t)rbsp[o + 3] << 24);
+            f[l] = ((uint32_t)rbsp[o] << 24) | ((uint32_t)rbsp[o + 1] << 16) | ((uint32_t)rbsp[o + 2] << 8) |
+                   (uint32_t)rbsp[o + 3];
         }
     }
     void commit(uint32_t chunk) {
@@ -304,11 +319,14 @@ struct SoloWin {
         const uint32_t o = (chunk * 64u + (uint32_t)lane) * 4u;
         f = *reinterpret_cast<const uint32_t *>(rbsp + (o < lim ? o : lim));
     }
-    // the copy is the first use of the staged load: the compiler waits for it here
+    // the copy is the first use of the staged load: the compiler waits for it
+    // here.  The window holds big-endian words (byte-swapped once per dword, by
+    // the lanes in parallel), so the engine's bit refill is scalar shifts only
     __device__ __forceinline__ void commit(uint32_t chunk) {
         const bool odd = (chunk & 1u) != 0;  // both written: no address select
-        r1 = odd ? f : r1;
-        r0 = odd ? r0 : f;
+        const uint32_t be = __builtin_bswap32(f);
+        r1 = odd ? be : r1;
+        r0 = odd ? r0 : be;
     }
     __device__ __forceinline__ Win view() const { return Win{r0, r1}; }
 #endif
@@ -448,7 +466,8 @@ HG_HD inline uint32_t bswap32(uint32_t w) {
 
 // next RBSP dword of the queue.  Normally a or b; a lane that drained both
 // inside one pass takes f (waiting for it) or loads synchronously.  Solo
-// mode: dword L.lb of the register window (filled between units).
+// mode: dword L.lb of the register window (filled between units), already
+// big-endian (be_pop).
 template <class EG>
 HG_HD inline uint32_t q_pop(Lane &L, const EG &G) {
     if constexpr (EG::kSolo) return G.win.get(L.lb++);
@@ -467,6 +486,13 @@ HG_HD inline uint32_t q_pop(Lane &L, const EG &G) {
         }
     }
     return w;
+}
+
+// the next 32 bits of the substream, MSB first
+template <class EG>
+HG_HD inline uint32_t be_pop(Lane &L, const EG &G) {
+    if constexpr (EG::kSolo) return q_pop(L, G);
+    return bswap32(q_pop(L, G));
 }
 
 // pass start (after pass_wait): land f, issue the next block
@@ -490,10 +516,21 @@ HG_HD inline void q_refill(Lane &L, const Eng &G) {
 template <class EG>
 HG_HD inline void vfill(Lane &L, const EG &G) {
     if (L.cn < 16) {
-        L.cur |= (uint64_t)bswap32(q_pop(L, G)) << (32 - L.cn);
+        L.cur |= (uint64_t)be_pop(L, G) << (32 - L.cn);
         L.cn += 32;
     }
-    L.value = (L.value << 16) | (uint32_t)(L.cur >> 48);
+#if !defined(HG_HOST_EMU) && defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (EG::kSolo) {
+        // scalar: the compiler turns this into a funnel shift, which only the VALU has
+        const uint32_t top = (uint32_t)(L.cur >> 48);
+        uint32_t nv;
+        asm("s_lshl_b32 %0, %1, 16\n\ts_or_b32 %0, %0, %2" : "=&s"(nv) : "s"(uni32(L.value)), "s"(uni32(top)) : "scc");
+        L.value = nv;
+    } else
+#endif
+    {
+        L.value = (L.value << 16) | (uint32_t)(L.cur >> 48);
+    }
     L.cur <<= 16;
     L.cn -= 16;
     L.k += 16;
@@ -515,7 +552,7 @@ HG_HD inline void engine_init(Lane &L, const EG &G, uint32_t start, uint32_t end
         L.fp = 0;
         L.lb = a0 + 32;
     }
-    L.cur = (uint64_t)bswap32(q_pop(L, G)) << (32 + sh);
+    L.cur = (uint64_t)be_pop(L, G) << (32 + sh);
     L.cn = 32 - (int)sh;
     L.budget = 8 * (int32_t)(end - start);
     L.value = 0;
@@ -544,6 +581,26 @@ HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
     const uint32_t lps = ((uint32_t)row >> ((L.range >> 3) & 24u)) & 0xffu;
     const uint32_t rm = L.range - lps;
     const uint32_t sr = rm << L.k;
+#if !defined(HG_HOST_EMU) && defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (EG::kSolo) {
+        // scalar engine: the LPS test as an integer straight from SCC (as a
+        // boolean the compiler carries a lane mask and rebuilds the bin
+        // through a VALU select and v_readfirstlane), then mask arithmetic.
+        // (uni32: the lanes are identical, but where the compiler cannot
+        // prove it, e.g. at engine start, the operands must be made scalar)
+        uint32_t lp;
+        asm("s_cmp_ge_u32 %1, %2\n\ts_cselect_b32 %0, 1, 0" : "=s"(lp) : "s"(uni32(L.value)), "s"(uni32(sr)) : "scc");
+        const uint32_t m = 0u - lp;
+        s = ((hi >> (8u & ~m)) & 0xffu) ^ mps;
+        L.value -= sr & m;
+        const uint32_t rn = (lps & m) | (rm & ~m);
+        const int nb = __builtin_clz(rn) - 23;
+        L.range = rn << nb;
+        L.k -= nb;
+        if (L.k < 8) vfill(L, G);
+        return (int)(mps ^ lp);
+    }
+#endif
     const bool isl = L.value >= sr;
     L.value -= isl ? sr : 0u;
     const uint32_t rn = isl ? lps : rm;
@@ -1425,6 +1482,9 @@ HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
 // U_SB: sub-block rc_i of residual_coding (7.3.8.11, 9.3.4.2.5-7)
 template <class EG>
 HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
+#if defined(HG_PARSE_PROF_SB) && !defined(HG_HOST_EMU)
+    uint64_t tsb = __builtin_amdgcn_s_memtime();
+#endif
     const int l2 = L.tb_log2, cidx = L.tb_cidx, i = L.rc_i;
     const int sbl = l2 - 2, sbw = 1 << sbl;
     const int sp = scan_pos(sbl, L.rc_scan, i);
@@ -1462,25 +1522,28 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             if ((xS | yS) == 0) seq &= ~0xfull;  // DC of the TB (scan position 0 of sub-block 0): sigCtx 0
             c0 = cb(0) | (cb(off) << 8) | (cb(off + 1) << 16) | (cb(off + 2) << 24);
         }
+        HG_SB_T(L, 0, tsb);
         if constexpr (EG::kSolo) {
             // scalar engine: slots 0..7 as one 64-bit word (a shift reads or
-            // writes a slot), slot 8 apart
+            // writes a slot), slot 8 apart; every select branch-free, the bin
+            // an integer, so an iteration is one scalar chain
             uint64_t cc = (uint64_t)c0 | ((uint64_t)c1 << 32);
-            for (int nn = nstart; nn >= 0; --nn) {
-                if (nn > 0 || !infer_dc) {
-                    const uint32_t slot = (uint32_t)(seq >> (4 * nn)) & 15u, sh = (slot & 7u) * 8u;
-                    uint32_t cs = slot < 8u ? (uint32_t)(cc >> sh) & 0xffu : c2;
-                    const int bin = dec_s(L, G, cs);
-                    if (slot < 8u) cc = (cc & ~(0xffull << sh)) | ((uint64_t)cs << sh);
-                    else c2 = cs;
-                    if (bin) {
-                        sig |= 1u << nn;
-                        infer_dc = false;
-                    }
-                } else {
-                    sig |= 1u;  // inferred DC of a coded sub-block
-                }
-            }
+            auto dec_slot = [&](uint32_t slot) -> uint32_t {
+                const uint32_t sh = (slot & 7u) * 8u;
+                const bool hi = slot >= 8u;
+                uint32_t cs = hi ? c2 : (uint32_t)(cc >> sh) & 0xffu;
+                const uint32_t bin = (uint32_t)dec_s(L, G, cs);
+                const uint64_t ncc = (cc & ~(0xffull << sh)) | ((uint64_t)cs << sh);
+                cc = hi ? cc : ncc;
+                c2 = hi ? cs : c2;
+                return bin;
+            };
+            // positions nstart .. 1 are always decoded; only position 0 of a
+            // coded sub-block with no other significant coefficient is inferred
+            uint32_t sg = sig;
+            for (int nn = nstart; nn > 0; --nn) sg |= dec_slot((uint32_t)(seq >> (4 * nn)) & 15u) << nn;
+            if (nstart >= 0) sg |= (infer_dc && sg == 0) ? 1u : dec_slot((uint32_t)seq & 15u);
+            sig = sg;
             c0 = (uint32_t)cc;
             c1 = (uint32_t)(cc >> 32);
         } else {
@@ -1510,6 +1573,10 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             cw(off + 1, c0 >> 16);
             cw(off + 2, c0 >> 24);
         }
+#if defined(HG_PARSE_PROF_SB) && !defined(HG_HOST_EMU)
+        L.psb[4] += (uint64_t)(nstart + 1);
+#endif
+        HG_SB_T(L, 1, tsb);
     }
     if (sig) {
         // greater1 / greater2 (9.3.4.2.6-7)
@@ -1542,6 +1609,7 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         L.rc_prev_c1 = c1;
         for (int k = 0; k < 4; ++k) ctx_st(L, G, gbase + k, (gc >> (8 * k)) & 0xffu);
         if (last_g1 >= 0 && dec(L, G, CTX_GT2 + ctx_set + (cidx ? 4 : 0))) g2 = 1u << last_g1;
+        HG_SB_T(L, 2, tsb);
         const bool sign_hidden = !(L.fl & F_BYPASS) && (last_sig - first_sig > 3);
         const bool hide = (P.flags & SP_SIGN_HIDING) && sign_hidden;
         const int nsign = __builtin_popcount(sig) - (hide ? 1 : 0);
@@ -1607,6 +1675,10 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
                 L.status |= ST_CAPACITY;
             ++num_sig;
         }
+#if defined(HG_PARSE_PROF_SB) && !defined(HG_HOST_EMU)
+        L.psb[5] += (uint64_t)__builtin_popcount(sig);
+#endif
+        HG_SB_T(L, 3, tsb);
     }
     if (--L.rc_i < 0) tb_done(L, ld, P);
 }
@@ -2189,6 +2261,9 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
     LanePic &P = s_pic[0];
     const bool live = in && w < NW && lane_init(L, P, ld, a, pic, row, 0, Spread ? (1 << 20) : NW);  // every lane alike
     if (!live) L.st = U_DONE;
+#if defined(HG_PARSE_PROF_SB)
+    for (int k = 0; k < 6; ++k) L.psb[k] = 0;
+#endif
     __syncthreads();
     if (!__builtin_amdgcn_readfirstlane(live ? 1 : 0)) return;
     const Env E = Spread ? Env{&a, s_lds, a.xprog + P.row_off, a.xctx + (size_t)P.row_off * CTX_PAD, row}
@@ -2202,7 +2277,13 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
     int want_seen = -1;  // the CTU whose want time is recorded
 #endif
+#if defined(HG_PARSE_PROF_SB)
+    uint64_t pw[2] = {0, 0};  // cycles of not-run iterations (WPP polls + sleeps); driver cycles of run ones
+#endif
     for (;;) {
+#if defined(HG_PARSE_PROF_SB)
+        const uint64_t t_top = __builtin_amdgcn_s_memtime();
+#endif
         // the wave's state (equal in every lane), made scalar
         int st = L.st, run = st != U_DONE && (st != U_CTU || ctu_ready<EG>(L, P, E));
 #if defined(HG_PARSE_PROF)
@@ -2222,6 +2303,9 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
             // the row above is not 2 CTUs ahead: sleep (~64 cycles a unit), so the
             // busy waves on this SIMD keep the issue slots
             __builtin_amdgcn_s_sleep(HG_SOLO_SLEEP);
+#if defined(HG_PARSE_PROF_SB)
+            pw[0] += __builtin_amdgcn_s_memtime() - t_top;
+#endif
             continue;
         }
         start = (uint32_t)__builtin_amdgcn_readfirstlane((int)start);
@@ -2247,10 +2331,19 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
 #endif
         }
 #if defined(HG_PARSE_PROF)
+#if defined(HG_PARSE_PROF_SB)
+        pw[1] += t1 - t_top;
+#else
         pf[st <= U_CTU ? 2 : st <= U_TT ? 3 : st - 1] += __builtin_amdgcn_s_memtime() - t1;
         ++pf[1];
 #endif
+#endif
     }
+#if defined(HG_PARSE_PROF_SB)
+    for (int k = 0; k < 6; ++k) pf[2 + k] = L.psb[k];
+    pf[1] = pw[0];
+    if (lane == 0) atomicAdd((unsigned long long *)&g_prof_lanes[8], (unsigned long long)pw[1]);
+#endif
 #if defined(HG_PARSE_PROF)
     pf[0] = __builtin_amdgcn_s_memtime() - t_start;
     if (lane == 0)
@@ -2296,10 +2389,14 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
 // for the product library (counters compiled out; `make prof` has them).
 extern "C" int heifgpu_debug_counters(uint64_t *out, int n) {
 #if defined(HG_PARSE_PROF)
-    uint64_t tmp[8] = {};
+    uint64_t tmp[16] = {};
     if (hipMemcpyFromSymbol(tmp, HIP_SYMBOL(hg::g_prof_lanes), sizeof(tmp)) != hipSuccess) return -1;
-    const uint64_t zero[8] = {};
+    const uint64_t zero[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_prof_lanes), zero, sizeof(zero)) != hipSuccess) return -1;
+#if defined(HG_PARSE_PROF_SB)
+    for (int k = 0; k < n && k < 16; ++k) out[k] = tmp[k];
+    return n < 16 ? n : 16;
+#endif
     for (int k = 0; k < n && k < 8; ++k) out[k] = tmp[k];
     if (n <= 8) return 8;
     // slots 8 on: the per-CTU times (3 per CTU), then zeroed

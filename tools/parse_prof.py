@@ -50,8 +50,23 @@ def main():
     torch.cuda.synchronize()
     parse_ms = ctx.stage_times()[0]
     lib.heifgpu_debug_counters(buf, 16)
-    c = dict(zip(LANES, buf[:k]))
     waves = geom["workgroups"] * geom["waves_per_workgroup"]
+    if "profsb" in str(_lib.LIB_PATH):  # `make prof-sb`: solo / spread sub-block phases
+        names = ["cycles", "wait", "sb_head", "sb_sig", "sb_g1", "sb_rest", "sig_bins", "coefs", "driver"]
+        c = dict(zip(names, buf[:9]))
+        res = {"images": n, "geometry": geom, "waves": waves, "parse_ms": round(parse_ms, 3),
+               "per_wave": {k2: round(c[k2] / waves, 1) for k2 in names},
+               "share_of_cycles": {k2: round(c[k2] / max(c["cycles"], 1), 3) for k2 in names[1:6] + ["driver"]},
+               "cycles_per_sig_bin": round(c["sb_sig"] / max(c["sig_bins"], 1), 1),
+               "cycles_per_coef_g1": round(c["sb_g1"] / max(c["coefs"], 1), 1),
+               "cycles_per_coef_rest": round(c["sb_rest"] / max(c["coefs"], 1), 1),
+               "bins_per_wave": round(n * BINS_PER_IMAGE / waves, 1),
+               "note": "s_memtime cycles; wait = iterations whose CTU could not start (WPP poll + sleep); driver = loop top to unit start of the units run; the rest is the units other than the sub-block"}
+        print(json.dumps(res))
+        if len(sys.argv) > 2:
+            pathlib.Path(sys.argv[2]).write_text(json.dumps(res, indent=1) + "\n")
+        return
+    c = dict(zip(LANES, buf[:k]))
     res = {
         "images": n,
         "geometry": geom,
