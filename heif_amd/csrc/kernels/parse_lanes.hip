@@ -101,11 +101,15 @@ struct LanePic {
     int w4, h4, w8, saoL, saoC;
     int R, lane0, ring;  // lanes of the picture, its first lane, rows wrap round the lanes (WPP rows > R)
     uint32_t flags, bits_off, bits_end, sub_first, row_off, tu_cap, coef_cap, pic;
-    int8_t *gqpy;
-    uint8_t *gflags, *gdepth;
-    SaoParams *gsao;
-    TuRec *tu_base;
-    Coef *coef_base;
+    // global memory, said so in the type: a generic pointer loaded from LDS
+    // would make every store through it a flat store, and flat stores count in
+    // lgkmcnt, so each later LDS read of the wave would wait for them
+    int8_t HG_GAS *gqpy;
+    uint8_t HG_GAS *gflags;
+    uint8_t HG_GAS *gdepth;
+    SaoParams HG_GAS *gsao;
+    TuRec HG_GAS *tu_base;
+    Coef HG_GAS *coef_base;
 };
 
 // syntax units (Lane.st)
@@ -1592,19 +1596,36 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         const int first_sig = 31 - __builtin_clz(sig & (0u - sig));
         const int last_sig = msb32(sig);
         int num_g1 = 0, last_g1 = -1;
-        for (uint32_t m = sig; m && num_g1 < 8;) {
-            const int nn = msb32(m);
-            m &= ~(1u << nn);
-            const int gs = (c1 < 3 ? c1 : 3) * 8;
-            uint32_t cs = (gc >> gs) & 0xffu;
-            const int f = dec_s(L, G, cs);
-            gc = (gc & ~(0xffu << gs)) | (cs << gs);
-            ++num_g1;
-            if (f) {
-                g1 |= 1u << nn;
-                if (last_g1 < 0) last_g1 = nn;
+        if constexpr (EG::kSolo) {
+            // scalar engine: the first 8 significant positions, every update a
+            // select on integers (no boolean carried across the engine's refill branch)
+            uint32_t m = sig;
+            for (int j = 0; j < 8 && m; ++j) {
+                const int nn = msb32(m);
+                m ^= 1u << nn;
+                const uint32_t gs = (uint32_t)(c1 < 3 ? c1 : 3) * 8u;
+                uint32_t cs = (gc >> gs) & 0xffu;
+                const uint32_t f = (uint32_t)dec_s(L, G, cs);
+                gc = (gc & ~(0xffu << gs)) | (cs << gs);
+                g1 |= f << nn;
+                last_g1 = (last_g1 < 0 && f) ? nn : last_g1;
+                c1 = (c1 > 0 && !f) ? c1 + 1 : 0;
             }
-            if (c1 > 0) c1 = f ? 0 : c1 + 1;
+        } else {
+            for (uint32_t m = sig; m && num_g1 < 8;) {
+                const int nn = msb32(m);
+                m &= ~(1u << nn);
+                const int gs = (c1 < 3 ? c1 : 3) * 8;
+                uint32_t cs = (gc >> gs) & 0xffu;
+                const int f = dec_s(L, G, cs);
+                gc = (gc & ~(0xffu << gs)) | (cs << gs);
+                ++num_g1;
+                if (f) {
+                    g1 |= 1u << nn;
+                    if (last_g1 < 0) last_g1 = nn;
+                }
+                if (c1 > 0) c1 = f ? 0 : c1 + 1;
+            }
         }
         L.rc_prev_c1 = c1;
         for (int k = 0; k < 4; ++k) ctx_st(L, G, gbase + k, (gc >> (8 * k)) & 0xffu);
@@ -1835,12 +1856,12 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
     P.tu_cap = pd.tu_cap_row;
     P.coef_cap = pd.coef_cap_row;
     P.pic = (uint32_t)pic;
-    P.gqpy = reinterpret_cast<int8_t *>(a.maps + pd.map_off);
-    P.gflags = a.maps + pd.map_off + (size_t)P.w4 * P.h4;
-    P.gdepth = a.maps + pd.map_off + 2 * (size_t)P.w4 * P.h4;
-    P.gsao = a.sao + pd.sao_off;
-    P.tu_base = a.tus + pd.tu_off;
-    P.coef_base = a.coefs + pd.coef_off;
+    P.gqpy = (int8_t HG_GAS *)(a.maps + pd.map_off);
+    P.gflags = (uint8_t HG_GAS *)(a.maps + pd.map_off + (size_t)P.w4 * P.h4);
+    P.gdepth = (uint8_t HG_GAS *)(a.maps + pd.map_off + 2 * (size_t)P.w4 * P.h4);
+    P.gsao = (SaoParams HG_GAS *)(a.sao + pd.sao_off);
+    P.tu_base = (TuRec HG_GAS *)(a.tus + pd.tu_off);
+    P.coef_base = (Coef HG_GAS *)(a.coefs + pd.coef_off);
     L.status = 0;
     L.cn = 0;
     L.k = 8;

@@ -57,6 +57,7 @@ inline void emu_syncthreads() {
 #define gridDim (::hg::g_emu.gdim)
 #define __syncthreads() ::hg::emu_syncthreads()
 #define HG_UNI(v) (v)
+#define HG_GAS
 #define HG_FENCE_ACQ() std::atomic_thread_fence(std::memory_order_acquire)
 #define HG_FENCE_REL() std::atomic_thread_fence(std::memory_order_release)
 #define HG_WAVE_SYNC() ((void)0)
@@ -85,6 +86,12 @@ namespace hg {
 constexpr int kWave = 64;
 }
 #define HG_UNI(v) __builtin_amdgcn_readfirstlane(v)
+// global address space (a pointer type qualifier; host emulation: none)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HG_GAS __attribute__((address_space(1)))
+#else
+#define HG_GAS
+#endif
 #define HG_FENCE_ACQ() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup")
 #define HG_FENCE_REL() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup")
 // Orders one wave's own LDS traffic across lanes (write by lane i, read by
