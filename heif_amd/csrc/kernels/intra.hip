@@ -567,8 +567,14 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
     progress[wave] = 0;  // every lane writes the same value
     __syncthreads();
     const uint32_t stride = (uint32_t)wctb + 1;
-    const int prev_wave = (wave + nw - 1) % nw;
-    for (int r = wave; r < hctb; r += nw) {
+    // split (a.intra_split): waves in pairs per CTB row, luma on the even one and
+    // Cb, Cr on the odd one.  Chroma prediction reads chroma neighbours only, so
+    // the two TB chains of a CTU run side by side instead of one after the other
+    const bool split = a.intra_split != 0 && ncomp == 3;
+    const int cls = split ? (wave & 1) : 0, rw = split ? wave >> 1 : wave, nrw = split ? nw >> 1 : nw;
+    const int k0 = split && cls ? 1 : 0, k1 = split && !cls ? 1 : ncomp;  // this wave's components
+    const int prev_wave = split ? ((rw + nrw - 1) % nrw) * 2 + cls : (wave + nw - 1) % nw;
+    for (int r = rw; r < hctb; r += nrw) {
         const uint32_t ntu = a.row_counts[2 * (pd.row_off + r)];
         const TuRec *tus = a.tus + pd.tu_off + (uint64_t)r * pd.tu_cap_row;
         int cur = -1;
@@ -602,6 +608,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                     // finish CTU `cur`: write the window back, keep its last column as `left`
                     _Pragma("unroll") for (int k = 0; k < 3; ++k) {
                         if (k >= ncomp) break;
+                        if (k < k0 || k >= k1) continue;
                         const Win<Pel> &w = win[k];
                         const int PW = k ? cw : W, PH = k ? ch : H;
                         const int vw = min(w.csx, PW - w.cx0), vh = min(w.csy, PH - w.cy0);
@@ -642,6 +649,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                 // start CTU c: the row above (corner .. above-right) and the residuals
                 _Pragma("unroll") for (int k = 0; k < 3; ++k) {
                     if (k >= ncomp) break;
+                    if (k < k0 || k >= k1) continue;
                     Win<Pel> &w = win[k];
                     const int PW = k ? cw : W, PH = k ? ch : H;
                     w.cx0 = c * w.csx;
@@ -656,7 +664,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                 wave_sync();
             }
             const int cidx = tu.flags & TU_CIDX_MASK;
-            if (cidx >= ncomp) continue;
+            if (cidx >= ncomp || cidx < k0 || cidx >= k1) continue;
             // field-wise selects on the wave-uniform cidx: indexing win[] with it (or
             // selecting one of its elements by reference) keeps the array in scratch memory
             Win<Pel> w;
@@ -701,6 +709,26 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
     }
 }
 
+// luma / chroma wave pairs (k_intra's split): for batches of few pictures,
+// where the per-picture TB chain is the latency (HEIFGPU_INTRA_SPLIT=0/1 forces it)
+static bool intra_split_for(const BatchArgs &a, int nw) {
+    static const int forced = [] {
+        const char *e = std::getenv("HEIFGPU_INTRA_SPLIT");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (a.chroma_format == 0) return false;
+    if (forced >= 0) return forced != 0;
+    return nw >= 4 && (long)a.n_pics * a.max_rows <= 4096;
+}
+
+// waves of a split workgroup: two per row in flight, within the LDS budget and kMaxWaves
+static int intra_split_waves(const BatchArgs &a, int nw) {
+    int cap = intra_waves(a.max_log2ctb, a.chroma_format, a.bytes_per_sample, 2 * a.max_rows);
+    int w = 2 * nw < cap ? 2 * nw : cap;
+    w &= ~1;
+    return w < 2 ? 2 : w;
+}
+
 static int intra_launch_waves(const BatchArgs &a) {
     // all pictures of a batch share bit depth and chroma format; the CTB size
     // may differ, so size for the largest one.  HEIFGPU_INTRA_WAVES caps the
@@ -730,8 +758,11 @@ static void emu_intra_cf(const BatchArgs &a, int nw) {
     if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t, CF>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
     else emu_launch(k_intra<uint16_t, CF>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
 }
-void emu_intra(const BatchArgs &a) {
-    const int nw = intra_launch_waves(a);
+void emu_intra(const BatchArgs &a0) {
+    BatchArgs a = a0;
+    int nw = intra_launch_waves(a);
+    a.intra_split = intra_split_for(a, nw) ? 1 : 0;
+    if (a.intra_split) nw = intra_split_waves(a, nw);
     switch (a.chroma_format) {
     case 0: emu_intra_cf<0>(a, nw); break;
     case 2: emu_intra_cf<2>(a, nw); break;
@@ -747,8 +778,11 @@ static void launch_intra_cf(const BatchArgs &a, int nw, size_t lds, hipStream_t 
     else
         hipLaunchKernelGGL((k_intra<uint16_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
 }
-hipError_t launch_intra(const BatchArgs &a, hipStream_t s) {
-    const int nw = intra_launch_waves(a);
+hipError_t launch_intra(const BatchArgs &a0, hipStream_t s) {
+    BatchArgs a = a0;
+    int nw = intra_launch_waves(a);
+    a.intra_split = intra_split_for(a, nw) ? 1 : 0;
+    if (a.intra_split) nw = intra_split_waves(a, nw);
     const size_t lds = intra_lds_bytes(a, nw);
     switch (a.chroma_format) {
     case 0: launch_intra_cf<0>(a, nw, lds, s); break;

@@ -59,6 +59,7 @@ struct BatchArgs {
     uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
     int has_assembly;          // some picture is PD_ASSEMBLY (launch_deblock runs k_assemble first)
+    int intra_split;           // k_intra: luma and chroma on separate waves (set by launch_intra)
 };
 
 // k_ycbcr_rgb (color.hip): one decoded image → interleaved RGB8, rotated

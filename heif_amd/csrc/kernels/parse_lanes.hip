@@ -689,10 +689,11 @@ HG_HD inline uint32_t div_range(uint32_t top, uint32_t r) {
 #if defined(HG_HOST_EMU)
     return top / r;
 #else
-    uint32_t q = (uint32_t)((float)top * __builtin_amdgcn_rcpf((float)r));
+    const uint32_t q = (uint32_t)((float)top * __builtin_amdgcn_rcpf((float)r));
     const int32_t rem = (int32_t)top - (int32_t)(q * r);
-    q = rem < 0 ? q - 1 : (rem >= (int32_t)r ? q + 1 : q);
-    return q;
+    // the correction as sign bits (|rem| < 2r): compares and selects here become
+    // a lane-mask boolean that the scalar engine rebuilds through the VALU
+    return q + ((uint32_t)((int32_t)r - 1 - rem) >> 31) - ((uint32_t)rem >> 31);
 #endif
 }
 
@@ -905,11 +906,21 @@ struct Env {
     int lane;
 };
 
-// WPP: the row above is two CTUs ahead of CTU L.c (or finished)
+// WPP, for parsing: a row's first CTU needs the contexts stored after CTU 1
+// of the row above (9.3.1), so two CTUs of it done; CTU c > 0 only reads the
+// CTU above it (split_cu_flag's CtDepth, sao_merge_up_flag; intra modes and
+// QP prediction stay inside the CTB row), so one CTU ahead is enough.  The
+// 2-CTU lag of the reconstruction (above-right neighbours) is k_intra's.
+// (HG_WPP_LAG2: two CTUs ahead throughout, as before r03.)
 template <class EG>
 HG_HD inline bool wpp_ready(const Lane &L, const LanePic &P, const Env &E) {
     if (!(L.fl & F_WPP) || L.row == 0) return true;
-    const uint32_t need = (uint32_t)(L.row - 1) * (uint32_t)P.wctb + (uint32_t)(L.c + 2 < P.wctb ? L.c + 2 : P.wctb);
+#if defined(HG_WPP_LAG2)
+    const int ahead = L.c + 2;
+#else
+    const int ahead = L.c == 0 ? 2 : L.c + 1;
+#endif
+    const uint32_t need = (uint32_t)(L.row - 1) * (uint32_t)P.wctb + (uint32_t)(ahead < P.wctb ? ahead : P.wctb);
     const uint32_t *pw = &E.prog[P.lane0 + (L.row - 1) % P.R];
     return (EG::kSpread ? load_agent(pw) : prog_load(pw)) >= need;
 }

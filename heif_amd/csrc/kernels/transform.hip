@@ -89,8 +89,10 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     const int W = sp.width, H = sp.height;
     const int cw = sp.chroma_format ? W >> chroma_sx(sp.chroma_format) : 0;
     const int ch = sp.chroma_format ? H >> chroma_sy(sp.chroma_format) : 0;
-    int16_t *res_plane[3] = {a.resid + pd.resid_off, a.resid + pd.resid_off + (size_t)W * H,
-                             a.resid + pd.resid_off + (size_t)W * H + (size_t)cw * ch};
+    // global memory in the type: selected by cidx the pointers would be flat,
+    // and flat stores count in lgkmcnt, so every LDS wait would wait for them
+    int16_t HG_GAS *const res0 = (int16_t HG_GAS *)(a.resid + pd.resid_off);
+    int16_t HG_GAS *res_plane[3] = {res0, res0 + (size_t)W * H, res0 + (size_t)W * H + (size_t)cw * ch};
     const int pitch[3] = {W, cw, cw};
     const bool scaling = (sp.flags & SP_SCALING_LIST) != 0;
     int16_t *d = tile[wave][0];
@@ -229,7 +231,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         wave_sync();
         const int rows = extent[wave][0] + 1, cols = extent[wave][1] + 1;  // d is zero beyond these
         const int bd2 = 20 - bd;
-        int16_t *dst = res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x;
+        int16_t HG_GAS *dst = res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x;
         if (bypass || ts) {
             // bypass: r = TransCoeffLevel; transform skip: r = (d << tsShift) then >> bdShift
             const int ts_shift = 5 + log2n;

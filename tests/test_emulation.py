@@ -30,13 +30,16 @@ def _run(exe, path, env_extra=None):
     return r.returncode, r.stdout + r.stderr
 
 
+# (k_intra: a single image runs luma / chroma wave pairs; "ppw1" forces the
+# unsplit kernel.)
 # k_parse_solo (one substream per wave: the automatic choice for a single
 # image), k_parse_lanes (one substream per lane) with its adaptive geometry
 # (one picture per wave for a single image), the full 64-lane packing of large
 # batches (four 16-row pictures per wave), and batch (unsorted) wave order
 LANES = {"HEIFGPU_PARSE": "lanes"}
 PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "spread"}, "lanes": LANES, "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0"},
-           "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1"}, "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
+           "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1", "HEIFGPU_INTRA_SPLIT": "0"},
+           "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
 
 
 @pytest.mark.parametrize("parser", list(PARSERS))
