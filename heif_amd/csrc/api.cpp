@@ -439,8 +439,14 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     int least = 0, greatest = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIP_TRY(hipStreamCreateWithPriority(&c->parse, hipStreamNonBlocking, prio ? greatest : least));
-    HIP_TRY(hipStreamCreateWithFlags(&c->xform, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&c->recon, hipStreamNonBlocking));
+    // HEIFGPU_RECON_PRIORITY=1: the transform and reconstruction streams at the
+    // highest priority instead (tuning knob; the recon stream sets the step)
+    static const bool rprio = [] {
+        const char *e = std::getenv("HEIFGPU_RECON_PRIORITY");
+        return e && std::atoi(e) != 0;
+    }();
+    HIP_TRY(hipStreamCreateWithPriority(&c->xform, hipStreamNonBlocking, rprio ? greatest : least));
+    HIP_TRY(hipStreamCreateWithPriority(&c->recon, hipStreamNonBlocking, rprio ? greatest : least));
     HIP_TRY(hipStreamCreateWithFlags(&c->upload, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
