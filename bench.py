@@ -463,7 +463,8 @@ def main():
                 ["parse", "transform", "intra", "deblock", "sao_out", "rbsp"], per_step)},
             "stage_ms_alone": {k: round(v, 3) for k, v in zip(
                 ["parse", "transform", "intra", "deblock", "sao_out", "rbsp"], alone)},
-            "pipeline": "decode n+1's k_rbsp+k_parse (parse stream) overlap decode n's reconstruction (recon stream); "
+            "pipeline": "three parse-output sets: decode n+2's k_rbsp+k_parse (parse stream), decode n+1's k_transform "
+                        "(transform stream) and decode n's intra/deblock/SAO (recon stream) overlap; "
                         "the timed region includes the pipeline fill and drain; stage_ms_per_step are means over the "
                         "timed steps (overlap included), stage_ms_alone one decode with nothing beside it",
             "latency_ms_one_step": round(sum(alone), 3),

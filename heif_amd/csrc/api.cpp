@@ -44,11 +44,13 @@ static_assert(sizeof(heifgpu_tile_params) == 55 * 4 + 64 * 4, "heifgpu_tile_para
 // which writes the caller's planes and so waits for everything the caller
 // enqueued on its stream before the call; the caller's stream waits for
 // k_sao_out.  A set is reused only after the reconstruction that read it.
-// HEIFGPU_PIPELINE=0 keeps one set (no overlap); HEIFGPU_PIPELINE=3 uses three
-// sets and a third stream for k_transform, so parse n + 2, transform n + 1 and
-// reconstruction n overlap (A/B at 20 steps: 15.32 / 15.33 vs 15.67 / 15.64
-// Gpix/s for two streams: the parse, the critical path, slows from 88 to 93 ms
-// beside two other streams).
+// HEIFGPU_PIPELINE=0 keeps one set (no overlap), 2 two sets on two streams;
+// the default, 3, uses three sets and a third stream for k_transform, so
+// parse n + 2, transform n + 1 and reconstruction n overlap.  While the parse
+// was the critical path (r02) three sets lost (15.32 / 15.33 vs 15.67 / 15.64
+// Gpix/s); since the r03 parse got faster the reconstruction stream sets the
+// step and three sets win (same-box pairs at 20 steps: 18.56 / 18.49 vs
+// 17.86 / 17.77 Gpix/s, profiles/r03d/ab_pipeline_sets.txt).
 constexpr int kTimingSlots = 32;
 struct heifgpu_ctx {
     int device = 0;
@@ -532,7 +534,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         HIP_TRY(hipEventCreateWithFlags(&b->uploaded, hipEventDisableTiming));
         static const int pipeline = [] {
             const char *e = std::getenv("HEIFGPU_PIPELINE");
-            return e ? std::atoi(e) : 2;
+            return e ? std::atoi(e) : 3;
         }();
         b->n_sets = pipeline == 0 ? 1 : (pipeline == 3 ? 3 : 2);
         for (int k = 0; k < b->n_sets; ++k) {

@@ -152,8 +152,11 @@ void heifgpu_batch_free(heifgpu_batch *batch);
  * decode calls since the previous query (or since timing was enabled) of
  * parse, transform, intra, deblock, sao/output, and (last) the
  * emulation-prevention pass k_rbsp; the query resets the mean.  k_rbsp and
- * k_parse run on an internal parse stream, the rest on an internal recon
- * stream, so decode n+1's parse overlaps decode n's reconstruction. */
+ * k_parse run on an internal parse stream, k_transform on an internal
+ * transform stream and the rest on an internal recon stream, over three sets
+ * of parse outputs, so decode n+2's parse, decode n+1's transform and decode
+ * n's reconstruction overlap (HEIFGPU_PIPELINE=2: two sets, the transform on
+ * the recon stream). */
 int heifgpu_set_timing(heifgpu_ctx *ctx, int enable);
 int heifgpu_stage_times(heifgpu_ctx *ctx, float ms[6]);
 /* convenience: prepare + decode + status + free */
