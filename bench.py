@@ -67,6 +67,100 @@ def dist_env():
     return rank, world, local
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """`--gpus N` without a torchrun environment: start N copies of this
+    script, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on
+    127.0.0.1), and return a non-zero code if any rank fails.  The parent
+    never imports torch or touches the GPU: it only waits, and ends the other
+    ranks when one fails so none is left blocked in a collective.  Rank 0
+    inherits stdout and prints the JSON line; the other ranks print nothing.
+    Images (and tiles) are what shard (/root/reference/src/heic/decoder.rs:114-119),
+    so there is no data-path collective to set up here."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(pathlib.Path(__file__).resolve())] + argv, env=env))
+
+    def _term(signum, frame):
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, _term)
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the others",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+    return rc
+
+
+def dry_run(args) -> None:
+    """`--dry-run`: the multi-rank skeleton of main() with no GPU (gloo):
+    rendezvous, this rank's shard, barrier + timed region + MAX reduction,
+    and rank 0's JSON line with `n_gpus` = world size.  Tests the launcher."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world, _ = dist_env()
+    if os.environ.get("BENCH_DRY_FAIL_RANK") == str(rank):  # the launcher test's failing rank
+        raise SystemExit(f"rank {rank}: failing on request")
+    if world > 1:
+        dist.init_process_group("gloo")
+    seeds = shard_seeds(args.batch, rank)
+    ranks = [(rank, os.getpid(), seeds)]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, (rank, os.getpid(), seeds))
+        dist.barrier()
+    t0 = time.perf_counter()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (no GPU)", "value": None, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "elapsed_s": elapsed,
+                          "ranks": [{"rank": r, "pid": p, "seeds": [s[0], s[-1] + 1] if s else []}
+                                    for r, p, s in ranks]}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def shard_seeds(batch_per_rank: int, rank: int) -> list:
     """Image seeds of this rank: a contiguous block of the global batch."""
     return list(range(rank * batch_per_rank, (rank + 1) * batch_per_rank))
@@ -231,14 +325,29 @@ def main():
     ap.add_argument("--ppw", type=int, default=0, help="lanes mode: pictures per wave (0 = adaptive)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-parse + upload + decode leg")
     ap.add_argument("--e2e-batches", type=int, default=6)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: only the rank launch, rendezvous (gloo) and timing reduction")
     args = ap.parse_args()
     tiles_split = args.split == "tiles"
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # plain `python bench.py --gpus N`: one child process per GPU, started
+        # before anything here initialises HIP (torchrun sets WORLD_SIZE itself)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    rank, world, local = dist_env()
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; measuring {world} rank(s)",
+              file=sys.stderr, flush=True)
+    if args.dry_run:
+        dry_run(args)
+        return
+
     import torch
 
-    rank, world, local = dist_env()
     # the CPU baseline's -march=native oracle must be selected before anything imports the oracle
-    cpu_build = native_oracle() if rank == 0 and not args.no_cpu_baseline else None
+    # (the CPU baseline runs on rank 0 at N=1 only)
+    with_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    cpu_build = native_oracle() if with_cpu else None
     if world > 1:
         import torch.distributed as dist
 
@@ -478,7 +587,7 @@ def main():
             line["e2e"] = e2e
         if gather:
             line["tile_split_gather"] = gather
-        if not args.no_cpu_baseline:
+        if with_cpu:
             build = cpu_build
             threads = effective_cpus()
             label = "synthetic 10-bit" if c5 else "halfmoonbay"

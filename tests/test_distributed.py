@@ -239,3 +239,49 @@ def test_tile_split_gather_to_rank0_over_gloo(world):
     assert bad == 0
     assert opened == world - 1
     assert live == 2  # rank 0's own two buffers; every peer mapping closed
+
+
+def _run_bench(args, extra_env=None, timeout=180):
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(extra_env or {})
+    p = subprocess.run([sys.executable, str(bench.ROOT / "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus 2` with no torchrun environment starts two
+    ranks itself (gloo dry run: no GPU), and rank 0 alone prints one line
+    with n_gpus 2 and both ranks' disjoint shards."""
+    rc, lines, err = _run_bench(["--gpus", "2", "--dry-run", "--batch", "3", "--steps", "4", "--warmup", "1"])
+    assert rc == 0, err
+    assert len(lines) == 1, lines
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["steps"] == 4 and line["warmup"] == 1
+    ranks = sorted(line["ranks"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert len({r["pid"] for r in ranks}) == 2
+    assert [r["seeds"] for r in ranks] == [[0, 3], [3, 6]]
+
+
+def test_bench_gpus_flag_fails_when_a_rank_fails():
+    """A failing rank makes the launcher exit non-zero (and ends the other
+    rank instead of leaving it blocked at the rendezvous)."""
+    rc, lines, err = _run_bench(["--gpus", "2", "--dry-run"], {"BENCH_DRY_FAIL_RANK": "1"}, timeout=120)
+    assert rc != 0
+    assert lines == []
+    assert "rank 1" in err
+
+
+def test_bench_torchrun_environment_is_used_as_is():
+    """Under torchrun (WORLD_SIZE set) bench.py does not spawn: the one
+    process is its rank."""
+    rc, lines, err = _run_bench(["--gpus", "1", "--dry-run", "--batch", "2"],
+                                {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 0, err
+    assert lines[0]["n_gpus"] == 1 and len(lines[0]["ranks"]) == 1
