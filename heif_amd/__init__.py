@@ -196,7 +196,7 @@ class DecodeContext:
 
     def prepare(self, images: Sequence[HeifImage], tile_stride: int = 1, tile_offset: int = 0,
                 reuse: Optional["DeviceBatch"] = None, wait: bool = True, parse: str = "auto",
-                pics_per_wave: int = 0) -> "DeviceBatch":
+                pics_per_wave: int = 0, pipeline_sets: int = 0) -> "DeviceBatch":
         """Device batch of `images` (heifgpu_batch_prepare_ex).  tile_stride /
         tile_offset select the grid tiles k % tile_stride == tile_offset (the
         single-image tile split across GPUs); `reuse` reloads an existing batch
@@ -205,9 +205,10 @@ class DecodeContext:
         "lanes" (one substream per lane, `pics_per_wave` pictures per wave, 0 =
         adaptive), "solo" (one substream per wave, a picture's rows in one
         workgroup) or "spread" (one substream per wave, one workgroup per row:
-        small-batch latency)."""
+        small-batch latency).  pipeline_sets: parse-output sets of a new batch
+        (0 = default 3; 1-3, include/heifgpu.h)."""
         arr = (ctypes.c_void_p * len(images))(*[im._h.value for im in images])
-        opts = _lib.BatchOpts(tile_stride, tile_offset, _lib.PARSE_MODES[parse], pics_per_wave)
+        opts = _lib.BatchOpts(tile_stride, tile_offset, _lib.PARSE_MODES[parse], pics_per_wave, pipeline_sets)
         if reuse is not None:
             _lib.check(lib.heifgpu_batch_prepare_ex(self._h, arr, len(images), ctypes.byref(opts),
                                                     ctypes.byref(reuse._h)))

@@ -112,7 +112,8 @@ class BatchOpts(ctypes.Structure):
     """heifgpu_batch_opts: decode only grid tiles k with k % tile_stride == tile_offset;
     parse_mode (PARSE_*) and, in lanes mode, pictures per wave (0 = adaptive)."""
     _fields_ = [("tile_stride", ctypes.c_uint32), ("tile_offset", ctypes.c_uint32),
-                ("parse_mode", ctypes.c_uint32), ("pics_per_wave", ctypes.c_uint32)]
+                ("parse_mode", ctypes.c_uint32), ("pics_per_wave", ctypes.c_uint32),
+                ("pipeline_sets", ctypes.c_uint32)]
 
 
 class IpcHandle(ctypes.Structure):

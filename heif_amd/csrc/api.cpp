@@ -28,7 +28,7 @@ struct heifgpu_image {
 // the C structs' layouts are part of the ABI (INTEGRATION.md's Rust binding mirrors them)
 static_assert(sizeof(heifgpu_image_info) == 80, "heifgpu_image_info: 20 x uint32");
 static_assert(sizeof(heifgpu_planes) == 40, "heifgpu_planes: 3 pointers + 3 int32 (+ padding)");
-static_assert(sizeof(heifgpu_batch_opts) == 16, "heifgpu_batch_opts: 4 x uint32");
+static_assert(sizeof(heifgpu_batch_opts) == 20, "heifgpu_batch_opts: 5 x uint32");
 static_assert(sizeof(heifgpu_ipc_handle) == 72, "heifgpu_ipc_handle: 64-byte HIP handle + uint64 offset");
 static_assert(HEIFGPU_PARSE_AUTO == PARSE_AUTO && HEIFGPU_PARSE_LANES == PARSE_LANES && HEIFGPU_PARSE_SOLO == PARSE_SOLO &&
                   HEIFGPU_PARSE_SPREAD == PARSE_SPREAD,
@@ -172,6 +172,24 @@ struct ParseSet {
     }
 };
 
+// The descriptors every stage reads (pictures, sequences, scaling factors,
+// output planes) and the sticky status, in two generations: a reload writes
+// the generation the previous load did not use, so it waits only for the
+// decodes of the load before that (`done`), not for the ones in flight.
+struct DescGen {
+    DevBuf<PicDesc> pics;
+    DevBuf<SeqParams> seqs;
+    DevBuf<uint8_t> sf;
+    DevBuf<OutImage> outs;
+    DevBuf<uint32_t> sticky;  // per picture: OR of every decode's status since the last heifgpu_batch_status
+    std::vector<OutImage> out_host;
+    hipEvent_t done = nullptr;  // the last decode that read this generation (recon stream)
+    bool pending = false;
+    ~DescGen() {
+        if (done) (void)hipEventDestroy(done);
+    }
+};
+
 struct heifgpu_batch {
     int device = 0;
     size_t n_images = 0;
@@ -181,15 +199,17 @@ struct heifgpu_batch {
     hipEvent_t uploaded = nullptr;  // the last load's H2D copies (upload stream)
     bool loaded = false;
     BatchArgs args{};
-    DevBuf<uint8_t> bits, rbsp, sf, recon;
-    DevBuf<PicDesc> pics;
+    // read by k_rbsp / the parse only: a reload waits for the parses in flight
+    DevBuf<uint8_t> bits, rbsp;
     DevBuf<uint32_t> subs, rsubs, porder, xprog;
     DevBuf<uint8_t> xctx;
-    DevBuf<SeqParams> seqs;
-    DevBuf<OutImage> outs;
+    // the sample arena: written by k_intra, which runs after every earlier
+    // decode's k_sao_out on the one recon stream
+    DevBuf<uint8_t> recon;
+    DescGen gen[2];
+    int cur = 0;
     ParseSet set[3];
     int n_sets = 1, next_set = 0, last_set = 0;
-    std::vector<OutImage> out_host;
     std::vector<uint32_t> pic_image;  // picture → image
     std::vector<heifgpu_image_info> infos;
     ~heifgpu_batch() {
@@ -536,19 +556,31 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
             const char *e = std::getenv("HEIFGPU_PIPELINE");
             return e ? std::atoi(e) : 3;
         }();
-        b->n_sets = pipeline == 0 ? 1 : (pipeline == 3 ? 3 : 2);
+        // sets of parse outputs: the batch's own choice, else HEIFGPU_PIPELINE (default 3)
+        const int sets = opts && opts->pipeline_sets ? int(opts->pipeline_sets) : pipeline;
+        b->n_sets = sets <= 1 ? 1 : (sets >= 3 ? 3 : 2);
         for (int k = 0; k < b->n_sets; ++k) {
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].parsed, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].transformed, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].recon_done, hipEventDisableTiming));
         }
+        for (DescGen &g : b->gen) HIP_TRY(hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
     }
-    // A reloaded batch: the upload stream waits for every decode still
-    // reading the old contents; the staging buffer is rewritten only after the
-    // previous load's copies (long finished in a double-buffered loop).
+    // A reloaded batch.  The staging buffer is rewritten only after the
+    // previous load's copies (long finished in a double-buffered loop).  The
+    // upload stream then waits for
+    // - the parses in flight (they read bits / rbsp / subs / the parse order);
+    // - the decodes of the load before the previous one, which read the
+    //   descriptor generation this load overwrites;
+    // not for the in-flight decodes' transform and reconstruction, which read
+    // only their parse set, the other generation and the sample arena (that
+    // one is ordered by the recon stream).
     if (b->loaded) HIP_TRY(hipEventSynchronize(b->uploaded));
+    const int gi = b->loaded ? b->cur ^ 1 : b->cur;
+    DescGen &G = b->gen[gi];
     for (int k = 0; k < b->n_sets; ++k)
-        if (b->set[k].pending) HIP_TRY(hipStreamWaitEvent(ctx->upload, b->set[k].recon_done, 0));
+        if (b->set[k].pending) HIP_TRY(hipStreamWaitEvent(ctx->upload, b->set[k].parsed, 0));
+    if (G.pending) HIP_TRY(hipStreamWaitEvent(ctx->upload, G.done, 0));
     std::vector<uint32_t> order;
     const int mode = parse_mode_for(int(mode_req), int(hb.pics.size()));
     const int solo_waves = solo_waves_for(hb.lane_rows);
@@ -568,26 +600,33 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows,
                                         mode == PARSE_SOLO ? 1 : ppw_req, order, by_bytes ? nullptr : cost.data());
     }
-    const bool grows = (order.size() > b->porder.cap || hb.bits_size > b->bits.cap || hb.pics.size() > b->pics.cap ||
-                                     hb.subs.size() > b->subs.cap || hb.seqs.size() > b->seqs.cap ||
-                                     hb.sf.size() > b->sf.cap || n > b->outs.cap || hb.recon_bytes > b->recon.cap ||
+    const bool grows = (order.size() > b->porder.cap || hb.bits_size > b->bits.cap || hb.pics.size() > G.pics.cap ||
+                                     hb.subs.size() > b->subs.cap || hb.seqs.size() > G.seqs.cap ||
+                                     hb.sf.size() > G.sf.cap || n > G.outs.cap || hb.recon_bytes > b->recon.cap ||
                                      hb.resid_elems > b->set[0].resid.cap || hb.tu_n > b->set[0].tus.cap ||
                                      hb.coef_n > b->set[0].coefs.cap || hb.map_bytes > b->set[0].maps.cap ||
                                      hb.sao_n > b->set[0].sao.cap || 2 * size_t(hb.rows) > b->set[0].row_counts.cap ||
-                                     hb.pics.size() > b->set[0].status.cap);
-    if (grows) HIP_TRY(hipStreamSynchronize(ctx->upload));  // reallocation: old contents fully drained
+                                     hb.pics.size() > b->set[0].status.cap || hb.pics.size() > G.sticky.cap ||
+                                     (mode == PARSE_SPREAD && (hb.rows > b->xprog.cap || hb.rows * CTX_PAD > b->xctx.cap)));
+    if (grows) {  // reallocation: every decode of the old contents fully drained
+        for (int k = 0; k < b->n_sets; ++k)
+            if (b->set[k].pending) HIP_TRY(hipEventSynchronize(b->set[k].recon_done));
+        HIP_TRY(hipStreamSynchronize(ctx->upload));
+    }
     // A failure from here on leaves the batch unusable until a reload succeeds
     // (its arguments may point at freed arenas): `loaded` is set again last.
     b->loaded = false;
     // ---- device arenas (reused when large enough)
     HIP_TRY(b->bits.alloc(hb.bits_size));
-    HIP_TRY(b->pics.alloc(hb.pics.size()));
+    HIP_TRY(G.pics.alloc(hb.pics.size()));
     HIP_TRY(b->subs.alloc(hb.subs.size()));
     HIP_TRY(b->rbsp.alloc(hb.bits_size));
     HIP_TRY(b->rsubs.alloc(hb.subs.size()));
-    HIP_TRY(b->seqs.alloc(hb.seqs.size()));
-    HIP_TRY(b->sf.alloc(hb.sf.size()));
-    HIP_TRY(b->outs.alloc(n));
+    HIP_TRY(G.seqs.alloc(hb.seqs.size()));
+    HIP_TRY(G.sf.alloc(hb.sf.size()));
+    HIP_TRY(G.outs.alloc(n));
+    HIP_TRY(G.sticky.alloc(hb.pics.size()));
+    HIP_TRY(hipMemsetAsync(G.sticky.p, 0, hb.pics.size() * sizeof(uint32_t), ctx->upload));
     for (int k = 0; k < b->n_sets; ++k) {
         ParseSet &ps = b->set[k];
         HIP_TRY(ps.tus.alloc(hb.tu_n));
@@ -596,8 +635,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         HIP_TRY(ps.maps.alloc(hb.map_bytes));
         HIP_TRY(ps.sao.alloc(hb.sao_n));
         HIP_TRY(ps.status.alloc(hb.pics.size()));
-        HIP_TRY(ps.resid.alloc(hb.resid_elems));
-        HIP_TRY(hipMemsetAsync(ps.status.p, 0, hb.pics.size() * sizeof(uint32_t), ctx->upload));
+        HIP_TRY(ps.resid.alloc(hb.resid_elems));  // (each decode zeroes its set's status before the parse)
     }
     HIP_TRY(b->recon.alloc(hb.recon_bytes));
     HIP_TRY(b->porder.alloc(order.size()));
@@ -613,10 +651,10 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     };
     const Seg segs[] = {
         {nullptr, hb.bits_size, b->bits.p},  // the payload pieces, copied below
-        {hb.pics.data(), hb.pics.size() * sizeof(PicDesc), b->pics.p},
+        {hb.pics.data(), hb.pics.size() * sizeof(PicDesc), G.pics.p},
         {hb.subs.data(), hb.subs.size() * sizeof(uint32_t), b->subs.p},
-        {hb.seqs.data(), hb.seqs.size() * sizeof(SeqParams), b->seqs.p},
-        {hb.sf.data(), hb.sf.size(), b->sf.p},
+        {hb.seqs.data(), hb.seqs.size() * sizeof(SeqParams), G.seqs.p},
+        {hb.sf.data(), hb.sf.size(), G.sf.p},
         {order.data(), order.size() * sizeof(uint32_t), b->porder.p},
     };
     size_t total = 0;
@@ -659,20 +697,21 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     b->infos = std::move(infos);
     b->pic_image = hb.pic_image;
     b->n_pics = int(hb.pics.size());
+    b->cur = gi;
     b->loaded = true;
     BatchArgs &a = b->args;
     a = BatchArgs{};
     a.bits = b->bits.p;
-    a.pics = b->pics.p;
+    a.pics = G.pics.p;
     a.subs = b->subs.p;
     a.rbsp = b->rbsp.p;
     a.rsubs = b->rsubs.p;
     a.parse_order = b->porder.p;
     a.n_slots = int(order.size());
     a.parse_group = parse_group;
-    a.seqs = b->seqs.p;
-    a.sf = b->sf.p;
-    a.outs = b->outs.p;
+    a.seqs = G.seqs.p;
+    a.sf = G.sf.p;
+    a.outs = G.outs.p;
     a.recon = b->recon.p;
     a.n_pics = b->n_pics;
     a.max_width = hb.max_w;
@@ -690,7 +729,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.total_rows = int(hb.rows);
     a.bytes_per_sample = hb.bps;
     a.chroma_format = hb.chroma;
-    b->out_host.assign(n, OutImage{});
+    G.out_host.assign(n, OutImage{});
     if (fresh) *inout = fresh.release();
     return HEIFGPU_OK;
 }
@@ -710,6 +749,7 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     if (!b->loaded) return fail(HEIFGPU_E_INVALID, "batch not loaded (its last prepare failed)");
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream, as in HIP
     HIP_TRY(hipSetDevice(ctx->device));
+    DescGen &G = b->gen[b->cur];
     bool changed = false;
     for (size_t i = 0; i < b->n_images; ++i) {
         OutImage o{};
@@ -721,13 +761,13 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
             return fail(HEIFGPU_E_INVALID, "missing output plane");
         o.width = int32_t(b->infos[i].width);
         o.height = int32_t(b->infos[i].height);
-        if (std::memcmp(&o, &b->out_host[i], sizeof(o)) != 0) {
-            b->out_host[i] = o;
+        if (std::memcmp(&o, &G.out_host[i], sizeof(o)) != 0) {
+            G.out_host[i] = o;
             changed = true;
         }
     }
     if (changed)
-        HIP_TRY(hipMemcpyAsync(b->outs.p, b->out_host.data(), b->n_images * sizeof(OutImage), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(G.outs.p, G.out_host.data(), b->n_images * sizeof(OutImage), hipMemcpyHostToDevice, s));
     // parse set of this call
     const int k = b->next_set;
     b->next_set = (k + 1) % b->n_sets;
@@ -757,6 +797,7 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         hipError_t (*fns[5])(const BatchArgs &, hipStream_t) = {launch_parse, launch_transform, launch_intra,
                                                                 launch_deblock, launch_sao_out};
         for (int i = 0; i < max_stages; ++i) HIP_TRY(fns[i](a, s));
+        HIP_TRY(launch_status_fold(ps.status.p, G.sticky.p, b->n_pics, s));
         return HEIFGPU_OK;
     }
     hipStream_t p = ctx->parse, r = ctx->recon;
@@ -804,8 +845,11 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     HIP_TRY(hipStreamWaitEvent(r, ctx->fork, 0));
     HIP_TRY(launch_sao_out(a, r));
     if (t) HIP_TRY(hipEventRecord(ev[8], r));
+    HIP_TRY(launch_status_fold(ps.status.p, G.sticky.p, b->n_pics, r));
     HIP_TRY(hipEventRecord(ps.recon_done, r));
     ps.pending = true;
+    HIP_TRY(hipEventRecord(G.done, r));
+    G.pending = true;
     HIP_TRY(hipEventRecord(ctx->join, r));
     HIP_TRY(hipStreamWaitEvent(s, ctx->join, 0));
     return HEIFGPU_OK;
@@ -826,12 +870,18 @@ int heifgpu_batch_parse_geometry(const heifgpu_batch *b, uint32_t *mode, uint32_
 
 int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *b, uint32_t *status, void *stream) {
     if (!ctx || !b) return fail(HEIFGPU_E_INVALID, "invalid argument");
+    if (b->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
+    if (!b->loaded) return fail(HEIFGPU_E_INVALID, "batch not loaded (its last prepare failed)");
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null stream, as in HIP
     HIP_TRY(hipSetDevice(ctx->device));
+    // every decode since the last query (or the load) ORed its status words
+    // into the sticky array (k_status_fold after k_sao_out); read and clear it
+    DescGen &G = b->gen[b->cur];
     std::vector<uint32_t> st(size_t(b->n_pics));
-    if (!st.empty())
-        HIP_TRY(hipMemcpyAsync(st.data(), b->set[b->last_set].status.p, st.size() * sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, s));
+    if (!st.empty()) {
+        HIP_TRY(hipMemcpyAsync(st.data(), G.sticky.p, st.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemsetAsync(G.sticky.p, 0, st.size() * sizeof(uint32_t), s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
     std::vector<uint32_t> per(b->n_images, 0);
     for (size_t p = 0; p < st.size(); ++p) per[b->pic_image[p]] |= st[p];

@@ -403,8 +403,12 @@ PictureParameterSet picture_parameter_set_rbsp(const std::vector<uint8_t> &rbsp,
         p.num_tile_rows = nr;
         p.uniform_spacing_flag = r.read_flag();
         if (!p.uniform_spacing_flag) {
-            for (int i = 0; i < nc - 1; ++i) p.column_widths.push_back(int(r.read_ue()) + 1);
-            for (int i = 0; i < nr - 1; ++i) p.row_heights.push_back(int(r.read_ue()) + 1);
+            // bounded by the picture (7.4.3.3.1), so the boundary sums in tile_boundaries cannot overflow
+            for (int i = 0; i < nc - 1; ++i)
+                p.column_widths.push_back(
+                    r.read_ue_max(uint32_t(sps.pic_width_in_ctbs_y() - 1), "column_width_minus1") + 1);
+            for (int i = 0; i < nr - 1; ++i)
+                p.row_heights.push_back(r.read_ue_max(uint32_t(sps.pic_height_in_ctbs_y() - 1), "row_height_minus1") + 1);
         }
         p.loop_filter_across_tiles_enabled_flag = r.read_flag();
     }

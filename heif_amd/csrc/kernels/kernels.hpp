@@ -162,6 +162,7 @@ hipError_t launch_transform(const BatchArgs &a, hipStream_t s);
 hipError_t launch_intra(const BatchArgs &a, hipStream_t s);
 hipError_t launch_deblock(const BatchArgs &a, hipStream_t s);
 hipError_t launch_sao_out(const BatchArgs &a, hipStream_t s);
+hipError_t launch_status_fold(const uint32_t *status, uint32_t *sticky, int n, hipStream_t s);
 #endif
 
 }  // namespace hg

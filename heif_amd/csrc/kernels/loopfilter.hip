@@ -364,6 +364,24 @@ hipError_t launch_sao_out(const BatchArgs &a, hipStream_t s) {
     else hipLaunchKernelGGL(k_sao_out<uint16_t>, grid, block, 0, s, a);
     return hipGetLastError();
 }
+
+// the batch's sticky status: every decode's per-picture status words ORed
+// into one array that heifgpu_batch_status reads and clears, so damage seen
+// by any of the pipelined decodes (three parse-output sets) is reported
+__global__ void __launch_bounds__(256) k_status_fold(const uint32_t *__restrict__ st, uint32_t *__restrict__ sticky,
+                                                     int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        const uint32_t v = st[i];
+        if (v) sticky[i] |= v;
+    }
+}
+
+hipError_t launch_status_fold(const uint32_t *status, uint32_t *sticky, int n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_status_fold, dim3((n + 255) / 256), dim3(256), 0, s, status, sticky, n);
+    return hipGetLastError();
+}
 #endif
 
 }  // namespace hg

@@ -2312,6 +2312,7 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
 #if defined(HG_PARSE_PROF_SB)
     uint64_t pw[2] = {0, 0};  // cycles of not-run iterations (WPP polls + sleeps); driver cycles of run ones
 #endif
+    uint32_t stalled = 0;  // consecutive not-run iterations (bounded: never hang the device)
     for (;;) {
 #if defined(HG_PARSE_PROF_SB)
         const uint64_t t_top = __builtin_amdgcn_s_memtime();
@@ -2338,8 +2339,16 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
 #if defined(HG_PARSE_PROF_SB)
             pw[0] += __builtin_amdgcn_s_memtime() - t_top;
 #endif
+            // a row waits at most one picture's parse (~1e6 iterations); far past
+            // that the row above can never arrive (a dispatch-order assumption
+            // broken): flag the picture and stop instead of spinning forever
+            if (++stalled > (1u << 25)) {
+                if (lane == 0) atomicOr(&a.status[P.pic], L.status | ST_SUBSTREAM_END);
+                break;
+            }
             continue;
         }
+        stalled = 0;
         start = (uint32_t)__builtin_amdgcn_readfirstlane((int)start);
         if (start != ~0u) sw.restart(a.rbsp, start, lim, lane);
         else sw.advance(a.rbsp, (uint32_t)__builtin_amdgcn_readfirstlane((int)rd), lim, lane);

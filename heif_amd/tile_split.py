@@ -66,20 +66,25 @@ def gather_to_rank0(backend, dist, outs, buf, full: Optional[list], rank: int, w
     blob = backend.export(buf)
     blobs = [None] * world
     dist.all_gather_object(blobs, blob)
-    if rank == 0:
-        for dst, src in zip(full, outs):
-            backend.gather_own(dst, src, world, 0)
-        bases = []
-        try:
-            for r in range(1, world):
-                base = backend.open(blobs[r])
-                bases.append(base)
-                b0 = backend.buffer_ptr(buf)  # every rank carved the same layout from its buffer
-                for dst, src in zip(full, outs):
-                    pl = backend.planes(src)
-                    backend.gather_from(dst, [base + (p - b0) for p, _ in pl], [pitch for _, pitch in pl], world, r)
-            backend.sync()  # the gather kernels have read the peer planes
-        finally:
-            for b in bases:
-                backend.close(b)
-    dist.barrier()  # peers keep their planes until rank 0 is done
+    # Every rank reaches the closing barrier, also when rank 0's gather fails
+    # (the error is raised after it), so no peer is left blocked in it.
+    try:
+        if rank == 0:
+            for dst, src in zip(full, outs):
+                backend.gather_own(dst, src, world, 0)
+            bases = []
+            try:
+                for r in range(1, world):
+                    base = backend.open(blobs[r])
+                    bases.append(base)
+                    b0 = backend.buffer_ptr(buf)  # every rank carved the same layout from its buffer
+                    for dst, src in zip(full, outs):
+                        pl = backend.planes(src)
+                        backend.gather_from(dst, [base + (p - b0) for p, _ in pl], [pitch for _, pitch in pl],
+                                            world, r)
+                backend.sync()  # the gather kernels have read the peer planes
+            finally:
+                for b in bases:
+                    backend.close(b)
+    finally:
+        dist.barrier()  # peers keep their planes until rank 0 is done

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define HEIFGPU_ABI_VERSION 3
+#define HEIFGPU_ABI_VERSION 4
 
 enum {
     HEIFGPU_OK = 0,
@@ -99,6 +99,13 @@ typedef struct {
     /* lanes mode: pictures per wavefront (0 = adaptive; larger values are
      * capped at 64 / CTB rows) */
     uint32_t pics_per_wave;
+    /* sets of parse outputs (ABI 4): 0 = the default (3, or HEIFGPU_PIPELINE);
+     * 1 = no overlap; 2 = parse n+1 beside the reconstruction of n; 3 = parse
+     * n+2, transform n+1 and reconstruction n overlap.  Every set holds its own
+     * TU / coefficient / residual / map arenas (~3.2 MB per 512x512 picture),
+     * so a memory-tight caller can ask for fewer.  Taken when the batch is
+     * created (the first prepare); reloads keep it. */
+    uint32_t pipeline_sets;
 } heifgpu_batch_opts;
 
 enum { HEIFGPU_PARSE_AUTO = 0, HEIFGPU_PARSE_LANES = 1, HEIFGPU_PARSE_SOLO = 2, HEIFGPU_PARSE_SPREAD = 3 };
@@ -140,7 +147,10 @@ const char *heifgpu_last_error(void);
  * the device's null stream, as everywhere in HIP) and returns immediately; out[i] receives
  * image i.  It may be called repeatedly on the same batch (the bench times
  * exactly this call).  heifgpu_batch_status synchronises the stream and
- * returns the per-image status words (0 = ok). */
+ * returns the per-image status words (0 = ok): the OR over every decode of
+ * the batch since the previous heifgpu_batch_status call or the last
+ * (re)load, so damage seen by any of several pipelined decodes is reported;
+ * the call clears them. */
 int heifgpu_batch_prepare(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n, heifgpu_batch **out);
 int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs, size_t n,
                              const heifgpu_batch_opts *opts, heifgpu_batch **inout);

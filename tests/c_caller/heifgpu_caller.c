@@ -71,8 +71,8 @@ static void write_planes(FILE *f, const DevPlanes *p) {
 
 int main(int argc, char **argv) {
     CHECK(argc >= 2, "usage: heifgpu_caller FILE [--decode OUT]");
-    CHECK(HEIFGPU_ABI_VERSION == 3, "ABI version");
-    CHECK(sizeof(heifgpu_batch_opts) == 16, "heifgpu_batch_opts is %zu bytes", sizeof(heifgpu_batch_opts));
+    CHECK(HEIFGPU_ABI_VERSION == 4, "ABI version");
+    CHECK(sizeof(heifgpu_batch_opts) == 20, "heifgpu_batch_opts is %zu bytes", sizeof(heifgpu_batch_opts));
     CHECK(sizeof(heifgpu_image_info) == 80, "heifgpu_image_info is %zu bytes", sizeof(heifgpu_image_info));
     size_t n = 0;
     unsigned char *data = read_file(argv[1], &n);
@@ -127,7 +127,7 @@ int main(int argc, char **argv) {
         for (uint32_t g = 0; g < 2; ++g) {
             alloc_planes(&part[g], &info);
             heifgpu_batch *b = NULL;
-            heifgpu_batch_opts o = {2, g, g ? HEIFGPU_PARSE_LANES : HEIFGPU_PARSE_SOLO, 0};
+            heifgpu_batch_opts o = {2, g, g ? HEIFGPU_PARSE_LANES : HEIFGPU_PARSE_SOLO, 0, g ? 2u : 0u};
             CHECK(heifgpu_batch_prepare_ex(ctx, one, 1, &o, &b) == HEIFGPU_OK, "prepare_ex");
             CHECK(heifgpu_batch_decode(ctx, b, &part[g].planes, NULL) == HEIFGPU_OK, "batch_decode");
             CHECK(heifgpu_batch_status(ctx, b, &status, NULL) == HEIFGPU_OK && status == 0, "batch_status");

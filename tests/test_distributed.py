@@ -241,6 +241,42 @@ def test_tile_split_gather_to_rank0_over_gloo(world):
     assert live == 2  # rank 0's own two buffers; every peer mapping closed
 
 
+class _FailingOpen(_ShmBackend):
+    def open(self, blob):
+        raise RuntimeError("ipc_open failed")
+
+
+def _gather_fail_worker(rank, world, port, out):
+    from heif_amd.tile_split import gather_to_rank0
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    be = _FailingOpen(rank)
+    outs, buf = be.alloc()
+    full, fbuf = be.alloc() if rank == 0 else (None, None)
+    try:
+        gather_to_rank0(be, dist, outs, buf, full, rank, world)
+        res = "returned"
+    except RuntimeError as e:
+        res = str(e)
+    out.put((rank, res))
+    for b in (buf, fbuf):
+        if b is not None:
+            b[0].close()
+            b[0].unlink()
+    dist.destroy_process_group()
+
+
+def test_tile_split_gather_failure_releases_peers():
+    """A failure inside rank 0's gather (here ipc_open) is raised on rank 0
+    after the closing barrier, so the peers return instead of blocking in it."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.start_processes(_gather_fail_worker, args=(2, _free_port(), q), nprocs=2, join=True, start_method="spawn")
+    res = dict(q.get() for _ in range(2))
+    assert res == {0: "ipc_open failed", 1: "returned"}
+
+
 def _run_bench(args, extra_env=None, timeout=180):
     import json
     import subprocess

@@ -122,21 +122,73 @@ def test_bench_shard_every_image(H, ctx, oracle_tiles, halfmoonbay, parse, geom)
     """The headline configuration itself (bench.py, config 4 shard): 128
     permuted 4032x3024 images = 6144 pictures.  The automatic choice packs four
     16-row pictures per k_parse_lanes wave (1536 waves); solo runs 6144
-    16-wave workgroups, spread 98,304 one-wave workgroups.  Every image is checked, decoded twice back to back
-    (both parse-output sets of the pipeline)."""
+    16-wave workgroups, spread 98,304 one-wave workgroups.  Every image is
+    checked, decoded three times back to back (all three parse-output sets of
+    the pipeline, each into its own planes)."""
     from heif_amd.synthetic import permuted_heic
 
     seeds = list(range(128))
     imgs = H.HeifImage.parse_many([permuted_heic(halfmoonbay, s) for s in seeds], threads=8)
     b = ctx.prepare(imgs, parse=parse)
     assert b.parse_geometry() == geom
-    outs = [ctx.alloc_outputs(imgs) for _ in range(2)]
+    outs = [ctx.alloc_outputs(imgs) for _ in range(3)]
     for o in outs:
         b.decode_async(o)
     assert not any(b.status())
     b.free()
     for o in outs:
         check_permuted(o, seeds, oracle_tiles)
+
+
+def _damaged_halfmoonbay(oracle_mod, data, tile=5):
+    """halfmoonbay with the last eighth of one grid tile's slice data
+    overwritten with 0xff: the host accepts it, the kernels flag it."""
+    items, _ = oracle_mod.list_tiles(data)
+    o, n = items[tile]
+    d = bytearray(data)
+    d[o + n - n // 8:o + n] = b"\xff" * (n // 8)
+    return bytes(d)
+
+
+@pytest.mark.parametrize("sets", [0, 2, 1])
+@pytest.mark.parametrize("parse", ["lanes", "spread"])
+def test_status_sticky_over_pipelined_decodes(H, ctx, oracle_mod, oracle_tiles, halfmoonbay, parse, sets):
+    """heifgpu_batch_status reports the OR over every decode since the last
+    query (/root/reference/src/heic/decoder.rs:109-112: errors reach the
+    caller): a batch with one damaged image decoded three times back to back
+    (every parse-output set) shows the damage after each decode and after the
+    three together, the clean images stay bit-exact, a query with no decode
+    since the last one reads zero, and a reload without the damaged image
+    reports clean."""
+    bad = _damaged_halfmoonbay(oracle_mod, halfmoonbay)
+    files = [halfmoonbay, bad, halfmoonbay]
+    imgs = H.HeifImage.parse_many(files, threads=4)
+    b = ctx.prepare(imgs, parse=parse, pipeline_sets=sets)
+    outs = [ctx.alloc_outputs(imgs) for _ in range(3)]
+    for o in outs:
+        b.decode_async(o)
+    st = b.status()
+    assert st[0] == 0 and st[2] == 0 and st[1] != 0, st
+    assert b.status() == [0, 0, 0]  # cleared by the query, nothing decoded since
+    for o in outs:  # one query per decode: each sees the damage
+        b.decode_async(o)
+        st = b.status()
+        assert st[0] == 0 and st[2] == 0 and st[1] != 0, st
+    ident = list(range(48))
+    for o in outs:
+        for i in (0, 2):
+            y, cb, cr = assemble(oracle_tiles, ident)
+            assert np.array_equal(o[i].y.cpu().numpy(), y)
+            assert np.array_equal(o[i].cb.cpu().numpy(), cb) and np.array_equal(o[i].cr.cpu().numpy(), cr)
+    # a reload starts a new record: the damaged load's last decode (in flight
+    # when the reload is issued) is not reported against the clean images
+    clean = H.HeifImage.parse_many([halfmoonbay] * 3, threads=4)
+    b.decode_async(outs[0])
+    ctx.prepare(clean, reuse=b, wait=False)
+    b.decode_async(outs[1])
+    b.decode_async(outs[2])
+    assert b.status() == [0, 0, 0]
+    b.free()
 
 
 def test_permuted_batch_row_parallel(H, ctx, oracle_tiles, halfmoonbay):
