@@ -598,7 +598,8 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         std::vector<float> cost;
         if (!by_bytes) parse_chain_cost(hb.pics.data(), int(hb.pics.size()), hb.subs.data(), hb.seqs.data(), cost);
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows,
-                                        mode == PARSE_SOLO ? 1 : ppw_req, order, by_bytes ? nullptr : cost.data());
+                                        mode == PARSE_SOLO ? 1 : ppw_req, order, by_bytes ? nullptr : cost.data(),
+                                        mode == PARSE_LANES && lanes_jobs_default());
     }
     const bool grows = (order.size() > b->porder.cap || hb.bits_size > b->bits.cap || hb.pics.size() > G.pics.cap ||
                                      hb.subs.size() > b->subs.cap || hb.seqs.size() > G.seqs.cap ||
@@ -721,6 +722,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.lane_rows = hb.lane_rows;
     a.parse_mode = mode;
     a.solo_waves = solo_waves;
+    a.lane_jobs = mode == PARSE_LANES && lanes_jobs_default() ? 1 : 0;
     a.xprog = mode == PARSE_SPREAD ? b->xprog.p : nullptr;
     a.xctx = mode == PARSE_SPREAD ? b->xctx.p : nullptr;
     // rows wrap round the lanes (waves) of a picture: the WPP context staging

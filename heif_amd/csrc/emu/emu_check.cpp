@@ -76,7 +76,9 @@ int main(int argc, char **argv) {
     const int solo_waves = solo_waves_for(hb.lane_rows);
     int parse_group = 1;
     if (mode == PARSE_SPREAD) spread_parse_order(hb.pics.data(), int(hb.pics.size()), order);
-    else parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0, order);
+    else
+        parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0,
+                                        order, nullptr, mode == PARSE_LANES && lanes_jobs_default());
     std::vector<uint32_t> xprog(hb.rows + 1);
     std::vector<uint8_t> xctx((hb.rows + 1) * size_t(CTX_PAD));
     a.parse_order = order.data();
@@ -101,6 +103,7 @@ int main(int argc, char **argv) {
     a.lane_rows = hb.lane_rows;
     a.parse_mode = mode;
     a.solo_waves = solo_waves;
+    a.lane_jobs = mode == PARSE_LANES && lanes_jobs_default() ? 1 : 0;
     a.xprog = xprog.data();
     a.xctx = xctx.data();
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;

@@ -56,6 +56,7 @@ struct BatchArgs {
     int wpp_ring;              // some WPP picture has more CTB rows than lanes (its rows wrap round its lanes)
     int parse_mode;            // PARSE_LANES (k_parse_lanes) or PARSE_SOLO (k_parse_solo)
     int solo_waves;            // k_parse_solo waves per workgroup (solo_waves_for(lane_rows))
+    int lane_jobs;             // lanes mode: k_parse_jobs (lanes take substreams from a per-wave job list)
     uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
     int has_assembly;          // some picture is PD_ASSEMBLY (launch_deblock runs k_assemble first)
@@ -109,7 +110,10 @@ constexpr int kSoloMaxWaves = 16;
 // ppw_force = 0: the adaptive choice.
 // cost (optional): per-picture parse cost to deal by (default: payload bytes)
 int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
-                      const float *cost = nullptr);
+                      const float *cost = nullptr, bool jobs = false);
+// lanes mode runs k_parse_jobs (substreams from a per-wave job list) unless HEIFGPU_LANES_JOBS=0
+bool lanes_jobs_default();
+constexpr int kJobsMaxPics = 16;  // k_parse_jobs pictures per wave at most
 // per-picture WPP critical path in payload bytes (the rows' bytes spread evenly
 // over their CTUs, row r's CTU c after row r-1's CTU c+1); non-WPP: all bytes
 void parse_chain_cost(const PicDesc *pics, int n, const uint32_t *subs, const SeqParams *seqs, std::vector<float> &cost);

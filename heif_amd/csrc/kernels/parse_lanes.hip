@@ -100,6 +100,7 @@ struct LanePic {
     int subx, suby;  // log2 SubWidthC, SubHeightC (Table 6-1)
     int w4, h4, w8, saoL, saoC;
     int R, lane0, ring;  // lanes of the picture, its first lane, rows wrap round the lanes (WPP rows > R)
+    int stage;           // the picture's WPP context staging block (job lanes), or -1: one per row slot
     uint32_t flags, bits_off, bits_end, sub_first, row_off, tu_cap, coef_cap, pic;
     // global memory, said so in the type: a generic pointer loaded from LDS
     // would make every store through it a flat store, and flat stores count in
@@ -906,6 +907,17 @@ struct Env {
     int lane;
 };
 
+// WPP context staging block read at the start of substream `row` (written
+// after CTU 1 of row - 1): per picture with job lanes (one block is enough:
+// row r + 1 writes it only after its own start, and row r + 2 cannot start
+// before that), else per row slot (lane / wave / spread row)
+HG_HD inline uint8_t *wpp_stage(const Env &E, const LanePic &P, int row) {
+    return E.wctx + (size_t)(P.stage >= 0 ? P.stage : P.lane0 + row % P.R) * CTX_PAD;
+}
+// progress word of substream `row` (monotone row * wctb + CTUs done, so a
+// slot shared by rows r and r + R never runs backwards)
+HG_HD inline uint32_t *prog_word(const Env &E, const LanePic &P, int row) { return &E.prog[P.lane0 + row % P.R]; }
+
 // WPP, for parsing: a row's first CTU needs the contexts stored after CTU 1
 // of the row above (9.3.1), so two CTUs of it done; CTU c > 0 only reads the
 // CTU above it (split_cu_flag's CtDepth, sao_merge_up_flag; intra modes and
@@ -921,7 +933,7 @@ HG_HD inline bool wpp_ready(const Lane &L, const LanePic &P, const Env &E) {
     const int ahead = L.c == 0 ? 2 : L.c + 1;
 #endif
     const uint32_t need = (uint32_t)(L.row - 1) * (uint32_t)P.wctb + (uint32_t)(ahead < P.wctb ? ahead : P.wctb);
-    const uint32_t *pw = &E.prog[P.lane0 + (L.row - 1) % P.R];
+    const uint32_t *pw = prog_word(E, P, L.row - 1);
     return (EG::kSpread ? load_agent(pw) : prog_load(pw)) >= need;
 }
 
@@ -978,7 +990,7 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
             } else if (wpp_copy) {
                 w = 0;
                 if (ln < CTX_PAD / 4) {
-                    const uint8_t *src = (EG::kSpread || P.ring) ? E.wctx + (size_t)E.lane * CTX_PAD : ld.ctx;
+                    const uint8_t *src = (EG::kSpread || P.ring) ? wpp_stage(E, P, L.row) : ld.ctx;
                     const uint32_t *sw = reinterpret_cast<const uint32_t *>(src) + ln;
                     w = EG::kSpread ? load_agent(sw) : *sw;
                 }
@@ -989,7 +1001,7 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
 #pragma nounroll
             for (int i = 0; i < CTX_NUM; ++i) ld.ctx[i] = ctx_init_state(c_ctx_init_l[i], P.sliceQp);
         } else if (wpp_copy && (EG::kSpread || P.ring)) {
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(E.wctx + (size_t)E.lane * CTX_PAD);
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(wpp_stage(E, P, L.row));
             uint32_t *dst = reinterpret_cast<uint32_t *>(ld.ctx);
 #pragma nounroll
             for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = EG::kSpread ? load_agent(src + k) : src[k];
@@ -1722,9 +1734,8 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     if ((L.fl & F_WPP) && L.c == 1 && L.row + 1 < P.hctb) {
         // 9.3.2.4 storage for the next row's substream: into its lane's block, or
         // its staging block when that lane may still be parsing an earlier row
-        const int nl = P.lane0 + (L.row + 1) % P.R;
-        uint32_t *dst =
-            reinterpret_cast<uint32_t *>((EG::kSpread || P.ring) ? E.wctx + (size_t)nl * CTX_PAD : E.lds[nl].ctx);
+        uint32_t *dst = reinterpret_cast<uint32_t *>((EG::kSpread || P.ring) ? wpp_stage(E, P, L.row + 1)
+                                                                              : E.lds[P.lane0 + (L.row + 1) % P.R].ctx);
         if constexpr (EG::kCtxReg) {
 #if !defined(HG_HOST_EMU)
             const int ln = (int)__lane_id();  // every lane stores its dword
@@ -1763,10 +1774,10 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     const uint32_t pv = (L.fl & F_STOP) ? kProgDone : (uint32_t)L.row * (uint32_t)P.wctb + (uint32_t)L.c;
     if constexpr (EG::kSpread) {
         stores_done();
-        store_agent(&E.prog[E.lane], pv);
+        store_agent(prog_word(E, P, L.row), pv);
     } else {
         release_fence();
-        prog_store(&E.prog[E.lane], pv);
+        prog_store(prog_word(E, P, L.row), pv);
     }
     if (!(L.fl & F_STOP) && L.c < P.wctb) {
         L.st = U_CTU;
@@ -1817,8 +1828,7 @@ HG_HD inline bool ctu_ready(const Lane &L, const LanePic &P, const Env &E) { ret
 
 // lane setup: picture constants, outputs, first state.  Returns false for an idle lane.
 // `cap` lanes (waves, solo mode) at most per picture.
-HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a, int pic, int row, int lane0,
-                            int cap) {
+HG_HD inline bool pic_init(LanePic &P, const BatchArgs &a, int pic, int lane0, int cap) {
     const PicDesc &pd = a.pics[pic];
     if (pd.flags & PD_ASSEMBLY) return false;  // no coded data of its own
     const SeqParams &sp = a.seqs[pd.seq];
@@ -1826,8 +1836,8 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
     const int hctb = (sp.height + ctb - 1) >> log2ctb;
     const bool wpp = (sp.flags & SP_WPP) != 0;
     const int R = wpp ? (hctb < cap ? hctb : cap) : 1;
-    if (row >= R) return false;
     P.R = R;
+    P.stage = -1;
     P.lane0 = lane0;
     P.ring = wpp && hctb > R;
     P.W = sp.width;
@@ -1873,18 +1883,29 @@ HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a
     P.gsao = (SaoParams HG_GAS *)(a.sao + pd.sao_off);
     P.tu_base = (TuRec HG_GAS *)(a.tus + pd.tu_off);
     P.coef_base = (Coef HG_GAS *)(a.coefs + pd.coef_off);
+    return true;
+}
+
+// lane state at the start of substream `row` of picture P
+HG_HD inline void lane_start(Lane &L, const LanePic &P, LaneLds &ld, int row) {
     L.status = 0;
     L.cn = 0;
     L.k = 8;
     L.ai = L.bv = L.fp = 0;
     L.lb = 0;
-    L.fl = wpp ? F_WPP : 0u;
+    L.fl = (P.flags & SP_WPP) ? F_WPP : 0u;
     L.row = row;
     L.c = 0;
-    L.qp_prev_last = pd.slice_qp;
+    L.qp_prev_last = P.sliceQp;
     row_outputs(L, P);
     for (int k = 0; k < 8; ++k) reinterpret_cast<uint32_t *>(&ld.sao)[k] = 0;
     L.st = U_CTU;
+}
+
+HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a, int pic, int row, int lane0,
+                            int cap) {
+    if (!pic_init(P, a, pic, lane0, cap) || row >= P.R) return false;
+    lane_start(L, P, ld, row);
     return true;
 }
 
@@ -1929,7 +1950,32 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
     return full;
 }
 
+// Job lanes (k_parse_jobs): about two substreams per lane, so each wave's WPP
+// ramps fill with other pictures' rows; fewer pictures per wave only while
+// that would leave under 3/4 of the SIMDs a wave (small batches).
+// HEIFGPU_LANES_PPW forces a value.
+inline int jobs_pics_per_wave(int lane_rows, int n_pics) {
+    static const int forced = [] {
+        const char *e = std::getenv("HEIFGPU_LANES_PPW");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (forced > 0) return forced < kJobsMaxPics ? forced : kJobsMaxPics;
+    const int rows = lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows);
+    int p = std::max(1, std::min(kJobsMaxPics, 128 / rows));
+    const long floor_waves = lanes_simds() * 3L / 4;
+    while (p > 1 && (n_pics + p - 1) / p < floor_waves) --p;
+    return p;
+}
+
 }  // namespace
+
+bool lanes_jobs_default() {
+    static const bool on = [] {
+        const char *e = std::getenv("HEIFGPU_LANES_JOBS");
+        return !e || std::atoi(e) != 0;
+    }();
+    return on;
+}
 
 // Wave slot -> picture.  A wave runs until its heaviest picture is parsed,
 // and every extra busy picture in it adds divergent units to each pass, so
@@ -1941,7 +1987,7 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
 // slots are ~0u.  HEIFGPU_PARSE_ORDER=0: batch order; HEIFGPU_PARSE_HEAVY
 // overrides the heavy count.
 int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
-                      const float *cost) {
+                      const float *cost, bool jobs) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
         return e ? std::atoi(e) : 1;
@@ -1950,8 +1996,9 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
         const char *e = std::getenv("HEIFGPU_PARSE_HEAVY");
         return e ? std::atoi(e) : -1;
     }();
-    const int full = 64 / (lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows));
-    const int ppw = ppw_force > 0 ? std::min(ppw_force, full) : lanes_pics_per_wave(lane_rows, n);
+    const int full = jobs ? kJobsMaxPics : 64 / (lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows));
+    const int ppw = ppw_force > 0 ? std::min(ppw_force, full)
+                                  : (jobs ? jobs_pics_per_wave(lane_rows, n) : lanes_pics_per_wave(lane_rows, n));
     if (!on || n <= 0) {
         order.resize((size_t)n);
         for (int i = 0; i < n; ++i) order[(size_t)i] = (uint32_t)i;
@@ -2092,6 +2139,91 @@ void emu_parse_lanes(const BatchArgs &a) {
     }
 }
 
+// job lanes (k_parse_jobs): the same pass structure, idle lanes taking the
+// next substream of the wave's job list (row order across its pictures) at
+// each pass start, in lane order
+void emu_parse_jobs(const BatchArgs &a) {
+    const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : jobs_pics_per_wave(a.lane_rows, a.n_pics);
+    const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
+    const int waves = (n_slots + ppw - 1) / ppw;
+    uint64_t tab[64], seq[15];
+    for (int i = 0; i < 64; ++i) tab[i] = state_row(i);
+    for (int i = 0; i < 15; ++i) seq[i] = sig_seq(i);
+    std::vector<LaneLds> lds(64);
+    std::vector<LanePic> pics((size_t)ppw);
+    std::vector<Lane> lanes(64);
+    std::vector<int> ps(64, 0);
+    std::vector<uint8_t> wctx((size_t)ppw * CTX_PAD);
+    std::vector<uint32_t> prog((size_t)ppw * a.max_rows), nsub((size_t)ppw);
+    static const bool stats = std::getenv("HEIFGPU_LANES_STATS") != nullptr;
+    for (int w = 0; w < waves; ++w) {
+        std::fill(prog.begin(), prog.end(), 0u);
+        uint32_t n_jobs = 0, next = 0;
+        for (int s = 0; s < ppw; ++s) {
+            const int slot = w * ppw + s;
+            const bool in = slot < n_slots && (!a.parse_order || a.parse_order[slot] != ~0u);
+            const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
+            LanePic &P = pics[(size_t)s];
+            nsub[(size_t)s] = 0;
+            if (in && pic_init(P, a, pic, s * a.max_rows, 1 << 20)) {
+                P.ring = 1;
+                P.stage = s;
+                nsub[(size_t)s] = (P.flags & SP_WPP) ? (uint32_t)P.hctb : 1u;
+            }
+            n_jobs = std::max(n_jobs, nsub[(size_t)s] * (uint32_t)ppw);
+        }
+        for (int l = 0; l < 64; ++l) lanes[(size_t)l].st = U_DONE;
+        Env E{&a, lds.data(), prog.data(), wctx.data(), 0};
+        long passes = 0, units = 0;
+        for (;; ++passes) {
+            for (int l = 0; l < 64 && next < n_jobs; ++l) {
+                if (lanes[(size_t)l].st != U_DONE) continue;
+                while (next < n_jobs) {
+                    const uint32_t j = next++;
+                    const int s = (int)(j % (uint32_t)ppw), row = (int)(j / (uint32_t)ppw);
+                    if ((uint32_t)row < nsub[(size_t)s]) {
+                        ps[(size_t)l] = s;
+                        lane_start(lanes[(size_t)l], pics[(size_t)s], lds[(size_t)l], row);
+                        break;
+                    }
+                }
+            }
+            bool any = false, progressed = false;
+            for (int l = 0; l < 64; ++l) any |= lanes[(size_t)l].st != U_DONE;
+            if (!any) break;
+            for (int l = 0; l < 64; ++l)
+                if (lanes[(size_t)l].st != U_DONE) {
+                    const LanePic &P = pics[(size_t)ps[(size_t)l]];
+                    const Eng G{lds[(size_t)l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
+                    q_refill(lanes[(size_t)l], G);
+                }
+            for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
+                for (int l = 0; l < 64; ++l) {
+                    Lane &L = lanes[(size_t)l];
+                    E.lane = l;
+                    LanePic &P = pics[(size_t)ps[(size_t)l]];
+                    if (L.st != kind || (kind == U_CTU && !ctu_ready(L, P, E))) continue;
+                    progressed = true;
+                    ++units;
+                    const Eng G{lds[(size_t)l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
+                    run_unit(kind, L, lds[(size_t)l], P, E, G);
+                }
+            }
+            if (!progressed) {  // cannot happen: a row's job follows the row above's
+                for (int l = 0; l < 64; ++l)
+                    if (lanes[(size_t)l].st != U_DONE) {
+                        lanes[(size_t)l].status |= ST_SUBSTREAM_END;
+                        atomicOr(&a.status[pics[(size_t)ps[(size_t)l]].pic], lanes[(size_t)l].status);
+                        lanes[(size_t)l].st = U_DONE;
+                    }
+                break;
+            }
+        }
+        if (stats)
+            printf("wave %d: %ld passes, %.1f units per pass\n", w, passes, (double)units / passes);
+    }
+}
+
 // solo mode: each picture's rows (waves) round-robin, one unit per ready wave
 // per round, with the GPU driver's window logic (SoloWin) per wave
 template <bool Spread>
@@ -2160,6 +2292,7 @@ void emu_parse_solo(const BatchArgs &a) {
 void emu_parse(const BatchArgs &a) {
     if (a.parse_mode == PARSE_SOLO) emu_parse_solo<false>(a);
     else if (a.parse_mode == PARSE_SPREAD) emu_parse_solo<true>(a);
+    else if (a.lane_jobs) emu_parse_jobs(a);
     else emu_parse_lanes(a);
 }
 #else
@@ -2237,6 +2370,122 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
         ++pf[1];
 #endif
         if (!progressed || pass > (1u << 30)) {  // every live lane waits: cannot happen (the top row never waits)
+            if (L.st != U_DONE) {
+                L.status |= ST_SUBSTREAM_END;
+                atomicOr(&a.status[P.pic], L.status);
+            }
+            break;
+        }
+    }
+#if defined(HG_PARSE_PROF)
+    pf[0] = __builtin_amdgcn_s_memtime() - t_start;
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[k], (unsigned long long)pf[k]);
+#endif
+}
+
+// Job lanes (BatchArgs::lane_jobs): the lanes of a wave are not tied to
+// pictures.  The wave holds `ppw` pictures (more rows than lanes, e.g. 8
+// pictures x 16 WPP rows = 128 substreams on 64 lanes), and a lane that
+// finishes a substream takes the next one from the wave's job list, in row
+// order across the pictures (row 0 of every picture, then row 1, ...).  The
+// WPP ramp of one picture (row r starts ~2r CTU-times late) then fills with
+// the early rows of the others: with equal CTUs, 8 pictures per wave take the
+// same 46 CTU-times as 4 pictures on statically assigned lanes, at twice the
+// lanes busy per pass (r03: 22.4 of 64).  A row's job comes after the row
+// above's, so every wait is on a substream some lane holds.  Progress words
+// are per (picture, row) in LDS; the WPP context hand-off goes through one
+// staging block per picture (wpp_stage).
+inline size_t jobs_lds_bytes(int ppw, int max_rows) {
+    return sizeof(LaneLds) * 64 + sizeof(LanePic) * (size_t)ppw + sizeof(uint32_t) * (size_t)ppw * max_rows +
+           (64 + 16) * sizeof(uint64_t) + (size_t)ppw * CTX_PAD + sizeof(uint32_t) * ((size_t)ppw + 4);
+}
+
+__global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_jobs(BatchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int ppw = a.parse_group;
+    LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
+    LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + 64);
+    uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_pic + ppw);
+    uint64_t *s_seq = s_tab + 64;
+    uint8_t *s_wctx = reinterpret_cast<uint8_t *>(s_seq + 16);
+    uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_wctx + (size_t)ppw * CTX_PAD);
+    uint32_t *s_nsub = s_prog + (size_t)ppw * a.max_rows;  // [ppw] substreams of the picture (0: none)
+    uint32_t *s_next = s_nsub + ppw;                        // [0] next job, [1] jobs (ppw * max substreams)
+    const int lane = threadIdx.x;
+    s_tab[lane] = state_row(lane);
+    if (lane < 15) s_seq[lane] = sig_seq(lane);
+    for (int i = lane; i < ppw * a.max_rows; i += 64) s_prog[i] = 0;
+    if (lane == 0) s_next[0] = s_next[1] = 0;
+    __syncthreads();
+    if (lane < ppw) {  // lane s sets up picture s of the wave
+        const int slot = (int)blockIdx.x * ppw + lane;
+        const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
+        const bool in = slot < n_slots && (!a.parse_order || a.parse_order[slot] != ~0u);
+        const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
+        LanePic &P = s_pic[lane];
+        uint32_t nsub = 0;
+        if (in && pic_init(P, a, pic, lane * a.max_rows, 1 << 20)) {
+            P.ring = 1;
+            P.stage = lane;
+            nsub = (P.flags & SP_WPP) ? (uint32_t)P.hctb : 1u;
+        }
+        s_nsub[lane] = nsub;
+        atomicMax(&s_next[1], nsub * (uint32_t)ppw);
+    }
+    __syncthreads();
+    const uint32_t n_jobs = s_next[1];
+    const Env E{&a, s_lds, s_prog, s_wctx, lane};
+    LaneLds &ld = s_lds[lane];
+    Lane L;
+    L.st = U_DONE;
+    int ps = 0;  // picture slot of the lane's substream
+    bool more = n_jobs > 0;
+#if defined(HG_PARSE_PROF)
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
+    for (uint32_t pass = 0;; ++pass) {
+        if (more && __any(L.st == U_DONE)) {  // idle lanes take the next substreams
+            bool got = false;
+            if (L.st == U_DONE) {
+                for (uint32_t j; (j = atomicAdd(&s_next[0], 1u)) < n_jobs;) {
+                    const int s = (int)(j % (uint32_t)ppw), row = (int)(j / (uint32_t)ppw);
+                    if ((uint32_t)row < s_nsub[s]) {
+                        ps = s;
+                        lane_start(L, s_pic[s], ld, row);
+                        got = true;
+                        break;
+                    }
+                }
+            }
+            more = !__any(L.st == U_DONE && !got);
+        }
+        if (!__any(L.st != U_DONE)) break;
+        pass_wait();
+        LanePic &P = s_pic[ps];
+        const Eng G{ld.ctx, s_tab, s_seq, a.rbsp, (P.bits_end + 64u) & ~3u};
+        if (L.st != U_DONE) q_refill(L, G);
+        bool progressed = false;
+#pragma unroll
+        for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
+            const bool mine = L.st == kind && (kind != U_CTU || ctu_ready(L, P, E));
+            if (!__any(mine)) continue;
+            progressed = true;
+#if defined(HG_PARSE_PROF)
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            pf[7] += (uint64_t)__popcll(__ballot(mine));  // lanes running a unit
+#endif
+            if (mine) run_unit(kind, L, ld, P, E, G);
+#if defined(HG_PARSE_PROF)
+            const uint64_t t2 = __builtin_amdgcn_s_memtime();
+            pf[kind <= U_CTU ? 2 : kind <= U_TT ? 3 : kind - 1] += t2 - t1;
+#endif
+        }
+#if defined(HG_PARSE_PROF)
+        ++pf[1];
+#endif
+        if (!progressed || pass > (1u << 30)) {  // every live lane waits: cannot happen (a row's job follows the row above's)
             if (L.st != U_DONE) {
                 L.status |= ST_SUBSTREAM_END;
                 atomicOr(&a.status[P.pic], L.status);
@@ -2413,11 +2662,15 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
         return hipGetLastError();
     }
     // the dealing of parse_order fixed the pictures per wave (lanes_parse_order)
-    const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : lanes_pics_per_wave(a.lane_rows, a.n_pics);
+    const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group
+                    : (a.lane_jobs ? jobs_pics_per_wave(a.lane_rows, a.n_pics) : lanes_pics_per_wave(a.lane_rows, a.n_pics));
     a.parse_group = ppw;
     const int waves = ((a.parse_order ? a.n_slots : a.n_pics) + ppw - 1) / ppw;
-    hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0), s,
-                       a);
+    if (a.lane_jobs)
+        hipLaunchKernelGGL(k_parse_jobs, dim3(waves), dim3(64), jobs_lds_bytes(ppw, a.max_rows), s, a);
+    else
+        hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0), s,
+                           a);
     return hipGetLastError();
 }
 #endif
