@@ -723,6 +723,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.parse_mode = mode;
     a.solo_waves = solo_waves;
     a.lane_jobs = mode == PARSE_LANES && lanes_jobs_default() ? 1 : 0;
+    a.lf_tiles = lf_tiles_for(hb.pics.data(), int(hb.pics.size()), hb.seqs.data());
     a.xprog = mode == PARSE_SPREAD ? b->xprog.p : nullptr;
     a.xctx = mode == PARSE_SPREAD ? b->xctx.p : nullptr;
     // rows wrap round the lanes (waves) of a picture: the WPP context staging

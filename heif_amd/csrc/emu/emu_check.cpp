@@ -104,6 +104,7 @@ int main(int argc, char **argv) {
     a.parse_mode = mode;
     a.solo_waves = solo_waves;
     a.lane_jobs = mode == PARSE_LANES && lanes_jobs_default() ? 1 : 0;
+    a.lf_tiles = lf_tiles_for(hb.pics.data(), int(hb.pics.size()), hb.seqs.data());
     a.xprog = xprog.data();
     a.xctx = xctx.data();
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;

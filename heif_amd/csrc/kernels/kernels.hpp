@@ -57,6 +57,7 @@ struct BatchArgs {
     int parse_mode;            // PARSE_LANES (k_parse_lanes) or PARSE_SOLO (k_parse_solo)
     int solo_waves;            // k_parse_solo waves per workgroup (solo_waves_for(lane_rows))
     int lane_jobs;             // lanes mode: k_parse_jobs (lanes take substreams from a per-wave job list)
+    int lf_tiles;              // k_loopfilter workgroups per picture (lf_tiles_for: the largest picture, assemblies included)
     uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
     int has_assembly;          // some picture is PD_ASSEMBLY (launch_deblock runs k_assemble first)
@@ -111,7 +112,9 @@ constexpr int kSoloMaxWaves = 16;
 // cost (optional): per-picture parse cost to deal by (default: payload bytes)
 int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
                       const float *cost = nullptr, bool jobs = false);
-// lanes mode runs k_parse_jobs (substreams from a per-wave job list) unless HEIFGPU_LANES_JOBS=0
+// k_loopfilter tiles of the largest picture of a batch (assembly pictures included)
+int lf_tiles_for(const PicDesc *pics, int n, const SeqParams *seqs);
+// lanes mode runs k_parse_jobs (substreams from a per-wave job list) with HEIFGPU_LANES_JOBS=1
 bool lanes_jobs_default();
 constexpr int kJobsMaxPics = 16;  // k_parse_jobs pictures per wave at most
 // per-picture WPP critical path in payload bytes (the rows' bytes spread evenly

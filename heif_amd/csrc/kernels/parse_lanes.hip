@@ -1969,10 +1969,17 @@ inline int jobs_pics_per_wave(int lane_rows, int n_pics) {
 
 }  // namespace
 
+// k_parse_jobs only with HEIFGPU_LANES_JOBS=1: measured slower than the
+// static mapping at the bench's batch (r04 A/B, same box: parse alone 75.7 ms
+// static vs 91.5 / 102.3 / 110.1 / 120.6 at 6 / 8 / 12 / 16 pictures per
+// wave).  Twice the lanes busy per pass, but the wave's passes get longer
+// (each divergent loop runs to its slowest busy lane) and a wave alone on a
+// SIMD hides less latency than the static 1.5 waves per SIMD.  Beside the
+// parse the reconstruction stream was much faster (47 vs 74 ms at 6 per wave).
 bool lanes_jobs_default() {
     static const bool on = [] {
         const char *e = std::getenv("HEIFGPU_LANES_JOBS");
-        return !e || std::atoi(e) != 0;
+        return e && std::atoi(e) != 0;
     }();
     return on;
 }

@@ -33,17 +33,17 @@ def _run(exe, path, env_extra=None):
 # (k_intra: a single image runs luma / chroma wave pairs; "ppw1" forces the
 # unsplit kernel.)
 # k_parse_solo (one substream per wave), k_parse_solo<true> (spread: the
-# automatic choice for a single image), the lanes mode's k_parse_jobs (lanes
-# take substreams from the wave's job list) with its adaptive geometry (one
-# picture per wave for a single image), the bench's packing (eight 16-row
-# pictures = 128 substreams on 64 lanes), an odd count (5 pictures), the
-# statically mapped k_parse_lanes with its 64-lane packing (four pictures per
-# wave), and batch (unsorted) wave order
+# automatic choice for a single image), k_parse_lanes (one substream per lane)
+# with its adaptive geometry (one picture per wave for a single image) and the
+# full 64-lane packing of large batches (four 16-row pictures per wave),
+# k_parse_jobs (lanes take substreams from the wave's job list: adaptive, 8
+# pictures = 128 substreams on 64 lanes, and an odd 5), and batch (unsorted)
+# wave order
 LANES = {"HEIFGPU_PARSE": "lanes"}
+JOBS = {**LANES, "HEIFGPU_LANES_JOBS": "1"}
 PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "spread"}, "lanes": LANES,
-           "packed": {**LANES, "HEIFGPU_LANES_PPW": "8"},
-           "jobs5": {**LANES, "HEIFGPU_LANES_PPW": "5"},
-           "static": {**LANES, "HEIFGPU_LANES_JOBS": "0", "HEIFGPU_PARSE_ADAPT": "0"},
+           "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0"},
+           "jobs": JOBS, "jobs8": {**JOBS, "HEIFGPU_LANES_PPW": "8"}, "jobs5": {**JOBS, "HEIFGPU_LANES_PPW": "5"},
            "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1", "HEIFGPU_INTRA_SPLIT": "0"},
            "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
 
@@ -54,7 +54,7 @@ def test_emulated_kernels_match_oracle(emu_check, parser):
     assert rc == 0 and "EMU PARITY OK" in out, out[-2000:]
 
 
-@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "static"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "jobs8"])
 def test_emulated_kernels_permuted_image(emu_check, tmp_path, halfmoonbay, parser):
     p = tmp_path / "perm.heic"
     p.write_bytes(permuted_heic(halfmoonbay, 42))
@@ -81,7 +81,7 @@ def _corrupt(data: bytes, mode: str) -> bytes:
     return bytes(d)
 
 
-@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "static"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "jobs8"])
 @pytest.mark.parametrize("mode", ["random", "zeroed"])
 def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode, parser):
     """Corrupt slice data must end in status bits, never in a crash (the same
