@@ -7,7 +7,7 @@ stills; image i is halfmoonbay.heic with its 48 grid tiles permuted by
 mt19937_64(seed=i) (heif_amd/synthetic.py).  A "step" is one decode of the
 whole batch: bitstreams, parameter sets and slice headers are resident in HBM
 before timing (host demux + upload happen once, outside the timed region);
-the step runs the five gfx950 kernels and writes every image's cropped
+the step runs the decode's gfx950 kernels and writes every image's cropped
 Y/Cb/Cr planes to HBM.  `value` = all ranks' output luma pixels / max-over-
 ranks wall time of K steps.
 

@@ -1659,9 +1659,91 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         const int nsign = __builtin_popcount(sig) - (hide ? 1 : 0);
         uint32_t signs = byp_bits(L, G, nsign);
         signs = nsign ? signs << (32 - nsign) : 0u;  // first decoded sign in bit 31
+        const int n = 1 << l2;
+#if !defined(HG_HOST_EMU)
+        if constexpr (EG::kSolo) {
+            // One substream per wave: only the coeff_abs_level_remaining bins
+            // are serial.  They are decoded for the coefficients that have one
+            // (base level 1 past the first eight, or base == the greater1 /
+            // greater2 ceiling), each value into lane nn of `remv`; then lane j
+            // assembles the coefficient at scan position j (level, sign by its
+            // rank in scan order, position) and the sub-block's coefficients
+            // leave in one store instruction instead of one per coefficient
+            // (the r03 serial loop cost ~780 cycles per coefficient).
+            uint32_t m8 = sig;  // the first eight significant positions (scan order = highest first)
+            for (int j = 0, mm = (int)sig; j < 8 && mm; ++j) mm &= ~(1 << msb32((uint32_t)mm)), m8 = (uint32_t)mm;
+            m8 = sig & ~m8;
+            const uint32_t lastb = last_g1 >= 0 ? 1u << last_g1 : 0u;
+            uint32_t need = (g1 & ~lastb) | g2 | (sig & ~m8);
+            const int j = (int)__lane_id();
+            uint32_t remv = 0;
+            int sum_rem = 0, last_abs = 0, last_rice = 0;
+            bool first_rem = true;
+            while (need) {
+                const int nn = msb32(need);
+                need ^= 1u << nn;
+                const int base = 1 + (int)((g1 >> nn) & 1) + (int)((g2 >> nn) & 1);
+                int k;
+                if (first_rem) {
+                    k = 0;
+                    first_rem = false;
+                } else {
+                    k = last_rice + (last_abs > 3 * (1 << last_rice) ? 1 : 0);
+                    k = k < 4 ? k : 4;
+                }
+                int rem = byp_rem(L, G, k);
+                if (rem < 0) {
+                    const int lim = 31 - (k + 1);
+                    int ones = 0;
+                    for (;;) {
+                        const int mm = lim + 1 - ones < 8 ? lim + 1 - ones : 8;
+                        const int p = byp_unary(L, G, mm);
+                        ones += p;
+                        if (p < mm || ones > lim) break;
+                    }
+                    if (ones > lim) {
+                        L.status |= ST_SYNTAX;
+                        rem = 0;
+                    } else {
+                        rem = (int)((4u << k) + (((1u << ones) - 1u) << (k + 1)) + byp_bits(L, G, ones + k + 1));
+                    }
+                }
+                last_abs = base + rem;
+                last_rice = k;
+                sum_rem += rem;
+                remv = j == nn ? (uint32_t)rem : remv;
+            }
+            const int nsig = __builtin_popcount(sig);
+            const int sum_abs = nsig + __builtin_popcount(g1) + __builtin_popcount(g2) + sum_rem;
+            const uint64_t sw = scan4_word(L.rc_scan);
+            {  // branch-free up to the one store (a divergent region here crashed the register allocator)
+                const uint32_t jj = (uint32_t)j & 15u;
+                const int rank = __builtin_popcount(sig >> jj) - 1;  // coefficients before it in scan order
+                int v = 1 + (int)((g1 >> jj) & 1) + (int)((g2 >> jj) & 1) + (int)remv;
+                const uint32_t sbit = (signs << (rank & 31)) >> 31;
+                const bool neg = (hide && (int)jj == first_sig) ? (sum_abs & 1) != 0 : sbit != 0;
+                v = neg ? -v : v;
+                v = v > 32767 ? 32767 : (v < -32768 ? -32768 : v);
+                const uint32_t pp = (uint32_t)(sw >> (4 * jj)) & 15u;
+                const int xC = (xS << 2) + (int)(pp & 3), yC = (yS << 2) + (int)(pp >> 2);
+                const uint32_t idx = L.ncoef + (uint32_t)rank;
+                const bool st = j < 16 && ((sig >> jj) & 1u) && idx < P.coef_cap;
+                const uint32_t w = ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC);
+                if (st) P.coef_base[L.coef_row + idx] = w;
+            }
+            if (L.ncoef + (uint32_t)nsig > P.coef_cap) {
+                L.status |= ST_CAPACITY;
+                L.ncoef = P.coef_cap;
+            } else {
+                L.ncoef += (uint32_t)nsig;
+            }
+            HG_SB_T(L, 3, tsb);
+            if (--L.rc_i < 0) tb_done(L, ld, P);
+            return;
+        }
+#endif
         int num_sig = 0, sum_abs = 0, last_abs = 0, last_rice = 0;
         bool first_rem = true;
-        const int n = 1 << l2;
         for (uint32_t m = sig; m;) {
             const int nn = msb32(m);
             m &= ~(1u << nn);
@@ -2673,11 +2755,16 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
                     : (a.lane_jobs ? jobs_pics_per_wave(a.lane_rows, a.n_pics) : lanes_pics_per_wave(a.lane_rows, a.n_pics));
     a.parse_group = ppw;
     const int waves = ((a.parse_order ? a.n_slots : a.n_pics) + ppw - 1) / ppw;
+    // HEIFGPU_PARSE_LDS_PAD: extra (unused) LDS per wave (tuning: residency beside the reconstruction kernels)
+    static const size_t pad = [] {
+        const char *e = std::getenv("HEIFGPU_PARSE_LDS_PAD");
+        return e ? (size_t)std::atoi(e) : (size_t)0;
+    }();
     if (a.lane_jobs)
-        hipLaunchKernelGGL(k_parse_jobs, dim3(waves), dim3(64), jobs_lds_bytes(ppw, a.max_rows), s, a);
+        hipLaunchKernelGGL(k_parse_jobs, dim3(waves), dim3(64), jobs_lds_bytes(ppw, a.max_rows) + pad, s, a);
     else
-        hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0), s,
-                           a);
+        hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64),
+                           lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0) + pad, s, a);
     return hipGetLastError();
 }
 #endif
