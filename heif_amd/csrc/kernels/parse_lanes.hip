@@ -87,7 +87,6 @@ constexpr uint32_t kProgDone = 0x7fffffffu;
 // per-lane LDS block
 struct alignas(16) LaneLds {
     uint8_t ctx[CTX_PAD];
-    SaoParams sao;               // SAO parameters of the last CTB (= the left CTB for merge_left)
     uint8_t ipmL[16], ipmA[16];  // IntraPredModeY (4x4 units): last written per row / per column
     uint8_t dL[8], dA[8];        // CtDepth (8x8 units)
     int8_t qL[8], qA[8];         // QpY (8x8 units)
@@ -1013,45 +1012,78 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
         int ml = 0, mu = 0;
         if (L.c > 0) ml = dec(L, G, CTX_SAO_MERGE);
         if (L.row > 0 && !ml) mu = dec(L, G, CTX_SAO_MERGE);
-        uint32_t *w = reinterpret_cast<uint32_t *>(&ld.sao);
-        if (ml) {
-            // ld.sao still holds the left CTB's parameters
-        } else if (mu) {
-            const uint32_t *src = reinterpret_cast<const uint32_t *>(P.gsao + (size_t)(L.row - 1) * P.wctb + L.c);
-            for (int k = 0; k < 8; ++k) w[k] = load_word_coherent(src + k);
+        // the CTB's SaoParams as 8 words (desc.hpp layout), built in registers:
+        // no per-lane LDS copy (merge-left re-reads the left CTB's entry, which
+        // this lane stored one CTU earlier)
+        uint32_t *dst = reinterpret_cast<uint32_t *>(P.gsao + (size_t)L.row * P.wctb + L.c);
+        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0, w6 = 0, w7 = 0;
+        if (ml || mu) {
+            const uint32_t *src = ml ? dst - 8 : reinterpret_cast<const uint32_t *>(P.gsao + (size_t)(L.row - 1) * P.wctb + L.c);
+            w0 = load_word_coherent(src + 0);
+            w1 = load_word_coherent(src + 1);
+            w2 = load_word_coherent(src + 2);
+            w3 = load_word_coherent(src + 3);
+            w4 = load_word_coherent(src + 4);
+            w5 = load_word_coherent(src + 5);
+            w6 = load_word_coherent(src + 6);
+            w7 = load_word_coherent(src + 7);
         } else {
-            for (int k = 0; k < 8; ++k) w[k] = 0;
-            SaoParams &s = ld.sao;
+            // byte b of the 32-byte record (every offset below is a constant after unrolling)
+            auto put8 = [&](int b, uint32_t v) {
+                const uint32_t m = (v & 0xffu) << (8 * (b & 3));
+                switch (b >> 2) {
+                case 0: w0 |= m; break;
+                case 1: w1 |= m; break;
+                case 2: w2 |= m; break;
+                case 3: w3 |= m; break;
+                case 4: w4 |= m; break;
+                case 5: w5 |= m; break;
+                case 6: w6 |= m; break;
+                default: w7 |= m; break;
+                }
+            };
+            auto put16 = [&](int b, int v) {
+                put8(b, (uint32_t)v);
+                put8(b + 1, (uint32_t)v >> 8);
+            };
             const int ncomp = P.chroma ? 3 : 1;
-            for (int cc = 0; cc < ncomp; ++cc) {
+            int type1 = 0, eo1 = 0;
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc) {
+                if (cc >= ncomp) break;
                 if (!((P.saoL && cc == 0) || (P.saoC && cc > 0))) continue;
-                if (cc < 2) s.type[cc] = (int8_t)(dec(L, G, CTX_SAO_TYPE) ? (byp(L, G) ? 2 : 1) : 0);
-                else s.type[2] = s.type[1];
-                if (!s.type[cc]) continue;
+                const int type = cc < 2 ? (dec(L, G, CTX_SAO_TYPE) ? (byp(L, G) ? 2 : 1) : 0) : type1;
+                if (cc == 1) type1 = type;
+                put8(cc, (uint32_t)type);
+                if (!type) continue;
                 const int bd = cc ? P.bdC : P.bdY;
                 const int cmax = (1 << ((bd < 10 ? bd : 10) - 5)) - 1;
-                // SaoOffsetVal straight into LDS, loops kept rolled (an unrolled
-                // local array here costs ~200 VGPRs in the kernel)
-#pragma nounroll
+                int o[4];
+#pragma unroll
                 for (int i = 0; i < 4; ++i) {  // TR(cMax), bypass
                     int v = 0;
                     while (v < cmax && byp(L, G)) ++v;
-                    s.off[cc][i] = (int16_t)v;
+                    o[i] = v;
                 }
-                if (s.type[cc] == 1) {
-#pragma nounroll
+                int band_eo;
+                if (type == 1) {
+#pragma unroll
                     for (int i = 0; i < 4; ++i)
-                        if (s.off[cc][i] && byp(L, G)) s.off[cc][i] = (int16_t)-s.off[cc][i];
-                    s.band_eo[cc] = (uint8_t)byp_bits(L, G, 5);
+                        if (o[i] && byp(L, G)) o[i] = -o[i];
+                    band_eo = (int)byp_bits(L, G, 5);
                 } else {
-                    if (cc < 2) s.band_eo[cc] = (uint8_t)byp_bits(L, G, 2);
-                    else s.band_eo[2] = s.band_eo[1];
-                    s.off[cc][2] = (int16_t)-s.off[cc][2];
-                    s.off[cc][3] = (int16_t)-s.off[cc][3];
+                    band_eo = cc < 2 ? (int)byp_bits(L, G, 2) : eo1;
+                    if (cc == 1) eo1 = band_eo;
+                    o[2] = -o[2];
+                    o[3] = -o[3];
                 }
+                put8(3 + cc, (uint32_t)band_eo);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) put16(6 + 8 * cc + 2 * i, o[i]);
             }
         }
-        uint32_t *dst = reinterpret_cast<uint32_t *>(P.gsao + (size_t)L.row * P.wctb + L.c);
+        const uint32_t w[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
+#pragma unroll
         for (int k = 0; k < 8; ++k) {
             if constexpr (EG::kSpread) store_agent(dst + k, w[k]);
             else dst[k] = w[k];
@@ -1980,7 +2012,6 @@ HG_HD inline void lane_start(Lane &L, const LanePic &P, LaneLds &ld, int row) {
     L.c = 0;
     L.qp_prev_last = P.sliceQp;
     row_outputs(L, P);
-    for (int k = 0; k < 8; ++k) reinterpret_cast<uint32_t *>(&ld.sao)[k] = 0;
     L.st = U_CTU;
 }
 
