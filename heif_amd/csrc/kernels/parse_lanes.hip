@@ -84,12 +84,21 @@ HG_HD inline uint64_t state_row(int st) {
 
 constexpr uint32_t kProgDone = 0x7fffffffu;
 
-// per-lane LDS block
+// per-lane LDS block.  HG_LANE_LDS_ODD: 212 bytes (53 dwords, odd), so the
+// 64 lanes' copies of one context byte fall in 64 different LDS banks (at 208
+// bytes = 52 dwords lanes l and l + 16 share a bank: 4-way conflicts)
+#if defined(HG_LANE_LDS_ODD)
+struct alignas(4) LaneLds {
+#else
 struct alignas(16) LaneLds {
+#endif
     uint8_t ctx[CTX_PAD];
     uint8_t ipmL[16], ipmA[16];  // IntraPredModeY (4x4 units): last written per row / per column
     uint8_t dL[8], dA[8];        // CtDepth (8x8 units)
     int8_t qL[8], qA[8];         // QpY (8x8 units)
+#if defined(HG_LANE_LDS_ODD)
+    uint8_t pad_odd[4];
+#endif
 };
 
 // picture constants and output pointers (LDS, one per picture of the wave)
@@ -200,6 +209,9 @@ struct Lane {
 #else
 #define HG_SB_T(L, i, t0) ((void)0)
 #endif
+
+// bytes of n lane blocks, rounded up so the LanePic after them stays 16-byte aligned
+HG_HD inline size_t lane_blocks_bytes(int n) { return (sizeof(LaneLds) * (size_t)n + 15) & ~(size_t)15; }
 
 // engine context of one lane (lanes mode: every lane its own substream)
 struct Eng {
@@ -2419,7 +2431,7 @@ void emu_parse(const BatchArgs &a) {
 // LDS of one wave: LaneLds per used lane, LanePic per picture, progress words,
 // engine tables, and the WPP context staging when rows wrap
 inline size_t lanes_lds_bytes(int ppw, int lane_rows, bool ring) {
-    return sizeof(LaneLds) * (size_t)(ppw * lane_rows) + sizeof(LanePic) * (size_t)ppw + 64 * sizeof(uint32_t) +
+    return lane_blocks_bytes(ppw * lane_rows) + sizeof(LanePic) * (size_t)ppw + 64 * sizeof(uint32_t) +
            (64 + 16) * sizeof(uint64_t) + (ring ? 64 * (size_t)CTX_PAD : 0);
 }
 
@@ -2433,7 +2445,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     const int ppw = a.parse_group;  // pictures per wave (launch_parse)
     const int nl = ppw * a.lane_rows;
     LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
-    LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + nl);
+    LanePic *s_pic = reinterpret_cast<LanePic *>(smem + lane_blocks_bytes(nl));
     uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + ppw);
     uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_prog + 64);
     uint64_t *s_seq = s_tab + 64;
@@ -2517,7 +2529,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
 // are per (picture, row) in LDS; the WPP context hand-off goes through one
 // staging block per picture (wpp_stage).
 inline size_t jobs_lds_bytes(int ppw, int max_rows) {
-    return sizeof(LaneLds) * 64 + sizeof(LanePic) * (size_t)ppw + sizeof(uint32_t) * (size_t)ppw * max_rows +
+    return lane_blocks_bytes(64) + sizeof(LanePic) * (size_t)ppw + sizeof(uint32_t) * (size_t)ppw * max_rows +
            (64 + 16) * sizeof(uint64_t) + (size_t)ppw * CTX_PAD + sizeof(uint32_t) * ((size_t)ppw + 4);
 }
 
@@ -2525,7 +2537,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_jobs(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ppw = a.parse_group;
     LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
-    LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + 64);
+    LanePic *s_pic = reinterpret_cast<LanePic *>(smem + lane_blocks_bytes(64));
     uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_pic + ppw);
     uint64_t *s_seq = s_tab + 64;
     uint8_t *s_wctx = reinterpret_cast<uint8_t *>(s_seq + 16);
@@ -2630,7 +2642,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_jobs(BatchArgs a) {
 // LDS, so the 2-CTU lag needs no memory traffic; waves waiting for the row
 // above sleep.
 inline size_t solo_lds_bytes(int nw, bool ring) {
-    return sizeof(LaneLds) * (size_t)nw + sizeof(LanePic) + 64 * sizeof(uint32_t) + 16 * sizeof(uint64_t) +
+    return lane_blocks_bytes(nw) + sizeof(LanePic) + 64 * sizeof(uint32_t) + 16 * sizeof(uint64_t) +
            (ring ? (size_t)nw * CTX_PAD : 0);
 }
 
@@ -2640,7 +2652,7 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int NW = Spread ? 1 : a.solo_waves;
     LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
-    LanePic *s_pic = reinterpret_cast<LanePic *>(s_lds + NW);
+    LanePic *s_pic = reinterpret_cast<LanePic *>(smem + lane_blocks_bytes(NW));
     uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + 1);
     uint64_t *s_seq = reinterpret_cast<uint64_t *>(s_prog + 64);
     uint8_t *s_wctx = a.wpp_ring ? reinterpret_cast<uint8_t *>(s_seq + 16) : nullptr;
