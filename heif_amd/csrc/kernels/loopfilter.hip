@@ -567,13 +567,17 @@ __global__ void __launch_bounds__(kLfWaves * 64) k_loopfilter(BatchArgs a) {
     });
 }
 
-// the fused loop filter unless HEIFGPU_LF=split (k_deblock x2 + k_sao_out)
+// The fused loop filter only with HEIFGPU_LF=fused.  r04 A/B (same box, 128
+// images): alone 9.2 ms against 2.9 + 4.1 for the three split kernels, and
+// beside the next decode's parse 53 ms against ~33, with k_transform (on its
+// own stream) 60 ms against 29.  Its 9.6 KB of LDS per workgroup competes with
+// the parse waves and k_transform for the LDS the parse leaves free, which is
+// what decides the reconstruction kernels' residency in the pipeline (a parse
+// padded by 4 KB of LDS per wave took 129 ms instead of 81 beside them).
+// (read at every launch, so a test can switch it within one process)
 inline bool lf_fused() {
-    static const bool on = [] {
-        const char *e = std::getenv("HEIFGPU_LF");
-        return !(e && std::string(e) == "split");
-    }();
-    return on;
+    const char *e = std::getenv("HEIFGPU_LF");
+    return e && std::string(e) == "fused";
 }
 inline int lf_tiles(const BatchArgs &a) { return a.lf_tiles; }
 

@@ -2080,10 +2080,8 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
 // that would leave under 3/4 of the SIMDs a wave (small batches).
 // HEIFGPU_LANES_PPW forces a value.
 inline int jobs_pics_per_wave(int lane_rows, int n_pics) {
-    static const int forced = [] {
-        const char *e = std::getenv("HEIFGPU_LANES_PPW");
-        return e ? std::atoi(e) : 0;
-    }();
+    const char *fe = std::getenv("HEIFGPU_LANES_PPW");
+    const int forced = fe ? std::atoi(fe) : 0;
     if (forced > 0) return forced < kJobsMaxPics ? forced : kJobsMaxPics;
     const int rows = lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows);
     int p = std::max(1, std::min(kJobsMaxPics, 128 / rows));
@@ -2101,12 +2099,9 @@ inline int jobs_pics_per_wave(int lane_rows, int n_pics) {
 // (each divergent loop runs to its slowest busy lane) and a wave alone on a
 // SIMD hides less latency than the static 1.5 waves per SIMD.  Beside the
 // parse the reconstruction stream was much faster (47 vs 74 ms at 6 per wave).
-bool lanes_jobs_default() {
-    static const bool on = [] {
-        const char *e = std::getenv("HEIFGPU_LANES_JOBS");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
+bool lanes_jobs_default() {  // (read at every prepare: tests switch it within one process)
+    const char *e = std::getenv("HEIFGPU_LANES_JOBS");
+    return e && std::atoi(e) != 0;
 }
 
 // Wave slot -> picture.  A wave runs until its heaviest picture is parsed,

@@ -45,6 +45,7 @@ PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "sprea
            "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0"},
            "jobs": JOBS, "jobs8": {**JOBS, "HEIFGPU_LANES_PPW": "8"}, "jobs5": {**JOBS, "HEIFGPU_LANES_PPW": "5"},
            "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1", "HEIFGPU_INTRA_SPLIT": "0"},
+           "lf_fused": {"HEIFGPU_LF": "fused"},
            "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
 
 
