@@ -136,7 +136,22 @@ struct TuRec {
 };
 static_assert(sizeof(TuRec) == 16, "TuRec layout");
 
-// Nonzero TransCoeffLevel: value in the high half, raster pos y*n+x low.
+// Coefficient words of a TB.  A coded TB is a run of 16-byte sub-block
+// records (SbRec: TuRec.coef = its first word, TuRec.ncoef = 4 x records),
+// in decoding order:
+//   w0: significance by scan position n (bit n) | the sign bins in decoding
+//       order (descending n) from bit 31 down;
+//   w1, w2: abs - 1 per scan position n as nibble n (15: escape, the level is
+//       in the row's escape list);
+//   w3: xS (3 bits) | yS << 3 (3) | scanIdx << 6 (2) | sign hidden << 8 |
+//       row-relative word index of the record's first escape << 9 (its later
+//       escapes, in descending n, at the indices below it: the escape list
+//       grows down from the end of the row's coefficient space).
+// The sign of a position of rank r (significant positions above it) is bit
+// 31 - r of w0, except the lowest significant position when the sign is
+// hidden: the parity of the sub-block's sum of levels (7.4.9.11).
+// A PCM TB (TU_PCM) instead holds one word per sample: value << 16 | raster
+// position.
 typedef uint32_t Coef;
 
 // SAO parameters of one CTB (7.3.8.3 semantics, SaoOffsetVal already signed).

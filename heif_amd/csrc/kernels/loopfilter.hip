@@ -607,8 +607,17 @@ void emu_sao_out(const BatchArgs &a) {
     else emu_launch(k_sao_out<uint16_t>, 1, a.n_pics, 1, a, true);
 }
 #else
+// workgroups per picture of the grid-stride loop filter kernels (tuning:
+// HEIFGPU_DBK_BLOCKS / HEIFGPU_SAO_BLOCKS; fewer, longer-lived workgroups need
+// fewer dispatches beside the parse)
+static int lf_blocks(const char *var, int dflt) {
+    const char *e = std::getenv(var);
+    const int v = e ? std::atoi(e) : dflt;
+    return v < 1 ? 1 : (v > 1024 ? 1024 : v);
+}
+
 hipError_t launch_deblock(const BatchArgs &a, hipStream_t s) {
-    dim3 grid(64, a.n_pics), block(256);
+    dim3 grid(lf_blocks("HEIFGPU_DBK_BLOCKS", 64), a.n_pics), block(256);
     if (a.has_assembly) {  // the assemblies' children are reconstructed: put them together first
         if (a.bytes_per_sample == 1) hipLaunchKernelGGL(k_assemble<uint8_t>, grid, block, 0, s, a);
         else hipLaunchKernelGGL(k_assemble<uint16_t>, grid, block, 0, s, a);
@@ -632,7 +641,7 @@ hipError_t launch_sao_out(const BatchArgs &a, hipStream_t s) {
         else hipLaunchKernelGGL(k_loopfilter<uint16_t>, g, b, lds, s, a);
         return hipGetLastError();
     }
-    dim3 grid(256, a.n_pics), block(256);
+    dim3 grid(lf_blocks("HEIFGPU_SAO_BLOCKS", 256), a.n_pics), block(256);
     if (a.bytes_per_sample == 1) hipLaunchKernelGGL(k_sao_out<uint8_t>, grid, block, 0, s, a);
     else hipLaunchKernelGGL(k_sao_out<uint16_t>, grid, block, 0, s, a);
     return hipGetLastError();

@@ -187,6 +187,7 @@ struct Lane {
     int rc_scan, rc_last_sub, rc_last_pos, rc_i, rc_prev_c1;
     uint64_t rc_csbf;  // coded_sub_block_flag, bit yS * 8 + xS
     uint32_t ntu, ncoef;
+    uint32_t nesc;              // escape levels of the row (stored down from the end of its coefficient space)
     uint32_t tu_row, coef_row;  // TuRec / Coef index of the current row's outputs
     // solo mode on the GPU: the context states, byte i of the LDS layout at
     // byte i & 3 of lane i >> 2 (35 lanes), read / written with v_readlane /
@@ -301,7 +302,7 @@ __device__ __forceinline__ void uni_state(Lane &L) {
     HG_U(tl); HG_U(td); HG_U(tcbf); HG_U(qp_prev_last); HG_U(qp_pred); HG_U(cu_qp_delta_val); HG_U(qpy_cur);
     HG_U(qg_x); HG_U(qg_y); HG_U(cu_modes); HG_U(cu_chroma); HG_U(tb_t); HG_U(tb_n); HG_U(tb_cidx); HG_U(tb_x);
     HG_U(tb_y); HG_U(tb_log2); HG_U(tb_mode); HG_U(tb_coef0); HG_U(rc_scan); HG_U(rc_last_sub); HG_U(rc_last_pos);
-    HG_U(rc_i); HG_U(rc_prev_c1); HG_U(ntu); HG_U(ncoef); HG_U(tu_row); HG_U(coef_row);
+    HG_U(rc_i); HG_U(rc_prev_c1); HG_U(ntu); HG_U(ncoef); HG_U(nesc); HG_U(tu_row); HG_U(coef_row);
 #undef HG_U
     L.cur = uni64(L.cur);
     L.rc_csbf = uni64(L.rc_csbf);
@@ -964,13 +965,20 @@ HG_HD inline uint32_t substream_start(const Lane &L, const LanePic &P, const Bat
 HG_HD inline void row_outputs(Lane &L, const LanePic &P) {
     L.tu_row = (uint32_t)L.row * P.tu_cap;
     L.coef_row = (uint32_t)L.row * P.coef_cap;
-    L.ntu = L.ncoef = 0;
+    L.ntu = L.ncoef = L.nesc = 0;
 }
 
 // one coefficient, one 4-byte store.  (Grouping four into a 16-byte store
 // through registers measured 5 % slower: the selects run on every lane of
 // every coefficient step, the saved stores were cheap.)
-HG_HD inline void coef_push(Lane &L, const LanePic &P, uint32_t w) { P.coef_base[L.coef_row + L.ncoef++] = w; }
+HG_HD inline void coef_push(Lane &L, const LanePic &P, uint32_t w) {
+#if defined(HG_NO_COEF_STORE)  // timing experiment only: the stores' share of the parse
+    ++L.ncoef;
+    (void)w;
+#else
+    P.coef_base[L.coef_row + L.ncoef++] = w;
+#endif
+}
 
 // ------------------------------------------------------------------ units
 // U_CTU: CTU start (7.3.8.2) and sao() (7.3.8.3).  Returns without a state
@@ -1183,7 +1191,7 @@ HG_HD inline void pcm_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             const uint32_t w = ((uint32_t)G.rbsp[b] << 16) | ((uint32_t)G.rbsp[b + 1] << 8) | (uint32_t)G.rbsp[b + 2];
             const uint32_t v = (w >> (24u - (bit & 7u) - (uint32_t)pbd)) & ((1u << pbd) - 1u);
             bit += (uint32_t)pbd;
-            if (L.ncoef < P.coef_cap) coef_push(L, P, ((v << sh) << 16) | (uint32_t)i);
+            if (L.ncoef + L.nesc < P.coef_cap) coef_push(L, P, ((v << sh) << 16) | (uint32_t)i);
             else L.status |= ST_CAPACITY;
         }
         tu_emit(L, P);
@@ -1550,6 +1558,38 @@ HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     L.st = U_SB;
 }
 
+// bit n of a 16-bit mask to bit 4n (a nibble per scan position)
+HG_HD inline uint64_t spread16_nib(uint32_t m) {
+    uint64_t x = m & 0xffffu;
+    x = (x | (x << 24)) & 0x000000ff000000ffull;
+    x = (x | (x << 12)) & 0x000f000f000f000full;
+    x = (x | (x << 6)) & 0x0303030303030303ull;
+    x = (x | (x << 3)) & 0x1111111111111111ull;
+    return x;
+}
+
+// the sub-block's record (SbRec): one 16-byte store (4 coefficient words); the
+// first escape of the record is the escape slot at L.nesc when it started
+template <class L_, class P_>
+HG_HD inline void sb_store(L_ &L, const P_ &P, uint32_t sig, uint32_t signs, uint64_t nib, int xS, int yS, bool hide) {
+    const uint32_t nesc_sb = (uint32_t)__builtin_popcountll(nib & (nib >> 1) & (nib >> 2) & (nib >> 3) & 0x1111111111111111ull);
+    const uint32_t esc0 = P.coef_cap - 1 - (L.nesc - nesc_sb);  // row-relative index of its first escape
+    const uint32_t w0 = (sig & 0xffffu) | (signs & 0xffff0000u);
+    const uint32_t w3 = (uint32_t)xS | ((uint32_t)yS << 3) | ((uint32_t)L.rc_scan << 6) | (hide ? 1u << 8 : 0u) |
+                        (esc0 << 9);
+    if (L.ncoef + L.nesc + 4 <= P.coef_cap) {
+#if defined(HG_NO_COEF_STORE)  // timing experiment only
+        (void)w0, (void)w3;
+#else
+        store_tu(reinterpret_cast<TuRec *>(P.coef_base + L.coef_row + L.ncoef), w0, (uint32_t)nib,
+                 (uint32_t)(nib >> 32), w3);
+#endif
+        L.ncoef += 4;
+    } else {
+        L.status |= ST_CAPACITY;
+    }
+}
+
 // U_SB: sub-block rc_i of residual_coding (7.3.8.11, 9.3.4.2.5-7)
 template <class EG>
 HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
@@ -1703,25 +1743,22 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         const int nsign = __builtin_popcount(sig) - (hide ? 1 : 0);
         uint32_t signs = byp_bits(L, G, nsign);
         signs = nsign ? signs << (32 - nsign) : 0u;  // first decoded sign in bit 31
-        const int n = 1 << l2;
-#if !defined(HG_HOST_EMU)
-        if constexpr (EG::kSolo) {
-            // One substream per wave: only the coeff_abs_level_remaining bins
-            // are serial.  They are decoded for the coefficients that have one
-            // (base level 1 past the first eight, or base == the greater1 /
-            // greater2 ceiling), each value into lane nn of `remv`; then lane j
-            // assembles the coefficient at scan position j (level, sign by its
-            // rank in scan order, position) and the sub-block's coefficients
-            // leave in one store instruction instead of one per coefficient
-            // (the r03 serial loop cost ~780 cycles per coefficient).
+        // The sub-block leaves as one 16-byte record (SbRec, desc.hpp): the
+        // significance map, the signs in decoding order, and abs - 1 of every
+        // scan position as a nibble (15: the level is in the row's escape list,
+        // which grows down from the end of the row's coefficient space).  abs - 1
+        // is greater1 + greater2 (bit masks spread to nibbles) plus
+        // coeff_abs_level_remaining where one is coded, so only those levels
+        // are visited, one at a time (their Rice parameters chain); the r03
+        // layout stored every coefficient with its own 4-byte store.
+        uint64_t nib = spread16_nib(g1) + spread16_nib(g2);
+        {
             uint32_t m8 = sig;  // the first eight significant positions (scan order = highest first)
-            for (int j = 0, mm = (int)sig; j < 8 && mm; ++j) mm &= ~(1 << msb32((uint32_t)mm)), m8 = (uint32_t)mm;
+            for (int j = 0; j < 8 && m8; ++j) m8 &= ~(1u << msb32(m8));
             m8 = sig & ~m8;
             const uint32_t lastb = last_g1 >= 0 ? 1u << last_g1 : 0u;
             uint32_t need = (g1 & ~lastb) | g2 | (sig & ~m8);
-            const int j = (int)__lane_id();
-            uint32_t remv = 0;
-            int sum_rem = 0, last_abs = 0, last_rice = 0;
+            int last_abs = 0, last_rice = 0;
             bool first_rem = true;
             while (need) {
                 const int nn = msb32(need);
@@ -1735,84 +1772,17 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
                     k = last_rice + (last_abs > 3 * (1 << last_rice) ? 1 : 0);
                     k = k < 4 ? k : 4;
                 }
-                int rem = byp_rem(L, G, k);
-                if (rem < 0) {
-                    const int lim = 31 - (k + 1);
-                    int ones = 0;
-                    for (;;) {
-                        const int mm = lim + 1 - ones < 8 ? lim + 1 - ones : 8;
-                        const int p = byp_unary(L, G, mm);
-                        ones += p;
-                        if (p < mm || ones > lim) break;
-                    }
-                    if (ones > lim) {
-                        L.status |= ST_SYNTAX;
-                        rem = 0;
-                    } else {
-                        rem = (int)((4u << k) + (((1u << ones) - 1u) << (k + 1)) + byp_bits(L, G, ones + k + 1));
-                    }
-                }
-                last_abs = base + rem;
-                last_rice = k;
-                sum_rem += rem;
-                remv = j == nn ? (uint32_t)rem : remv;
-            }
-            const int nsig = __builtin_popcount(sig);
-            const int sum_abs = nsig + __builtin_popcount(g1) + __builtin_popcount(g2) + sum_rem;
-            const uint64_t sw = scan4_word(L.rc_scan);
-            {  // branch-free up to the one store (a divergent region here crashed the register allocator)
-                const uint32_t jj = (uint32_t)j & 15u;
-                const int rank = __builtin_popcount(sig >> jj) - 1;  // coefficients before it in scan order
-                int v = 1 + (int)((g1 >> jj) & 1) + (int)((g2 >> jj) & 1) + (int)remv;
-                const uint32_t sbit = (signs << (rank & 31)) >> 31;
-                const bool neg = (hide && (int)jj == first_sig) ? (sum_abs & 1) != 0 : sbit != 0;
-                v = neg ? -v : v;
-                v = v > 32767 ? 32767 : (v < -32768 ? -32768 : v);
-                const uint32_t pp = (uint32_t)(sw >> (4 * jj)) & 15u;
-                const int xC = (xS << 2) + (int)(pp & 3), yC = (yS << 2) + (int)(pp >> 2);
-                const uint32_t idx = L.ncoef + (uint32_t)rank;
-                const bool st = j < 16 && ((sig >> jj) & 1u) && idx < P.coef_cap;
-                const uint32_t w = ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC);
-                if (st) P.coef_base[L.coef_row + idx] = w;
-            }
-            if (L.ncoef + (uint32_t)nsig > P.coef_cap) {
-                L.status |= ST_CAPACITY;
-                L.ncoef = P.coef_cap;
-            } else {
-                L.ncoef += (uint32_t)nsig;
-            }
-            HG_SB_T(L, 3, tsb);
-            if (--L.rc_i < 0) tb_done(L, ld, P);
-            return;
-        }
-#endif
-        int num_sig = 0, sum_abs = 0, last_abs = 0, last_rice = 0;
-        bool first_rem = true;
-        for (uint32_t m = sig; m;) {
-            const int nn = msb32(m);
-            m &= ~(1u << nn);
-            const int base = 1 + (int)((g1 >> nn) & 1) + (int)((g2 >> nn) & 1);
-            int rem = 0;
-            if (base == ((num_sig < 8) ? ((nn == last_g1) ? 3 : 2) : 1)) {
-                int k;
-                if (first_rem) {
-                    k = 0;
-                    first_rem = false;
-                } else {
-                    k = last_rice + (last_abs > 3 * (1 << last_rice) ? 1 : 0);
-                    k = k < 4 ? k : 4;
-                }
                 // coeff_abs_level_remaining (decoder.rs:230-261): TR(4 << k, k) prefix, EG(k + 1) escape
-                rem = byp_rem(L, G, k);
+                int rem = byp_rem(L, G, k);
                 if (rem < 0) {
                     // EG(k + 1) prefix: unary ones, up to 8 per division, at most 31 - (k + 1)
                     const int lim = 31 - (k + 1);
                     int ones = 0;
                     for (;;) {
                         const int mm = lim + 1 - ones < 8 ? lim + 1 - ones : 8;
-                        const int p = byp_unary(L, G, mm);
-                        ones += p;
-                        if (p < mm || ones > lim) break;  // the terminating 0 read, or too many ones
+                        const int pz = byp_unary(L, G, mm);
+                        ones += pz;
+                        if (pz < mm || ones > lim) break;  // the terminating 0 read, or too many ones
                     }
                     if (ones > lim) {
                         L.status |= ST_SYNTAX;
@@ -1823,32 +1793,19 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
                 }
                 last_abs = base + rem;
                 last_rice = k;
+                const int am1 = base - 1 + rem;  // abs - 1
+                nib = (nib & ~(0xfull << (4 * nn))) | ((uint64_t)(am1 < 15 ? am1 : 15) << (4 * nn));
+                if (am1 >= 15) {  // escape: the whole level, in descending scan order from the row's end
+                    if (L.ncoef + L.nesc + 4 < P.coef_cap)
+                        P.coef_base[L.coef_row + P.coef_cap - 1 - L.nesc] = (uint32_t)last_abs;
+                    else
+                        L.status |= ST_CAPACITY;
+                    ++L.nesc;
+                }
             }
-            int v = base + rem;
-            bool neg;
-            if (hide && nn == first_sig) {
-                sum_abs += v;
-                neg = (sum_abs & 1) != 0;
-            } else {
-                neg = (signs >> 31) != 0;
-                signs <<= 1;
-                if (hide) sum_abs += v;
-            }
-            if (neg) v = -v;
-            const uint32_t pp = (uint32_t)(scan4_word(L.rc_scan) >> (4 * nn)) & 15u;
-            const int xC = (xS << 2) + (int)(pp & 3), yC = (yS << 2) + (int)(pp >> 2);
-            if (v > 32767) v = 32767;
-            if (v < -32768) v = -32768;
-            if (L.ncoef < P.coef_cap)
-                coef_push(L, P, ((uint32_t)(uint16_t)(int16_t)v << 16) | (uint32_t)(yC * n + xC));
-            else
-                L.status |= ST_CAPACITY;
-            ++num_sig;
         }
-#if defined(HG_PARSE_PROF_SB) && !defined(HG_HOST_EMU)
-        L.psb[5] += (uint64_t)__builtin_popcount(sig);
-#endif
         HG_SB_T(L, 3, tsb);
+        sb_store(L, P, sig, signs, nib, xS, yS, hide);
     }
     if (--L.rc_i < 0) tb_done(L, ld, P);
 }

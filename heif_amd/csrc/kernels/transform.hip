@@ -16,6 +16,7 @@
 // fill.  Integer sums on VALU with the DCT matrix in LDS — no MFMA (the
 // products are exact int32, and TBs are at most 32x32).
 #include "kernels.hpp"
+#include "tables.hpp"
 
 namespace hg {
 
@@ -59,6 +60,58 @@ __constant__ int16_t c_level_scale[6] = {40, 45, 51, 57, 64, 72};
 #define wave_sync() HG_WAVE_SYNC()
 
 __device__ __forceinline__ int clip16(int64_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : (int)v); }
+
+// One sub-block record (SbRec, desc.hpp) of a TB's coefficient words.
+struct SbRec {
+    uint32_t w0, w1, w2, w3;
+    __device__ __forceinline__ uint32_t sig() const { return w0 & 0xffffu; }
+    __device__ __forceinline__ uint64_t nib() const { return (uint64_t)w1 | ((uint64_t)w2 << 32); }
+    // nibble mask of the escapes (bit 4n set where abs - 1 is coded as 15)
+    __device__ __forceinline__ uint64_t esc() const {
+        const uint64_t x = nib();
+        return x & (x >> 1) & (x >> 2) & (x >> 3) & 0x1111111111111111ull;
+    }
+    __device__ __forceinline__ uint32_t esc0() const { return w3 >> 9; }
+    // raster position in an n-wide TB (log2n) of scan position nn
+    __device__ __forceinline__ int pos(int nn, int log2n) const {
+        const uint32_t pp = (uint32_t)(kScan4Pos[(w3 >> 6) & 3u] >> (4 * nn)) & 15u;
+        const int x = (int)((w3 & 7u) << 2) + (int)(pp & 3u), y = (int)(((w3 >> 3) & 7u) << 2) + (int)(pp >> 2);
+        return (y << log2n) + x;
+    }
+    // the hidden sign's parity: the sum of the sub-block's levels
+    __device__ __forceinline__ int sum_abs(const Coef *row) const {
+        const uint64_t x = nib();
+        const uint64_t t = (x & 0x0f0f0f0f0f0f0f0full) + ((x >> 4) & 0x0f0f0f0f0f0f0f0full);
+        int s = __builtin_popcount(sig()) + (int)((t * 0x0101010101010101ull) >> 56);
+        const int ne = __builtin_popcountll(esc());
+        for (int k = 0; k < ne; ++k) s += (int)row[esc0() - (uint32_t)k] - 16;
+        return s;
+    }
+    // TransCoeffLevel at scan position nn (significant), given the number of
+    // escapes at higher positions
+    __device__ __forceinline__ int level(int nn, int esc_above, const Coef *row) const {
+        const int a = (int)((nib() >> (4 * nn)) & 15u);
+        const int abs_v = a < 15 ? a + 1 : (int)row[esc0() - (uint32_t)esc_above];
+        const uint32_t s = sig();
+        bool neg;
+        if (((w3 >> 8) & 1u) && nn == __builtin_ctz(s)) {
+            neg = (sum_abs(row) & 1) != 0;
+        } else {
+            const int rank = __builtin_popcount(s >> (nn + 1));
+            neg = ((w0 << rank) >> 31) != 0;
+        }
+        const int v = neg ? -abs_v : abs_v;
+        return v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
+    }
+};
+__device__ __forceinline__ SbRec load_rec(const Coef *p) {
+#if defined(HG_HOST_EMU)
+    return SbRec{p[0], p[1], p[2], p[3]};
+#else
+    const uint4 v = *reinterpret_cast<const uint4 *>(p);  // one 16-byte load
+    return SbRec{v.x, v.y, v.z, v.w};
+#endif
+}
 
 }  // namespace
 
@@ -134,12 +187,23 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
             for (int vl = lane; vl < 64; vl += kWave) {
                 TuRec tu;
                 const int l16 = vl & 15;
-                if (!grp(vl, tu) || l16 >= (int)tu.ncoef) continue;
+                if (!grp(vl, tu)) continue;
                 const int cidx = tu.flags & TU_CIDX_MASK;
                 const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
-                const Coef c = coefs[tu.coef + l16];
-                const int pos = (int)(c & 15u);
-                int dv = (int)(int16_t)(c >> 16);
+                int pos, dv;
+                if (tu.flags & TU_PCM) {  // one word per sample
+                    if (l16 >= (int)tu.ncoef) continue;
+                    const Coef c = coefs[tu.coef + l16];
+                    pos = (int)(c & 15u);
+                    dv = (int)(int16_t)(c >> 16);
+                } else {  // one sub-block record; lane l16 decodes scan position l16
+                    if (tu.ncoef < 4) continue;
+                    const SbRec r = load_rec(coefs + tu.coef);
+                    if (!((r.sig() >> l16) & 1u)) continue;
+                    const int above = l16 < 15 ? __builtin_popcountll(r.esc() >> (4 * l16 + 4)) : 0;  // (a shift by 64 is undefined)
+                    dv = r.level(l16, above, coefs);
+                    pos = r.pos(l16, 2);
+                }
                 if (!(tu.flags & TU_BYPASS)) {
                     const int qp = tu.qp, bd_shift = bd - 3;
                     const int ls = c_level_scale[qp % 6] << (qp / 6);
@@ -211,10 +275,8 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         const bool use_m = scaling && !(ts && n > 4);
         const uint8_t *mtab = a.sf + sp.sf_off + sf_size_offset(log2n - 2) + (uint32_t)cidx * (uint32_t)(n * n);
         int my_row = 0, my_col = 0;
-        for (int k = lane; k < tu.ncoef; k += kWave) {
-            const Coef c = coefs[tu.coef + k];
-            const int pos = (int)(c & 0xffffu) & (n * n - 1);
-            const int v = (int)(int16_t)(c >> 16);
+        auto put = [&](int pos, int v) {
+            pos &= n * n - 1;
             int dv;
             if (bypass) {
                 dv = v;
@@ -225,6 +287,23 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
             d[pos] = (int16_t)dv;
             my_row = max(my_row, pos >> log2n);
             my_col = max(my_col, pos & (n - 1));
+        };
+        if (tu.flags & TU_PCM) {  // one word per sample
+            for (int k = lane; k < tu.ncoef; k += kWave) {
+                const Coef c = coefs[tu.coef + k];
+                put((int)(c & 0xffffu), (int)(int16_t)(c >> 16));
+            }
+        } else {  // a lane per sub-block record, its positions in decoding order
+            for (int k = lane; k < (int)(tu.ncoef >> 2); k += kWave) {
+                const SbRec r = load_rec(coefs + tu.coef + 4 * k);
+                int above = 0;
+                for (uint32_t m = r.sig(); m;) {
+                    const int nn = 31 - __builtin_clz(m);
+                    m ^= 1u << nn;
+                    put(r.pos(nn, log2n), r.level(nn, above, coefs));
+                    above += (int)((r.nib() >> (4 * nn)) & 15u) == 15;
+                }
+            }
         }
         if (my_row) atomicMax(&extent[wave][0], my_row);
         if (my_col) atomicMax(&extent[wave][1], my_col);
