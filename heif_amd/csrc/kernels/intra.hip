@@ -424,9 +424,12 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     if (cbf && sl + 32 < n * n) r1 = w.res[(size_t)(y0 + ((sl + 32) >> log2n)) * PW + x0 + ((sl + 32) & (n - 1))];
     int16_t *left = L->left + 33 * h, *top = L->top + 33 * h;
     // 1. neighbours in search order (8.4.4.2.2), chunk k = search positions sl + 32 k
-    int val[2] = {0, 0};
-    uint32_t hm[2] = {0, 0};
-    for (int k = 0; k < nch; ++k) {
+    // (two named registers, not arrays: indexed by a runtime chunk they went to scratch)
+    int val0 = 0, val1 = 0;
+    uint32_t hm0 = 0, hm1 = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (k >= nch) break;
         const int s = sl + 32 * k;
         int xn, yn;
         if (s < 2 * n) {
@@ -441,28 +444,38 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
         }
         const bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
                         nb_avail(zc, xn << 1, yn << 1, bx0, by0, csl);
-        val[k] = av ? w.fetch(xn, yn) : 0;
-        hm[k] = (uint32_t)(__ballot(av) >> (32 * h));
+        const int vk = av ? w.fetch(xn, yn) : 0;
+        const uint32_t hk = (uint32_t)(__ballot(av) >> (32 * h));
+        if (k == 0) {
+            val0 = vk;
+            hm0 = hk;
+        } else {
+            val1 = vk;
+            hm1 = hk;
+        }
     }
     // 2. substitution: nearest available predecessor, else the first available
-    const bool any = (hm[0] | hm[1]) != 0;
-    for (int k = 0; k < nch; ++k) {
+    const bool any = (hm0 | hm1) != 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (k >= nch) break;
         const int s = sl + 32 * k;
+        const uint32_t hmk = k ? hm1 : hm0;
         int sc = k, src = sl;
-        if (any && !((hm[k] >> sl) & 1u)) {
-            const uint32_t below = hm[k] & ((1u << sl) - 1u);
+        if (any && !((hmk >> sl) & 1u)) {
+            const uint32_t below = hmk & ((1u << sl) - 1u);
             if (below) {
                 src = 31 - __builtin_clz(below);
-            } else if (k == 1 && hm[0]) {
+            } else if (k == 1 && hm0) {
                 sc = 0;
-                src = 31 - __builtin_clz(hm[0]);
+                src = 31 - __builtin_clz(hm0);
             } else {
-                sc = hm[0] ? 0 : 1;
-                src = __builtin_ctz(hm[sc]);
+                sc = hm0 ? 0 : 1;
+                src = __builtin_ctz(sc ? hm1 : hm0);
             }
         }
-        const int v0 = __shfl(val[0], 32 * h + src, 64);
-        const int v1 = nch > 1 ? __shfl(val[1], 32 * h + src, 64) : 0;
+        const int v0 = __shfl(val0, 32 * h + src, 64);
+        const int v1 = nch > 1 ? __shfl(val1, 32 * h + src, 64) : 0;
         const int v = !any ? (1 << (bd - 1)) : (sc == 0 ? v0 : v1);
         if (s < 2 * n) left[2 * n - s] = (int16_t)v;
         else if (s == 2 * n) {
