@@ -74,7 +74,9 @@ struct SbRec {
     __device__ __forceinline__ uint32_t esc0() const { return w3 >> 9; }
     // raster position in an n-wide TB (log2n) of scan position nn
     __device__ __forceinline__ int pos(int nn, int log2n) const {
-        const uint32_t pp = (uint32_t)(kScan4Pos[(w3 >> 6) & 3u] >> (4 * nn)) & 15u;
+        const uint32_t sc = (w3 >> 6) & 3u;  // (selected, not indexed: the words stay immediates)
+        const uint64_t sw = sc == 0 ? kScan4Pos[0] : (sc == 1 ? kScan4Pos[1] : kScan4Pos[2]);
+        const uint32_t pp = (uint32_t)(sw >> (4 * nn)) & 15u;
         const int x = (int)((w3 & 7u) << 2) + (int)(pp & 3u), y = (int)(((w3 >> 3) & 7u) << 2) + (int)(pp >> 2);
         return (y << log2n) + x;
     }
@@ -293,16 +295,14 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                 const Coef c = coefs[tu.coef + k];
                 put((int)(c & 0xffffu), (int)(int16_t)(c >> 16));
             }
-        } else {  // a lane per sub-block record, its positions in decoding order
-            for (int k = lane; k < (int)(tu.ncoef >> 2); k += kWave) {
-                const SbRec r = load_rec(coefs + tu.coef + 4 * k);
-                int above = 0;
-                for (uint32_t m = r.sig(); m;) {
-                    const int nn = 31 - __builtin_clz(m);
-                    m ^= 1u << nn;
-                    put(r.pos(nn, log2n), r.level(nn, above, coefs));
-                    above += (int)((r.nib() >> (4 * nn)) & 15u) == 15;
-                }
+        } else {  // 16 lanes per sub-block record, a scan position each (no serial loop per lane)
+            const int nrec = (int)(tu.ncoef >> 2);
+            for (int q = lane; q < 16 * nrec; q += kWave) {
+                const SbRec r = load_rec(coefs + tu.coef + 4 * (q >> 4));  // (16 lanes, one address)
+                const int nn = q & 15;
+                if (!((r.sig() >> nn) & 1u)) continue;
+                const int above = nn < 15 ? __builtin_popcountll(r.esc() >> (4 * nn + 4)) : 0;
+                put(r.pos(nn, log2n), r.level(nn, above, coefs));
             }
         }
         if (my_row) atomicMax(&extent[wave][0], my_row);
