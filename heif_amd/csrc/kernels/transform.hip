@@ -15,8 +15,7 @@
 // second only over the nonzero first-stage columns, and a DC-only TB is a
 // fill.  Integer sums on VALU with the DCT matrix in LDS — no MFMA (the
 // products are exact int32, and TBs are at most 32x32).
-#include "kernels.hpp"
-#include "tables.hpp"
+#include "xform.hpp"
 
 namespace hg {
 
@@ -27,93 +26,7 @@ namespace {
 #endif
 constexpr int kWaves = HG_XF_WAVES;
 
-// transMatrix of 8.6.4.2 (32x32 DCT; smaller sizes use rows k * 32/n)
-struct TransMatrix {
-    int8_t m[32][32];
-};
-constexpr TransMatrix make_matrix() {
-    TransMatrix t{};
-    constexpr int odd[16] = {90, 90, 88, 85, 82, 78, 73, 67, 61, 54, 46, 38, 31, 22, 13, 4};
-    constexpr int e2[8] = {90, 87, 80, 70, 57, 43, 25, 9};
-    constexpr int e4[4] = {89, 75, 50, 18};
-    int cv[33] = {};
-    cv[0] = 64;
-    cv[8] = 83;
-    cv[16] = 64;
-    cv[24] = 36;
-    cv[32] = 0;
-    for (int i = 0; i < 16; ++i) cv[2 * i + 1] = odd[i];
-    for (int i = 0; i < 8; ++i) cv[2 * (2 * i + 1)] = e2[i];
-    for (int i = 0; i < 4; ++i) cv[4 * (2 * i + 1)] = e4[i];
-    for (int k = 0; k < 32; ++k)
-        for (int n = 0; n < 32; ++n) {
-            int j = ((2 * n + 1) * k) % 128;
-            int v = j <= 32 ? cv[j] : j <= 64 ? -cv[64 - j] : j <= 96 ? -cv[j - 64] : cv[128 - j];
-            t.m[k][n] = (int8_t)v;
-        }
-    return t;
-}
-__constant__ TransMatrix c_tm = make_matrix();
-__constant__ int8_t c_dst[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
-__constant__ int16_t c_level_scale[6] = {40, 45, 51, 57, 64, 72};
-
 #define wave_sync() HG_WAVE_SYNC()
-
-__device__ __forceinline__ int clip16(int64_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : (int)v); }
-
-// One sub-block record (SbRec, desc.hpp) of a TB's coefficient words.
-struct SbRec {
-    uint32_t w0, w1, w2, w3;
-    __device__ __forceinline__ uint32_t sig() const { return w0 & 0xffffu; }
-    __device__ __forceinline__ uint64_t nib() const { return (uint64_t)w1 | ((uint64_t)w2 << 32); }
-    // nibble mask of the escapes (bit 4n set where abs - 1 is coded as 15)
-    __device__ __forceinline__ uint64_t esc() const {
-        const uint64_t x = nib();
-        return x & (x >> 1) & (x >> 2) & (x >> 3) & 0x1111111111111111ull;
-    }
-    __device__ __forceinline__ uint32_t esc0() const { return w3 >> 9; }
-    // raster position in an n-wide TB (log2n) of scan position nn
-    __device__ __forceinline__ int pos(int nn, int log2n) const {
-        const uint32_t sc = (w3 >> 6) & 3u;  // (selected, not indexed: the words stay immediates)
-        const uint64_t sw = sc == 0 ? kScan4Pos[0] : (sc == 1 ? kScan4Pos[1] : kScan4Pos[2]);
-        const uint32_t pp = (uint32_t)(sw >> (4 * nn)) & 15u;
-        const int x = (int)((w3 & 7u) << 2) + (int)(pp & 3u), y = (int)(((w3 >> 3) & 7u) << 2) + (int)(pp >> 2);
-        return (y << log2n) + x;
-    }
-    // the hidden sign's parity: the sum of the sub-block's levels
-    __device__ __forceinline__ int sum_abs(const Coef *row) const {
-        const uint64_t x = nib();
-        const uint64_t t = (x & 0x0f0f0f0f0f0f0f0full) + ((x >> 4) & 0x0f0f0f0f0f0f0f0full);
-        int s = __builtin_popcount(sig()) + (int)((t * 0x0101010101010101ull) >> 56);
-        const int ne = __builtin_popcountll(esc());
-        for (int k = 0; k < ne; ++k) s += (int)row[esc0() - (uint32_t)k] - 16;
-        return s;
-    }
-    // TransCoeffLevel at scan position nn (significant), given the number of
-    // escapes at higher positions
-    __device__ __forceinline__ int level(int nn, int esc_above, const Coef *row) const {
-        const int a = (int)((nib() >> (4 * nn)) & 15u);
-        const int abs_v = a < 15 ? a + 1 : (int)row[esc0() - (uint32_t)esc_above];
-        const uint32_t s = sig();
-        bool neg;
-        if (((w3 >> 8) & 1u) && nn == __builtin_ctz(s)) {
-            neg = (sum_abs(row) & 1) != 0;
-        } else {
-            const int rank = __builtin_popcount(s >> (nn + 1));
-            neg = ((w0 << rank) >> 31) != 0;
-        }
-        const int v = neg ? -abs_v : abs_v;
-        return v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
-    }
-};
-__device__ __forceinline__ SbRec load_rec(const Coef *p) {
-#if defined(HG_HOST_EMU)
-    return SbRec{p[0], p[1], p[2], p[3]};
-#else
-    const uint4 v = *reinterpret_cast<const uint4 *>(p);  // one 16-byte load
-    return SbRec{v.x, v.y, v.z, v.w};
-#endif
-}
 
 }  // namespace
 
@@ -262,105 +175,10 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         if (!(tu.flags & TU_CBF)) continue;
         if (tu.log2 == 2) continue;  // pass A
         const int cidx = tu.flags & TU_CIDX_MASK;
-        const int log2n = tu.log2, n = 1 << log2n;
-        if (log2n < 2 || log2n > 5 || cidx > 2 || tu.x + n > pitch[cidx] || tu.y + n > (cidx ? ch : H)) continue;
-        const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
-        const bool bypass = (tu.flags & TU_BYPASS) != 0, ts = (tu.flags & TU_TSKIP) != 0;
-        // 1. zero the tile, scatter d[y][x] (scaled unless bypass)
-        for (int i = lane; i < n * n / 2; i += kWave) reinterpret_cast<int32_t *>(d)[i] = 0;
-        if (lane == 0) extent[wave][0] = extent[wave][1] = 0;
-        wave_sync();
-        const int qp = tu.qp;
-        const int bd_shift = bd + log2n - 5;
-        const int64_t rnd = (int64_t)1 << (bd_shift - 1);
-        const int ls = c_level_scale[qp % 6] << (qp / 6);
-        const bool use_m = scaling && !(ts && n > 4);
-        const uint8_t *mtab = a.sf + sp.sf_off + sf_size_offset(log2n - 2) + (uint32_t)cidx * (uint32_t)(n * n);
-        int my_row = 0, my_col = 0;
-        auto put = [&](int pos, int v) {
-            pos &= n * n - 1;
-            int dv;
-            if (bypass) {
-                dv = v;
-            } else {
-                const int m = use_m ? mtab[pos] : 16;
-                dv = clip16(((int64_t)v * m * ls + rnd) >> bd_shift);
-            }
-            d[pos] = (int16_t)dv;
-            my_row = max(my_row, pos >> log2n);
-            my_col = max(my_col, pos & (n - 1));
-        };
-        if (tu.flags & TU_PCM) {  // one word per sample
-            for (int k = lane; k < tu.ncoef; k += kWave) {
-                const Coef c = coefs[tu.coef + k];
-                put((int)(c & 0xffffu), (int)(int16_t)(c >> 16));
-            }
-        } else {  // 16 lanes per sub-block record, a scan position each (no serial loop per lane)
-            const int nrec = (int)(tu.ncoef >> 2);
-            for (int q = lane; q < 16 * nrec; q += kWave) {
-                const SbRec r = load_rec(coefs + tu.coef + 4 * (q >> 4));  // (16 lanes, one address)
-                const int nn = q & 15;
-                if (!((r.sig() >> nn) & 1u)) continue;
-                const int above = nn < 15 ? __builtin_popcountll(r.esc() >> (4 * nn + 4)) : 0;
-                put(r.pos(nn, log2n), r.level(nn, above, coefs));
-            }
-        }
-        if (my_row) atomicMax(&extent[wave][0], my_row);
-        if (my_col) atomicMax(&extent[wave][1], my_col);
-        wave_sync();
-        const int rows = extent[wave][0] + 1, cols = extent[wave][1] + 1;  // d is zero beyond these
-        const int bd2 = 20 - bd;
-        int16_t HG_GAS *dst = res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x;
-        if (bypass || ts) {
-            // bypass: r = TransCoeffLevel; transform skip: r = (d << tsShift) then >> bdShift
-            const int ts_shift = 5 + log2n;
-            for (int i = lane; i < n * n; i += kWave) {
-                int r = d[i];
-                if (!bypass) r = (r * (1 << ts_shift) + (1 << (bd2 - 1))) >> bd2;
-                dst[(i >> log2n) * pitch[cidx] + (i & (n - 1))] = (int16_t)clip16(r);
-            }
-            wave_sync();
-            continue;
-        }
-        const bool dst_tr = (tu.flags & TU_DST) != 0;
-        const int kstep = 32 >> log2n;
-        if (!dst_tr && rows == 1 && cols == 1) {
-            // DC only: both stages are constant (transMatrix[0][*] = 64)
-            const int g0 = clip16(((int64_t)64 * d[0] + 64) >> 7);
-            const int16_t r = (int16_t)clip16(((int64_t)64 * g0 + (1 << (bd2 - 1))) >> bd2);
-            for (int i = lane; i < n * n; i += kWave) dst[(i >> log2n) * pitch[cidx] + (i & (n - 1))] = r;
-            wave_sync();
-            continue;
-        }
-        // 2. vertical (column) pass over the nonzero columns:
-        //    e[y][x] = sum_{j < rows} M[j][y] d[j][x]; g = clip16((e + 64) >> 7)
-        // columns padded to a power of two: shifts instead of a division per output
-        const int lc = cols > 1 ? 32 - __builtin_clz((unsigned)(cols - 1)) : 0;
-        for (int o = lane; o < (n << lc); o += kWave) {
-            const int y = o >> lc, x = o & ((1 << lc) - 1);
-            if (x >= cols) continue;
-            int32_t s = 0;
-            if (dst_tr) {
-                for (int j = 0; j < rows; ++j) s += (int32_t)s_dst[j * 4 + y] * d[j * n + x];
-            } else {
-                for (int j = 0; j < rows; ++j) s += (int32_t)s_tm[(j * kstep) * 32 + y] * d[j * n + x];
-            }
-            g[y * n + x] = (int16_t)clip16(((int64_t)s + 64) >> 7);
-        }
-        wave_sync();
-        // 3. horizontal (row) pass: r[y][x] = sum_{j < cols} M[j][x] g[y][j]; (r + rnd) >> (20 - bitDepth)
-        //    (|g| <= 2^15 after clipping and |M| <= 90, so |sum| < 32 * 90 * 2^15 < 2^31: 32-bit)
-        for (int o = lane; o < n * n; o += kWave) {
-            const int y = o >> log2n, x = o & (n - 1);
-            int32_t s = 0;
-            if (dst_tr) {
-                for (int j = 0; j < cols; ++j) s += (int32_t)s_dst[j * 4 + x] * g[y * n + j];
-            } else {
-                for (int j = 0; j < cols; ++j) s += (int32_t)s_tm[(j * kstep) * 32 + x] * g[y * n + j];
-            }
-            dst[y * pitch[cidx] + x] = (int16_t)clip16((s + (1 << (bd2 - 1))) >> bd2);
-        }
-        wave_sync();
+        const int n = 1 << tu.log2;
+        if (tu.log2 > 5 || cidx > 2 || tu.x + n > pitch[cidx] || tu.y + n > (cidx ? ch : H)) continue;
+        transform_tb(tu, coefs, sp, a.sf, XfScratch{d, g, extent[wave], s_tm, s_dst},
+                     res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x, pitch[cidx], lane);
     }
 }
 
