@@ -607,17 +607,21 @@ void emu_sao_out(const BatchArgs &a) {
     else emu_launch(k_sao_out<uint16_t>, 1, a.n_pics, 1, a, true);
 }
 #else
-// workgroups per picture of the grid-stride loop filter kernels (tuning:
-// HEIFGPU_DBK_BLOCKS / HEIFGPU_SAO_BLOCKS; fewer, longer-lived workgroups need
-// fewer dispatches beside the parse)
-static int lf_blocks(const char *var, int dflt) {
+// Workgroups per picture of the grid-stride loop filter kernels: about
+// `total` workgroups for the batch, within [lo, hi] per picture.  A full batch
+// (128 images) gets few long-lived workgroups per picture: beside the next
+// decode's parse, 2 / 4 instead of 64 / 256 took deblocking 21 -> 7.7 ms and
+// the step 85.9 -> 85.6 ms (r04 A/B); small batches keep many, for latency.
+// HEIFGPU_DBK_BLOCKS / HEIFGPU_SAO_BLOCKS force a count.
+static int lf_blocks(const char *var, int n_pics, int total, int lo, int hi) {
     const char *e = std::getenv(var);
-    const int v = e ? std::atoi(e) : dflt;
+    int v = e ? std::atoi(e) : total / (n_pics > 0 ? n_pics : 1);
+    if (!e) v = v < lo ? lo : (v > hi ? hi : v);
     return v < 1 ? 1 : (v > 1024 ? 1024 : v);
 }
 
 hipError_t launch_deblock(const BatchArgs &a, hipStream_t s) {
-    dim3 grid(lf_blocks("HEIFGPU_DBK_BLOCKS", 64), a.n_pics), block(256);
+    dim3 grid(lf_blocks("HEIFGPU_DBK_BLOCKS", a.n_pics, 8192, 2, 64), a.n_pics), block(256);
     if (a.has_assembly) {  // the assemblies' children are reconstructed: put them together first
         if (a.bytes_per_sample == 1) hipLaunchKernelGGL(k_assemble<uint8_t>, grid, block, 0, s, a);
         else hipLaunchKernelGGL(k_assemble<uint16_t>, grid, block, 0, s, a);
@@ -641,7 +645,7 @@ hipError_t launch_sao_out(const BatchArgs &a, hipStream_t s) {
         else hipLaunchKernelGGL(k_loopfilter<uint16_t>, g, b, lds, s, a);
         return hipGetLastError();
     }
-    dim3 grid(lf_blocks("HEIFGPU_SAO_BLOCKS", 256), a.n_pics), block(256);
+    dim3 grid(lf_blocks("HEIFGPU_SAO_BLOCKS", a.n_pics, 24576, 4, 256), a.n_pics), block(256);
     if (a.bytes_per_sample == 1) hipLaunchKernelGGL(k_sao_out<uint8_t>, grid, block, 0, s, a);
     else hipLaunchKernelGGL(k_sao_out<uint16_t>, grid, block, 0, s, a);
     return hipGetLastError();

@@ -114,14 +114,15 @@ def check_permuted(outs, seeds, oracle_tiles):
 
 
 @pytest.mark.parametrize("parse,geom", [
-    ("auto", {"mode": "lanes", "workgroups": 1536, "pics_per_wave": 4, "waves_per_workgroup": 1}),
+    ("auto", {"mode": "lanes", "workgroups": 2048, "pics_per_wave": 3, "waves_per_workgroup": 1}),
     ("solo", {"mode": "solo", "workgroups": 6144, "pics_per_wave": 1, "waves_per_workgroup": 16}),
     ("spread", {"mode": "spread", "workgroups": 98304, "pics_per_wave": 1, "waves_per_workgroup": 1}),
+    ("lanes4", {"mode": "lanes", "workgroups": 1536, "pics_per_wave": 4, "waves_per_workgroup": 1}),
 ])
 def test_bench_shard_every_image(H, ctx, oracle_tiles, halfmoonbay, parse, geom):
     """The headline configuration itself (bench.py, config 4 shard): 128
-    permuted 4032x3024 images = 6144 pictures.  The automatic choice packs four
-    16-row pictures per k_parse_lanes wave (1536 waves); solo runs 6144
+    permuted 4032x3024 images = 6144 pictures.  The automatic choice packs three
+    16-row pictures per k_parse_lanes wave (2048 waves, two per SIMD); solo runs 6144
     16-wave workgroups, spread 98,304 one-wave workgroups.  Every image is
     checked, decoded three times back to back (all three parse-output sets of
     the pipeline, each into its own planes)."""
@@ -129,7 +130,7 @@ def test_bench_shard_every_image(H, ctx, oracle_tiles, halfmoonbay, parse, geom)
 
     seeds = list(range(128))
     imgs = H.HeifImage.parse_many([permuted_heic(halfmoonbay, s) for s in seeds], threads=8)
-    b = ctx.prepare(imgs, parse=parse)
+    b = ctx.prepare(imgs, parse="lanes" if parse == "lanes4" else parse, pics_per_wave=4 if parse == "lanes4" else 0)
     assert b.parse_geometry() == geom
     outs = [ctx.alloc_outputs(imgs) for _ in range(3)]
     for o in outs:
