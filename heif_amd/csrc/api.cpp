@@ -163,12 +163,17 @@ struct ParseSet {
     DevBuf<uint8_t> maps;
     DevBuf<SaoParams> sao;
     DevBuf<int16_t> resid;  // k_transform -> k_intra
-    hipEvent_t parsed = nullptr, transformed = nullptr, recon_done = nullptr;
+    // spread mode: per-row WPP progress words and (streaming) TU counts, per set
+    // because k_intra_stream of this set's decode polls them while the next
+    // decode's parse already runs
+    DevBuf<uint32_t> xprog, xntu;
+    hipEvent_t parsed = nullptr, transformed = nullptr, recon_done = nullptr, progreset = nullptr;
     bool pending = false;  // recon_done recorded and not yet waited for by a parse
     ~ParseSet() {
         if (parsed) (void)hipEventDestroy(parsed);
         if (transformed) (void)hipEventDestroy(transformed);
         if (recon_done) (void)hipEventDestroy(recon_done);
+        if (progreset) (void)hipEventDestroy(progreset);
     }
 };
 
@@ -201,7 +206,7 @@ struct heifgpu_batch {
     BatchArgs args{};
     // read by k_rbsp / the parse only: a reload waits for the parses in flight
     DevBuf<uint8_t> bits, rbsp;
-    DevBuf<uint32_t> subs, rsubs, porder, xprog;
+    DevBuf<uint32_t> subs, rsubs, porder;
     DevBuf<uint8_t> xctx;
     // the sample arena: written by k_intra, which runs after every earlier
     // decode's k_sao_out on the one recon stream
@@ -563,6 +568,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].parsed, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].transformed, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].recon_done, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&b->set[k].progreset, hipEventDisableTiming));
         }
         for (DescGen &g : b->gen) HIP_TRY(hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
     }
@@ -608,7 +614,8 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
                                      hb.coef_n > b->set[0].coefs.cap || hb.map_bytes > b->set[0].maps.cap ||
                                      hb.sao_n > b->set[0].sao.cap || 2 * size_t(hb.rows) > b->set[0].row_counts.cap ||
                                      hb.pics.size() > b->set[0].status.cap || hb.pics.size() > G.sticky.cap ||
-                                     (mode == PARSE_SPREAD && (hb.rows > b->xprog.cap || hb.rows * CTX_PAD > b->xctx.cap)));
+                                     (mode == PARSE_SPREAD && (hb.rows > b->set[0].xprog.cap || hb.rows > b->set[0].xntu.cap ||
+                                                               hb.rows * CTX_PAD > b->xctx.cap)));
     if (grows) {  // reallocation: every decode of the old contents fully drained
         for (int k = 0; k < b->n_sets; ++k)
             if (b->set[k].pending) HIP_TRY(hipEventSynchronize(b->set[k].recon_done));
@@ -641,7 +648,10 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     HIP_TRY(b->recon.alloc(hb.recon_bytes));
     HIP_TRY(b->porder.alloc(order.size()));
     if (mode == PARSE_SPREAD) {  // per-row WPP progress words and context hand-off blocks
-        HIP_TRY(b->xprog.alloc(std::max<size_t>(hb.rows, 1)));
+        for (int k = 0; k < b->n_sets; ++k) {
+            HIP_TRY(b->set[k].xprog.alloc(std::max<size_t>(hb.rows, 1)));
+            HIP_TRY(b->set[k].xntu.alloc(std::max<size_t>(hb.rows, 1)));
+        }
         HIP_TRY(b->xctx.alloc(std::max<size_t>(hb.rows, 1) * CTX_PAD));
     }
     // ---- one pinned staging image of every upload, copied asynchronously
@@ -724,8 +734,10 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.solo_waves = solo_waves;
     a.lane_jobs = mode == PARSE_LANES && lanes_jobs_default() ? 1 : 0;
     a.lf_tiles = lf_tiles_for(hb.pics.data(), int(hb.pics.size()), hb.seqs.data());
-    a.xprog = mode == PARSE_SPREAD ? b->xprog.p : nullptr;
+    a.xprog = nullptr;  // (per parse set: heifgpu_batch_decode)
     a.xctx = mode == PARSE_SPREAD ? b->xctx.p : nullptr;
+    a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
+    a.xntu = nullptr;
     // rows wrap round the lanes (waves) of a picture: the WPP context staging
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
@@ -784,12 +796,18 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     a.sao = ps.sao.p;
     a.status = ps.status.p;
     a.resid = ps.resid.p;
+    if (a.parse_mode == PARSE_SPREAD) {
+        a.xprog = ps.xprog.p;
+        a.xntu = a.intra_stream ? ps.xntu.p : nullptr;
+    }
     // bring-up knob: HEIFGPU_STAGES=k launches only the first k stages (in order, on the caller's stream)
     static const int max_stages = [] {
         const char *e = std::getenv("HEIFGPU_STAGES");
         return e ? std::atoi(e) : 5;
     }();
     if (max_stages < 5) {
+        a.intra_stream = 0;  // (stages one after another: k_transform, then the plain k_intra)
+        a.xntu = nullptr;
         HIP_TRY(hipStreamSynchronize(ctx->upload));
         HIP_TRY(hipStreamSynchronize(ctx->parse));
         HIP_TRY(hipStreamSynchronize(ctx->xform));
@@ -824,22 +842,39 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), p));
     // rows a stopped substream never reaches keep zero TBs
     HIP_TRY(hipMemsetAsync(ps.row_counts.p, 0, size_t(2) * uint32_t(b->args.total_rows) * sizeof(uint32_t), p));
+    if (a.intra_stream) {
+        // k_intra_stream polls this set's progress words and TU counts from its
+        // start: cleared first (launch_parse leaves them alone in this mode)
+        HIP_TRY(hipMemsetAsync(ps.xprog.p, 0, size_t(b->args.total_rows) * sizeof(uint32_t), p));
+        HIP_TRY(hipMemsetAsync(ps.xntu.p, 0, size_t(b->args.total_rows) * sizeof(uint32_t), p));
+        HIP_TRY(hipEventRecord(ps.progreset, p));
+    }
     if (t) HIP_TRY(hipEventRecord(ev[0], p));
     HIP_TRY(launch_rbsp(a, p));
     if (t) HIP_TRY(hipEventRecord(ev[1], p));
     HIP_TRY(launch_parse(a, p));
     if (t) HIP_TRY(hipEventRecord(ev[2], p));
     HIP_TRY(hipEventRecord(ps.parsed, p));
-    // transform stream (the recon stream with two sets): this set's parse
-    hipStream_t x = b->n_sets >= 3 ? ctx->xform : r;
-    HIP_TRY(hipStreamWaitEvent(x, ps.parsed, 0));
-    if (t) HIP_TRY(hipEventRecord(ev[3], x));
-    HIP_TRY(launch_transform(a, x));
-    if (t) HIP_TRY(hipEventRecord(ev[4], x));
-    HIP_TRY(hipEventRecord(ps.transformed, x));
-    // recon stream: this set's transform, and the caller's prior work before the planes are written
     HIP_TRY(hipEventRecord(ctx->fork, s));
-    HIP_TRY(hipStreamWaitEvent(r, ps.transformed, 0));
+    if (a.intra_stream) {
+        // streaming (small batches): no k_transform; the
+        // reconstruction starts beside this decode's parse and trails it
+        HIP_TRY(hipStreamWaitEvent(r, ps.progreset, 0));
+        if (t) {
+            HIP_TRY(hipEventRecord(ev[3], r));
+            HIP_TRY(hipEventRecord(ev[4], r));
+        }
+    } else {
+        // transform stream (the recon stream with two sets): this set's parse
+        hipStream_t x = b->n_sets >= 3 ? ctx->xform : r;
+        HIP_TRY(hipStreamWaitEvent(x, ps.parsed, 0));
+        if (t) HIP_TRY(hipEventRecord(ev[3], x));
+        HIP_TRY(launch_transform(a, x));
+        if (t) HIP_TRY(hipEventRecord(ev[4], x));
+        HIP_TRY(hipEventRecord(ps.transformed, x));
+        // recon stream: this set's transform, and the caller's prior work before the planes are written
+        HIP_TRY(hipStreamWaitEvent(r, ps.transformed, 0));
+    }
     if (t) HIP_TRY(hipEventRecord(ev[5], r));
     HIP_TRY(launch_intra(a, r));
     if (t) HIP_TRY(hipEventRecord(ev[6], r));

@@ -79,7 +79,7 @@ int main(int argc, char **argv) {
     else
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0,
                                         order, nullptr, mode == PARSE_LANES && lanes_jobs_default());
-    std::vector<uint32_t> xprog(hb.rows + 1);
+    std::vector<uint32_t> xprog(hb.rows + 1), xntu(hb.rows + 1, 0);
     std::vector<uint8_t> xctx((hb.rows + 1) * size_t(CTX_PAD));
     a.parse_order = order.data();
     a.n_slots = int(order.size());
@@ -107,6 +107,8 @@ int main(int argc, char **argv) {
     a.lf_tiles = lf_tiles_for(hb.pics.data(), int(hb.pics.size()), hb.seqs.data());
     a.xprog = xprog.data();
     a.xctx = xctx.data();
+    a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
+    a.xntu = a.intra_stream ? xntu.data() : nullptr;
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);
@@ -141,7 +143,7 @@ int main(int argc, char **argv) {
     }
     printf("parse mode: %s\n", mode == PARSE_SOLO ? "solo" : mode == PARSE_SPREAD ? "spread" : "lanes");
     printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);
-    if (stages >= 2) emu_transform(a);
+    if (stages >= 2 && !a.intra_stream) emu_transform(a);  // (streaming: k_intra_stream transforms each TB)
     if (stages >= 3) emu_intra(a);
     if (stages >= 4) emu_deblock(a);
     if (stages >= 5) {

@@ -21,6 +21,7 @@
 // filtering, prediction and residual add run one sample per lane — and the
 // finished CTU is written to the picture once.
 #include "kernels.hpp"
+#include "xform.hpp"
 
 namespace hg {
 
@@ -140,7 +141,9 @@ using Quad = typename QuadT<Pel>::type;
 template <typename Pel>
 struct Win {
     Pel *cur, *left, *above;
-    const int16_t *res;  // the component's residual plane (k_transform), pitch = plane width
+    const int16_t *res;  // the component's residual plane (k_transform), pitch = plane width, or in
+                         // streaming mode the TB's residual in LDS, offset so res[y * PW + x] still reads it
+    int rp;              // residual pitch (the plane width; streaming mode: the TB width)
     int csx, csy;        // CTB width, height in component samples (4:2:2 chroma: csy = 2 csx)
     int cx0, cy0;        // CTB origin in component samples
     // a decoded neighbour (xn, yn) in picture coordinates; only called for
@@ -169,7 +172,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     const int zc = zidx(((x0 << subx) - bx0) >> 2, ((y0 << suby) - by0) >> 2);
     // residual of a 4x4 / 8x8 TB (one sample per lane): loaded now, used after
     // the neighbour and filter phases, so the load latency hides behind them
-    const int r0 = (cbf && n <= 8 && lane < n * n) ? w.res[(size_t)(y0 + (lane >> log2n)) * PW + x0 + (lane & (n - 1))] : 0;
+    const int r0 = (cbf && n <= 8 && lane < n * n) ? w.res[(ptrdiff_t)(y0 + (lane >> log2n)) * w.rp + x0 + (lane & (n - 1))] : 0;
     // 1. gather neighbours in search order (8.4.4.2.2): s < 2n left column bottom-up,
     //    s == 2n corner, s > 2n top row left-to-right
 #if defined(HG_HOST_EMU)
@@ -378,7 +381,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         }
         const int li = (ly0 + y) * w.csx + lx0 + x;
         if (tu.flags & TU_PCM) pv = 0;  // the residual is the PCM sample itself
-        if (cbf) pv += (n <= 8 && o == lane) ? r0 : w.res[(size_t)(y0 + y) * PW + x0 + x];
+        if (cbf) pv += (n <= 8 && o == lane) ? r0 : w.res[(ptrdiff_t)(y0 + y) * w.rp + x0 + x];
         pv = min(max(pv, 0), maxv);
         w.cur[li] = (Pel)pv;
     }
@@ -409,6 +412,7 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     w.left = h ? wr.left : wb.left;
     w.above = h ? wr.above : wb.above;
     w.res = h ? wr.res : wb.res;
+    w.rp = wb.rp;
     w.csx = wb.csx;
     w.csy = wb.csy;
     w.cx0 = wb.cx0;
@@ -420,8 +424,8 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     const int zc = zidx(((x0 << 1) - bx0) >> 2, ((y0 << 1) - by0) >> 2);
     // residuals (sample sl and sl + 32 of this half), used after the neighbour phase
     int r0 = 0, r1 = 0;
-    if (cbf && sl < n * n) r0 = w.res[(size_t)(y0 + (sl >> log2n)) * PW + x0 + (sl & (n - 1))];
-    if (cbf && sl + 32 < n * n) r1 = w.res[(size_t)(y0 + ((sl + 32) >> log2n)) * PW + x0 + ((sl + 32) & (n - 1))];
+    if (cbf && sl < n * n) r0 = w.res[(ptrdiff_t)(y0 + (sl >> log2n)) * w.rp + x0 + (sl & (n - 1))];
+    if (cbf && sl + 32 < n * n) r1 = w.res[(ptrdiff_t)(y0 + ((sl + 32) >> log2n)) * w.rp + x0 + ((sl + 32) & (n - 1))];
     int16_t *left = L->left + 33 * h, *top = L->top + 33 * h;
     // 1. neighbours in search order (8.4.4.2.2), chunk k = search positions sl + 32 k
     // (two named registers, not arrays: indexed by a runtime chunk they went to scratch)
@@ -539,13 +543,18 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 #endif
 // CF: the batch's chroma_format_idc (a compile-time constant: the 4:2:0 build
 // carries no per-format arithmetic)
-template <typename Pel, int CF>
-__global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArgs a) {
-#if defined(HG_HOST_EMU)
-    unsigned char *smem = g_emu.smem;
-#else
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-#endif
+// LDS of k_intra's streaming mode beyond the windows: the transform tables
+// (workgroup) and per wave the transform tiles (transform_tb, xform.hpp)
+constexpr size_t kXfTablesBytes = 1088, kXfWaveBytes = 2 * 32 * 32 * sizeof(int16_t) + 16;
+
+// Stream: k_intra_stream, launched beside the spread parse of the same decode:
+// each row's TU records are consumed as the parse publishes them (agent-scope
+// per-row TU counts behind its progress words) and every coded TB is
+// transformed by the wave itself (transform_tb into LDS) right before its
+// prediction, so no k_transform pass and no residual planes; the
+// reconstruction trails the parse by a CTU instead of starting after it.
+template <typename Pel, int CF, bool Stream>
+__device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs &a, unsigned char *smem) {
     const int nw = (int)HG_UNI(blockDim.x >> 6);
     const int pic = a.pic0 + blockIdx.x;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -567,6 +576,15 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
     const WinLayout lay = win_layout(log2ctb, chroma, (int)sizeof(Pel));
     uint32_t *progress = reinterpret_cast<uint32_t *>(smem);  // [nw], 64 B reserved
     unsigned char *blk = smem + 64 + (size_t)wave * lay.bytes;
+    XfScratch X{};
+    if constexpr (Stream) {
+        unsigned char *tab = smem + 64 + (size_t)nw * lay.bytes;
+        unsigned char *xw = tab + kXfTablesBytes + (size_t)wave * kXfWaveBytes;
+        X = XfScratch{reinterpret_cast<int16_t *>(xw), reinterpret_cast<int16_t *>(xw + 2048),
+                      reinterpret_cast<int32_t *>(xw + 4096), reinterpret_cast<int8_t *>(tab),
+                      reinterpret_cast<int8_t *>(tab + 1024)};
+        xf_tables(reinterpret_cast<int8_t *>(tab), reinterpret_cast<int8_t *>(tab + 1024), lane);
+    }
     IntraScratch *S = reinterpret_cast<IntraScratch *>(blk);
     Win<Pel> win[3];
     for (int k = 0; k < 3; ++k) {
@@ -574,6 +592,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
         win[k].left = reinterpret_cast<Pel *>(blk + lay.left[k]);
         win[k].above = reinterpret_cast<Pel *>(blk + lay.above[k]);
         win[k].res = resp[k];
+        win[k].rp = k ? cw : W;
         win[k].csx = lay.csx[k];
         win[k].csy = lay.csy[k];
     }
@@ -587,25 +606,66 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
     const int cls = split ? (wave & 1) : 0, rw = split ? wave >> 1 : wave, nrw = split ? nw >> 1 : nw;
     const int k0 = split && cls ? 1 : 0, k1 = split && !cls ? 1 : ncomp;  // this wave's components
     const int prev_wave = split ? ((rw + nrw - 1) % nrw) * 2 + cls : (wave + nw - 1) % nw;
+    const bool wpp = (sp.flags & SP_WPP) != 0;
     for (int r = rw; r < hctb; r += nrw) {
-        const uint32_t ntu = a.row_counts[2 * (pd.row_off + r)];
+        // streaming: TUs [0, ntu) of the row are known written; `done` once the parse finished the row
+        uint32_t ntu = Stream ? 0u : a.row_counts[2 * (pd.row_off + r)];
+        bool row_done = !Stream;
         const TuRec *tus = a.tus + pd.tu_off + (uint64_t)r * pd.tu_cap_row;
+        const CoefSrc<Stream> coefs{a.coefs + pd.coef_off + (uint64_t)r * pd.coef_cap_row};
         int cur = -1;
 #if !defined(HG_HOST_EMU)
         uint4 tblk = make_uint4(0, 0, 0, 0);  // lane l: TuRec t0 + l (one coalesced load per 64 TBs)
         uint32_t t0 = 0;
 #endif
-        for (uint32_t t = 0; t <= ntu; ++t) {
+        for (uint32_t t = 0;; ++t) {
+            bool reload = false;
+            if constexpr (Stream) {
+                if (t >= ntu && !row_done) {
+                    // wait until the parse has published TU t of this row or finished the row
+                    const uint32_t *pw = a.xprog + pd.row_off + (wpp ? r : 0);
+                    const uint32_t *nw_ = a.xntu + pd.row_off + r;
+                    const uint32_t fin = (uint32_t)(r + 1) * (uint32_t)wctb;
+                    for (uint32_t spin = 0;; ++spin) {
+                        const uint32_t n_ = (uint32_t)HG_UNI(hg_load_agent(nw_));
+                        if (n_ > t) {
+                            ntu = n_;
+                            break;
+                        }
+                        if ((uint32_t)HG_UNI(hg_load_agent(pw)) >= fin) {  // row finished (or stopped: kProgDone)
+                            ntu = (uint32_t)HG_UNI(hg_load_agent(nw_));
+                            row_done = true;
+                            break;
+                        }
+                        if (spin > (1u << 26)) {  // bounded: never hang the device
+                            if (lane == 0) atomicOr(&a.status[pic], ST_SUBSTREAM_END);
+                            row_done = true;
+                            break;
+                        }
+                        HG_SLEEP();
+                    }
+                    reload = true;
+                }
+            }
+            if (t > ntu || (t == ntu && !row_done)) break;  // (stalled: the status says so)
             TuRec tu{};
             int c = wctb;  // sentinel after the last TB: finish the open CTU
             if (t < ntu) {
 #if defined(HG_HOST_EMU)
                 tu = tus[t];
+                (void)reload;
 #else
-                if ((t & 63u) == 0) {
-                    t0 = t;
-                    const uint32_t i = t + (uint32_t)lane;
-                    tblk = i < ntu ? *reinterpret_cast<const uint4 *>(tus + i) : make_uint4(0, 0, 0, 0);
+                if ((t & 63u) == 0 || reload) {
+                    t0 = t & ~63u;
+                    const uint32_t i = t0 + (uint32_t)lane;
+                    if constexpr (Stream) {
+                        const uint64_t *q = reinterpret_cast<const uint64_t *>(tus + i);
+                        const uint64_t lo = i < ntu ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                        const uint64_t hi = i < ntu ? __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                        tblk = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+                    } else {
+                        tblk = i < ntu ? *reinterpret_cast<const uint4 *>(tus + i) : make_uint4(0, 0, 0, 0);
+                    }
                 }
                 const int sel = (int)(t - t0);
                 const uint4 r = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)tblk.x, sel),
@@ -685,6 +745,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
             w.left = cidx == 0 ? win[0].left : (cidx == 1 ? win[1].left : win[2].left);
             w.above = cidx == 0 ? win[0].above : (cidx == 1 ? win[1].above : win[2].above);
             w.res = cidx == 0 ? win[0].res : (cidx == 1 ? win[1].res : win[2].res);
+            w.rp = cidx == 0 ? W : cw;
             w.csx = cidx == 0 ? win[0].csx : (cidx == 1 ? win[1].csx : win[2].csx);
             w.csy = cidx == 0 ? win[0].csy : (cidx == 1 ? win[1].csy : win[2].csy);
             w.cx0 = cidx == 0 ? win[0].cx0 : (cidx == 1 ? win[1].cx0 : win[2].cx0);
@@ -696,10 +757,20 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
                 tu.x < w.cx0 || tu.y < w.cy0 || tu.x + (1 << tu.log2) > w.cx0 + w.csx ||
                 tu.y + (1 << tu.log2) > w.cy0 + w.csy)
                 continue;
+            if constexpr (Stream) {
+                // the TB's residual, transformed by this wave into LDS; predict_tb reads it
+                // through w.res with the plane pitch (offset so that (y0, x0) lands on X.d[0])
+                if (tu.flags & TU_CBF) {
+                    const int n = 1 << tu.log2;
+                    transform_tb<true>(tu, coefs, sp, a.sf, X, X.d, n, lane);
+                    w.res = X.d - ((ptrdiff_t)tu.y * n + tu.x);
+                    w.rp = n;
+                }
+            }
 #if !defined(HG_HOST_EMU) && !defined(HG_INTRA_NO_PAIR)
             // a 4x4 / 8x8 Cb TB followed by its Cr TB (same TU; the next record of this 64-record block):
             // both in one pass
-            if (cidx == 1 && chroma == 1 && tu.log2 <= 3 && t + 1 < ntu && ((t + 1) & 63u) != 0) {
+            if (!Stream && cidx == 1 && chroma == 1 && tu.log2 <= 3 && t + 1 < ntu && ((t + 1) & 63u) != 0) {
                 const int sel = (int)(t + 1 - t0);
                 const uint4 r = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)tblk.x, sel),
                                            (uint32_t)__builtin_amdgcn_readlane((int)tblk.y, sel),
@@ -720,6 +791,27 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
         HG_FENCE_REL();
         hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
     }
+}
+
+template <typename Pel, int CF>
+__global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArgs a) {
+#if defined(HG_HOST_EMU)
+    unsigned char *smem = g_emu.smem;
+#else
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#endif
+    intra_body<Pel, CF, false>(a, smem);
+}
+
+// (no waves-per-EU cap: the transform's registers come on top of the prediction's)
+template <typename Pel, int CF>
+__global__ void __launch_bounds__(kMaxWaves * 64) k_intra_stream(BatchArgs a) {
+#if defined(HG_HOST_EMU)
+    unsigned char *smem = g_emu.smem;
+#else
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#endif
+    intra_body<Pel, CF, true>(a, smem);
 }
 
 // luma / chroma wave pairs (k_intra's split): for batches of few pictures,
@@ -762,20 +854,35 @@ static int intra_launch_waves(const BatchArgs &a) {
 }
 
 static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
-    return 64 + (size_t)nw * win_layout(a.max_log2ctb, a.chroma_format, a.bytes_per_sample).bytes;
+    size_t b = 64 + (size_t)nw * win_layout(a.max_log2ctb, a.chroma_format, a.bytes_per_sample).bytes;
+    if (a.intra_stream) b += kXfTablesBytes + (size_t)nw * kXfWaveBytes;
+    return b;
+}
+
+// waves of a launch, the streaming mode's extra LDS included (pairs stay pairs)
+static int intra_fit_waves(const BatchArgs &a, int nw) {
+    while (nw > 1 && intra_lds_bytes(a, nw) > kIntraLdsBudget) nw -= a.intra_split ? 2 : 1;
+    return nw < 1 ? 1 : nw;
 }
 
 #if defined(HG_HOST_EMU)
 template <int CF>
 static void emu_intra_cf(const BatchArgs &a, int nw) {
-    if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t, CF>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
-    else emu_launch(k_intra<uint16_t, CF>, a.n_pics, 1, nw, a, false, intra_lds_bytes(a, nw));
+    const size_t lds = intra_lds_bytes(a, nw);
+    if (a.intra_stream) {
+        if (a.bytes_per_sample == 1) emu_launch(k_intra_stream<uint8_t, CF>, a.n_pics, 1, nw, a, false, lds);
+        else emu_launch(k_intra_stream<uint16_t, CF>, a.n_pics, 1, nw, a, false, lds);
+        return;
+    }
+    if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t, CF>, a.n_pics, 1, nw, a, false, lds);
+    else emu_launch(k_intra<uint16_t, CF>, a.n_pics, 1, nw, a, false, lds);
 }
 void emu_intra(const BatchArgs &a0) {
     BatchArgs a = a0;
     int nw = intra_launch_waves(a);
     a.intra_split = intra_split_for(a, nw) ? 1 : 0;
     if (a.intra_split) nw = intra_split_waves(a, nw);
+    nw = intra_fit_waves(a, nw);
     switch (a.chroma_format) {
     case 0: emu_intra_cf<0>(a, nw); break;
     case 2: emu_intra_cf<2>(a, nw); break;
@@ -786,6 +893,13 @@ void emu_intra(const BatchArgs &a0) {
 #else
 template <int CF>
 static void launch_intra_cf(const BatchArgs &a, int nw, size_t lds, hipStream_t s) {
+    if (a.intra_stream) {
+        if (a.bytes_per_sample == 1)
+            hipLaunchKernelGGL((k_intra_stream<uint8_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_intra_stream<uint16_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
+        return;
+    }
     if (a.bytes_per_sample == 1)
         hipLaunchKernelGGL((k_intra<uint8_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
     else
@@ -796,6 +910,7 @@ hipError_t launch_intra(const BatchArgs &a0, hipStream_t s) {
     int nw = intra_launch_waves(a);
     a.intra_split = intra_split_for(a, nw) ? 1 : 0;
     if (a.intra_split) nw = intra_split_waves(a, nw);
+    nw = intra_fit_waves(a, nw);
     const size_t lds = intra_lds_bytes(a, nw);
     switch (a.chroma_format) {
     case 0: launch_intra_cf<0>(a, nw, lds, s); break;
@@ -806,5 +921,14 @@ hipError_t launch_intra(const BatchArgs &a0, hipStream_t s) {
     return hipGetLastError();
 }
 #endif
+
+// Streaming reconstruction (k_intra_stream beside the spread parse) for the
+// small batches where everything it and the parse need is resident at once
+// (up to 96 pictures: two 4032x3024 images); HEIFGPU_STREAM=0 turns it off.
+bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly) {
+    const char *e = std::getenv("HEIFGPU_STREAM");
+    if (e && std::atoi(e) == 0) return false;
+    return parse_mode == PARSE_SPREAD && !has_assembly && n_pics > 0 && n_pics <= kStreamMaxPics;
+}
 
 }  // namespace hg

@@ -60,6 +60,8 @@ struct BatchArgs {
     int lf_tiles;              // k_loopfilter workgroups per picture (lf_tiles_for: the largest picture, assemblies included)
     uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
+    uint32_t *xntu;            // streaming mode: per-row TU records written so far (null otherwise)
+    int intra_stream;          // k_intra transforms and reconstructs each row behind the spread parse (same launch window)
     int has_assembly;          // some picture is PD_ASSEMBLY (launch_deblock runs k_assemble first)
     int intra_split;           // k_intra: luma and chroma on separate waves (set by launch_intra)
 };
@@ -112,6 +114,9 @@ constexpr int kSoloMaxWaves = 16;
 // cost (optional): per-picture parse cost to deal by (default: payload bytes)
 int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
                       const float *cost = nullptr, bool jobs = false);
+// k_intra_stream (reconstruction behind the spread parse, k_transform folded in) for this batch
+constexpr int kStreamMaxPics = 96;
+bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly);
 // k_loopfilter tiles of the largest picture of a batch (assembly pictures included)
 int lf_tiles_for(const PicDesc *pics, int n, const SeqParams *seqs);
 // lanes mode runs k_parse_jobs (substreams from a per-wave job list) with HEIFGPU_LANES_JOBS=1

@@ -431,6 +431,7 @@ template <class T>
 inline void store_agent(T *p, T v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
 inline uint32_t load_agent(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 inline void stores_done() { std::atomic_thread_fence(std::memory_order_release); }
+inline void agent_release() { std::atomic_thread_fence(std::memory_order_release); }
 #else
 template <class T>
 __device__ __forceinline__ void store_agent(T *p, T v) {
@@ -441,6 +442,13 @@ __device__ __forceinline__ uint32_t load_agent(const uint32_t *p) {
 }
 // s_waitcnt vmcnt(0): every store of this wave has completed
 __device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0x0f70); }
+// this wave's plain stores (TU and coefficient records) written back to where
+// another XCD's agent-scope loads see them (buffer_wbl2); the explicit wait
+// after it keeps a later flag store from overtaking the write-back
+__device__ __forceinline__ void agent_release() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+}
 #endif
 
 HG_HD inline uint8_t load_byte_coherent(const uint8_t *p) {
@@ -1863,6 +1871,10 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     ++L.c;
     const uint32_t pv = (L.fl & F_STOP) ? kProgDone : (uint32_t)L.row * (uint32_t)P.wctb + (uint32_t)L.c;
     if constexpr (EG::kSpread) {
+        if (E.a->xntu) {  // k_intra's streaming mode reads this row's records as they appear
+            agent_release();
+            store_agent(E.a->xntu + P.row_off + L.row, L.ntu);
+        }
         stores_done();
         store_agent(prog_word(E, P, L.row), pv);
     } else {
@@ -2357,7 +2369,7 @@ void emu_parse_solo(const BatchArgs &a) {
         }
         const uint32_t lim = (P.bits_end + 64u) & ~3u;
         if (Spread)
-            for (int w = 0; w < NW; ++w) a.xprog[P.row_off + (uint32_t)w < (uint32_t)a.total_rows ? P.row_off + w : 0] = 0;
+            for (int w = 0; w < P.R; ++w) a.xprog[P.row_off + (uint32_t)w] = 0;  // this picture's words only
         Env E = Spread ? Env{&a, lds.data(), a.xprog + P.row_off, a.xctx + (size_t)P.row_off * CTX_PAD, 0}
                        : Env{&a, lds.data(), prog, wctx.data(), 0};
         for (;;) {
@@ -2756,9 +2768,12 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
     if (a.parse_mode == PARSE_SPREAD) {
         if (!a.parse_order || !a.xprog || !a.xctx) return hipErrorInvalidValue;
         if (a.n_slots <= 0) return hipSuccess;
-        // progress words start at 0 for every decode
-        hipError_t e = hipMemsetAsync(a.xprog, 0, (size_t)a.total_rows * sizeof(uint32_t), s);
-        if (e != hipSuccess) return e;
+        // progress words start at 0 for every decode (streaming mode: the caller
+        // cleared them, and the TU counts, before k_intra started polling them)
+        if (!a.intra_stream) {
+            hipError_t e = hipMemsetAsync(a.xprog, 0, (size_t)a.total_rows * sizeof(uint32_t), s);
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL(k_parse_solo<true>, dim3(a.n_slots), dim3(64), solo_lds_bytes(1, false), s, a);
         return hipGetLastError();
     }

@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint32_t ntu = a.row_counts[2 * (pd.row_off + row)];
     const TuRec *tus = a.tus + pd.tu_off + (uint64_t)row * pd.tu_cap_row;
-    const Coef *coefs = a.coefs + pd.coef_off + (uint64_t)row * pd.coef_cap_row;
+    const CoefSrc<false> coefs{a.coefs + pd.coef_off + (uint64_t)row * pd.coef_cap_row};
     const int W = sp.width, H = sp.height;
     const int cw = sp.chroma_format ? W >> chroma_sx(sp.chroma_format) : 0;
     const int ch = sp.chroma_format ? H >> chroma_sy(sp.chroma_format) : 0;
@@ -108,12 +108,12 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                 int pos, dv;
                 if (tu.flags & TU_PCM) {  // one word per sample
                     if (l16 >= (int)tu.ncoef) continue;
-                    const Coef c = coefs[tu.coef + l16];
+                    const Coef c = coefs.word(tu.coef + (uint32_t)l16);
                     pos = (int)(c & 15u);
                     dv = (int)(int16_t)(c >> 16);
                 } else {  // one sub-block record; lane l16 decodes scan position l16
                     if (tu.ncoef < 4) continue;
-                    const SbRec r = load_rec(coefs + tu.coef);
+                    const SbRec r = load_rec(coefs, tu.coef);
                     if (!((r.sig() >> l16) & 1u)) continue;
                     const int above = l16 < 15 ? __builtin_popcountll(r.esc() >> (4 * l16 + 4)) : 0;  // (a shift by 64 is undefined)
                     dv = r.level(l16, above, coefs);

@@ -66,6 +66,8 @@ template <class T>
 inline T hg_atomic_load(T *p) {
     return __atomic_load_n(p, __ATOMIC_ACQUIRE);
 }
+// a word another kernel of the same decode writes (agent scope on the GPU)
+inline uint32_t hg_load_agent(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 template <class T>
 inline void hg_atomic_store(T *p, T v) {
     __atomic_store_n(p, v, __ATOMIC_RELEASE);
@@ -108,6 +110,10 @@ constexpr int kWave = 64;
 template <class T>
 __device__ __forceinline__ T hg_atomic_load(T *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// a word another kernel of the same decode writes (agent scope: coherent across XCDs)
+__device__ __forceinline__ uint32_t hg_load_agent(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 template <class T>
 __device__ __forceinline__ void hg_atomic_store(T *p, T v) {

@@ -42,6 +42,20 @@ __constant__ int16_t c_level_scale[6] = {40, 45, 51, 57, 64, 72};
 
 __device__ __forceinline__ int clip16(int64_t v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : (int)v); }
 
+// A row's coefficient words.  Coherent: read with agent-scope loads, for a
+// reader that runs beside the parse writing them (k_intra's streaming mode:
+// the lines may sit stale in this XCD's L2 from an earlier decode).
+template <bool Coherent>
+struct CoefSrc {
+    const Coef *p;
+    __device__ __forceinline__ uint32_t word(uint32_t i) const {
+#if !defined(HG_HOST_EMU)
+        if constexpr (Coherent) return __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        return p[i];
+    }
+};
+
 // One sub-block record (SbRec, desc.hpp) of a TB's coefficient words.
 struct SbRec {
     uint32_t w0, w1, w2, w3;
@@ -62,19 +76,21 @@ struct SbRec {
         return (y << log2n) + x;
     }
     // the hidden sign's parity: the sum of the sub-block's levels
-    __device__ __forceinline__ int sum_abs(const Coef *row) const {
+    template <class Src>
+    __device__ __forceinline__ int sum_abs(const Src &row) const {
         const uint64_t x = nib();
         const uint64_t t = (x & 0x0f0f0f0f0f0f0f0full) + ((x >> 4) & 0x0f0f0f0f0f0f0f0full);
         int s = __builtin_popcount(sig()) + (int)((t * 0x0101010101010101ull) >> 56);
         const int ne = __builtin_popcountll(esc());
-        for (int k = 0; k < ne; ++k) s += (int)row[esc0() - (uint32_t)k] - 16;
+        for (int k = 0; k < ne; ++k) s += (int)row.word(esc0() - (uint32_t)k) - 16;
         return s;
     }
     // TransCoeffLevel at scan position nn (significant), given the number of
     // escapes at higher positions
-    __device__ __forceinline__ int level(int nn, int esc_above, const Coef *row) const {
+    template <class Src>
+    __device__ __forceinline__ int level(int nn, int esc_above, const Src &row) const {
         const int a = (int)((nib() >> (4 * nn)) & 15u);
-        const int abs_v = a < 15 ? a + 1 : (int)row[esc0() - (uint32_t)esc_above];
+        const int abs_v = a < 15 ? a + 1 : (int)row.word(esc0() - (uint32_t)esc_above);
         const uint32_t s = sig();
         bool neg;
         if (((w3 >> 8) & 1u) && nn == __builtin_ctz(s)) {
@@ -87,11 +103,19 @@ struct SbRec {
         return v < -32768 ? -32768 : (v > 32767 ? 32767 : v);
     }
 };
-__device__ __forceinline__ SbRec load_rec(const Coef *p) {
+template <bool Coherent>
+__device__ __forceinline__ SbRec load_rec(const CoefSrc<Coherent> &src, uint32_t i) {
 #if defined(HG_HOST_EMU)
+    const Coef *p = src.p + i;
     return SbRec{p[0], p[1], p[2], p[3]};
 #else
-    const uint4 v = *reinterpret_cast<const uint4 *>(p);  // one 16-byte load
+    if constexpr (Coherent) {  // two agent-scope 8-byte loads
+        const uint64_t *q = reinterpret_cast<const uint64_t *>(src.p + i);
+        const uint64_t lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return SbRec{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    }
+    const uint4 v = *reinterpret_cast<const uint4 *>(src.p + i);  // one 16-byte load
     return SbRec{v.x, v.y, v.z, v.w};
 #endif
 }
@@ -113,8 +137,11 @@ __device__ __forceinline__ void xf_tables(int8_t *s_tm, int8_t *s_dst, int lane)
 
 // Residual of coded TB `tu` into dst (row pitch `pitch` samples) by one wave.
 // The caller has checked that the TB lies inside its plane.
-__device__ __forceinline__ void transform_tb(const TuRec &tu, const Coef *coefs, const SeqParams &sp, const uint8_t *sf,
-                                             const XfScratch &X, int16_t HG_GAS *dst, int pitch, int lane) {
+// dst: the residual plane (global) or, in k_intra's streaming mode, X.d itself
+// (pitch n: the last pass no longer reads d)
+template <bool Coherent, class DstPtr>
+__device__ __forceinline__ void transform_tb(const TuRec &tu, const CoefSrc<Coherent> &coefs, const SeqParams &sp,
+                                             const uint8_t *sf, const XfScratch &X, DstPtr dst, int pitch, int lane) {
     int16_t *d = X.d, *g = X.g;
     const int8_t *s_tm = X.tm, *s_dst = X.dst;
     const bool scaling = (sp.flags & SP_SCALING_LIST) != 0;
@@ -149,13 +176,13 @@ __device__ __forceinline__ void transform_tb(const TuRec &tu, const Coef *coefs,
     };
     if (tu.flags & TU_PCM) {  // one word per sample
         for (int k = lane; k < tu.ncoef; k += kWave) {
-            const Coef c = coefs[tu.coef + k];
+            const Coef c = coefs.word(tu.coef + (uint32_t)k);
             put((int)(c & 0xffffu), (int)(int16_t)(c >> 16));
         }
     } else {  // 16 lanes per sub-block record, a scan position each (no serial loop per lane)
         const int nrec = (int)(tu.ncoef >> 2);
         for (int q = lane; q < 16 * nrec; q += kWave) {
-            const SbRec r = load_rec(coefs + tu.coef + 4 * (q >> 4));  // (16 lanes, one address)
+            const SbRec r = load_rec(coefs, tu.coef + 4u * (uint32_t)(q >> 4));  // (16 lanes, one address)
             const int nn = q & 15;
             if (!((r.sig() >> nn) & 1u)) continue;
             const int above = nn < 15 ? __builtin_popcountll(r.esc() >> (4 * nn + 4)) : 0;
