@@ -93,6 +93,9 @@ struct alignas(4) LaneLds {
 struct alignas(16) LaneLds {
 #endif
     uint8_t ctx[CTX_PAD];
+    uint8_t ipmL[16], ipmA[16];  // IntraPredModeY (4x4 units): last written per row / per column
+    uint8_t dL[8], dA[8];        // CtDepth (8x8 units)
+    int8_t qL[8], qA[8];         // QpY (8x8 units)
 #if defined(HG_LANE_LDS_ODD)
     uint8_t pad_odd[4];
 #endif
@@ -190,12 +193,6 @@ struct Lane {
     // byte i & 3 of lane i >> 2 (35 lanes), read / written with v_readlane /
     // v_writelane; the one field whose lanes differ
     uint32_t cx;
-    // neighbour state, one byte per entry in 64-bit words (registers, not LDS:
-    // the lanes' LDS blocks are what limits the parse's residency beside the
-    // reconstruction kernels): IntraPredModeY per 4x4 unit, last written per
-    // row (ipmL, 16 entries) and per column (ipmA) of the CTB; CtDepth (dL, dA)
-    // and QpY (qL, qA) per 8x8 unit (8 entries)
-    uint64_t ipmL0, ipmL1, ipmA0, ipmA1, dL, dA, qL, qA;
     uint32_t reinit;  // F_REINIT: RBSP byte (absolute) where the engine restarts after PCM samples
 #if defined(HG_PARSE_PROF_SB)
     // solo tuning build: s_memtime cycles of unit_sb's phases (header, sig loop,
@@ -817,24 +814,6 @@ HG_HD inline void update_qpy(Lane &L, const LanePic &P) {
     L.qpy_cur = ((L.qp_pred + L.cu_qp_delta_val + 52 + 2 * P.qpbdY) % (52 + P.qpbdY)) - P.qpbdY;
 }
 
-// neighbour-state bytes (Lane::ipmL0 ...)
-HG_HD inline uint32_t nb_byte(uint64_t w, int i) { return (uint32_t)(w >> (8 * (i & 7))) & 0xffu; }
-// bytes [lo, lo + cnt) of the 8 in w (lo may be negative: the word holds entries 8k..8k+7) := v
-HG_HD inline uint64_t nb_fill(uint64_t w, int lo, int cnt, uint32_t v) {
-    const int a = lo < 0 ? 0 : lo, b = lo + cnt > 8 ? 8 : lo + cnt;
-    if (a >= b) return w;
-    const uint64_t m = (b - a == 8 ? ~0ull : ((1ull << (8 * (b - a))) - 1ull)) << (8 * a);
-    return (w & ~m) | ((0x0101010101010101ull * (uint64_t)(v & 0xffu)) & m);
-}
-HG_HD inline int ipmL_get(const Lane &L, int i) { return (int)nb_byte(i < 8 ? L.ipmL0 : L.ipmL1, i); }
-HG_HD inline int ipmA_get(const Lane &L, int i) { return (int)nb_byte(i < 8 ? L.ipmA0 : L.ipmA1, i); }
-HG_HD inline void ipm_fill(Lane &L, int by, int bx, int cnt, int m) {
-    L.ipmL0 = nb_fill(L.ipmL0, by, cnt, (uint32_t)m);
-    L.ipmL1 = nb_fill(L.ipmL1, by - 8, cnt, (uint32_t)m);
-    L.ipmA0 = nb_fill(L.ipmA0, bx, cnt, (uint32_t)m);
-    L.ipmA1 = nb_fill(L.ipmA1, bx - 8, cnt, (uint32_t)m);
-}
-
 // 8.6.1 qPY_PRED of the current quantization group
 HG_HD inline void derive_qp_pred(Lane &L, const LaneLds &ld, const LanePic &P) {
     int prev;
@@ -848,16 +827,16 @@ HG_HD inline void derive_qp_pred(Lane &L, const LaneLds &ld, const LanePic &P) {
         prev = L.qp_prev_last;
     }
     const int mask = (1 << P.log2ctb) - 1;
-    const int qa = (L.qg_x & mask) ? (int)(int8_t)nb_byte(L.qL, (L.qg_y - L.ctby) >> 3) : prev;
-    const int qb = (L.qg_y & mask) ? (int)(int8_t)nb_byte(L.qA, (L.qg_x - L.ctbx) >> 3) : prev;
+    const int qa = (L.qg_x & mask) ? ld.qL[(L.qg_y - L.ctby) >> 3] : prev;
+    const int qb = (L.qg_y & mask) ? ld.qA[(L.qg_x - L.ctbx) >> 3] : prev;
     L.qp_pred = (qa + qb + 1) >> 1;
 }
 
 // 8.4.2 luma intra prediction mode of the PB at (xPb, yPb)
 HG_HD inline int derive_luma_mode(const Lane &L, const LaneLds &ld, int xPb, int yPb, int prev, int mpm_idx,
                                   int rem) {
-    const int ca = xPb <= 0 ? 1 : ipmL_get(L, (yPb - L.ctby) >> 2);
-    const int cb = (yPb - 1 < L.ctby) ? 1 : ipmA_get(L, (xPb - L.ctbx) >> 2);  // above CTB (or picture edge) → DC
+    const int ca = xPb <= 0 ? 1 : ld.ipmL[(yPb - L.ctby) >> 2];
+    const int cb = (yPb - 1 < L.ctby) ? 1 : ld.ipmA[(xPb - L.ctbx) >> 2];  // above CTB (or picture edge) → DC
     int l0, l1, l2;
     if (ca == cb) {
         if (ca < 2) {
@@ -1150,11 +1129,11 @@ HG_HD inline void unit_cqt(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         bool split;
         if (L.qx + n <= P.W && L.qy + n <= P.H && L.ql > P.minCb) {
             int cond = 0;  // 9.3.4.2.2 ctxInc of split_cu_flag
-            if (L.qx > 0 && (int)nb_byte(L.dL, (L.qy - L.ctby) >> 3) > L.qd) ++cond;
+            if (L.qx > 0 && ld.dL[(L.qy - L.ctby) >> 3] > L.qd) ++cond;
             if (L.qy > 0) {
                 const int ad = (L.qy - 1 < L.ctby)
                                    ? load_byte_coherent(P.gdepth + (size_t)(L.row - 1) * P.w8 + (L.qx >> 3))
-                                   : (int)nb_byte(L.dA, (L.qx - L.ctbx) >> 3);
+                                   : ld.dA[(L.qx - L.ctbx) >> 3];
                 if (ad > L.qd) ++cond;
             }
             split = dec(L, G, CTX_SPLIT_CU + cond) != 0;
@@ -1190,7 +1169,11 @@ template <class EG>
 HG_HD inline void pcm_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     const int n = 1 << L.ql;
     {
-        ipm_fill(L, (L.qy - L.ctby) >> 2, (L.qx - L.ctbx) >> 2, n >> 2, 1);
+        const int nb = n >> 2, by = (L.qy - L.ctby) >> 2, bx = (L.qx - L.ctbx) >> 2;
+        for (int k = 0; k < nb; ++k) {
+            ld.ipmL[by + k] = 1;
+            ld.ipmA[bx + k] = 1;
+        }
     }
     // bits consumed so far: 8 * end - budget - k (absolute RBSP bit position)
     uint32_t bit = (uint32_t)(8 * (int32_t)P.bits_end - L.budget - L.k + 7) & ~7u;
@@ -1260,8 +1243,11 @@ HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     const bool pcm = !nxn && (P.flags & SP_PCM) && L.ql >= P.pcmMin && L.ql <= P.pcmMax && term(L, G);
     {  // CtDepth of the CU
         const int nd = 1 << (L.ql - 3);
-        L.dL = nb_fill(L.dL, (L.qy - L.ctby) >> 3, nd, (uint32_t)L.qd);
-        L.dA = nb_fill(L.dA, (L.qx - L.ctbx) >> 3, nd, (uint32_t)L.qd);
+        const int dy = (L.qy - L.ctby) >> 3, dx = (L.qx - L.ctbx) >> 3;
+        for (int k = 0; k < nd; ++k) {
+            ld.dL[dy + k] = (uint8_t)L.qd;
+            ld.dA[dx + k] = (uint8_t)L.qd;
+        }
     }
     if (pcm) {
         pcm_cu(L, ld, P, G);
@@ -1280,7 +1266,11 @@ HG_HD inline void unit_cu(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         const int xPb = L.qx + (i & 1) * pb, yPb = L.qy + (i >> 1) * pb;
         const int m = derive_luma_mode(L, ld, xPb, yPb, p, mpm, rem);
         modes |= m << (8 * i);
-        ipm_fill(L, (yPb - L.ctby) >> 2, (xPb - L.ctbx) >> 2, pb >> 2, m);
+        const int nb = pb >> 2, by = (yPb - L.ctby) >> 2, bx = (xPb - L.ctbx) >> 2;
+        for (int k = 0; k < nb; ++k) {
+            ld.ipmL[by + k] = (uint8_t)m;
+            ld.ipmA[bx + k] = (uint8_t)m;
+        }
     }
     L.cu_modes = modes;
     if (P.chroma) {  // intra_chroma_pred_mode: per PB with 4:4:4, else per CU; 8.4.3
@@ -1449,8 +1439,11 @@ HG_HD inline void tb_done(Lane &L, LaneLds &ld, LanePic &P) {
 HG_HD inline void cu_done(Lane &L, LaneLds &ld, LanePic &P) {
     {
         const int n = 1 << L.ql, nd = n >> 3;
-        L.qL = nb_fill(L.qL, (L.qy - L.ctby) >> 3, nd, (uint32_t)(uint8_t)(int8_t)L.qpy_cur);
-        L.qA = nb_fill(L.qA, (L.qx - L.ctbx) >> 3, nd, (uint32_t)(uint8_t)(int8_t)L.qpy_cur);
+        const int dy = (L.qy - L.ctby) >> 3, dx = (L.qx - L.ctbx) >> 3;
+        for (int k = 0; k < nd; ++k) {
+            ld.qL[dy + k] = (int8_t)L.qpy_cur;
+            ld.qA[dx + k] = (int8_t)L.qpy_cur;
+        }
         const int nb = n >> 2, gx0 = L.qx >> 2, gy0 = L.qy >> 2;
         const int wx = gx0 + nb <= P.w4 ? nb : P.w4 - gx0, hy = gy0 + nb <= P.h4 ? nb : P.h4 - gy0;
         for (int y = 0; y < hy; ++y) {
@@ -1855,8 +1848,8 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
         const int nb8 = 1 << (P.log2ctb - 3), col0 = L.ctbx >> 3;
         uint8_t *line = P.gdepth + (size_t)L.row * P.w8;
         for (int k = 0; k < nb8 && col0 + k < P.w8; ++k) {
-            if constexpr (EG::kSpread) store_agent(line + col0 + k, (uint8_t)nb_byte(L.dA, k));
-            else line[col0 + k] = (uint8_t)nb_byte(L.dA, k);
+            if constexpr (EG::kSpread) store_agent(line + col0 + k, ld.dA[k]);
+            else line[col0 + k] = ld.dA[k];
         }
     }
     const bool last_in_pic = L.row == P.hctb - 1 && L.c == P.wctb - 1;
@@ -1904,10 +1897,8 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
 // only lanes in that unit).  One unit kind per pass keeps the dispatch a
 // uniform branch: a divergent switch over the units would linearise them, and
 // every L field a unit updates would then need a register per unit.
-// (always inlined: a call would pass Lane by reference and put it in scratch memory)
 template <class EG>
-HG_HD __attribute__((always_inline)) inline void run_unit(int kind, Lane &L, LaneLds &ld, LanePic &P, const Env &E,
-                                                          const EG &G) {
+HG_HD inline void run_unit(int kind, Lane &L, LaneLds &ld, LanePic &P, const Env &E, const EG &G) {
     if constexpr (EG::kSolo) {
         if (L.fl & F_REINIT) {  // after PCM samples: the driver has moved the window to L.reinit
             engine_init(L, G, L.reinit, P.bits_end);
@@ -2001,7 +1992,6 @@ HG_HD inline void lane_start(Lane &L, const LanePic &P, LaneLds &ld, int row) {
     L.row = row;
     L.c = 0;
     L.qp_prev_last = P.sliceQp;
-    L.ipmL0 = L.ipmL1 = L.ipmA0 = L.ipmA1 = L.dL = L.dA = L.qL = L.qA = 0;
     row_outputs(L, P);
     L.st = U_CTU;
 }
