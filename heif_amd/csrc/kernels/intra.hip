@@ -141,9 +141,10 @@ using Quad = typename QuadT<Pel>::type;
 template <typename Pel>
 struct Win {
     Pel *cur, *left, *above;
-    const int16_t *res;  // the component's residual plane (k_transform), pitch = plane width, or in
-                         // streaming mode the TB's residual in LDS, offset so res[y * PW + x] still reads it
+    const int16_t *res;  // the component's residual plane (k_transform), or in streaming mode the
+                         // current TB's residual in LDS
     int rp;              // residual pitch (the plane width; streaming mode: the TB width)
+    int rx0, ry0;        // the sample res[0] holds (plane: 0, 0; streaming: the TB's origin)
     int csx, csy;        // CTB width, height in component samples (4:2:2 chroma: csy = 2 csx)
     int cx0, cy0;        // CTB origin in component samples
     // a decoded neighbour (xn, yn) in picture coordinates; only called for
@@ -172,7 +173,10 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     const int zc = zidx(((x0 << subx) - bx0) >> 2, ((y0 << suby) - by0) >> 2);
     // residual of a 4x4 / 8x8 TB (one sample per lane): loaded now, used after
     // the neighbour and filter phases, so the load latency hides behind them
-    const int r0 = (cbf && n <= 8 && lane < n * n) ? w.res[(ptrdiff_t)(y0 + (lane >> log2n)) * w.rp + x0 + (lane & (n - 1))] : 0;
+    // (the TB's first residual, formed only where it is in bounds: a pointer moved
+    // before an LDS buffer is out of the object, and its flat address lost the aperture on the GPU)
+    const int16_t *rt = cbf ? w.res + ((ptrdiff_t)(y0 - w.ry0) * w.rp + (x0 - w.rx0)) : w.res;
+    const int r0 = (cbf && n <= 8 && lane < n * n) ? rt[(lane >> log2n) * w.rp + (lane & (n - 1))] : 0;
     // 1. gather neighbours in search order (8.4.4.2.2): s < 2n left column bottom-up,
     //    s == 2n corner, s > 2n top row left-to-right
 #if defined(HG_HOST_EMU)
@@ -381,7 +385,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         }
         const int li = (ly0 + y) * w.csx + lx0 + x;
         if (tu.flags & TU_PCM) pv = 0;  // the residual is the PCM sample itself
-        if (cbf) pv += (n <= 8 && o == lane) ? r0 : w.res[(ptrdiff_t)(y0 + y) * w.rp + x0 + x];
+        if (cbf) pv += (n <= 8 && o == lane) ? r0 : rt[y * w.rp + x];
         pv = min(max(pv, 0), maxv);
         w.cur[li] = (Pel)pv;
     }
@@ -593,6 +597,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
         win[k].above = reinterpret_cast<Pel *>(blk + lay.above[k]);
         win[k].res = resp[k];
         win[k].rp = k ? cw : W;
+        win[k].rx0 = win[k].ry0 = 0;
         win[k].csx = lay.csx[k];
         win[k].csy = lay.csy[k];
     }
@@ -746,6 +751,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
             w.above = cidx == 0 ? win[0].above : (cidx == 1 ? win[1].above : win[2].above);
             w.res = cidx == 0 ? win[0].res : (cidx == 1 ? win[1].res : win[2].res);
             w.rp = cidx == 0 ? W : cw;
+            w.rx0 = w.ry0 = 0;
             w.csx = cidx == 0 ? win[0].csx : (cidx == 1 ? win[1].csx : win[2].csx);
             w.csy = cidx == 0 ? win[0].csy : (cidx == 1 ? win[1].csy : win[2].csy);
             w.cx0 = cidx == 0 ? win[0].cx0 : (cidx == 1 ? win[1].cx0 : win[2].cx0);
@@ -758,13 +764,14 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                 tu.y + (1 << tu.log2) > w.cy0 + w.csy)
                 continue;
             if constexpr (Stream) {
-                // the TB's residual, transformed by this wave into LDS; predict_tb reads it
-                // through w.res with the plane pitch (offset so that (y0, x0) lands on X.d[0])
+                // the TB's residual, transformed by this wave into LDS (pitch n, origin the TB's)
                 if (tu.flags & TU_CBF) {
                     const int n = 1 << tu.log2;
                     transform_tb<true>(tu, coefs, sp, a.sf, X, X.d, n, lane);
-                    w.res = X.d - ((ptrdiff_t)tu.y * n + tu.x);
+                    w.res = X.d;
                     w.rp = n;
+                    w.rx0 = tu.x;
+                    w.ry0 = tu.y;
                 }
             }
 #if !defined(HG_HOST_EMU) && !defined(HG_INTRA_NO_PAIR)
