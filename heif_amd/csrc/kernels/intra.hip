@@ -91,6 +91,12 @@ int intra_waves(int log2ctb, int chroma, int bps, int max_rows) {
 }
 
 #define wave_sync() HG_WAVE_SYNC()
+// k_intra_stream's wait for the parse (tuning: HG_STREAM_SLEEP_N, s_sleep units of 64 clocks)
+#if defined(HG_HOST_EMU) || !defined(HG_STREAM_SLEEP_N)
+#define HG_STREAM_SLEEP() HG_SLEEP()
+#else
+#define HG_STREAM_SLEEP() __builtin_amdgcn_s_sleep(HG_STREAM_SLEEP_N)
+#endif
 
 
 // 6.4.1 availability of a neighbouring luma location (xl, yl) for a TB of the
@@ -647,7 +653,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                             row_done = true;
                             break;
                         }
-                        HG_SLEEP();
+                        HG_STREAM_SLEEP();
                     }
                     reload = true;
                 }

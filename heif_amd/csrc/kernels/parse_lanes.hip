@@ -83,6 +83,9 @@ HG_HD inline uint64_t state_row(int st) {
 }
 
 constexpr uint32_t kProgDone = 0x7fffffffu;
+// LanePic.flags bit above the SP_ flags: k_intra_stream reads this picture's TU
+// and coefficient records while the parse writes them (agent-scope stores)
+constexpr uint32_t PF_COHERENT = 1u << 31;
 
 // per-lane LDS block.  HG_LANE_LDS_ODD: 212 bytes (53 dwords, odd), so the
 // 64 lanes' copies of one context byte fall in 64 different LDS banks (at 208
@@ -385,6 +388,8 @@ inline void store_tu(TuRec *d, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
     p[2] = z;
     p[3] = w;
 }
+inline void store_tu_agent(TuRec *d, uint32_t x, uint32_t y, uint32_t z, uint32_t w) { store_tu(d, x, y, z, w); }
+inline void store_word_agent(uint32_t *p, uint32_t v) { *p = v; }
 #else
 __device__ __forceinline__ uint32_t prog_load(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -402,6 +407,16 @@ __device__ __forceinline__ uint32_t load_word_coherent(const uint32_t *p) {
 __device__ __forceinline__ void release_fence() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
 __device__ __forceinline__ void store_tu(TuRec *d, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
     *reinterpret_cast<uint4 *>(d) = make_uint4(x, y, z, w);
+}
+// the same as agent-scope (sc1) stores: coherent across the XCDs' L2s once
+// complete, so the spread parse publishes them with a wait, not an L2 write-back
+__device__ __forceinline__ void store_tu_agent(TuRec *d, uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+    uint64_t *q = reinterpret_cast<uint64_t *>(d);
+    __hip_atomic_store(q, (uint64_t)x | ((uint64_t)y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (uint64_t)z | ((uint64_t)w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_word_agent(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 #endif
 
@@ -428,7 +443,6 @@ template <class T>
 inline void store_agent(T *p, T v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
 inline uint32_t load_agent(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 inline void stores_done() { std::atomic_thread_fence(std::memory_order_release); }
-inline void agent_release() { std::atomic_thread_fence(std::memory_order_release); }
 #else
 template <class T>
 __device__ __forceinline__ void store_agent(T *p, T v) {
@@ -439,13 +453,6 @@ __device__ __forceinline__ uint32_t load_agent(const uint32_t *p) {
 }
 // s_waitcnt vmcnt(0): every store of this wave has completed
 __device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0x0f70); }
-// this wave's plain stores (TU and coefficient records) written back to where
-// another XCD's agent-scope loads see them (buffer_wbl2); the explicit wait
-// after it keeps a later flag store from overtaking the write-back
-__device__ __forceinline__ void agent_release() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __builtin_amdgcn_s_waitcnt(0x0f70);
-}
 #endif
 
 HG_HD inline uint8_t load_byte_coherent(const uint8_t *p) {
@@ -984,7 +991,8 @@ HG_HD inline void coef_push(Lane &L, const LanePic &P, uint32_t w) {
     ++L.ncoef;
     (void)w;
 #else
-    P.coef_base[L.coef_row + L.ncoef++] = w;
+    if (P.flags & PF_COHERENT) store_word_agent((uint32_t *)(P.coef_base + L.coef_row + L.ncoef++), w);
+    else P.coef_base[L.coef_row + L.ncoef++] = w;
 #endif
 }
 
@@ -1395,9 +1403,11 @@ HG_HD inline void tu_emit(Lane &L, const LanePic &P) {
     if (L.fl & F_PCM) f |= TU_PCM | TU_BYPASS;
     if (L.tb_cidx == 0 && L.tb_log2 == 2) f |= TU_DST;
     if (L.ntu < P.tu_cap) {
-        store_tu(P.tu_base + L.tu_row + L.ntu, (uint32_t)L.tb_x | ((uint32_t)L.tb_y << 16),
-                 (uint32_t)L.tb_log2 | (f << 8) | ((uint32_t)L.tb_mode << 16) | ((uint32_t)(uint8_t)qp << 24),
-                 L.tb_coef0, (L.ncoef - L.tb_coef0) | ((uint32_t)L.c << 16));
+        const uint32_t w0 = (uint32_t)L.tb_x | ((uint32_t)L.tb_y << 16);
+        const uint32_t w1 = (uint32_t)L.tb_log2 | (f << 8) | ((uint32_t)L.tb_mode << 16) | ((uint32_t)(uint8_t)qp << 24);
+        const uint32_t w3 = (L.ncoef - L.tb_coef0) | ((uint32_t)L.c << 16);
+        if (P.flags & PF_COHERENT) store_tu_agent(P.tu_base + L.tu_row + L.ntu, w0, w1, L.tb_coef0, w3);
+        else store_tu(P.tu_base + L.tu_row + L.ntu, w0, w1, L.tb_coef0, w3);
         ++L.ntu;
     } else {
         L.status |= ST_CAPACITY;
@@ -1589,8 +1599,9 @@ HG_HD inline void sb_store(L_ &L, const P_ &P, uint32_t sig, uint32_t signs, uin
 #if defined(HG_NO_COEF_STORE)  // timing experiment only
         (void)w0, (void)w3;
 #else
-        store_tu(reinterpret_cast<TuRec *>(P.coef_base + L.coef_row + L.ncoef), w0, (uint32_t)nib,
-                 (uint32_t)(nib >> 32), w3);
+        TuRec *d = (TuRec *)(P.coef_base + L.coef_row + L.ncoef);
+        if (P.flags & PF_COHERENT) store_tu_agent(d, w0, (uint32_t)nib, (uint32_t)(nib >> 32), w3);
+        else store_tu(d, w0, (uint32_t)nib, (uint32_t)(nib >> 32), w3);
 #endif
         L.ncoef += 4;
     } else {
@@ -1804,10 +1815,13 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
                 const int am1 = base - 1 + rem;  // abs - 1
                 nib = (nib & ~(0xfull << (4 * nn))) | ((uint64_t)(am1 < 15 ? am1 : 15) << (4 * nn));
                 if (am1 >= 15) {  // escape: the whole level, in descending scan order from the row's end
-                    if (L.ncoef + L.nesc + 4 < P.coef_cap)
-                        P.coef_base[L.coef_row + P.coef_cap - 1 - L.nesc] = (uint32_t)last_abs;
-                    else
+                    if (L.ncoef + L.nesc + 4 < P.coef_cap) {
+                        Coef HG_GAS *e = P.coef_base + L.coef_row + P.coef_cap - 1 - L.nesc;
+                        if (P.flags & PF_COHERENT) store_word_agent((uint32_t *)e, (uint32_t)last_abs);
+                        else *e = (uint32_t)last_abs;
+                    } else {
                         L.status |= ST_CAPACITY;
+                    }
                     ++L.nesc;
                 }
             }
@@ -1865,7 +1879,10 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     const uint32_t pv = (L.fl & F_STOP) ? kProgDone : (uint32_t)L.row * (uint32_t)P.wctb + (uint32_t)L.c;
     if constexpr (EG::kSpread) {
         if (E.a->xntu) {  // k_intra's streaming mode reads this row's records as they appear
-            agent_release();
+#if defined(HG_REC_WBL2) && !defined(HG_HOST_EMU)  // tuning variant: plain record stores, then an L2 write-back
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+            stores_done();  // (the records went out as agent-scope stores: PF_COHERENT)
             store_agent(E.a->xntu + P.row_off + L.row, L.ntu);
         }
         stores_done();
@@ -1964,7 +1981,11 @@ HG_HD inline bool pic_init(LanePic &P, const BatchArgs &a, int pic, int lane0, i
     P.w8 = (sp.width + 7) >> 3;
     P.saoL = pd.sao_luma;
     P.saoC = pd.sao_chroma;
+#if defined(HG_REC_WBL2)
     P.flags = sp.flags;
+#else
+    P.flags = sp.flags | (a.xntu ? PF_COHERENT : 0u);
+#endif
     P.bits_off = (uint32_t)pd.bits_off;
     P.bits_end = (uint32_t)pd.bits_off + a.rsubs[pd.sub_first + pd.n_sub];  // RBSP end (k_rbsp)
     P.sub_first = pd.sub_first;

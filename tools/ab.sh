@@ -18,7 +18,7 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 s, a = d["stage_ms_per_step"], d["stage_ms_alone"]
 print(f"{sys.argv[2]:>12} {d['value']:9.1f} Mpix/s {d['ms_per_step']:7.2f} ms/step | pipe " +
       " ".join(f"{k[:5]} {v:6.2f}" for k, v in s.items()) + " | alone " + " ".join(f"{v:6.2f}" for v in a.values()) +
-      f" | geom {d['roofline']['parse_geometry']}", flush=True)
+      f" | lat {d['latency_ms_one_step']:6.2f} | geom {d['roofline']['parse_geometry']}", flush=True)
 PY
     done
 done
