@@ -614,7 +614,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
                                      hb.coef_n > b->set[0].coefs.cap || hb.map_bytes > b->set[0].maps.cap ||
                                      hb.sao_n > b->set[0].sao.cap || 2 * size_t(hb.rows) > b->set[0].row_counts.cap ||
                                      hb.pics.size() > b->set[0].status.cap || hb.pics.size() > G.sticky.cap ||
-                                     (mode == PARSE_SPREAD && (hb.rows > b->set[0].xprog.cap || hb.rows > b->set[0].xntu.cap ||
+                                     (mode == PARSE_SPREAD && (hb.rows > b->set[0].xprog.cap || hb.rows + hb.pics.size() > b->set[0].xntu.cap ||
                                                                hb.rows * CTX_PAD > b->xctx.cap)));
     if (grows) {  // reallocation: every decode of the old contents fully drained
         for (int k = 0; k < b->n_sets; ++k)
@@ -650,7 +650,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     if (mode == PARSE_SPREAD) {  // per-row WPP progress words and context hand-off blocks
         for (int k = 0; k < b->n_sets; ++k) {
             HIP_TRY(b->set[k].xprog.alloc(std::max<size_t>(hb.rows, 1)));
-            HIP_TRY(b->set[k].xntu.alloc(std::max<size_t>(hb.rows, 1)));
+            HIP_TRY(b->set[k].xntu.alloc(hb.rows + hb.pics.size() + 1));  // TU counts, then k_intra_stream's done words
         }
         HIP_TRY(b->xctx.alloc(std::max<size_t>(hb.rows, 1) * CTX_PAD));
     }
@@ -738,6 +738,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.xctx = mode == PARSE_SPREAD ? b->xctx.p : nullptr;
     a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
     a.xntu = nullptr;
+    a.stream_patience_us = stream_patience_us();
     // rows wrap round the lanes (waves) of a picture: the WPP context staging
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
@@ -839,18 +840,13 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     // parse stream: the batch's uploads, and this set's previous reconstruction must be done with it
     HIP_TRY(hipStreamWaitEvent(p, b->uploaded, 0));
     if (ps.pending) HIP_TRY(hipStreamWaitEvent(p, ps.recon_done, 0));
-    HIP_TRY(hipMemsetAsync(ps.status.p, 0, size_t(b->n_pics) * sizeof(uint32_t), p));
-    // rows a stopped substream never reaches keep zero TBs
-    HIP_TRY(hipMemsetAsync(ps.row_counts.p, 0, size_t(2) * uint32_t(b->args.total_rows) * sizeof(uint32_t), p));
-    if (a.intra_stream) {
-        // k_intra_stream polls this set's progress words and TU counts from its
-        // start: cleared first (launch_parse leaves them alone in this mode)
-        HIP_TRY(hipMemsetAsync(ps.xprog.p, 0, size_t(b->args.total_rows) * sizeof(uint32_t), p));
-        HIP_TRY(hipMemsetAsync(ps.xntu.p, 0, size_t(b->args.total_rows) * sizeof(uint32_t), p));
-        HIP_TRY(hipEventRecord(ps.progreset, p));
-    }
+    // k_rbsp also zeroes this set's status words and row counts (rows a stopped
+    // substream never reaches keep zero TBs) and, streaming, the progress words,
+    // TU counts and done words k_intra_stream polls from its start (launch_parse
+    // leaves them alone in that mode)
     if (t) HIP_TRY(hipEventRecord(ev[0], p));
     HIP_TRY(launch_rbsp(a, p));
+    if (a.intra_stream) HIP_TRY(hipEventRecord(ps.progreset, p));
     if (t) HIP_TRY(hipEventRecord(ev[1], p));
     HIP_TRY(launch_parse(a, p));
     if (t) HIP_TRY(hipEventRecord(ev[2], p));
@@ -877,6 +873,14 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     }
     if (t) HIP_TRY(hipEventRecord(ev[5], r));
     HIP_TRY(launch_intra(a, r));
+    if (a.intra_stream) {
+        // the second launch, after the parse: the pictures the first one gave up
+        // on (none, unless the parse did not run beside it); the rest exit at once
+        HIP_TRY(hipStreamWaitEvent(r, ps.parsed, 0));
+        BatchArgs a2 = a;
+        a2.stream_redo = 1;
+        HIP_TRY(launch_intra(a2, r));
+    }
     if (t) HIP_TRY(hipEventRecord(ev[6], r));
     HIP_TRY(launch_deblock(a, r));
     if (t) HIP_TRY(hipEventRecord(ev[7], r));

@@ -79,7 +79,7 @@ int main(int argc, char **argv) {
     else
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0,
                                         order, nullptr, mode == PARSE_LANES && lanes_jobs_default());
-    std::vector<uint32_t> xprog(hb.rows + 1), xntu(hb.rows + 1, 0);
+    std::vector<uint32_t> xprog(hb.rows + 1), xntu(hb.rows + hb.pics.size() + 1, 0);
     std::vector<uint8_t> xctx((hb.rows + 1) * size_t(CTX_PAD));
     a.parse_order = order.data();
     a.n_slots = int(order.size());
@@ -109,6 +109,7 @@ int main(int argc, char **argv) {
     a.xctx = xctx.data();
     a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
     a.xntu = a.intra_stream ? xntu.data() : nullptr;
+    a.stream_patience_us = stream_patience_us();
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);
@@ -118,6 +119,12 @@ int main(int argc, char **argv) {
         printf("host ok: %zu pictures\n", hb.pics.size());
         return 0;
     }
+    // k_rbsp zeroes the decode's status words, row counts, progress words and TU
+    // counts: start them as garbage, as a reused parse-output set holds them
+    std::fill(rc.begin(), rc.end(), 0xa5a5a5a5u);
+    std::fill(status.begin(), status.end(), 0x5au);
+    std::fill(xprog.begin(), xprog.end(), 0x7777u);
+    std::fill(xntu.begin(), xntu.end(), 0x3333u);
     emu_rbsp(a);
     emu_parse(a);
     uint32_t st = 0;
@@ -144,7 +151,14 @@ int main(int argc, char **argv) {
     printf("parse mode: %s\n", mode == PARSE_SOLO ? "solo" : mode == PARSE_SPREAD ? "spread" : "lanes");
     printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);
     if (stages >= 2 && !a.intra_stream) emu_transform(a);  // (streaming: k_intra_stream transforms each TB)
-    if (stages >= 3) emu_intra(a);
+    if (stages >= 3) {
+        emu_intra(a);
+        if (a.intra_stream) {  // the second launch: the pictures the first gave up on
+            BatchArgs a2 = a;
+            a2.stream_redo = 1;
+            emu_intra(a2);
+        }
+    }
     if (stages >= 4) emu_deblock(a);
     if (stages >= 5) {
         emu_sao_out(a);

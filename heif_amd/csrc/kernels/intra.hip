@@ -556,6 +556,8 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 // LDS of k_intra's streaming mode beyond the windows: the transform tables
 // (workgroup) and per wave the transform tiles (transform_tb, xform.hpp)
 constexpr size_t kXfTablesBytes = 1088, kXfWaveBytes = 2 * 32 * 32 * sizeof(int16_t) + 16;
+constexpr uint32_t kGaveUp = ~0u;                 // a wave's progress word: it gave its rows up
+constexpr uint64_t kRedoPatience = 200000000ull;  // 2 s (10 ns ticks): the parse is over by then
 
 // Stream: k_intra_stream, launched beside the spread parse of the same decode:
 // each row's TU records are consumed as the parse publishes them (agent-scope
@@ -570,6 +572,8 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const PicDesc pd = a.pics[pic];
     if (pd.flags & PD_ASSEMBLY) return;  // no coded data of its own (uniform: the whole workgroup leaves)
+    // second launch: only the pictures the first gave up (its done word, after the TU counts)
+    if (Stream && a.stream_redo && hg_load_agent(a.xntu + a.total_rows + pic) != 0) return;
     const SeqParams sp = a.seqs[pd.seq];
     const int W = sp.width, H = sp.height, log2ctb = sp.log2_ctb;
     const int wctb = (W + (1 << log2ctb) - 1) >> log2ctb, hctb = (H + (1 << log2ctb) - 1) >> log2ctb;
@@ -618,6 +622,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
     const int k0 = split && cls ? 1 : 0, k1 = split && !cls ? 1 : ncomp;  // this wave's components
     const int prev_wave = split ? ((rw + nrw - 1) % nrw) * 2 + cls : (wave + nw - 1) % nw;
     const bool wpp = (sp.flags & SP_WPP) != 0;
+    bool gave_up = false;  // (streaming, first launch: no parse progress for a while)
     for (int r = rw; r < hctb; r += nrw) {
         // streaming: TUs [0, ntu) of the row are known written; `done` once the parse finished the row
         uint32_t ntu = Stream ? 0u : a.row_counts[2 * (pd.row_off + r)];
@@ -637,24 +642,46 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                     const uint32_t *pw = a.xprog + pd.row_off + (wpp ? r : 0);
                     const uint32_t *nw_ = a.xntu + pd.row_off + r;
                     const uint32_t fin = (uint32_t)(r + 1) * (uint32_t)wctb;
-                    for (uint32_t spin = 0;; ++spin) {
+                    // Patience: nothing guarantees that the parse runs beside this kernel (a
+                    // profiler that serialises dispatches, a busy device), so after `patience`
+                    // without progress the first launch gives the picture up, and the second
+                    // launch (after the parse) reconstructs it; there a stall is an error.
+                    const uint64_t patience = (uint64_t)a.stream_patience_us * 100u;
+                    uint32_t seen_n = ~0u, seen_p = ~0u;
+                    uint64_t t_last = 0;
+                    for (;;) {
+                        if (!a.stream_redo && !patience) {  // (test knob: every picture to the second launch)
+                            gave_up = true;
+                            break;
+                        }
                         const uint32_t n_ = (uint32_t)HG_UNI(hg_load_agent(nw_));
                         if (n_ > t) {
                             ntu = n_;
                             break;
                         }
-                        if ((uint32_t)HG_UNI(hg_load_agent(pw)) >= fin) {  // row finished (or stopped: kProgDone)
+                        const uint32_t pv = (uint32_t)HG_UNI(hg_load_agent(pw));
+                        if (pv >= fin) {  // row finished (or stopped: kProgDone)
                             ntu = (uint32_t)HG_UNI(hg_load_agent(nw_));
                             row_done = true;
                             break;
                         }
-                        if (spin > (1u << 26)) {  // bounded: never hang the device
-                            if (lane == 0) atomicOr(&a.status[pic], ST_SUBSTREAM_END);
-                            row_done = true;
+                        const uint64_t now = hg_clock_10ns();
+                        if (n_ != seen_n || pv != seen_p) {
+                            seen_n = n_;
+                            seen_p = pv;
+                            t_last = now;
+                        } else if (now - t_last > (a.stream_redo ? kRedoPatience : patience)) {
+                            if (!a.stream_redo) {
+                                gave_up = true;
+                            } else {  // bounded: never hang the device
+                                if (lane == 0) atomicOr(&a.status[pic], ST_SUBSTREAM_END);
+                                row_done = true;
+                            }
                             break;
                         }
                         HG_STREAM_SLEEP();
                     }
+                    if (gave_up) break;
                     reload = true;
                 }
             }
@@ -721,13 +748,20 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                 cur = c;
                 if (r > 0) {
                     const uint32_t need = (uint32_t)(r - 1) * stride + (uint32_t)min(c + 2, wctb);
-                    for (uint32_t spin = 0; (uint32_t)HG_UNI(hg_atomic_load(&progress[prev_wave])) < need; ++spin) {
+                    for (uint32_t spin = 0;; ++spin) {
+                        const uint32_t v = (uint32_t)HG_UNI(hg_atomic_load(&progress[prev_wave]));
+                        if (Stream && v == kGaveUp) {  // the row above was given up: so is this one
+                            gave_up = true;
+                            break;
+                        }
+                        if (v >= need) break;
                         if (spin > (1u << 24)) {  // bounded: never hang the device
                             if (lane == 0) atomicOr(&a.status[pic], ST_SUBSTREAM_END);
                             break;
                         }
                         HG_SLEEP();
                     }
+                    if (gave_up) break;
                     HG_FENCE_ACQ();
                 }
                 // start CTU c: the row above (corner .. above-right) and the residuals
@@ -801,8 +835,21 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
 #endif
             predict_tb<Pel, CF>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, lane);
         }
+        if (gave_up) {  // (the waves below see it and give up too)
+            hg_atomic_store(&progress[wave], kGaveUp);
+            break;
+        }
         HG_FENCE_REL();
         hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
+    }
+    if constexpr (Stream) {
+        // first launch: the picture is done unless a wave gave up (its words then say kGaveUp)
+        __syncthreads();
+        if (!a.stream_redo && wave == 0) {
+            bool ok = true;
+            for (int w = 0; w < nw; ++w) ok = ok && hg_atomic_load(&progress[w]) != kGaveUp;
+            if (lane == 0) a.xntu[a.total_rows + pic] = ok ? 1u : 0u;
+        }
     }
 }
 
@@ -938,6 +985,14 @@ hipError_t launch_intra(const BatchArgs &a0, hipStream_t s) {
 // Streaming reconstruction (k_intra_stream beside the spread parse) for the
 // small batches where everything it and the parse need is resident at once
 // (up to 96 pictures: two 4032x3024 images); HEIFGPU_STREAM=0 turns it off.
+// k_intra_stream's patience: how long (us) the first launch waits without
+// parse progress before it gives a picture up to the second launch.
+// HEIFGPU_STREAM_PATIENCE_US overrides (0: give every picture up, a test knob).
+uint32_t stream_patience_us() {
+    const char *e = std::getenv("HEIFGPU_STREAM_PATIENCE_US");
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 200000u;
+}
+
 bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly) {
     const char *e = std::getenv("HEIFGPU_STREAM");
     if (e && std::atoi(e) == 0) return false;

@@ -2779,12 +2779,7 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
     if (a.parse_mode == PARSE_SPREAD) {
         if (!a.parse_order || !a.xprog || !a.xctx) return hipErrorInvalidValue;
         if (a.n_slots <= 0) return hipSuccess;
-        // progress words start at 0 for every decode (streaming mode: the caller
-        // cleared them, and the TU counts, before k_intra started polling them)
-        if (!a.intra_stream) {
-            hipError_t e = hipMemsetAsync(a.xprog, 0, (size_t)a.total_rows * sizeof(uint32_t), s);
-            if (e != hipSuccess) return e;
-        }
+        // (the progress words start at 0: k_rbsp of this decode cleared them)
         hipLaunchKernelGGL(k_parse_solo<true>, dim3(a.n_slots), dim3(64), solo_lds_bytes(1, false), s, a);
         return hipGetLastError();
     }

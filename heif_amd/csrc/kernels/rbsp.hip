@@ -26,6 +26,26 @@
 
 namespace hg {
 
+// This decode's per-picture words that start at zero, cleared here instead of
+// by memsets on the parse stream (each of those waited ~5 ms for a slot behind
+// the previous decode's k_transform, on the parse's critical path): the
+// status word, the picture's row counts, its spread-parse progress words and,
+// for k_intra_stream, its TU counts and done word.
+__device__ inline void zero_outputs(const BatchArgs &a, int pic, int lane, int nl) {
+    const PicDesc &pd = a.pics[pic];
+    if (lane == 0) a.status[pic] = 0;
+    if (pd.flags & PD_ASSEMBLY) return;  // no rows of its own
+    const SeqParams &sp = a.seqs[pd.seq];
+    const int hctb = (sp.height + (1 << sp.log2_ctb) - 1) >> sp.log2_ctb;
+    for (int i = lane; i < 2 * hctb; i += nl) a.row_counts[2 * (size_t)pd.row_off + i] = 0;
+    if (a.xprog)  // spread parse: one progress word per row
+        for (int i = lane; i < hctb; i += nl) a.xprog[pd.row_off + i] = 0;
+    if (a.intra_stream && a.xntu) {
+        for (int i = lane; i < hctb; i += nl) a.xntu[pd.row_off + i] = 0;
+        if (lane == 0) a.xntu[a.total_rows + pic] = 0;
+    }
+}
+
 #if defined(HG_HOST_EMU)
 // host restatement of the kernel's result (tests only)
 void emu_rbsp(const BatchArgs &a) {
@@ -47,6 +67,7 @@ void emu_rbsp(const BatchArgs &a) {
             const uint32_t e = a.subs[pd.sub_first + s] & SUB_OFFSET, fl = a.subs[pd.sub_first + s] & ~SUB_OFFSET;
             a.rsubs[pd.sub_first + s] = (e < len ? e - removed_before[e] : len - r) | fl;
         }
+        zero_outputs(a, p, 0, 1);
     }
 }
 #else
@@ -141,6 +162,7 @@ __global__ void __launch_bounds__(64) k_rbsp(BatchArgs a) {
     // the RBSP length, and entries at or past the payload end (corrupt headers)
     for (uint32_t idx = (uint32_t)lane; idx < nent; idx += 64)
         if ((subs[idx] & SUB_OFFSET) >= len) rsubs[idx] = (len - run) | (subs[idx] & ~SUB_OFFSET);
+    zero_outputs(a, pic, lane, 64);
 }
 
 hipError_t launch_rbsp(const BatchArgs &a, hipStream_t s) {

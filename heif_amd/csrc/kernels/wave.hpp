@@ -15,6 +15,7 @@
 #if defined(HG_HOST_EMU)
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -68,6 +69,11 @@ inline T hg_atomic_load(T *p) {
 }
 // a word another kernel of the same decode writes (agent scope on the GPU)
 inline uint32_t hg_load_agent(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+// a clock in 10 ns ticks (the GPU's 100 MHz real-time counter)
+inline uint64_t hg_clock_10ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count() / 10;
+}
 template <class T>
 inline void hg_atomic_store(T *p, T v) {
     __atomic_store_n(p, v, __ATOMIC_RELEASE);
@@ -115,6 +121,8 @@ __device__ __forceinline__ T hg_atomic_load(T *p) {
 __device__ __forceinline__ uint32_t hg_load_agent(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a clock in 10 ns ticks (s_memrealtime: the 100 MHz real-time counter, one for the whole chip)
+__device__ __forceinline__ uint64_t hg_clock_10ns() { return __builtin_amdgcn_s_memrealtime(); }
 template <class T>
 __device__ __forceinline__ void hg_atomic_store(T *p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -46,6 +46,9 @@ PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "sprea
            "jobs": JOBS, "jobs8": {**JOBS, "HEIFGPU_LANES_PPW": "8"}, "jobs5": {**JOBS, "HEIFGPU_LANES_PPW": "5"},
            "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1", "HEIFGPU_INTRA_SPLIT": "0"},
            "lf_fused": {"HEIFGPU_LF": "fused"},
+           # spread with k_intra_stream giving every picture up to its second launch, and without streaming
+           "spread_redo": {"HEIFGPU_PARSE": "spread", "HEIFGPU_STREAM_PATIENCE_US": "0"},
+           "spread_nostream": {"HEIFGPU_PARSE": "spread", "HEIFGPU_STREAM": "0"},
            "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
 
 
@@ -82,7 +85,7 @@ def _corrupt(data: bytes, mode: str) -> bytes:
     return bytes(d)
 
 
-@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "jobs8"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "spread_redo", "lanes", "packed", "jobs8"])
 @pytest.mark.parametrize("mode", ["random", "zeroed"])
 def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode, parser):
     """Corrupt slice data must end in status bits, never in a crash (the same
