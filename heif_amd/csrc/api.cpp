@@ -739,6 +739,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
     a.xntu = nullptr;
     a.stream_patience_us = stream_patience_us();
+    a.intra_fused = !a.intra_stream && intra_fused_default() ? 1 : 0;
     // rows wrap round the lanes (waves) of a picture: the WPP context staging
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
@@ -856,6 +857,13 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         // streaming (small batches): no k_transform; the
         // reconstruction starts beside this decode's parse and trails it
         HIP_TRY(hipStreamWaitEvent(r, ps.progreset, 0));
+        if (t) {
+            HIP_TRY(hipEventRecord(ev[3], r));
+            HIP_TRY(hipEventRecord(ev[4], r));
+        }
+    } else if (a.intra_fused) {
+        // fused: no k_transform; k_intra_fused transforms each TB itself after the parse
+        HIP_TRY(hipStreamWaitEvent(r, ps.parsed, 0));
         if (t) {
             HIP_TRY(hipEventRecord(ev[3], r));
             HIP_TRY(hipEventRecord(ev[4], r));

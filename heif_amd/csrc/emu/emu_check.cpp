@@ -110,6 +110,7 @@ int main(int argc, char **argv) {
     a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
     a.xntu = a.intra_stream ? xntu.data() : nullptr;
     a.stream_patience_us = stream_patience_us();
+    a.intra_fused = !a.intra_stream && intra_fused_default() ? 1 : 0;
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);
@@ -150,7 +151,7 @@ int main(int argc, char **argv) {
     }
     printf("parse mode: %s\n", mode == PARSE_SOLO ? "solo" : mode == PARSE_SPREAD ? "spread" : "lanes");
     printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);
-    if (stages >= 2 && !a.intra_stream) emu_transform(a);  // (streaming: k_intra_stream transforms each TB)
+    if (stages >= 2 && !a.intra_stream && !a.intra_fused) emu_transform(a);  // (streaming: k_intra_stream transforms each TB)
     if (stages >= 3) {
         emu_intra(a);
         if (a.intra_stream) {  // the second launch: the pictures the first gave up on

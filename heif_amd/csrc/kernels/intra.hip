@@ -556,24 +556,30 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 // LDS of k_intra's streaming mode beyond the windows: the transform tables
 // (workgroup) and per wave the transform tiles (transform_tb, xform.hpp)
 constexpr size_t kXfTablesBytes = 1088, kXfWaveBytes = 2 * 32 * 32 * sizeof(int16_t) + 16;
+constexpr int kIntraPlanes = 0, kIntraStream = 1, kIntraFused = 2;
 constexpr uint32_t kGaveUp = ~0u;                 // a wave's progress word: it gave its rows up
 constexpr uint64_t kRedoPatience = 200000000ull;  // 2 s (10 ns ticks): the parse is over by then
 
-// Stream: k_intra_stream, launched beside the spread parse of the same decode:
+// Mode kIntraPlanes: k_intra, residuals from k_transform's planes.
+// Mode kIntraStream: k_intra_stream, launched beside the spread parse of the same decode:
 // each row's TU records are consumed as the parse publishes them (agent-scope
 // per-row TU counts behind its progress words) and every coded TB is
 // transformed by the wave itself (transform_tb into LDS) right before its
 // prediction, so no k_transform pass and no residual planes; the
 // reconstruction trails the parse by a CTU instead of starting after it.
-template <typename Pel, int CF, bool Stream>
+// Mode kIntraFused: k_intra_fused, after the parse like k_intra but with the
+// TBs transformed in-line as in the streaming mode (no k_transform stage).
+template <typename Pel, int CF, int Mode>
 __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs &a, unsigned char *smem) {
+    constexpr bool Poll = Mode == kIntraStream;       // rows consumed while the parse writes them
+    constexpr bool XfInline = Mode != kIntraPlanes;   // each TB transformed by the wave (no k_transform)
     const int nw = (int)HG_UNI(blockDim.x >> 6);
     const int pic = a.pic0 + blockIdx.x;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const PicDesc pd = a.pics[pic];
     if (pd.flags & PD_ASSEMBLY) return;  // no coded data of its own (uniform: the whole workgroup leaves)
     // second launch: only the pictures the first gave up (its done word, after the TU counts)
-    if (Stream && a.stream_redo && hg_load_agent(a.xntu + a.total_rows + pic) != 0) return;
+    if (Poll && a.stream_redo && hg_load_agent(a.xntu + a.total_rows + pic) != 0) return;
     const SeqParams sp = a.seqs[pd.seq];
     const int W = sp.width, H = sp.height, log2ctb = sp.log2_ctb;
     const int wctb = (W + (1 << log2ctb) - 1) >> log2ctb, hctb = (H + (1 << log2ctb) - 1) >> log2ctb;
@@ -591,7 +597,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
     uint32_t *progress = reinterpret_cast<uint32_t *>(smem);  // [nw], 64 B reserved
     unsigned char *blk = smem + 64 + (size_t)wave * lay.bytes;
     XfScratch X{};
-    if constexpr (Stream) {
+    if constexpr (XfInline) {
         unsigned char *tab = smem + 64 + (size_t)nw * lay.bytes;
         unsigned char *xw = tab + kXfTablesBytes + (size_t)wave * kXfWaveBytes;
         X = XfScratch{reinterpret_cast<int16_t *>(xw), reinterpret_cast<int16_t *>(xw + 2048),
@@ -625,10 +631,10 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
     bool gave_up = false;  // (streaming, first launch: no parse progress for a while)
     for (int r = rw; r < hctb; r += nrw) {
         // streaming: TUs [0, ntu) of the row are known written; `done` once the parse finished the row
-        uint32_t ntu = Stream ? 0u : a.row_counts[2 * (pd.row_off + r)];
-        bool row_done = !Stream;
+        uint32_t ntu = Poll ? 0u : a.row_counts[2 * (pd.row_off + r)];
+        bool row_done = !Poll;
         const TuRec *tus = a.tus + pd.tu_off + (uint64_t)r * pd.tu_cap_row;
-        const CoefSrc<Stream> coefs{a.coefs + pd.coef_off + (uint64_t)r * pd.coef_cap_row};
+        const CoefSrc<Poll> coefs{a.coefs + pd.coef_off + (uint64_t)r * pd.coef_cap_row};
         int cur = -1;
 #if !defined(HG_HOST_EMU)
         uint4 tblk = make_uint4(0, 0, 0, 0);  // lane l: TuRec t0 + l (one coalesced load per 64 TBs)
@@ -636,7 +642,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
 #endif
         for (uint32_t t = 0;; ++t) {
             bool reload = false;
-            if constexpr (Stream) {
+            if constexpr (Poll) {
                 if (t >= ntu && !row_done) {
                     // wait until the parse has published TU t of this row or finished the row
                     const uint32_t *pw = a.xprog + pd.row_off + (wpp ? r : 0);
@@ -696,7 +702,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                 if ((t & 63u) == 0 || reload) {
                     t0 = t & ~63u;
                     const uint32_t i = t0 + (uint32_t)lane;
-                    if constexpr (Stream) {
+                    if constexpr (Poll) {
                         const uint64_t *q = reinterpret_cast<const uint64_t *>(tus + i);
                         const uint64_t lo = i < ntu ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
                         const uint64_t hi = i < ntu ? __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
@@ -750,7 +756,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                     const uint32_t need = (uint32_t)(r - 1) * stride + (uint32_t)min(c + 2, wctb);
                     for (uint32_t spin = 0;; ++spin) {
                         const uint32_t v = (uint32_t)HG_UNI(hg_atomic_load(&progress[prev_wave]));
-                        if (Stream && v == kGaveUp) {  // the row above was given up: so is this one
+                        if (Poll && v == kGaveUp) {  // the row above was given up: so is this one
                             gave_up = true;
                             break;
                         }
@@ -803,11 +809,11 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                 tu.x < w.cx0 || tu.y < w.cy0 || tu.x + (1 << tu.log2) > w.cx0 + w.csx ||
                 tu.y + (1 << tu.log2) > w.cy0 + w.csy)
                 continue;
-            if constexpr (Stream) {
+            if constexpr (XfInline) {
                 // the TB's residual, transformed by this wave into LDS (pitch n, origin the TB's)
                 if (tu.flags & TU_CBF) {
                     const int n = 1 << tu.log2;
-                    transform_tb<true>(tu, coefs, sp, a.sf, X, X.d, n, lane);
+                    transform_tb<Poll>(tu, coefs, sp, a.sf, X, X.d, n, lane);
                     w.res = X.d;
                     w.rp = n;
                     w.rx0 = tu.x;
@@ -817,7 +823,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
 #if !defined(HG_HOST_EMU) && !defined(HG_INTRA_NO_PAIR)
             // a 4x4 / 8x8 Cb TB followed by its Cr TB (same TU; the next record of this 64-record block):
             // both in one pass
-            if (!Stream && cidx == 1 && chroma == 1 && tu.log2 <= 3 && t + 1 < ntu && ((t + 1) & 63u) != 0) {
+            if (!XfInline && cidx == 1 && chroma == 1 && tu.log2 <= 3 && t + 1 < ntu && ((t + 1) & 63u) != 0) {
                 const int sel = (int)(t + 1 - t0);
                 const uint4 r = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)tblk.x, sel),
                                            (uint32_t)__builtin_amdgcn_readlane((int)tblk.y, sel),
@@ -842,7 +848,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
         HG_FENCE_REL();
         hg_atomic_store(&progress[wave], (uint32_t)r * stride + (uint32_t)wctb);
     }
-    if constexpr (Stream) {
+    if constexpr (Poll) {
         // first launch: the picture is done unless a wave gave up (its words then say kGaveUp)
         __syncthreads();
         if (!a.stream_redo && wave == 0) {
@@ -860,7 +866,7 @@ __global__ void __launch_bounds__(kMaxWaves * 64) HG_INTRA_ATTR k_intra(BatchArg
 #else
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #endif
-    intra_body<Pel, CF, false>(a, smem);
+    intra_body<Pel, CF, kIntraPlanes>(a, smem);
 }
 
 // (no waves-per-EU cap: the transform's registers come on top of the prediction's)
@@ -871,7 +877,17 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra_stream(BatchArgs a) {
 #else
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #endif
-    intra_body<Pel, CF, true>(a, smem);
+    intra_body<Pel, CF, kIntraStream>(a, smem);
+}
+
+template <typename Pel, int CF>
+__global__ void __launch_bounds__(kMaxWaves * 64) k_intra_fused(BatchArgs a) {
+#if defined(HG_HOST_EMU)
+    unsigned char *smem = g_emu.smem;
+#else
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#endif
+    intra_body<Pel, CF, kIntraFused>(a, smem);
 }
 
 // luma / chroma wave pairs (k_intra's split): for batches of few pictures,
@@ -915,7 +931,7 @@ static int intra_launch_waves(const BatchArgs &a) {
 
 static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
     size_t b = 64 + (size_t)nw * win_layout(a.max_log2ctb, a.chroma_format, a.bytes_per_sample).bytes;
-    if (a.intra_stream) b += kXfTablesBytes + (size_t)nw * kXfWaveBytes;
+    if (a.intra_stream || a.intra_fused) b += kXfTablesBytes + (size_t)nw * kXfWaveBytes;
     return b;
 }
 
@@ -932,6 +948,11 @@ static void emu_intra_cf(const BatchArgs &a, int nw) {
     if (a.intra_stream) {
         if (a.bytes_per_sample == 1) emu_launch(k_intra_stream<uint8_t, CF>, a.n_pics, 1, nw, a, false, lds);
         else emu_launch(k_intra_stream<uint16_t, CF>, a.n_pics, 1, nw, a, false, lds);
+        return;
+    }
+    if (a.intra_fused) {
+        if (a.bytes_per_sample == 1) emu_launch(k_intra_fused<uint8_t, CF>, a.n_pics, 1, nw, a, false, lds);
+        else emu_launch(k_intra_fused<uint16_t, CF>, a.n_pics, 1, nw, a, false, lds);
         return;
     }
     if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t, CF>, a.n_pics, 1, nw, a, false, lds);
@@ -958,6 +979,13 @@ static void launch_intra_cf(const BatchArgs &a, int nw, size_t lds, hipStream_t 
             hipLaunchKernelGGL((k_intra_stream<uint8_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
         else
             hipLaunchKernelGGL((k_intra_stream<uint16_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
+        return;
+    }
+    if (a.intra_fused) {
+        if (a.bytes_per_sample == 1)
+            hipLaunchKernelGGL((k_intra_fused<uint8_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
+        else
+            hipLaunchKernelGGL((k_intra_fused<uint16_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
         return;
     }
     if (a.bytes_per_sample == 1)
@@ -991,6 +1019,13 @@ hipError_t launch_intra(const BatchArgs &a0, hipStream_t s) {
 uint32_t stream_patience_us() {
     const char *e = std::getenv("HEIFGPU_STREAM_PATIENCE_US");
     return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 200000u;
+}
+
+// k_intra_fused (the transform folded into the reconstruction after the parse)
+// instead of k_transform + k_intra: HEIFGPU_FUSED=1 (read per prepare)
+bool intra_fused_default() {
+    const char *e = std::getenv("HEIFGPU_FUSED");
+    return e && std::atoi(e) != 0;
 }
 
 bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly) {

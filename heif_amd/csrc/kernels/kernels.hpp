@@ -62,6 +62,7 @@ struct BatchArgs {
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
     uint32_t *xntu;            // streaming mode: per-row TU records written so far (null otherwise)
     int intra_stream;          // k_intra transforms and reconstructs each row behind the spread parse (same launch window)
+    int intra_fused;           // k_intra_fused after the parse: TBs transformed in-line, no k_transform stage
     int stream_redo;           // k_intra_stream's second launch (after the parse): the pictures the first gave up on
     uint32_t stream_patience_us;  // first launch: give a picture up after this long without parse progress (0: at once)
     int has_assembly;          // some picture is PD_ASSEMBLY (launch_deblock runs k_assemble first)
@@ -121,6 +122,8 @@ constexpr int kStreamMaxPics = 96;
 bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly);
 // k_intra_stream's patience (us) before its first launch gives a picture up to the second
 uint32_t stream_patience_us();
+// k_intra_fused in place of k_transform + k_intra (HEIFGPU_FUSED)
+bool intra_fused_default();
 // k_loopfilter tiles of the largest picture of a batch (assembly pictures included)
 int lf_tiles_for(const PicDesc *pics, int n, const SeqParams *seqs);
 // lanes mode runs k_parse_jobs (substreams from a per-wave job list) with HEIFGPU_LANES_JOBS=1

@@ -49,6 +49,9 @@ PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "sprea
            # spread with k_intra_stream giving every picture up to its second launch, and without streaming
            "spread_redo": {"HEIFGPU_PARSE": "spread", "HEIFGPU_STREAM_PATIENCE_US": "0"},
            "spread_nostream": {"HEIFGPU_PARSE": "spread", "HEIFGPU_STREAM": "0"},
+           # k_intra_fused: the transform folded into the reconstruction after the parse
+           "fused": {**LANES, "HEIFGPU_FUSED": "1"},
+           "fused_solo": {"HEIFGPU_PARSE": "solo", "HEIFGPU_FUSED": "1"},
            "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
 
 
