@@ -286,8 +286,12 @@ void validate_sps(const SequenceParameterSet &s) {
          s.pcm_bit_depth_luma > 8 + s.bit_depth_luma_minus8 ||
          s.pcm_bit_depth_chroma > 8 + s.bit_depth_chroma_minus8))
         throw HeifError("PCM parameters out of range");
-    if (s.bit_depth_luma_minus8 > 2 || s.bit_depth_chroma_minus8 > 2)
-        throw UnsupportedError("bit depth above 10 (only 8..10-bit streams are parity-tested on this path)");
+    // up to 12 bits (Main 12 / RExt 12-bit profiles): without extended_precision_processing
+    // (a range-extension tool, rejected) the coefficients keep 16 bits and a residual
+    // clipped to int16 still reconstructs exactly for sample depths below 16; parity-tested
+    // at 8..12 bits (tests/test_synth.py)
+    if (s.bit_depth_luma_minus8 > 4 || s.bit_depth_chroma_minus8 > 4)
+        throw UnsupportedError("bit depth above 12 (only 8..12-bit streams are parity-tested on this path)");
 }
 
 SequenceParameterSet sequence_parameter_set_rbsp(const std::vector<uint8_t> &rbsp) {

@@ -929,6 +929,19 @@ static int intra_launch_waves(const BatchArgs &a) {
     return cap < nw ? cap : nw;
 }
 
+// k_intra_stream: four waves per picture (rows r, r + 4, ...), no luma / chroma
+// split.  It only has to keep up with the parse, and its waves share the CUs
+// with the parse's: one image, same box, 4 waves 28.2-28.3 ms per pipelined
+// step against 28.9-29.4 with 16 (latency 28.0-28.1 either way, the parse's)
+static int stream_waves(int nw) {
+    static const int forced = [] {
+        const char *e = std::getenv("HEIFGPU_INTRA_WAVES");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (forced > 0) return nw;
+    return nw < 4 ? nw : 4;
+}
+
 static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
     size_t b = 64 + (size_t)nw * win_layout(a.max_log2ctb, a.chroma_format, a.bytes_per_sample).bytes;
     if (a.intra_stream || a.intra_fused) b += kXfTablesBytes + (size_t)nw * kXfWaveBytes;
@@ -961,7 +974,8 @@ static void emu_intra_cf(const BatchArgs &a, int nw) {
 void emu_intra(const BatchArgs &a0) {
     BatchArgs a = a0;
     int nw = intra_launch_waves(a);
-    a.intra_split = intra_split_for(a, nw) ? 1 : 0;
+    if (a.intra_stream) nw = stream_waves(nw);
+    a.intra_split = !a.intra_stream && intra_split_for(a, nw) ? 1 : 0;
     if (a.intra_split) nw = intra_split_waves(a, nw);
     nw = intra_fit_waves(a, nw);
     switch (a.chroma_format) {
@@ -996,7 +1010,8 @@ static void launch_intra_cf(const BatchArgs &a, int nw, size_t lds, hipStream_t 
 hipError_t launch_intra(const BatchArgs &a0, hipStream_t s) {
     BatchArgs a = a0;
     int nw = intra_launch_waves(a);
-    a.intra_split = intra_split_for(a, nw) ? 1 : 0;
+    if (a.intra_stream) nw = stream_waves(nw);
+    a.intra_split = !a.intra_stream && intra_split_for(a, nw) ? 1 : 0;
     if (a.intra_split) nw = intra_split_waves(a, nw);
     nw = intra_fit_waves(a, nw);
     const size_t lds = intra_lds_bytes(a, nw);

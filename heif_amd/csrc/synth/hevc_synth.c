@@ -931,7 +931,7 @@ long synth_pps(const synth_params *P, uint8_t *out, size_t cap) {
 
 int synth_check_params(const synth_params *P) {
     if (P->chroma_format < 0 || P->chroma_format > 3) return -1;
-    if (P->bit_depth < 8 || P->bit_depth > 10) return -1;
+    if (P->bit_depth < 8 || P->bit_depth > 12) return -1;
     if (P->log2_min_cb < 3 || P->log2_ctb < 4 || P->log2_ctb > 6 || P->log2_min_cb > P->log2_ctb) return -1;
     if (P->log2_min_tb != 2 || P->log2_max_tb < P->log2_min_tb || P->log2_max_tb > 5 ||
         P->log2_max_tb > P->log2_ctb || P->log2_min_tb >= P->log2_min_cb)

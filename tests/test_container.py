@@ -11,7 +11,7 @@ planes as the plain layout.
 Then malformed inputs that must end in a clean HEIFGPU_E_PARSE /
 HEIFGPU_E_UNSUPPORTED error instead of a wild host read or a device fault:
 wrapping iloc offsets, conformance windows outside the picture, block-size
-ladders and QPs outside their H.265 ranges, bit depths above 10.
+ladders and QPs outside their H.265 ranges, bit depths above 12.
 """
 import hashlib
 
@@ -146,8 +146,14 @@ def test_valid_pcm_sps_accepted():
     assert H.HeifImage.parse(d).info.width == 128
 
 
-def test_bit_depth_above_10_is_unsupported():
-    _assert_error(_with_sets(sps=W.sps(bit_depth=12)), unsupported=True)
+def test_bit_depth_above_12_is_unsupported():
+    _assert_error(_with_sets(sps=W.sps(bit_depth=13)), unsupported=True)
+    _assert_error(_with_sets(sps=W.sps(bit_depth=16)), unsupported=True)
+
+
+def test_bit_depth_12_accepted():
+    """Main 12 (no extended precision): 8..12-bit streams decode (tests/test_synth.py main12 cases)."""
+    assert H.HeifImage.parse(_with_sets(sps=W.sps(bit_depth=12))).info.width == 128
 
 
 @pytest.mark.parametrize("over", [dict(cb_qp_offset=13), dict(cr_qp_offset=-13), dict(diff_cu_qp_delta_depth=3),

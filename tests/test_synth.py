@@ -26,6 +26,12 @@ CASES = [
     ("main10", dict(bit_depth=10)),
     ("mono10", dict(bit_depth=10, chroma_format=0)),
     ("mono8", dict(chroma_format=0)),
+    # Main 12 / RExt 12-bit: QpBdOffset 24, tc and beta scaled by 16, SAO offsets
+    # capped at 31 without scaling (log2_sao_offset_scale is a rejected RExt tool)
+    ("main12", dict(bit_depth=12)),
+    ("mono12_bypass", dict(bit_depth=12, chroma_format=0, tq_bypass=1)),
+    ("c444_12b_pcm", dict(chroma_format=3, bit_depth=12, pcm=1, pcm_pct=30, pcm_bd_y=12, pcm_bd_c=11)),
+    ("b11_lowqp_dense", dict(bit_depth=11, init_qp=22, slice_qp_delta=-40, density=80, transform_skip=1)),
     ("b9_ctb16", dict(bit_depth=9, log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2, diff_cu_qp_delta_depth=0)),
     ("ctb64_tskip_bypass", dict(bit_depth=10, log2_ctb=6, max_th_depth_intra=3, diff_cu_qp_delta_depth=2,
                                 transform_skip=1, tq_bypass=1)),
@@ -127,7 +133,7 @@ def test_generator_rejects_bad_parameters():
     with pytest.raises(ValueError):
         S.picture(params(dict(width=100)), 0)      # not a multiple of MinCbSize
     with pytest.raises(ValueError):
-        S.picture(params(dict(bit_depth=12)), 0)
+        S.picture(params(dict(bit_depth=13)), 0)
     with pytest.raises(ValueError):
         S.picture(params(dict(log2_max_tb=6, log2_ctb=6)), 0)
 
