@@ -188,11 +188,17 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
             const int pctb = 1 << ps.sps.log2_ctb_size;
             const int pw = ps.sps.pic_width_in_ctbs_y(), ph = ps.sps.pic_height_in_ctbs_y();
             if (ps.pps.tiles_enabled_flag) {
+                // substreams in tile scan: one per tile, or with WPP one per CTB row of each tile
                 const int ntc = int(ps.col_bd.size()) - 1, ntr = int(ps.row_bd.size()) - 1;
+                const bool wpp = ps.pps.entropy_coding_sync_enabled_flag;
+                int s = 0;
                 for (int ht = 0; ht < ntc * ntr; ++ht) {
                     const int tc = ht % ntc, tr = ht / ntc;
-                    subs_of.push_back({ps.col_bd[size_t(tc)], ps.row_bd[size_t(tr)], ps.col_bd[size_t(tc) + 1],
-                                       ps.row_bd[size_t(tr) + 1], 0, 1, ht, ht + 1, ht + 1 < ntc * ntr});
+                    const int y0 = ps.row_bd[size_t(tr)], y1 = ps.row_bd[size_t(tr) + 1];
+                    const int n = wpp ? y1 - y0 : 1;
+                    subs_of.push_back({ps.col_bd[size_t(tc)], y0, ps.col_bd[size_t(tc) + 1], y1, 0, 1, s, s + n,
+                                       ht + 1 < ntc * ntr});
+                    s += n;
                 }
             } else {
                 for (size_t k = 0; k < tj.segs.size();) {  // one sub-picture per slice

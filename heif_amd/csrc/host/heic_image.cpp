@@ -17,9 +17,8 @@ void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p
     if (s.separate_colour_plane_flag) throw UnsupportedError("separate_colour_plane_flag");
     if (s.bit_depth_luma_minus8 != s.bit_depth_chroma_minus8) throw UnsupportedError("luma/chroma bit depth differ");
     if (s.range_extension_tools || p.range_extension_tools) throw UnsupportedError("range-extension coding tools");
-    // HEVC tiles decode as sub-pictures (batch.cpp)
-    if (p.tiles_enabled_flag && p.entropy_coding_sync_enabled_flag)
-        throw UnsupportedError("HEVC tiles together with WPP");
+    // HEVC tiles decode as sub-pictures (batch.cpp), with WPP each tile's CTB rows
+    // its substreams (9.3.1: a row of a tile syncs with the tile's row above)
     if (s.pic_width_in_luma_samples > 8192 || s.pic_height_in_luma_samples > 8192)
         throw UnsupportedError("picture larger than 8192");
     if (s.pic_width_in_luma_samples % (1 << s.log2_min_luma_coding_block_size) ||
@@ -77,9 +76,13 @@ void check_segments(TileJob &job, const ParamSet &ps) {
             throw UnsupportedError("slices filtered across their boundaries with different deblocking values");
     }
     const size_t ntiles = (ps.col_bd.size() - 1) * (ps.row_bd.size() - 1);
-    if (pps.tiles_enabled_flag && size_t(job.segs[0].sh.num_entry_point_offsets) + 1 != ntiles)
-        throw HeifError("tiled picture without one entry point per tile");
-    if (pps.entropy_coding_sync_enabled_flag)
+    // tiles: one substream per tile, or with WPP one per CTB row of each tile
+    const size_t nsub_tiles = pps.entropy_coding_sync_enabled_flag
+                                  ? (ps.col_bd.size() - 1) * size_t(sps.pic_height_in_ctbs_y())
+                                  : ntiles;
+    if (pps.tiles_enabled_flag && size_t(job.segs[0].sh.num_entry_point_offsets) + 1 != nsub_tiles)
+        throw HeifError("tiled picture without one entry point per tile (per tile row with WPP)");
+    if (pps.entropy_coding_sync_enabled_flag && !pps.tiles_enabled_flag)
         for (size_t k = 0; k < job.segs.size(); ++k) {
             const uint32_t r0 = job.segs[k].sh.slice_segment_address / pw;
             const uint32_t r1 = k + 1 < job.segs.size() ? job.segs[k + 1].sh.slice_segment_address / pw

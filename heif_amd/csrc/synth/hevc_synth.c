@@ -955,7 +955,7 @@ int synth_check_params(const synth_params *P) {
         return -1;
     if (tiles_on(P)) {
         int ctb = 1 << P->log2_ctb, wctb = (P->width + ctb - 1) / ctb, hctb = (P->height + ctb - 1) / ctb;
-        if (P->wpp || P->tile_cols < 1 || P->tile_rows < 1 || P->tile_cols > wctb || P->tile_rows > hctb) return -1;
+        if (P->tile_cols < 1 || P->tile_rows < 1 || P->tile_cols > wctb || P->tile_rows > hctb) return -1;
         if (!P->tile_uniform) {
             int sw = 0, sh = 0;
             for (int i = 0; i + 1 < P->tile_cols; i++) { if (P->tile_col_w[i] < 1) return -1; sw += P->tile_col_w[i]; }
@@ -1064,13 +1064,17 @@ static long synth_impl(const synth_params *P, uint64_t seed, uint8_t *out, size_
             }
         }
         p->slice_rs[rs] = cur_slice;
-        if (seg_start || (P->wpp && rx == 0) || tile_start) {
+        /* WPP: each CTB row of a tile is a substream (9.3.1: the CTB to its left is in another tile) */
+        const int wpp_row = P->wpp && (rx == 0 || p->tile_rs[rs] != p->tile_rs[rs - 1]);
+        if (seg_start || wpp_row || tile_start) {
             ce_start(&p->c, &subs[nsub]);
             sg->nsub++;
             if (ts == 0 || tile_start) {
                 ce_init_ctx(&p->c, slice_qp);
-            } else if (P->wpp && rx == 0) {
-                const int t_ok = saved && p->wctb > 1 && p->slice_rs[rs - p->wctb + 1] == cur_slice;
+            } else if (wpp_row) {
+                /* T = the CTB above-right: in the picture, the same tile and the same slice */
+                const int t_ok = saved && rx + 1 < p->wctb && p->slice_rs[rs - p->wctb + 1] == cur_slice &&
+                                 p->tile_rs[rs - p->wctb + 1] == p->tile_rs[rs];
                 if (t_ok) { memcpy(p->c.st, wst, C_NUM); memcpy(p->c.mps, wmps, C_NUM); }
                 else ce_init_ctx(&p->c, slice_qp);
             } else if (sg->dependent && seg_start) {
@@ -1082,10 +1086,15 @@ static long synth_impl(const synth_params *P, uint64_t seed, uint8_t *out, size_
         }
         if (sao_l || sao_c) sao_syntax(p, rx, ry, sao_l, sao_c);
         coding_quadtree(p, rx << p->log2ctb, ry << p->log2ctb, p->log2ctb, 0);
-        if (P->wpp && rx == 1) { memcpy(wst, p->c.st, C_NUM); memcpy(wmps, p->c.mps, C_NUM); saved = 1; }
+        /* 9.3.2.2 storage: CtbAddrInRs % PicWidthInCtbs == 1, or its tile differs from CtbAddrInRs - 2's */
+        if (P->wpp && (rs % p->wctb == 1 || (rs > 1 && p->tile_rs[rs] != p->tile_rs[rs - 2]))) {
+            memcpy(wst, p->c.st, C_NUM);
+            memcpy(wmps, p->c.mps, C_NUM);
+            saved = 1;
+        }
         const int seg_end = ts == nctb - 1 || (ts + 1) % seg_ctus == 0;
         ce_term(&p->c, seg_end); /* end_of_slice_segment_flag */
-        if (seg_end || (P->wpp && rx == p->wctb - 1) || p->tile_rs[p->ts2rs[ts + 1]] != p->tile_rs[rs]) {
+        if (seg_end || (P->wpp && p->ts2rs[ts + 1] / p->wctb != ry) || p->tile_rs[p->ts2rs[ts + 1]] != p->tile_rs[rs]) {
             if (!seg_end) ce_term(&p->c, 1); /* end_of_subset_one_bit */
             ce_finish(&p->c);
             bw_align1(&subs[nsub++]); /* byte_alignment() / rbsp_slice_segment_trailing_bits() */

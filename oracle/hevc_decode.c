@@ -1115,14 +1115,29 @@ static void update_qpy(pic_t *p) {
 }
 
 /* 8.6.1 first part: qPY_PRED for the quantization group */
+/* 9.3.1 / 8.6.1: the CTB (rx, ry) starts a CTB row within its tile (the CTB to
+ * its left is outside the picture or in another tile) */
+static int first_ctb_in_tile_row(const pic_t *p, int rx, int ry) {
+    const int rs = ry * p->wctb + rx;
+    return rx == 0 || p->tile_rs[rs] != p->tile_rs[rs - 1];
+}
+
+/* 9.3.2.2: the WPP storage process runs after the CTB at raster address rs when
+ * CtbAddrInRs % PicWidthInCtbsY == 1, or CtbAddrInRs > 1 and its tile differs
+ * from that of CtbAddrInRs - 2 (so the state kept is the one after the second
+ * CTB of the tile's row; a one-CTB-wide tile never syncs: its T is unavailable) */
+static int wpp_storage_point(const pic_t *p, int rs) {
+    return rs % p->wctb == 1 || (rs > 1 && p->tile_rs[rs] != p->tile_rs[rs - 2]);
+}
+
 static void derive_qp_pred(pic_t *p) {
     int prev;
     int first_in_ctb = (p->qg_x == p->ctb_x && p->qg_y == p->ctb_y);
     if (p->first_qg_in_slice) { /* first QG in the slice or in a tile */
         prev = p->slice_qp;
         p->first_qg_in_slice = 0;
-    } else if (p->pps->wpp && first_in_ctb && p->ctb_x == 0) {
-        prev = p->slice_qp;
+    } else if (p->pps->wpp && first_in_ctb && first_ctb_in_tile_row(p, p->ctb_x >> p->log2ctb, p->ctb_y >> p->log2ctb)) {
+        prev = p->slice_qp; /* 8.6.1: first QG of a CTB row within a tile, WPP */
     } else {
         prev = p->qp_prev_last;
     }
@@ -1970,7 +1985,6 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *item, size_t item_le
     const hevc_sps *s = &ps->sps;
     const hevc_pps *pp = &ps->pps;
     if (s->range_ext_any || pp->range_ext_any) return oracle_fail("range extension tools not supported");
-    if (pp->tiles && pp->wpp) return oracle_fail("HEVC tiles together with WPP not supported");
     if (s->separate_colour_plane) return oracle_fail("separate_colour_plane_flag not supported");
     /* the VCL NAL units, 4-byte length prefixes */
     const uint8_t *nals[MAX_SEGMENTS];
@@ -2092,7 +2106,7 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *item, size_t item_le
                 const int tile_start = ctbAddr == 0 || p->tile_rs[rs] != p->tile_rs[p->ts2rs[ctbAddr - 1]];
                 if (tile_start) {
                     cabac_init_ctx(&p->c, p->slice_qp);
-                } else if (pp->wpp && rx == 0) {
+                } else if (pp->wpp && first_ctb_in_tile_row(p, rx, ry)) {
                     if (p->wpp_saved && avail_zs(p, p->ctb_x, p->ctb_y, p->ctb_x + p->ctb, p->ctb_y - p->ctb)) {
                         memcpy(p->c.st, p->wpp_st, CTX_NUM);
                         memcpy(p->c.mps, p->wpp_mps, CTX_NUM);
@@ -2112,7 +2126,7 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *item, size_t item_le
             }
             if (p->sao_luma || p->sao_chroma) parse_sao(p, rx, ry);
             if (coding_quadtree(p, p->ctb_x, p->ctb_y, p->log2ctb, 0)) goto out;
-            if (pp->wpp && rx == 1) {
+            if (pp->wpp && wpp_storage_point(p, rs)) {
                 memcpy(p->wpp_st, p->c.st, CTX_NUM);
                 memcpy(p->wpp_mps, p->c.mps, CTX_NUM);
                 p->wpp_saved = 1;
@@ -2120,7 +2134,8 @@ static int decode_picture(const hevc_ps *ps, const uint8_t *item, size_t item_le
             int end = dec_term(&p->c);
             ctbAddr++;
             int cut_end = !end && ctbAddr == nctb && (g_debug_flags & 4);
-            int row_end = pp->wpp && (ctbAddr % p->wctb) == 0;
+            /* WPP: every CTB row of a tile is a substream (the next CTB in tile scan is on another row) */
+            int row_end = pp->wpp && (ctbAddr == nctb || p->ts2rs[ctbAddr] / p->wctb != ry);
             int tile_end = pp->tiles && ctbAddr < nctb && p->tile_rs[p->ts2rs[ctbAddr]] != p->tile_rs[rs];
             if (end || row_end || tile_end || cut_end) {
                 int ok = 1;

@@ -73,9 +73,11 @@ class SubPicture:
 
 
 def split_tiles(p, nal: bytes) -> List[SubPicture]:
-    """p: the SynthParams the tiled picture was written with (wpp = 0; the
-    slice header has no deblocking override and no loop-filter-across-slices
-    flag, as hevc_synth.c writes it)."""
+    """p: the SynthParams the tiled picture was written with (with or without
+    WPP; the slice header has no deblocking override and no loop-filter-across-
+    slices flag, as hevc_synth.c writes it).  With WPP a tile's CTB rows are
+    its substreams, and a tile alone is a WPP picture of the tile's size (9.3.1:
+    a row syncs with the above-right CTB only inside its tile)."""
     rbsp = _unescape(nal[2:])
     r = _Reader(rbsp)
     assert r.u(1) == 1            # first_slice_segment_in_pic_flag
@@ -105,10 +107,15 @@ def split_tiles(p, nal: bytes) -> List[SubPicture]:
     wctb, hctb = -(-p.width // ctb), -(-p.height // ctb)
     cols = tile_bounds(p.tile_cols, wctb, p.tile_uniform, p.tile_col_w)
     rows = tile_bounds(p.tile_rows, hctb, p.tile_uniform, p.tile_row_h)
-    assert len(starts) - 1 == p.tile_cols * p.tile_rows
+    # substreams in tile scan: one per tile, or with WPP one per CTB row of each tile
+    nsub = [rows[k // p.tile_cols + 1] - rows[k // p.tile_cols] if p.wpp else 1
+            for k in range(p.tile_cols * p.tile_rows)]
+    assert len(starts) - 1 == sum(nsub)
     subs = []
+    s0 = 0
     for k in range(p.tile_cols * p.tile_rows):
         tc, tr = k % p.tile_cols, k // p.tile_cols
+        s1 = s0 + nsub[k]
         x0, y0 = cols[tc] * ctb, rows[tr] * ctb
         w = min(cols[tc + 1] * ctb, p.width) - x0
         h = min(rows[tr + 1] * ctb, p.height) - y0
@@ -124,9 +131,18 @@ def split_tiles(p, nal: bytes) -> List[SubPicture]:
         for f in sao:
             hw.u(f, 1)
         hw.se(qp_delta)
+        if p.wpp:  # the tile's rows keep their sizes as the stand-alone picture's entry points
+            lens = [starts[j + 1] - starts[j] for j in range(s0, s1 - 1)]
+            hw.ue(len(lens))
+            if lens:
+                ln = max(1, (max(lens) - 1).bit_length())
+                hw.ue(ln - 1)
+                for n in lens:
+                    hw.u(n - 1, ln)
         hw.trailing()
-        sub_nal = nal[:2] + _ep(hw.bytes()) + nal[starts[k]:starts[k + 1]]
+        sub_nal = nal[:2] + _ep(hw.bytes()) + nal[starts[s0]:starts[s1]]
         subs.append(SubPicture(x0, y0, sp, sub_nal))
+        s0 = s1
     return subs
 
 

@@ -15,8 +15,8 @@ filters' reach of a tile boundary.
 GPU: the host decodes a tiled picture as one picture per tile
 (heif_amd/csrc/host/batch.cpp); with loop_filter_across_tiles = 1 the tiles
 are children of an assembly picture that k_assemble puts together before the
-loop filters run on it whole (desc.hpp PD_ASSEMBLY).  Tiles together with WPP
-are HEIFGPU_E_UNSUPPORTED.
+loop filters run on it whole (desc.hpp PD_ASSEMBLY).  Tiles together with WPP:
+each tile is a WPP picture whose substreams are the tile's CTB rows.
 """
 import os
 import subprocess
@@ -47,6 +47,14 @@ CASES = [
                              slice_qp_delta=-30, density=80, beta_offset_div2=3, tc_offset_div2=-2)),
     ("c422_3x2", dict(chroma_format=2, tile_cols=3, tile_rows=2)),
     ("c444_2x2_10b", dict(chroma_format=3, bit_depth=10, tile_cols=2, tile_rows=2, scaling_list=1)),
+    # tiles together with WPP: every CTB row of a tile a substream, synced with
+    # the tile's row above (one-CTB-wide tiles never sync), qPY_PREV restarting
+    # at each row of a tile (slice.rs:155-171 reads the entry points for both)
+    ("wpp_3x2", dict(width=256, height=192, tile_cols=3, tile_rows=2, wpp=1)),
+    ("wpp_explicit_1ctb_col_10b", dict(width=200, height=160, bit_depth=10, tile_cols=3, tile_rows=2, tile_uniform=0,
+                                       tile_col_w=(1, 3), tile_row_h=(2,), wpp=1, conf_right=6)),
+    ("wpp_c444_ctb16", dict(chroma_format=3, log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2, tile_cols=2,
+                            tile_rows=2, wpp=1)),
 ]
 
 
@@ -76,7 +84,9 @@ def test_oracle_tiles_equal_standalone_tiles(oracle_mod, name, over):
     for seed in range(3):
         nal = S.picture(p, seed)
         img = oracle_mod.decode_heic(S.single_heic(p, nal=nal))
-        assert checks_ok(img) and len(img.checks) == p.tile_cols * p.tile_rows, (name, seed)
+        ctb = 1 << p.log2_ctb
+        nsub = p.tile_cols * (-(-p.height // ctb)) if p.wpp else p.tile_cols * p.tile_rows
+        assert checks_ok(img) and len(img.checks) == nsub, (name, seed)
         want = _split_decode(oracle_mod, p, nal)
         for got, ref, c in zip((img.y, img.cb, img.cr), want, "YUV"):
             if ref is None:
@@ -124,23 +134,25 @@ def test_oracle_tiles_loop_filter_across(oracle_mod, name, over):
 
 def test_synth_tiled_stream_layout():
     """The generator writes tiles_enabled_flag, the tile layout, one entry
-    point per tile, and refuses tiles with WPP or explicit sizes that leave
-    no CTB for the last column."""
+    point per tile (per CTB row of each tile with WPP), and refuses explicit
+    sizes that leave no CTB for the last column."""
     p = params(dict(tile_cols=3, tile_rows=2))
     subs = split_tiles(p, S.picture(p, 0))
     assert len(subs) == 6
     assert [(s.x0, s.y0) for s in subs] == [(0, 0), (32, 0), (64, 0), (0, 32), (32, 32), (64, 32)]
     assert [(s.params.width, s.params.height) for s in subs][:3] == [(32, 32), (32, 32), (64, 32)]
-    with pytest.raises(ValueError):
-        S.picture(params(dict(tile_cols=2, tile_rows=2, wpp=1)), 0)
+    pw = params(dict(width=128, height=160, tile_cols=2, tile_rows=2, wpp=1))  # 5 CTB rows: tiles of 2 and 3
+    subs = split_tiles(pw, S.picture(pw, 0))
+    assert [(s.x0, s.y0, s.params.height, s.params.wpp) for s in subs] == [
+        (0, 0, 64, 1), (64, 0, 64, 1), (0, 64, 96, 1), (64, 64, 96, 1)]
     with pytest.raises(ValueError):
         S.picture(params(dict(tile_cols=2, tile_rows=1, tile_uniform=0, tile_col_w=(4,))), 0)
 
 
-def test_host_accepts_tiles_rejects_tiles_with_wpp(oracle_mod):
-    """Host parse: tiles with and without loop filtering across them are
-    accepted; tiles + WPP is a valid stream outside this path
-    (UnsupportedError / HEIFGPU_E_UNSUPPORTED) which the oracle also refuses."""
+def test_host_accepts_tiles_and_tiles_with_wpp(oracle_mod):
+    """Host parse: tiles with and without loop filtering across them, and
+    tiles together with WPP, are accepted; a tiles + WPP PPS over slice data
+    with one entry point per tile (not per tile row) is a malformed stream."""
     import heif_amd as H
     import ps_writer as W
 
@@ -148,11 +160,13 @@ def test_host_accepts_tiles_rejects_tiles_with_wpp(oracle_mod):
     inf = H.HeifImage.parse(S.single_heic(p, seed=1)).info
     assert (inf.width, inf.height) == (128, 96)
     H.HeifImage.parse(S.single_heic(params(dict(tile_cols=2, tile_rows=2), across=1), seed=1))
+    H.HeifImage.parse(S.single_heic(params(dict(tile_cols=2, tile_rows=2, wpp=1)), seed=1))
     vps, sps, _ = S.parameter_sets(p)
     pps = W.pps(wpp=1, tiles=dict(cols=2, rows=2))
     both = S.single_heic(p, param_sets=(vps, sps, pps), nal=S.picture(p, 1))
-    with pytest.raises(H.UnsupportedError):
+    with pytest.raises(H.HeifGpuError) as e:
         H.HeifImage.parse(both)
+    assert not isinstance(e.value, H.UnsupportedError)
     # explicit column widths that overrun the picture (4 CTB columns)
     bad = W.pps(wpp=0, tiles=dict(cols=2, rows=1, uniform=0, col_w=(5,), row_h=()))
     with pytest.raises(H.HeifGpuError) as e:
