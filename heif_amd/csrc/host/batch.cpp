@@ -189,15 +189,26 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
             const int pw = ps.sps.pic_width_in_ctbs_y(), ph = ps.sps.pic_height_in_ctbs_y();
             if (ps.pps.tiles_enabled_flag) {
                 // substreams in tile scan: one per tile, or with WPP one per CTB row of each tile
+                // in the slice segment holding the tile (segments of whole tiles, heic_image.cpp)
                 const int ntc = int(ps.col_bd.size()) - 1, ntr = int(ps.row_bd.size()) - 1;
                 const bool wpp = ps.pps.entropy_coding_sync_enabled_flag;
+                size_t seg = 0;
                 int s = 0;
                 for (int ht = 0; ht < ntc * ntr; ++ht) {
                     const int tc = ht % ntc, tr = ht / ntc;
                     const int y0 = ps.row_bd[size_t(tr)], y1 = ps.row_bd[size_t(tr) + 1];
+                    const uint32_t addr = uint32_t(y0 * pw + ps.col_bd[size_t(tc)]);
+                    if (seg + 1 < tj.segs.size() && tj.segs[seg + 1].sh.slice_segment_address == addr) {
+                        ++seg;
+                        s = 0;
+                    }
                     const int n = wpp ? y1 - y0 : 1;
-                    subs_of.push_back({ps.col_bd[size_t(tc)], y0, ps.col_bd[size_t(tc) + 1], y1, 0, 1, s, s + n,
-                                       ht + 1 < ntc * ntr});
+                    if (s + n > tj.segs[seg].sh.num_entry_point_offsets + 1)
+                        throw HeifError("slice segment without one entry point per tile (per tile row with WPP)");
+                    // a tile other than its segment's last ends in end_of_subset_one_bit
+                    const bool seg_last = s + n == tj.segs[seg].sh.num_entry_point_offsets + 1;
+                    subs_of.push_back({ps.col_bd[size_t(tc)], y0, ps.col_bd[size_t(tc) + 1], y1, seg, 1, s, s + n,
+                                       !seg_last});
                     s += n;
                 }
             } else {

@@ -1,6 +1,7 @@
 // heic_image.cpp — see heic_image.hpp.
 #include "heic_image.hpp"
 
+#include <algorithm>
 #include <map>
 
 namespace hg {
@@ -31,7 +32,9 @@ void check_supported(const SequenceParameterSet &s, const PictureParameterSet &p
 // slice's header values (7.4.7.1), copied in here.  The GPU path decodes
 // several slices as one sub-picture per slice (batch.cpp), so every segment
 // must start at a CTB row (a slice's dependent segments are concatenated);
-// HEVC tiles must come with a single segment.  Loop filtering across the
+// with HEVC tiles every segment must start at a tile (slices of whole tiles,
+// each tile a sub-picture with its slice's values) and nothing is filtered
+// across the tiles.  Loop filtering across the
 // slices' boundaries is either off for all (independent sub-pictures) or on
 // for all, with one set of deblocking values (sub-pictures of an assembly
 // filtered whole).
@@ -60,7 +63,18 @@ void check_segments(TileJob &job, const ParamSet &ps) {
         if (k > 0 && sh.slice_segment_address <= job.segs[k - 1].sh.slice_segment_address)
             throw HeifError("slice segments out of order");
         if (k == 0) continue;
-        if (pps.tiles_enabled_flag) throw UnsupportedError("several slice segments together with HEVC tiles");
+        if (pps.tiles_enabled_flag) {
+            // slices of whole tiles (7.4.7.1 allows that or tiles of whole slices): each
+            // tile decodes with its slice's header values; nothing may be filtered across
+            const uint32_t x = sh.slice_segment_address % pw, y = sh.slice_segment_address / pw;
+            const bool at_tile = std::find(ps.col_bd.begin(), ps.col_bd.end(), int(x)) != ps.col_bd.end() &&
+                                 std::find(ps.row_bd.begin(), ps.row_bd.end(), int(y)) != ps.row_bd.end();
+            if (!at_tile)
+                throw UnsupportedError("several slice segments together with HEVC tiles (a segment starting inside a tile)");
+            if (pps.loop_filter_across_tiles_enabled_flag)
+                throw UnsupportedError("several slice segments together with HEVC tiles filtered across tiles");
+            continue;
+        }
         if (sh.slice_segment_address % pw) throw UnsupportedError("a slice segment starting inside a CTB row");
         if (sh.dependent_slice_segment_flag) continue;  // the loop-filter rules below are per slice
         size_t second = 1;  // the second slice
@@ -80,7 +94,9 @@ void check_segments(TileJob &job, const ParamSet &ps) {
     const size_t nsub_tiles = pps.entropy_coding_sync_enabled_flag
                                   ? (ps.col_bd.size() - 1) * size_t(sps.pic_height_in_ctbs_y())
                                   : ntiles;
-    if (pps.tiles_enabled_flag && size_t(job.segs[0].sh.num_entry_point_offsets) + 1 != nsub_tiles)
+    size_t nsub_segs = 0;
+    for (const SliceSeg &g : job.segs) nsub_segs += size_t(g.sh.num_entry_point_offsets) + 1;
+    if (pps.tiles_enabled_flag && nsub_segs != nsub_tiles)
         throw HeifError("tiled picture without one entry point per tile (per tile row with WPP)");
     if (pps.entropy_coding_sync_enabled_flag && !pps.tiles_enabled_flag)
         for (size_t k = 0; k < job.segs.size(); ++k) {

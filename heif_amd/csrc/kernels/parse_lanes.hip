@@ -2651,6 +2651,10 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
     // wave index made scalar: every value of the substream state derives from uniform inputs, so the
     // compiler can keep the engine in SGPRs and branch with s_cbranch
     const int w = Spread ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = (int)threadIdx.x & 63;
+#if defined(HG_SOLO_SETPRIO)
+    // tuning: the substream chain wins issue arbitration against k_intra_stream's waves on its SIMD
+    __builtin_amdgcn_s_setprio(HG_SOLO_SETPRIO);
+#endif
     if (threadIdx.x < 15) s_seq[threadIdx.x] = sig_seq((int)threadIdx.x);
     if (threadIdx.x < 64) s_prog[threadIdx.x] = 0;
     const uint64_t trow = state_row(lane);

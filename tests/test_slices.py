@@ -21,7 +21,8 @@ segment ends or, without WPP, where the engine runs on); when every slice is
 filtered across its upper boundary (one set of deblocking values) the slices
 are children of an assembly picture filtered whole (desc.hpp PD_ASSEMBLY).
 Segments starting inside a CTB row, filtering across some slice boundaries
-only and several segments with HEVC tiles are HEIFGPU_E_UNSUPPORTED.
+only and segments starting inside an HEVC tile are HEIFGPU_E_UNSUPPORTED;
+slices of whole tiles decode as one sub-picture per tile.
 """
 import os
 import subprocess
@@ -75,6 +76,19 @@ DEP_CASES = [
     ("dep_crop_10b_dbk", dict(width=200, height=120, conf_right=6, conf_bottom=2, bit_depth=10, slice_ctus=14,
                               slice_dependent=1, wpp=1, slice_dbk_vary=1)),
     ("dep_alt_across", dict(width=128, height=192, slice_ctus=4, slice_dependent=2, wpp=1, slice_lf_across=1)),
+]
+
+
+# slices of whole HEVC tiles (7.4.7.1's other option than tiles of whole slices):
+# each tile a sub-picture with its own slice's header values (QP, SAO flags,
+# deblocking), independent and dependent segments, with and without WPP;
+# nothing filtered across tiles (256x192, CTB 32: 8x6 CTBs)
+TILE_SLICE_CASES = [
+    ("tile_per_slice_dbk", dict(width=256, height=192, tile_cols=2, tile_rows=2, slice_ctus=12, slice_dbk_vary=1)),
+    ("two_tiles_per_slice_dep_wpp", dict(width=256, height=192, tile_cols=2, tile_rows=2, slice_ctus=24,
+                                         slice_dependent=2, wpp=1)),
+    ("cols4_dependent_10b", dict(width=256, height=192, tile_cols=4, tile_rows=1, slice_ctus=12, slice_dependent=1,
+                                 bit_depth=10)),
 ]
 
 
@@ -173,6 +187,18 @@ def test_host_rejects_unsupported_slice_layouts(over, why):
         H.HeifImage.parse(S.single_heic(params(over), seed=1))
 
 
+@pytest.mark.parametrize("name,over", TILE_SLICE_CASES, ids=[c[0] for c in TILE_SLICE_CASES])
+def test_oracle_and_host_take_slices_of_whole_tiles(oracle_mod, name, over):
+    """Slices of whole tiles: every substream of every segment ends at its
+    entry point in the oracle, and the host accepts the layout."""
+    import heif_amd as H
+
+    d = S.single_heic(params(over), seed=3)
+    img = oracle_mod.decode_heic(d)
+    assert img.checks and all(c["term_ok"] for c in img.checks), name
+    H.HeifImage.parse(d)
+
+
 def test_host_rejects_segments_out_of_order():
     import heif_amd as H
     import struct
@@ -210,6 +236,17 @@ def test_emulated_kernels_slices(emu_check, tmp_path, name, across, parse):
     p = params({**dict(ROW_CASES + DEP_CASES)[name], "slice_lf_across": across})
     path = tmp_path / "s.heic"
     path.write_bytes(S.single_heic(p, seed=5))
+    r = subprocess.run([emu_check, str(path), "5"], capture_output=True, text=True, timeout=600,
+                       env={**os.environ, "HEIFGPU_PARSE": parse})
+    assert r.returncode == 0 and "EMU PARITY OK" in r.stdout + r.stderr, (r.stdout + r.stderr)[-2000:]
+
+
+@pytest.mark.parametrize("parse", ["lanes", "solo", "spread"])
+@pytest.mark.parametrize("name", [c[0] for c in TILE_SLICE_CASES])
+def test_emulated_kernels_slices_of_tiles(emu_check, tmp_path, name, parse):
+    """Slices of whole tiles through the kernels compiled for the host, bit-exact vs the oracle."""
+    path = tmp_path / "t.heic"
+    path.write_bytes(S.single_heic(params(dict(TILE_SLICE_CASES)[name]), seed=5))
     r = subprocess.run([emu_check, str(path), "5"], capture_output=True, text=True, timeout=600,
                        env={**os.environ, "HEIFGPU_PARSE": parse})
     assert r.returncode == 0 and "EMU PARITY OK" in r.stdout + r.stderr, (r.stdout + r.stderr)[-2000:]
@@ -267,5 +304,24 @@ def test_gpu_row_slices_bit_exact(H, oracle_mod, parse):
         assert not any(b.status()), (depth, chroma)
         for k, (d, o) in enumerate(zip(datas, outs)):
             _assert_equal(_planes(o), oracle_mod.decode_heic(d, with_checks=False), (depth, chroma, k))
+        b.free()
+    ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parse", ["lanes", "spread"])
+def test_gpu_slices_of_tiles_bit_exact(H, oracle_mod, parse):
+    """Slices of whole tiles on the GPU, two seeds per case, against the oracle."""
+    ctx = H.DecodeContext(0)
+    for depth in (8, 10):
+        datas = [S.single_heic(params(over), seed=s) for _, over in TILE_SLICE_CASES
+                 for s in (1, 2) if params(over).bit_depth == depth]
+        imgs = [H.HeifImage.parse(d) for d in datas]
+        b = ctx.prepare(imgs, parse=parse)
+        outs = ctx.alloc_outputs(imgs)
+        b.decode_async(outs)
+        assert not any(b.status()), depth
+        for k, (d, o) in enumerate(zip(datas, outs)):
+            _assert_equal(_planes(o), oracle_mod.decode_heic(d, with_checks=False), (depth, k))
         b.free()
     ctx.close()
