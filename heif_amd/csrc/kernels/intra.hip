@@ -1025,9 +1025,6 @@ hipError_t launch_intra(const BatchArgs &a0, hipStream_t s) {
 }
 #endif
 
-// Streaming reconstruction (k_intra_stream beside the spread parse) for the
-// small batches where everything it and the parse need is resident at once
-// (up to 96 pictures: two 4032x3024 images); HEIFGPU_STREAM=0 turns it off.
 // k_intra_stream's patience: how long (us) the first launch waits without
 // parse progress before it gives a picture up to the second launch.
 // HEIFGPU_STREAM_PATIENCE_US overrides (0: give every picture up, a test knob).
@@ -1043,10 +1040,15 @@ bool intra_fused_default() {
     return e && std::atoi(e) != 0;
 }
 
+// Streaming reconstruction (k_intra_stream beside the spread parse) for the
+// small batches (up to 192 pictures: four 4032x3024 images, kStreamMaxPics);
+// HEIFGPU_STREAM=0 turns it off.
 bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly) {
     const char *e = std::getenv("HEIFGPU_STREAM");
     if (e && std::atoi(e) == 0) return false;
-    return parse_mode == PARSE_SPREAD && !has_assembly && n_pics > 0 && n_pics <= kStreamMaxPics;
+    const char *m = std::getenv("HEIFGPU_STREAM_MAX_PICS");  // (tuning)
+    const int max_pics = m && *m ? std::atoi(m) : kStreamMaxPics;
+    return parse_mode == PARSE_SPREAD && !has_assembly && n_pics > 0 && n_pics <= max_pics;
 }
 
 }  // namespace hg

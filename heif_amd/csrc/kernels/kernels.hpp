@@ -118,7 +118,9 @@ constexpr int kSoloMaxWaves = 16;
 int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
                       const float *cost = nullptr, bool jobs = false);
 // k_intra_stream (reconstruction behind the spread parse, k_transform folded in) for this batch
-constexpr int kStreamMaxPics = 96;
+// (same box, spread, one-decode latency: 4 images 28.3 vs 33.7 ms streamed; 8
+// images 44.4 vs 40.5, the reconstruction no longer keeps up with the parse)
+constexpr int kStreamMaxPics = 192;
 bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly);
 // k_intra_stream's patience (us) before its first launch gives a picture up to the second
 uint32_t stream_patience_us();
