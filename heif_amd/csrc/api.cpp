@@ -56,17 +56,26 @@ struct heifgpu_ctx {
     int device = 0;
     bool timing = false;
     hipStream_t parse = nullptr, xform = nullptr, recon = nullptr, upload = nullptr;
+    // k_rbsp of the next decode (its parse set's RBSP and zeroed words) beside the
+    // running parse instead of in front of the next one on the parse stream
+    hipStream_t prep = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    // timing ring, one slot per timed decode call: rbsp start, rbsp end = parse
-    // start, parse end, transform start, transform end, recon start, 3 stage
-    // ends.  heifgpu_stage_times folds every call since the previous query (a
+    // timing ring, one slot per timed decode call: rbsp start, rbsp end, parse
+    // end, transform start, transform end, recon start, 3 stage ends, parse
+    // start.  heifgpu_stage_times folds every call since the previous query (a
     // slot about to be reused is folded first).
-    hipEvent_t tev[kTimingSlots][9] = {};
+    hipEvent_t tev[kTimingSlots][10] = {};
     int timed_calls = 0, folded = 0;
     double acc[6] = {};
 };
 
 namespace {
+// k_rbsp on its own stream (HEIFGPU_PREP_STREAM=0/1, read at context creation)
+bool prep_stream_default() {
+    const char *e = std::getenv("HEIFGPU_PREP_STREAM");
+    return e && std::atoi(e) != 0;
+}
+
 // adds the stage times of the decode call recorded in `slot` to ctx->acc
 hipError_t fold_timing(heifgpu_ctx *ctx, int slot) {
     hipEvent_t *e = ctx->tev[slot];
@@ -75,7 +84,7 @@ hipError_t fold_timing(heifgpu_ctx *ctx, int slot) {
     float t = 0.f;
     if ((r = hipEventElapsedTime(&t, e[0], e[1])) != hipSuccess) return r;
     ctx->acc[5] += t;  // k_rbsp
-    if ((r = hipEventElapsedTime(&t, e[1], e[2])) != hipSuccess) return r;
+    if ((r = hipEventElapsedTime(&t, e[9], e[2])) != hipSuccess) return r;
     ctx->acc[0] += t;  // k_parse
     if ((r = hipEventElapsedTime(&t, e[3], e[4])) != hipSuccess) return r;
     ctx->acc[1] += t;  // k_transform
@@ -167,13 +176,18 @@ struct ParseSet {
     // because k_intra_stream of this set's decode polls them while the next
     // decode's parse already runs
     DevBuf<uint32_t> xprog, xntu;
-    hipEvent_t parsed = nullptr, transformed = nullptr, recon_done = nullptr, progreset = nullptr;
+    // k_rbsp's output, per set so that the next decode's k_rbsp can run while
+    // this set's parse still reads it
+    DevBuf<uint8_t> rbsp;
+    DevBuf<uint32_t> rsubs;
+    hipEvent_t parsed = nullptr, transformed = nullptr, recon_done = nullptr, progreset = nullptr, prepped = nullptr;
     bool pending = false;  // recon_done recorded and not yet waited for by a parse
     ~ParseSet() {
         if (parsed) (void)hipEventDestroy(parsed);
         if (transformed) (void)hipEventDestroy(transformed);
         if (recon_done) (void)hipEventDestroy(recon_done);
         if (progreset) (void)hipEventDestroy(progreset);
+        if (prepped) (void)hipEventDestroy(prepped);
     }
 };
 
@@ -205,8 +219,8 @@ struct heifgpu_batch {
     bool loaded = false;
     BatchArgs args{};
     // read by k_rbsp / the parse only: a reload waits for the parses in flight
-    DevBuf<uint8_t> bits, rbsp;
-    DevBuf<uint32_t> subs, rsubs, porder;
+    DevBuf<uint8_t> bits;
+    DevBuf<uint32_t> subs, porder;
     DevBuf<uint8_t> xctx;
     // the sample arena: written by k_intra, which runs after every earlier
     // decode's k_sao_out on the one recon stream
@@ -475,6 +489,7 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     HIP_TRY(hipStreamCreateWithPriority(&c->xform, hipStreamNonBlocking, rprio ? greatest : least));
     HIP_TRY(hipStreamCreateWithPriority(&c->recon, hipStreamNonBlocking, rprio ? greatest : least));
     HIP_TRY(hipStreamCreateWithFlags(&c->upload, hipStreamNonBlocking));
+    if (prep_stream_default()) HIP_TRY(hipStreamCreateWithFlags(&c->prep, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&c->fork, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->join, hipEventDisableTiming));
     for (auto &row : c->tev)
@@ -496,6 +511,7 @@ void heifgpu_destroy(heifgpu_ctx *ctx) {
     if (ctx->xform) (void)hipStreamDestroy(ctx->xform);
     if (ctx->recon) (void)hipStreamDestroy(ctx->recon);
     if (ctx->upload) (void)hipStreamDestroy(ctx->upload);
+    if (ctx->prep) (void)hipStreamDestroy(ctx->prep);
     delete ctx;
 }
 
@@ -569,6 +585,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].transformed, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].recon_done, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&b->set[k].progreset, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&b->set[k].prepped, hipEventDisableTiming));
         }
         for (DescGen &g : b->gen) HIP_TRY(hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
     }
@@ -607,7 +624,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
                                         mode == PARSE_SOLO ? 1 : ppw_req, order, by_bytes ? nullptr : cost.data(),
                                         mode == PARSE_LANES && lanes_jobs_default());
     }
-    const bool grows = (order.size() > b->porder.cap || hb.bits_size > b->bits.cap || hb.pics.size() > G.pics.cap ||
+    const bool grows = (order.size() > b->porder.cap || hb.bits_size > b->bits.cap || hb.bits_size > b->set[0].rbsp.cap || hb.pics.size() > G.pics.cap ||
                                      hb.subs.size() > b->subs.cap || hb.seqs.size() > G.seqs.cap ||
                                      hb.sf.size() > G.sf.cap || n > G.outs.cap || hb.recon_bytes > b->recon.cap ||
                                      hb.resid_elems > b->set[0].resid.cap || hb.tu_n > b->set[0].tus.cap ||
@@ -628,8 +645,6 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     HIP_TRY(b->bits.alloc(hb.bits_size));
     HIP_TRY(G.pics.alloc(hb.pics.size()));
     HIP_TRY(b->subs.alloc(hb.subs.size()));
-    HIP_TRY(b->rbsp.alloc(hb.bits_size));
-    HIP_TRY(b->rsubs.alloc(hb.subs.size()));
     HIP_TRY(G.seqs.alloc(hb.seqs.size()));
     HIP_TRY(G.sf.alloc(hb.sf.size()));
     HIP_TRY(G.outs.alloc(n));
@@ -644,6 +659,8 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         HIP_TRY(ps.sao.alloc(hb.sao_n));
         HIP_TRY(ps.status.alloc(hb.pics.size()));
         HIP_TRY(ps.resid.alloc(hb.resid_elems));  // (each decode zeroes its set's status before the parse)
+        HIP_TRY(ps.rbsp.alloc(hb.bits_size));
+        HIP_TRY(ps.rsubs.alloc(hb.subs.size()));
     }
     HIP_TRY(b->recon.alloc(hb.recon_bytes));
     HIP_TRY(b->porder.alloc(order.size()));
@@ -700,7 +717,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         }
         off += (g.bytes + 255) & ~size_t(255);
     }
-    HIP_TRY(hipMemsetAsync(b->rbsp.p, 0, hb.bits_size, ctx->upload));
+    for (int k = 0; k < b->n_sets; ++k) HIP_TRY(hipMemsetAsync(b->set[k].rbsp.p, 0, hb.bits_size, ctx->upload));
     HIP_TRY(hipEventRecord(b->uploaded, ctx->upload));
     b->n_images = n;
     b->tile_stride = stride;
@@ -715,8 +732,8 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.bits = b->bits.p;
     a.pics = G.pics.p;
     a.subs = b->subs.p;
-    a.rbsp = b->rbsp.p;
-    a.rsubs = b->rsubs.p;
+    a.rbsp = nullptr;  // (per parse set: heifgpu_batch_decode)
+    a.rsubs = nullptr;
     a.parse_order = b->porder.p;
     a.n_slots = int(order.size());
     a.parse_group = parse_group;
@@ -798,6 +815,8 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     a.sao = ps.sao.p;
     a.status = ps.status.p;
     a.resid = ps.resid.p;
+    a.rbsp = ps.rbsp.p;
+    a.rsubs = ps.rsubs.p;
     if (a.parse_mode == PARSE_SPREAD) {
         a.xprog = ps.xprog.p;
         a.xntu = a.intra_stream ? ps.xntu.p : nullptr;
@@ -838,17 +857,25 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         ev = ctx->tev[slot];
         ++ctx->timed_calls;
     }
-    // parse stream: the batch's uploads, and this set's previous reconstruction must be done with it
-    HIP_TRY(hipStreamWaitEvent(p, b->uploaded, 0));
-    if (ps.pending) HIP_TRY(hipStreamWaitEvent(p, ps.recon_done, 0));
-    // k_rbsp also zeroes this set's status words and row counts (rows a stopped
-    // substream never reaches keep zero TBs) and, streaming, the progress words,
-    // TU counts and done words k_intra_stream polls from its start (launch_parse
-    // leaves them alone in that mode)
-    if (t) HIP_TRY(hipEventRecord(ev[0], p));
-    HIP_TRY(launch_rbsp(a, p));
-    if (a.intra_stream) HIP_TRY(hipEventRecord(ps.progreset, p));
-    if (t) HIP_TRY(hipEventRecord(ev[1], p));
+    // k_rbsp (prep stream, or the parse stream itself): the batch's uploads, and
+    // this set's previous reconstruction must be done with it.  It also zeroes
+    // this set's status words and row counts (rows a stopped substream never
+    // reaches keep zero TBs) and, streaming, the progress words, TU counts and
+    // done words k_intra_stream polls from its start (launch_parse leaves them
+    // alone in that mode).  On the prep stream it runs beside the previous
+    // decode's parse, so the parse stream goes from one k_parse to the next.
+    hipStream_t q = ctx->prep ? ctx->prep : p;
+    HIP_TRY(hipStreamWaitEvent(q, b->uploaded, 0));
+    if (ps.pending) HIP_TRY(hipStreamWaitEvent(q, ps.recon_done, 0));
+    if (t) HIP_TRY(hipEventRecord(ev[0], q));
+    HIP_TRY(launch_rbsp(a, q));
+    if (a.intra_stream) HIP_TRY(hipEventRecord(ps.progreset, q));
+    if (t) HIP_TRY(hipEventRecord(ev[1], q));
+    if (q != p) {
+        HIP_TRY(hipEventRecord(ps.prepped, q));
+        HIP_TRY(hipStreamWaitEvent(p, ps.prepped, 0));
+    }
+    if (t) HIP_TRY(hipEventRecord(ev[9], p));
     HIP_TRY(launch_parse(a, p));
     if (t) HIP_TRY(hipEventRecord(ev[2], p));
     HIP_TRY(hipEventRecord(ps.parsed, p));
