@@ -116,6 +116,27 @@ def test_halfmoonbay_streaming_modes(H, ctx, oracle_halfmoonbay, halfmoonbay, mo
         assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("parse", ["lanes", "spread"])
+def test_prep_stream_option(H, oracle_halfmoonbay, halfmoonbay, monkeypatch, parse):
+    """HEIFGPU_PREP_STREAM=1 (read when a context is created): k_rbsp of each
+    decode on its own stream, into the decode's parse set; three pipelined
+    decodes (every set once) stay bit-exact with status 0."""
+    monkeypatch.setenv("HEIFGPU_PREP_STREAM", "1")
+    c = H.DecodeContext(0)
+    try:
+        img = H.HeifImage.parse(halfmoonbay)
+        b = c.prepare([img], parse=parse)
+        out = c.alloc_outputs([img])
+        for _ in range(3):
+            b.decode_async(out)
+        assert b.status() == [0]
+        b.free()
+        for got, want in zip(planes_np(out[0]), (oracle_halfmoonbay.y, oracle_halfmoonbay.cb, oracle_halfmoonbay.cr)):
+            assert np.array_equal(got, want)
+    finally:
+        c.close()
+
+
 def check_permuted(outs, seeds, oracle_tiles):
     """Every image of a permuted batch, tile window by tile window against the
     oracle's 48 tile decodes placed by the image's permutation (the per-tile
