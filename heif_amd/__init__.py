@@ -314,11 +314,32 @@ class DeviceBatch:
             _lib.check(rc)
         return list(st)
 
+    def status_previous(self, stream: Optional[int] = None) -> List[int]:
+        """Per-image status of the load before the current one (its decodes
+        that were in flight at the reload), read and cleared
+        (heifgpu_batch_status_previous); [] if there was no previous load."""
+        torch = self.ctx._torch
+        if stream is None:
+            stream = torch.cuda.current_stream(self.ctx.device).cuda_stream
+        n = ctypes.c_size_t()
+        rc = lib.heifgpu_batch_status_previous(self.ctx._h, self._h, None, 0, ctypes.byref(n),
+                                               ctypes.c_void_p(stream))
+        if n.value == 0:
+            _lib.check(rc)
+            return []
+        st = (ctypes.c_uint32 * n.value)()
+        rc = lib.heifgpu_batch_status_previous(self.ctx._h, self._h, st, n.value, ctypes.byref(n),
+                                               ctypes.c_void_p(stream))
+        if rc not in (_lib.HEIFGPU_OK, _lib.HEIFGPU_E_DECODE):
+            _lib.check(rc)
+        return list(st)
+
     def parse_geometry(self) -> dict:
         """The CABAC parse launch of this batch (heifgpu_batch_parse_geometry)."""
         v = [ctypes.c_uint32() for _ in range(4)]
         _lib.check(lib.heifgpu_batch_parse_geometry(self._h, *[ctypes.byref(x) for x in v]))
-        mode = {_lib.PARSE_LANES: "lanes", _lib.PARSE_SOLO: "solo", _lib.PARSE_SPREAD: "spread"}[v[0].value]
+        mode = {_lib.PARSE_LANES: "lanes", _lib.PARSE_SOLO: "solo", _lib.PARSE_SPREAD: "spread",
+                _lib.PARSE_ROWS: "rows"}[v[0].value]
         return {"mode": mode, "workgroups": v[1].value, "pics_per_wave": v[2].value,
                 "waves_per_workgroup": v[3].value}
 

@@ -121,8 +121,9 @@ class IpcHandle(ctypes.Structure):
     _fields_ = [("handle", ctypes.c_uint8 * 64), ("offset", ctypes.c_uint64)]
 
 
-PARSE_AUTO, PARSE_LANES, PARSE_SOLO, PARSE_SPREAD = 0, 1, 2, 3
-PARSE_MODES = {"auto": PARSE_AUTO, "lanes": PARSE_LANES, "solo": PARSE_SOLO, "spread": PARSE_SPREAD}
+PARSE_AUTO, PARSE_LANES, PARSE_SOLO, PARSE_SPREAD, PARSE_ROWS = 0, 1, 2, 3, 4
+PARSE_MODES = {"auto": PARSE_AUTO, "lanes": PARSE_LANES, "solo": PARSE_SOLO, "spread": PARSE_SPREAD,
+               "rows": PARSE_ROWS}
 
 
 # every symbol include/heifgpu.h declares (checked by tests/test_abi.py)
@@ -135,7 +136,7 @@ EXPORTS = (
     "heifgpu_bins_coeff_abs_level_remaining", "heifgpu_bins_exp_golomb", "heifgpu_image_tile_params", "heifgpu_debug_counters",
     "heifgpu_image_parse_item", "heifgpu_ycbcr_to_rgb", "heifgpu_batch_prepare_ex", "heifgpu_gather_tiles",
     "heifgpu_image_parse_many", "heifgpu_batch_parse_geometry", "heifgpu_ipc_export", "heifgpu_ipc_open",
-    "heifgpu_ipc_close",
+    "heifgpu_ipc_close", "heifgpu_batch_status_previous", "heifgpu_abi_version",
 )
 
 
@@ -182,6 +183,8 @@ def _load() -> ctypes.CDLL:
         "heifgpu_batch_prepare": (I32, [VP, P(VP), SZ, P(VP)]),
         "heifgpu_batch_decode": (I32, [VP, VP, P(Planes), VP]),
         "heifgpu_batch_status": (I32, [VP, VP, P(U32), VP]),
+        "heifgpu_batch_status_previous": (I32, [VP, VP, P(U32), SZ, P(SZ), VP]),
+        "heifgpu_abi_version": (I32, []),
         "heifgpu_batch_free": (None, [VP]),
         "heifgpu_set_timing": (I32, [VP, I32]),
         "heifgpu_stage_times": (I32, [VP, P(ctypes.c_float)]),

@@ -31,7 +31,7 @@ static_assert(sizeof(heifgpu_planes) == 40, "heifgpu_planes: 3 pointers + 3 int3
 static_assert(sizeof(heifgpu_batch_opts) == 20, "heifgpu_batch_opts: 5 x uint32");
 static_assert(sizeof(heifgpu_ipc_handle) == 72, "heifgpu_ipc_handle: 64-byte HIP handle + uint64 offset");
 static_assert(HEIFGPU_PARSE_AUTO == PARSE_AUTO && HEIFGPU_PARSE_LANES == PARSE_LANES && HEIFGPU_PARSE_SOLO == PARSE_SOLO &&
-                  HEIFGPU_PARSE_SPREAD == PARSE_SPREAD,
+                  HEIFGPU_PARSE_SPREAD == PARSE_SPREAD && HEIFGPU_PARSE_ROWS == PARSE_ROWS,
               "parse modes");
 static_assert(sizeof(heifgpu_tile_params) == 55 * 4 + 64 * 4, "heifgpu_tile_params: 55 int32 + 64 uint32");
 
@@ -44,8 +44,9 @@ static_assert(sizeof(heifgpu_tile_params) == 55 * 4 + 64 * 4, "heifgpu_tile_para
 // which writes the caller's planes and so waits for everything the caller
 // enqueued on its stream before the call; the caller's stream waits for
 // k_sao_out.  A set is reused only after the reconstruction that read it.
-// HEIFGPU_PIPELINE=0 keeps one set (no overlap), 2 two sets on two streams;
-// the default, 3, uses three sets and a third stream for k_transform, so
+// HEIFGPU_PIPELINE=0 or 1 keeps one set (no overlap), 2 two sets on two
+// streams (before r04 every value but 0 and 3 meant two); the default, 3 (or
+// more), uses three sets and a third stream for k_transform, so
 // parse n + 2, transform n + 1 and reconstruction n overlap.  While the parse
 // was the critical path (r02) three sets lost (15.32 / 15.33 vs 15.67 / 15.64
 // Gpix/s); since the r03 parse got faster the reconstruction stream sets the
@@ -70,6 +71,11 @@ struct heifgpu_ctx {
 };
 
 namespace {
+// per-set words of the spread and rows parses: one progress word per CTB row, then the job counter
+size_t xprog_words(const HostBatch &hb) { return size_t(hb.rows) + 1; }
+// k_intra_stream: one TU count per CTB row, then one done word per picture (+ 1 spare)
+size_t xntu_words(const HostBatch &hb) { return size_t(hb.rows) + hb.pics.size() + 1; }
+
 // k_rbsp on its own stream (HEIFGPU_PREP_STREAM=0/1, read at context creation)
 bool prep_stream_default() {
     const char *e = std::getenv("HEIFGPU_PREP_STREAM");
@@ -204,6 +210,11 @@ struct DescGen {
     std::vector<OutImage> out_host;
     hipEvent_t done = nullptr;  // the last decode that read this generation (recon stream)
     bool pending = false;
+    // the load this generation holds: picture -> image, image count (heifgpu_batch_status_previous
+    // maps the sticky words of the load before the current one with these)
+    std::vector<uint32_t> pic_image;
+    size_t n_images = 0;
+    bool loaded = false;
     ~DescGen() {
         if (done) (void)hipEventDestroy(done);
     }
@@ -545,7 +556,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     const uint32_t offset = opts ? opts->tile_offset : 0u;
     if (offset >= stride) return fail(HEIFGPU_E_INVALID, "tile_offset must be below tile_stride");
     const uint32_t mode_req = opts ? opts->parse_mode : 0u;
-    if (mode_req > HEIFGPU_PARSE_SPREAD) return fail(HEIFGPU_E_INVALID, "parse_mode");
+    if (mode_req > HEIFGPU_PARSE_ROWS) return fail(HEIFGPU_E_INVALID, "parse_mode");
     const int ppw_req = opts ? int(std::min<uint32_t>(opts->pics_per_wave, 64u)) : 0;
     if (*inout && (*inout)->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
     HIP_TRY(hipSetDevice(ctx->device));
@@ -611,6 +622,8 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     if (mode == PARSE_SPREAD) {
         if (spread_parse_order(hb.pics.data(), int(hb.pics.size()), order) < 0)
             return fail(HEIFGPU_E_UNSUPPORTED, "spread parse: over 2^20 pictures or 4096 substreams per picture");
+    } else if (mode == PARSE_ROWS) {
+        parse_group = rows_parse_order(hb.pics.data(), int(hb.pics.size()), order);
     } else {
         // deal pictures by payload size; HEIFGPU_PARSE_COST=chain deals by their WPP critical
         // path instead (A/B r03, 128 images: 16,911 / 16,863 vs 17,002 / 16,950 Mpix/s by bytes)
@@ -624,6 +637,9 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
                                         mode == PARSE_SOLO ? 1 : ppw_req, order, by_bytes ? nullptr : cost.data(),
                                         mode == PARSE_LANES && lanes_jobs_default());
     }
+    // spread and rows parses: WPP neighbours in other waves (progress words,
+    // context hand-off blocks, the job counter after the progress words)
+    const bool cross_rows = mode == PARSE_SPREAD || mode == PARSE_ROWS;
     const bool grows = (order.size() > b->porder.cap || hb.bits_size > b->bits.cap || hb.bits_size > b->set[0].rbsp.cap || hb.pics.size() > G.pics.cap ||
                                      hb.subs.size() > b->subs.cap || hb.seqs.size() > G.seqs.cap ||
                                      hb.sf.size() > G.sf.cap || n > G.outs.cap || hb.recon_bytes > b->recon.cap ||
@@ -631,8 +647,8 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
                                      hb.coef_n > b->set[0].coefs.cap || hb.map_bytes > b->set[0].maps.cap ||
                                      hb.sao_n > b->set[0].sao.cap || 2 * size_t(hb.rows) > b->set[0].row_counts.cap ||
                                      hb.pics.size() > b->set[0].status.cap || hb.pics.size() > G.sticky.cap ||
-                                     (mode == PARSE_SPREAD && (hb.rows > b->set[0].xprog.cap || hb.rows + hb.pics.size() > b->set[0].xntu.cap ||
-                                                               hb.rows * CTX_PAD > b->xctx.cap)));
+                                     (cross_rows && (xprog_words(hb) > b->set[0].xprog.cap || hb.rows * CTX_PAD > b->xctx.cap)) ||
+                                     (mode == PARSE_SPREAD && xntu_words(hb) > b->set[0].xntu.cap));
     if (grows) {  // reallocation: every decode of the old contents fully drained
         for (int k = 0; k < b->n_sets; ++k)
             if (b->set[k].pending) HIP_TRY(hipEventSynchronize(b->set[k].recon_done));
@@ -664,10 +680,10 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     }
     HIP_TRY(b->recon.alloc(hb.recon_bytes));
     HIP_TRY(b->porder.alloc(order.size()));
-    if (mode == PARSE_SPREAD) {  // per-row WPP progress words and context hand-off blocks
+    if (cross_rows) {  // per-row WPP progress words (+ the job counter) and context hand-off blocks
         for (int k = 0; k < b->n_sets; ++k) {
-            HIP_TRY(b->set[k].xprog.alloc(std::max<size_t>(hb.rows, 1)));
-            HIP_TRY(b->set[k].xntu.alloc(hb.rows + hb.pics.size() + 1));  // TU counts, then k_intra_stream's done words
+            HIP_TRY(b->set[k].xprog.alloc(xprog_words(hb)));
+            if (mode == PARSE_SPREAD) HIP_TRY(b->set[k].xntu.alloc(xntu_words(hb)));
         }
         HIP_TRY(b->xctx.alloc(std::max<size_t>(hb.rows, 1) * CTX_PAD));
     }
@@ -724,6 +740,9 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     b->tile_offset = offset;
     b->infos = std::move(infos);
     b->pic_image = hb.pic_image;
+    G.pic_image = hb.pic_image;
+    G.n_images = n;
+    G.loaded = true;
     b->n_pics = int(hb.pics.size());
     b->cur = gi;
     b->loaded = true;
@@ -752,7 +771,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.lane_jobs = mode == PARSE_LANES && lanes_jobs_default() ? 1 : 0;
     a.lf_tiles = lf_tiles_for(hb.pics.data(), int(hb.pics.size()), hb.seqs.data());
     a.xprog = nullptr;  // (per parse set: heifgpu_batch_decode)
-    a.xctx = mode == PARSE_SPREAD ? b->xctx.p : nullptr;
+    a.xctx = cross_rows ? b->xctx.p : nullptr;
     a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
     a.xntu = nullptr;
     a.stream_patience_us = stream_patience_us();
@@ -817,8 +836,9 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     a.resid = ps.resid.p;
     a.rbsp = ps.rbsp.p;
     a.rsubs = ps.rsubs.p;
-    if (a.parse_mode == PARSE_SPREAD) {
+    if (a.parse_mode == PARSE_SPREAD || a.parse_mode == PARSE_ROWS) {
         a.xprog = ps.xprog.p;
+        a.xjob = ps.xprog.p + a.total_rows;
         a.xntu = a.intra_stream ? ps.xntu.p : nullptr;
     }
     // bring-up knob: HEIFGPU_STAGES=k launches only the first k stages (in order, on the caller's stream)
@@ -936,10 +956,10 @@ int heifgpu_batch_parse_geometry(const heifgpu_batch *b, uint32_t *mode, uint32_
                                  uint32_t *pics_per_wave, uint32_t *waves_per_workgroup) {
     if (!b || !b->loaded) return fail(HEIFGPU_E_INVALID, "invalid batch");
     const BatchArgs &a = b->args;
-    const bool solo = a.parse_mode == PARSE_SOLO, lanes = a.parse_mode == PARSE_LANES;
-    const uint32_t ppw = lanes ? uint32_t(std::max(1, a.parse_group)) : 1u;
+    const bool solo = a.parse_mode == PARSE_SOLO, lanes = a.parse_mode == PARSE_LANES, rows = a.parse_mode == PARSE_ROWS;
+    const uint32_t ppw = lanes ? uint32_t(std::max(1, a.parse_group)) : rows ? 64u : 1u;
     if (mode) *mode = uint32_t(a.parse_mode);
-    if (workgroups) *workgroups = (uint32_t(a.n_slots) + ppw - 1) / ppw;
+    if (workgroups) *workgroups = rows ? uint32_t(a.parse_group) * uint32_t(a.max_rows) : (uint32_t(a.n_slots) + ppw - 1) / ppw;
     if (pics_per_wave) *pics_per_wave = ppw;
     if (waves_per_workgroup) *waves_per_workgroup = solo ? uint32_t(a.solo_waves) : 1u;
     return HEIFGPU_OK;
@@ -969,6 +989,42 @@ int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *b, uint32_t *status, v
     }
     return bad ? fail(HEIFGPU_E_DECODE, "one or more pictures failed the kernel bitstream checks") : HEIFGPU_OK;
 }
+
+// The load before the current one: decodes of it still in flight when the
+// batch was reloaded fold their status into that load's generation, which
+// heifgpu_batch_status (current load only) does not read.  This reads and
+// clears it, per image of that load (errors must reach the
+// caller, /root/reference/src/heic/decoder.rs:109-112).
+int heifgpu_batch_status_previous(heifgpu_ctx *ctx, heifgpu_batch *b, uint32_t *status, size_t cap, size_t *n_prev,
+                                  void *stream) {
+    if (!ctx || !b || !n_prev) return fail(HEIFGPU_E_INVALID, "invalid argument");
+    if (b->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
+    *n_prev = 0;
+    if (!b->loaded) return fail(HEIFGPU_E_INVALID, "batch not loaded (its last prepare failed)");
+    DescGen &P = b->gen[b->cur ^ 1];
+    if (!P.loaded || P.pic_image.empty()) return HEIFGPU_OK;  // no previous load
+    *n_prev = P.n_images;
+    if (!status) return HEIFGPU_OK;  // the size query: nothing read or cleared
+    if (cap < P.n_images) return fail(HEIFGPU_E_INVALID, "status array smaller than the previous load");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (P.pending) HIP_TRY(hipStreamWaitEvent(s, P.done, 0));  // its last decode
+    std::vector<uint32_t> st(P.pic_image.size());
+    HIP_TRY(hipMemcpyAsync(st.data(), P.sticky.p, st.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemsetAsync(P.sticky.p, 0, st.size() * sizeof(uint32_t), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<uint32_t> per(P.n_images, 0);
+    for (size_t p = 0; p < st.size(); ++p) per[P.pic_image[p]] |= st[p];
+    bool bad = false;
+    for (size_t i = 0; i < P.n_images; ++i) {
+        status[i] = per[i];
+        bad |= per[i] != 0;
+    }
+    return bad ? fail(HEIFGPU_E_DECODE, "one or more pictures of the previous load failed the kernel bitstream checks")
+               : HEIFGPU_OK;
+}
+
+int heifgpu_abi_version(void) { return HEIFGPU_ABI_VERSION; }
 
 void heifgpu_batch_free(heifgpu_batch *b) {
     if (!b) return;

@@ -76,10 +76,11 @@ int main(int argc, char **argv) {
     const int solo_waves = solo_waves_for(hb.lane_rows);
     int parse_group = 1;
     if (mode == PARSE_SPREAD) spread_parse_order(hb.pics.data(), int(hb.pics.size()), order);
+    else if (mode == PARSE_ROWS) parse_group = rows_parse_order(hb.pics.data(), int(hb.pics.size()), order);
     else
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0,
                                         order, nullptr, mode == PARSE_LANES && lanes_jobs_default());
-    std::vector<uint32_t> xprog(hb.rows + 1), xntu(hb.rows + hb.pics.size() + 1, 0);
+    std::vector<uint32_t> xprog(hb.rows + 1), xntu(hb.rows + hb.pics.size() + 1, 0);  // (+ the job counter)
     std::vector<uint8_t> xctx((hb.rows + 1) * size_t(CTX_PAD));
     a.parse_order = order.data();
     a.n_slots = int(order.size());
@@ -107,6 +108,7 @@ int main(int argc, char **argv) {
     a.lf_tiles = lf_tiles_for(hb.pics.data(), int(hb.pics.size()), hb.seqs.data());
     a.xprog = xprog.data();
     a.xctx = xctx.data();
+    a.xjob = xprog.data() + hb.rows;
     a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
     a.xntu = a.intra_stream ? xntu.data() : nullptr;
     a.stream_patience_us = stream_patience_us();
@@ -149,7 +151,10 @@ int main(int argc, char **argv) {
                 }
             }
     }
-    printf("parse mode: %s\n", mode == PARSE_SOLO ? "solo" : mode == PARSE_SPREAD ? "spread" : "lanes");
+    printf("parse mode: %s\n", mode == PARSE_SOLO     ? "solo"
+                               : mode == PARSE_SPREAD ? "spread"
+                               : mode == PARSE_ROWS   ? "rows"
+                                                      : "lanes");
     printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);
     if (stages >= 2 && !a.intra_stream && !a.intra_fused) emu_transform(a);  // (streaming: k_intra_stream transforms each TB)
     if (stages >= 3) {

@@ -61,6 +61,7 @@ struct BatchArgs {
     uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
     uint32_t *xntu;            // streaming mode: per-row TU records written so far (null otherwise)
+    uint32_t *xjob;            // spread / rows parse: the job counter each workgroup dequeues its substream job from
     int intra_stream;          // k_intra transforms and reconstructs each row behind the spread parse (same launch window)
     int intra_fused;           // k_intra_fused after the parse: TBs transformed in-line, no k_transform stage
     int stream_redo;           // k_intra_stream's second launch (after the parse): the pictures the first gave up on
@@ -108,7 +109,7 @@ inline void color_coefs(uint32_t matrix, bool full, ColorArgs &c) {
 }
 
 // parse modes (BatchArgs::parse_mode; heifgpu_batch_opts::parse_mode)
-enum : int { PARSE_AUTO = 0, PARSE_LANES = 1, PARSE_SOLO = 2, PARSE_SPREAD = 3 };
+enum : int { PARSE_AUTO = 0, PARSE_LANES = 1, PARSE_SOLO = 2, PARSE_SPREAD = 3, PARSE_ROWS = 4 };
 constexpr int kSoloMaxWaves = 16;
 // host: BatchArgs::parse_order for a batch (size-balanced k_parse_lanes waves,
 // or for solo mode with ppw_force = 1 one picture per workgroup, heaviest
@@ -138,6 +139,9 @@ void parse_chain_cost(const PicDesc *pics, int n, const uint32_t *subs, const Se
 int parse_mode_for(int requested, int n_pics);
 // spread mode's wave slots (row << 20 | picture); -1 if the batch exceeds the encoding
 int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order);
+// rows mode (k_parse_rows): groups of 64 pictures by payload size, slot g * 64 + lane
+// (~0u: empty); returns the number of groups (BatchArgs::parse_group)
+int rows_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order);
 int solo_waves_for(int lane_rows);
 
 #if defined(HG_HOST_EMU)

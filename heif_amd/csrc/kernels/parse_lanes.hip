@@ -223,10 +223,14 @@ struct Lane {
 // bytes of n lane blocks, rounded up so the LanePic after them stays 16-byte aligned
 HG_HD inline size_t lane_blocks_bytes(int n) { return (sizeof(LaneLds) * (size_t)n + 15) & ~(size_t)15; }
 
-// engine context of one lane (lanes mode: every lane its own substream)
-struct Eng {
+// engine context of one lane (lanes mode: every lane its own substream).
+// Spread = true: the row waves of k_parse_rows, whose WPP neighbours are other
+// waves (progress, context hand-off, SAO and depth lines through coherent
+// global memory, as in spread mode)
+template <bool Spread>
+struct EngLanesT {
     static constexpr bool kSolo = false;
-    static constexpr bool kSpread = false;
+    static constexpr bool kSpread = Spread;
     static constexpr bool kCtxReg = false;  // contexts in LDS (ctx)
     uint8_t *ctx;
     const uint64_t *tab;  // per pStateIdx: rangeTabLps[4] | transIdxLps << 32 | transIdxMps << 40 (LDS)
@@ -235,6 +239,8 @@ struct Eng {
     uint32_t lim;         // no loads at or past this offset (the picture's RBSP end + 64)
     HG_HD uint64_t row(uint32_t st) const { return tab[st]; }
 };
+using Eng = EngLanesT<false>;
+using EngRows = EngLanesT<true>;
 
 // Solo mode (k_parse_solo): one substream per WAVE, run by its lane 0 alone,
 // so the engine state is wave-uniform.  The state rows live in two VGPRs
@@ -534,7 +540,8 @@ HG_HD inline uint32_t be_pop(Lane &L, const EG &G) {
 }
 
 // pass start (after pass_wait): land f, issue the next block
-HG_HD inline void q_refill(Lane &L, const Eng &G) {
+template <class EG>
+HG_HD inline void q_refill(Lane &L, const EG &G) {
     if (L.fp && !L.bv) {
         L.b0 = L.f0, L.b1 = L.f1, L.b2 = L.f2, L.b3 = L.f3;
         L.bv = 1;
@@ -2172,14 +2179,19 @@ int parse_mode_for(int requested, int n_pics) {
         const char *e = std::getenv("HEIFGPU_PARSE");
         if (!e) return PARSE_AUTO;
         const std::string v(e);
-        return v == "solo" ? PARSE_SOLO : v == "spread" ? PARSE_SPREAD : v == "lanes" ? PARSE_LANES : PARSE_AUTO;
+        return v == "solo"     ? PARSE_SOLO
+               : v == "spread" ? PARSE_SPREAD
+               : v == "lanes"  ? PARSE_LANES
+               : v == "rows"   ? PARSE_ROWS
+                               : PARSE_AUTO;
     }();
     static const int max_pics = [] {
         const char *e = std::getenv("HEIFGPU_SOLO_MAX_PICS");
         return e ? std::atoi(e) : 768;
     }();
     if (env != PARSE_AUTO) return env;
-    if (requested == PARSE_LANES || requested == PARSE_SOLO || requested == PARSE_SPREAD) return requested;
+    if (requested == PARSE_LANES || requested == PARSE_SOLO || requested == PARSE_SPREAD || requested == PARSE_ROWS)
+        return requested;
     return n_pics <= max_pics ? PARSE_SPREAD : PARSE_LANES;
 }
 
@@ -2190,7 +2202,8 @@ int solo_waves_for(int lane_rows) { return lane_rows < 1 ? 1 : (lane_rows > kSol
 // spread mode: one wave slot per substream, entry row << 20 | picture; the
 // pictures by payload size (heaviest first, so the longest WPP chains start
 // first), a picture's rows consecutive and in order (a row waits only for a
-// lower slot, which the in-order dispatch has already placed)
+// lower slot, which a running wave holds: k_parse_solo<true> takes its slot
+// from the job counter)
 int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order) {
     std::vector<uint32_t> by_size((size_t)n);
     for (int i = 0; i < n; ++i) by_size[(size_t)i] = (uint32_t)i;
@@ -2202,6 +2215,47 @@ int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order)
         for (uint32_t r = 0; r < pics[p].n_sub; ++r) order.push_back(p | (r << 20));
     }
     return 1;
+}
+
+// rows mode: the pictures by payload size (heaviest first), 64 consecutive
+// ranks per group, so a row wave's lanes carry similar work.
+// HEIFGPU_ROWS_DEAL=K (measurement control for batches with repeated
+// bitstreams, such as the bench's tile permutations): pictures of equal
+// payload size (copies of one tile there) are spread so that each group holds
+// copies of K different sizes, the K adjacent ones; "copies": of all of them.
+// A batch of distinct photos (no two payloads of equal size) is unaffected.
+int rows_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order) {
+    static const long band = [] {
+        const char *e = std::getenv("HEIFGPU_ROWS_DEAL");
+        if (!e) return 1L;
+        return std::string(e) == "copies" ? (1L << 30) : std::max(1L, std::atol(e));
+    }();
+    std::vector<uint32_t> by_size;
+    for (int i = 0; i < n; ++i)
+        if (!(pics[i].flags & PD_ASSEMBLY)) by_size.push_back((uint32_t)i);
+    std::stable_sort(by_size.begin(), by_size.end(),
+                     [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
+    if (band > 1) {  // key: (band of K sizes, copy number within its size, size rank)
+        std::vector<uint32_t> nth(by_size.size()), cls(by_size.size());
+        for (size_t i = 0; i < by_size.size(); ++i) {
+            const bool same = i && pics[by_size[i]].bits_len == pics[by_size[i - 1]].bits_len;
+            nth[i] = same ? nth[i - 1] + 1 : 0;
+            cls[i] = i == 0 ? 0 : cls[i - 1] + (same ? 0 : 1);
+        }
+        std::vector<size_t> idx(by_size.size());
+        for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
+        std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) {
+            const long bx = cls[x] / band, by = cls[y] / band;
+            return bx != by ? bx < by : nth[x] < nth[y];
+        });
+        std::vector<uint32_t> t(by_size.size());
+        for (size_t i = 0; i < idx.size(); ++i) t[i] = by_size[idx[i]];
+        by_size.swap(t);
+    }
+    const int groups = ((int)by_size.size() + 63) / 64;
+    order.assign((size_t)groups * 64, ~0u);
+    std::copy(by_size.begin(), by_size.end(), order.begin());
+    return groups;
 }
 
 #if defined(HG_HOST_EMU)
@@ -2419,7 +2473,77 @@ void emu_parse_solo(const BatchArgs &a) {
     }
 }
 
+// rows mode: a group's row waves round-robin, one pass per wave per round
+void emu_parse_rows(const BatchArgs &a) {
+    const int groups = a.parse_group, R = a.max_rows;
+    uint64_t tab[64], seq[15];
+    for (int i = 0; i < 64; ++i) tab[i] = state_row(i);
+    for (int i = 0; i < 15; ++i) seq[i] = sig_seq(i);
+    std::vector<LaneLds> lds((size_t)R * 64);
+    std::vector<LanePic> pics((size_t)R * 64);
+    std::vector<Lane> lanes((size_t)R * 64);
+    std::vector<uint8_t> live((size_t)R * 64);
+    static const bool stats = std::getenv("HEIFGPU_LANES_STATS") != nullptr;
+    for (int g = 0; g < groups; ++g) {
+        for (int r = 0; r < R; ++r)
+            for (int l = 0; l < 64; ++l) {
+                const size_t i = (size_t)r * 64 + (size_t)l;
+                const int slot = g * 64 + l;
+                const bool in = slot < a.n_slots && a.parse_order[slot] != ~0u;
+                live[i] = in && pic_init(pics[i], a, a.pic0 + (int)a.parse_order[slot], 0, 1 << 20) && r < pics[i].R;
+                if (live[i]) lane_start(lanes[i], pics[i], lds[i], r);
+                else lanes[i].st = U_DONE;
+            }
+        long passes = 0, units = 0;
+        for (;;) {
+            bool any = false, progressed = false;
+            for (int r = 0; r < R; ++r) {
+                bool wave_any = false;
+                for (int l = 0; l < 64; ++l) wave_any |= lanes[(size_t)r * 64 + (size_t)l].st != U_DONE;
+                if (!wave_any) continue;
+                any = true;
+                const long units0 = units;
+                for (int l = 0; l < 64; ++l) {
+                    const size_t i = (size_t)r * 64 + (size_t)l;
+                    if (lanes[i].st == U_DONE) continue;
+                    const EngRows G{lds[i].ctx, tab, seq, a.rbsp, (pics[i].bits_end + 64u) & ~3u};
+                    q_refill(lanes[i], G);
+                }
+                for (int kind = U_CTU; kind <= U_CTU_END; ++kind)
+                    for (int l = 0; l < 64; ++l) {
+                        const size_t i = (size_t)r * 64 + (size_t)l;
+                        Lane &L = lanes[i];
+                        LanePic &P = pics[i];
+                        if (L.st != kind) continue;
+                        const Env E{&a, nullptr, a.xprog + P.row_off, a.xctx + (size_t)P.row_off * CTX_PAD, l};
+                        if (kind == U_CTU && !ctu_ready<EngRows>(L, P, E)) continue;
+                        progressed = true;
+                        ++units;
+                        const EngRows G{lds[i].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
+                        run_unit(kind, L, lds[i], P, E, G);
+                    }
+                passes += units != units0;  // (a pass without progress is a sleep on the GPU)
+            }
+            if (!any) break;
+            if (!progressed) {  // every live lane of the group waits: cannot happen (row 0 never waits)
+                for (size_t i = 0; i < lanes.size(); ++i)
+                    if (lanes[i].st != U_DONE) {
+                        lanes[i].status |= ST_SUBSTREAM_END;
+                        atomicOr(&a.status[pics[i].pic], lanes[i].status);
+                        lanes[i].st = U_DONE;
+                    }
+                break;
+            }
+        }
+        if (stats) printf("group %d: %ld wave passes, %.1f units per pass\n", g, passes, (double)units / passes);
+    }
+}
+
 void emu_parse(const BatchArgs &a) {
+    if (a.parse_mode == PARSE_ROWS) {
+        emu_parse_rows(a);
+        return;
+    }
     if (a.parse_mode == PARSE_SOLO) emu_parse_solo<false>(a);
     else if (a.parse_mode == PARSE_SPREAD) emu_parse_solo<true>(a);
     else if (a.lane_jobs) emu_parse_jobs(a);
@@ -2630,6 +2754,110 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_jobs(BatchArgs a) {
 #endif
 }
 
+// Row waves (k_parse_rows, PARSE_ROWS): lane = picture, wave = one WPP CTB
+// row of a group of up to 64 pictures of similar payload (rows_parse_order).
+// In k_parse_lanes a picture's 16 rows share a wave, and the WPP ramp (row r
+// starts about 2r CTU-times after row 0) leaves two thirds of the lanes of an
+// issuing wave masked off (r04: 17.5 of 48 per pass).  Here every lane of a
+// wave is at the same row, so the lanes wait together: a wave whose row above
+// is not far enough ahead in any lane sleeps (s_sleep) and gives its SIMD's
+// issue to the other waves, instead of issuing masked passes.  The row above
+// is another wave, possibly on another XCD: progress words, the context
+// hand-off after CTU 1, SAO parameters and the CtDepth line go through
+// coherent (agent-scope) global memory, as in spread mode (EngRows).
+//
+// Jobs (group g, row r) are numbered row-major, j = r * groups + g, and each
+// workgroup dequeues its job from a counter (a.xjob, zeroed by k_rbsp) rather
+// than taking blockIdx.x: a job's predecessor (g, r - 1) has a lower number,
+// so it is held by a wave that is already running, whatever order the
+// hardware dispatches the workgroups in.
+inline size_t rows_lds_bytes() {
+    return lane_blocks_bytes(64) + sizeof(LanePic) * 64 + (64 + 16) * sizeof(uint64_t);
+}
+
+// the job counter: lane 0 takes the next number, the wave shares it
+__device__ __forceinline__ uint32_t dequeue_job(uint32_t *ctr) {
+    uint32_t j = 0;
+    if (__lane_id() == 0) j = atomicAdd(ctr, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+}
+
+__global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_rows(BatchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
+    LanePic *s_pic = reinterpret_cast<LanePic *>(smem + lane_blocks_bytes(64));
+    uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_pic + 64);
+    uint64_t *s_seq = s_tab + 64;
+    const int lane = threadIdx.x;
+#if HG_PARSE_SETPRIO > 0
+    __builtin_amdgcn_s_setprio(HG_PARSE_SETPRIO);
+#endif
+    s_tab[lane] = state_row(lane);
+    if (lane < 15) s_seq[lane] = sig_seq(lane);
+    const uint32_t groups = (uint32_t)a.parse_group;
+    const uint32_t j = dequeue_job(a.xjob);
+    const int row = (int)(j / groups), slot = (int)(j % groups) * 64 + lane;
+    const bool in = row < a.max_rows && slot < a.n_slots && a.parse_order[slot] != ~0u;
+    Lane L;
+    LaneLds &ld = s_lds[lane];
+    LanePic &P = s_pic[lane];
+    const bool live = in && pic_init(P, a, a.pic0 + (int)a.parse_order[slot], 0, 1 << 20) && row < P.R;
+    if (live) lane_start(L, P, ld, row);
+    else L.st = U_DONE;
+    __syncthreads();
+    const Env E{&a, s_lds, a.xprog + (live ? P.row_off : 0u), a.xctx + (live ? (size_t)P.row_off * CTX_PAD : 0), lane};
+    const EngRows G{ld.ctx, s_tab, s_seq, a.rbsp, live ? (P.bits_end + 64u) & ~3u : 0u};
+#if defined(HG_PARSE_PROF)
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+#endif
+    uint32_t stalled = 0;  // consecutive passes without progress (bounded: never hang the device)
+    for (;;) {
+        if (!__any(L.st != U_DONE)) break;
+        pass_wait();
+        if (live) q_refill(L, G);
+        bool progressed = false;
+#pragma unroll
+        for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
+            const bool mine = L.st == kind && (kind != U_CTU || ctu_ready<EngRows>(L, P, E));
+            if (!__any(mine)) continue;
+            progressed = true;
+            // the rows above (contexts, SAO parameters, depth line) after their progress words
+            if (kind == U_CTU) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#if defined(HG_PARSE_PROF)
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            pf[7] += (uint64_t)__popcll(__ballot(mine));
+#endif
+            if (mine) run_unit(kind, L, ld, P, E, G);
+#if defined(HG_PARSE_PROF)
+            const uint64_t t2 = __builtin_amdgcn_s_memtime();
+            pf[kind <= U_CTU ? 2 : kind <= U_TT ? 3 : kind - 1] += t2 - t1;
+#endif
+        }
+#if defined(HG_PARSE_PROF)
+        ++pf[1];
+#endif
+        if (progressed) {
+            stalled = 0;
+            continue;
+        }
+        // every live lane waits for the row above: sleep, leaving the SIMD's issue to the busy waves
+        __builtin_amdgcn_s_sleep(HG_SOLO_SLEEP);
+        if (++stalled > (1u << 25)) {  // the row above never arrives (a corrupt picture stopped it)
+            if (L.st != U_DONE) {
+                atomicOr(&a.status[P.pic], L.status | ST_SUBSTREAM_END);
+                store_agent(prog_word(E, P, L.row), kProgDone);  // the rows below stop waiting too
+            }
+            break;
+        }
+    }
+#if defined(HG_PARSE_PROF)
+    pf[0] = __builtin_amdgcn_s_memtime() - t_start;
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[k], (unsigned long long)pf[k]);
+#endif
+}
+
 // Solo mode: one workgroup per picture, one wave per WPP row (rows beyond 16
 // wrap round the waves).  All 64 lanes of a wave run the same substream in
 // lockstep (identical state in every lane, so exec stays full: the window and
@@ -2665,7 +2893,10 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
     if (threadIdx.x < 64) s_prog[threadIdx.x] = 0;
     const uint64_t trow = state_row(lane);
     const uint32_t tlo = (uint32_t)trow, thi = (uint32_t)(trow >> 32);
-    const int slot = (int)blockIdx.x;
+    // spread: the slot from the job counter (a row's predecessor is the slot
+    // before it, so it is already held by a running wave whatever order the
+    // workgroups are dispatched in); solo: the workgroup's own picture
+    const int slot = Spread ? (int)dequeue_job(a.xjob) : (int)blockIdx.x;
     const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
     const uint32_t ent = slot < n_slots ? (a.parse_order ? a.parse_order[slot] : (uint32_t)slot) : ~0u;
     const bool in = ent != ~0u;
@@ -2727,6 +2958,13 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
             // broken): flag the picture and stop instead of spinning forever
             if (++stalled > (1u << 25)) {
                 if (lane == 0) atomicOr(&a.status[P.pic], L.status | ST_SUBSTREAM_END);
+                // publish the row as finished (the TU count as it stands), so the
+                // rows below and k_intra_stream stop waiting on it at once
+                if (Spread) {
+                    if (a.xntu) store_agent(a.xntu + P.row_off + L.row, L.ntu);
+                    stores_done();
+                    store_agent(prog_word(E, P, L.row), kProgDone);
+                }
                 break;
             }
             continue;
@@ -2787,10 +3025,18 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
         return hipGetLastError();
     }
     if (a.parse_mode == PARSE_SPREAD) {
-        if (!a.parse_order || !a.xprog || !a.xctx) return hipErrorInvalidValue;
+        if (!a.parse_order || !a.xprog || !a.xctx || !a.xjob) return hipErrorInvalidValue;
         if (a.n_slots <= 0) return hipSuccess;
         // (the progress words start at 0: k_rbsp of this decode cleared them)
         hipLaunchKernelGGL(k_parse_solo<true>, dim3(a.n_slots), dim3(64), solo_lds_bytes(1, false), s, a);
+        return hipGetLastError();
+    }
+    if (a.parse_mode == PARSE_ROWS) {
+        if (!a.parse_order || !a.xprog || !a.xctx || !a.xjob || a.parse_group < 1) return hipErrorInvalidValue;
+        const long jobs = (long)a.parse_group * a.max_rows;
+        if (jobs <= 0) return hipSuccess;
+        if (jobs >= (1L << 31)) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_parse_rows, dim3((unsigned)jobs), dim3(64), rows_lds_bytes(), s, a);
         return hipGetLastError();
     }
     // the dealing of parse_order fixed the pictures per wave (lanes_parse_order)

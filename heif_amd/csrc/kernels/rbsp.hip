@@ -34,6 +34,7 @@ namespace hg {
 __device__ inline void zero_outputs(const BatchArgs &a, int pic, int lane, int nl) {
     const PicDesc &pd = a.pics[pic];
     if (lane == 0) a.status[pic] = 0;
+    if (pic == a.pic0 && lane == 0 && a.xjob) *a.xjob = 0;  // spread / rows parse: the job counter
     if (pd.flags & PD_ASSEMBLY) return;  // no rows of its own
     const SeqParams &sp = a.seqs[pd.seq];
     const int hctb = (sp.height + (1 << sp.log2_ctb) - 1) >> sp.log2_ctb;

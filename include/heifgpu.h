@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define HEIFGPU_ABI_VERSION 4
+#define HEIFGPU_ABI_VERSION 5
 
 enum {
     HEIFGPU_OK = 0,
@@ -94,7 +94,9 @@ typedef struct {
      * HEIFGPU_PARSE_LANES packs one substream per lane (throughput);
      * HEIFGPU_PARSE_SOLO runs one substream per wavefront, a picture's rows in
      * one workgroup; HEIFGPU_PARSE_SPREAD one substream per wavefront, every
-     * row its own workgroup (latency of small batches). */
+     * row its own workgroup (latency of small batches); HEIFGPU_PARSE_ROWS
+     * (ABI 5) one picture per lane, one CTB row of up to 64 pictures per
+     * wavefront (throughput). */
     uint32_t parse_mode;
     /* lanes mode: pictures per wavefront (0 = adaptive; larger values are
      * capped at 64 / CTB rows) */
@@ -108,7 +110,13 @@ typedef struct {
     uint32_t pipeline_sets;
 } heifgpu_batch_opts;
 
-enum { HEIFGPU_PARSE_AUTO = 0, HEIFGPU_PARSE_LANES = 1, HEIFGPU_PARSE_SOLO = 2, HEIFGPU_PARSE_SPREAD = 3 };
+enum {
+    HEIFGPU_PARSE_AUTO = 0,
+    HEIFGPU_PARSE_LANES = 1,
+    HEIFGPU_PARSE_SOLO = 2,
+    HEIFGPU_PARSE_SPREAD = 3,
+    HEIFGPU_PARSE_ROWS = 4
+};
 
 /* ---- host: demux + parameter sets + slice headers ------------------- */
 /* data is copied; the returned image owns its bytes. */
@@ -156,6 +164,19 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
                              const heifgpu_batch_opts *opts, heifgpu_batch **inout);
 int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *batch, const heifgpu_planes *out, void *stream);
 int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *batch, uint32_t *status, void *stream);
+/* ABI 5.  A reload does not wait for the previous load's decodes in flight;
+ * their status words stay with that load (heifgpu_batch_status reports the
+ * current load only).  This reads and clears them: per image of the load
+ * before the current one (*n_prev images, 0 if there is none; status must
+ * hold cap >= *n_prev words; status = NULL only sets *n_prev and reads
+ * nothing), after its last decode.  The words survive until the batch is
+ * reloaded again.  Returns HEIFGPU_E_DECODE if any is nonzero. */
+int heifgpu_batch_status_previous(heifgpu_ctx *ctx, heifgpu_batch *batch, uint32_t *status, size_t cap,
+                                  size_t *n_prev, void *stream);
+/* HEIFGPU_ABI_VERSION of the library (a caller built against another
+ * version's structs, e.g. the 16-byte ABI 3 heifgpu_batch_opts, must not
+ * call it: check this first) */
+int heifgpu_abi_version(void);
 void heifgpu_batch_free(heifgpu_batch *batch);
 /* stage timing (ms per decode call, from HIP events on the streams the
  * kernels run on, enabled with heifgpu_set_timing(ctx, 1)): the mean over the

@@ -71,7 +71,9 @@ static void write_planes(FILE *f, const DevPlanes *p) {
 
 int main(int argc, char **argv) {
     CHECK(argc >= 2, "usage: heifgpu_caller FILE [--decode OUT]");
-    CHECK(HEIFGPU_ABI_VERSION == 4, "ABI version");
+    CHECK(HEIFGPU_ABI_VERSION == 5, "ABI version");
+    CHECK(heifgpu_abi_version() == HEIFGPU_ABI_VERSION, "library ABI %d, header %d", heifgpu_abi_version(),
+          HEIFGPU_ABI_VERSION);
     CHECK(sizeof(heifgpu_batch_opts) == 20, "heifgpu_batch_opts is %zu bytes", sizeof(heifgpu_batch_opts));
     CHECK(sizeof(heifgpu_image_info) == 80, "heifgpu_image_info is %zu bytes", sizeof(heifgpu_image_info));
     size_t n = 0;

@@ -38,7 +38,8 @@ def _run(exe, path, env_extra=None):
 # full 64-lane packing of large batches (four 16-row pictures per wave),
 # k_parse_jobs (lanes take substreams from the wave's job list: adaptive, 8
 # pictures = 128 substreams on 64 lanes, and an odd 5), and batch (unsorted)
-# wave order
+# wave order; k_parse_rows (lane = picture, wave = one CTB row of the group,
+# WPP through coherent global memory) in size-sorted and copies-apart dealing
 LANES = {"HEIFGPU_PARSE": "lanes"}
 JOBS = {**LANES, "HEIFGPU_LANES_JOBS": "1"}
 PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "spread"}, "lanes": LANES,
@@ -52,7 +53,9 @@ PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "sprea
            # k_intra_fused: the transform folded into the reconstruction after the parse
            "fused": {**LANES, "HEIFGPU_FUSED": "1"},
            "fused_solo": {"HEIFGPU_PARSE": "solo", "HEIFGPU_FUSED": "1"},
-           "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
+           "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"},
+           "rows": {"HEIFGPU_PARSE": "rows"},
+           "rows_copies": {"HEIFGPU_PARSE": "rows", "HEIFGPU_ROWS_DEAL": "copies"}}
 
 
 @pytest.mark.parametrize("parser", list(PARSERS))
@@ -61,7 +64,7 @@ def test_emulated_kernels_match_oracle(emu_check, parser):
     assert rc == 0 and "EMU PARITY OK" in out, out[-2000:]
 
 
-@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "jobs8"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "jobs8", "rows"])
 def test_emulated_kernels_permuted_image(emu_check, tmp_path, halfmoonbay, parser):
     p = tmp_path / "perm.heic"
     p.write_bytes(permuted_heic(halfmoonbay, 42))
@@ -88,7 +91,7 @@ def _corrupt(data: bytes, mode: str) -> bytes:
     return bytes(d)
 
 
-@pytest.mark.parametrize("parser", ["solo", "spread", "spread_redo", "lanes", "packed", "jobs8"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "spread_redo", "lanes", "packed", "jobs8", "rows"])
 @pytest.mark.parametrize("mode", ["random", "zeroed"])
 def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode, parser):
     """Corrupt slice data must end in status bits, never in a crash (the same

@@ -77,12 +77,13 @@ def test_halfmoonbay_bit_exact(H, oracle_halfmoonbay, halfmoonbay):
     ("spread", 0, {"mode": "spread", "workgroups": 768, "pics_per_wave": 1, "waves_per_workgroup": 1}),
     ("lanes", 0, {"mode": "lanes", "workgroups": 48, "pics_per_wave": 1, "waves_per_workgroup": 1}),
     ("lanes", 4, {"mode": "lanes", "workgroups": 12, "pics_per_wave": 4, "waves_per_workgroup": 1}),
+    ("rows", 0, {"mode": "rows", "workgroups": 16, "pics_per_wave": 64, "waves_per_workgroup": 1}),
 ])
 def test_halfmoonbay_parse_modes(H, ctx, oracle_halfmoonbay, halfmoonbay, parse, ppw, geom):
     """Config 3 in every parse geometry: solo (a workgroup of 16 waves per
     tile, one WPP row per wave), spread (one single-wave workgroup per WPP
-    row: 768), lanes with one tile per wave and lanes packed four tiles per
-    wave."""
+    row: 768), lanes with one tile per wave, lanes packed four tiles per
+    wave, and rows (one wave per CTB row of all 48 tiles, lane = tile)."""
     img = H.HeifImage.parse(halfmoonbay)
     b = ctx.prepare([img], parse=parse, pics_per_wave=ppw)
     assert b.parse_geometry() == geom
@@ -161,6 +162,7 @@ def check_permuted(outs, seeds, oracle_tiles):
     ("solo", {"mode": "solo", "workgroups": 6144, "pics_per_wave": 1, "waves_per_workgroup": 16}),
     ("spread", {"mode": "spread", "workgroups": 98304, "pics_per_wave": 1, "waves_per_workgroup": 1}),
     ("lanes4", {"mode": "lanes", "workgroups": 1536, "pics_per_wave": 4, "waves_per_workgroup": 1}),
+    ("rows", {"mode": "rows", "workgroups": 1536, "pics_per_wave": 64, "waves_per_workgroup": 1}),
 ])
 def test_bench_shard_every_image(H, ctx, oracle_tiles, halfmoonbay, parse, geom):
     """The headline configuration itself (bench.py, config 4 shard): 128
@@ -173,7 +175,8 @@ def test_bench_shard_every_image(H, ctx, oracle_tiles, halfmoonbay, parse, geom)
 
     seeds = list(range(128))
     imgs = H.HeifImage.parse_many([permuted_heic(halfmoonbay, s) for s in seeds], threads=8)
-    b = ctx.prepare(imgs, parse="lanes" if parse == "lanes4" else parse, pics_per_wave=4 if parse == "lanes4" else 0)
+    mode = {"lanes4": "lanes"}.get(parse, parse)
+    b = ctx.prepare(imgs, parse=mode, pics_per_wave=4 if parse == "lanes4" else 0)
     assert b.parse_geometry() == geom
     outs = [ctx.alloc_outputs(imgs) for _ in range(3)]
     for o in outs:
@@ -195,7 +198,7 @@ def _damaged_halfmoonbay(oracle_mod, data, tile=5):
 
 
 @pytest.mark.parametrize("sets", [0, 2, 1])
-@pytest.mark.parametrize("parse", ["lanes", "spread"])
+@pytest.mark.parametrize("parse", ["lanes", "spread", "rows"])
 def test_status_sticky_over_pipelined_decodes(H, ctx, oracle_mod, oracle_tiles, halfmoonbay, parse, sets):
     """heifgpu_batch_status reports the OR over every decode since the last
     query (/root/reference/src/heic/decoder.rs:109-112: errors reach the
@@ -225,13 +228,17 @@ def test_status_sticky_over_pipelined_decodes(H, ctx, oracle_mod, oracle_tiles, 
             assert np.array_equal(o[i].y.cpu().numpy(), y)
             assert np.array_equal(o[i].cb.cpu().numpy(), cb) and np.array_equal(o[i].cr.cpu().numpy(), cr)
     # a reload starts a new record: the damaged load's last decode (in flight
-    # when the reload is issued) is not reported against the clean images
+    # when the reload is issued) is not reported against the clean images, but
+    # it reaches the caller through heifgpu_batch_status_previous
     clean = H.HeifImage.parse_many([halfmoonbay] * 3, threads=4)
     b.decode_async(outs[0])
     ctx.prepare(clean, reuse=b, wait=False)
     b.decode_async(outs[1])
     b.decode_async(outs[2])
     assert b.status() == [0, 0, 0]
+    prev = b.status_previous()
+    assert len(prev) == 3 and prev[0] == 0 and prev[2] == 0 and prev[1] != 0, prev
+    assert b.status_previous() == [0, 0, 0]  # read and cleared
     b.free()
 
 
