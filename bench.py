@@ -263,6 +263,49 @@ def verify_images(outs, seeds, src, info, stride, offset, threads) -> int:
     return len(outs)
 
 
+def config4u_files(S, seeds):
+    """The distinct-tile control images; BENCH_C4U_CACHE names an .npz that
+    keeps them between runs on one box (generation takes ~0.5 s per image)."""
+    import numpy as np
+
+    cache = os.environ.get("BENCH_C4U_CACHE")
+    if cache and os.path.exists(cache):
+        with np.load(cache) as z:
+            if list(z["seeds"]) == list(seeds):
+                return [z[f"f{i}"].tobytes() for i in range(len(seeds))]
+    files = [S.config4u_image(s, threads=effective_cpus()) for s in seeds]
+    if cache:
+        np.savez(cache, seeds=np.array(seeds), **{f"f{i}": np.frombuffer(f, np.uint8) for i, f in enumerate(files)})
+    return files
+
+
+def verify_distinct(outs, files, info, stride, offset, threads) -> int:
+    """Every given image (each with tiles of its own) against the oracle's
+    decode of each of its tiles, placed in grid order.  Returns the number of
+    images checked."""
+    import numpy as np
+
+    from oracle import oracle
+
+    tw, th, n, cols = info.tile_width, info.tile_height, info.num_tiles, info.grid_cols
+    with cf.ThreadPoolExecutor(max(1, threads)) as ex:
+        for f, o in zip(files, outs):
+            tiles, (ho, hl) = oracle.list_tiles(f)
+            hvcc = f[ho:ho + hl]
+            ks = list(range(offset, n, stride))
+            ref = list(ex.map(lambda k: oracle.decode_tile(hvcc, f[tiles[k][0]:tiles[k][0] + tiles[k][1]], tw, th), ks))
+            planes = [t.cpu().numpy().astype(np.uint16) for t in (o.y, o.cb, o.cr) if t is not None]
+            for k, rk in zip(ks, ref):
+                r, c = divmod(k, cols)
+                for ci, pl in enumerate(planes):
+                    sh = 1 if ci else 0
+                    w, h = tw >> sh, th >> sh
+                    win = pl[h * r:h * (r + 1), w * c:w * (c + 1)]
+                    if not np.array_equal(win, rk[ci][:win.shape[0], :win.shape[1]]):
+                        raise SystemExit(f"distinct-tile image: tile {k} plane {ci}: GPU planes differ from the oracle")
+    return len(outs)
+
+
 def end_to_end(H, ctx, files, outs0, n_batches, threads, stream, info) -> dict:
     """Host parse + pinned upload + decode of n_batches batches of `files`
     (re-parsed every time), two device batches reloaded alternately so the
@@ -314,7 +357,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["config4", "config5"], default="config4")
+    ap.add_argument("--workload", choices=["config4", "config5", "config4u"], default="config4",
+                    help="config4u: config-4 geometry with 48 distinct synthetic tiles per image (control)")
     ap.add_argument("--verify", type=int, default=-1,
                     help="images checked bit-exact against the oracle on rank 0 (-1 = every image)")
     ap.add_argument("--split", choices=["images", "tiles"], default="images",
@@ -358,6 +402,7 @@ def main():
     from heif_amd.synthetic import permuted_heic
 
     c5 = args.workload == "config5"
+    c4u = args.workload == "config4u"
     if c5:
         from heif_amd import synth_encoder as S
         from heif_amd.synthetic import permutation
@@ -371,6 +416,11 @@ def main():
     if c5:
         files = [S.grid_heic(S.CONFIG5["out_w"], S.CONFIG5["out_h"], p5,
                              pictures=[pool[j] for j in permutation(135, s)]) for s in seeds]
+    elif c4u:
+        from heif_amd import synth_encoder as S
+
+        files = config4u_files(S, seeds)
+        src = files[0]
     else:
         files = [permuted_heic(src, s) for s in seeds]
     # host demux + parameter sets + slice headers alone (heifgpu_image_parse_many)
@@ -441,7 +491,7 @@ def main():
     # the image split (default), one image is decoded tile-split for this check.
     gather = None
     g_full, g_seeds = None, None
-    if world > 1:
+    if world > 1 and not c4u:  # (the distinct-tile control is a one-GPU measurement)
         from heif_amd.tile_split import DeviceBackend, gather_to_rank0
 
         if tiles_split:
@@ -480,7 +530,9 @@ def main():
         verified = 0
         if args.verify:
             n_check = len(files) if args.verify < 0 else min(args.verify, len(files))
-            if tiles_split and g_full is not None:  # the gathered images, every tile
+            if c4u:  # every image has its own tiles: each decoded by the oracle
+                verified = verify_distinct(outs[:n_check], files[:n_check], info, stride, offset, host_threads)
+            elif tiles_split and g_full is not None:  # the gathered images, every tile
                 verified = verify_images(g_full[:n_check], g_seeds[:n_check], src, info, 1, 0, host_threads)
             else:
                 verified = verify_images(outs[:n_check], seeds[:n_check], src, info, stride, offset, host_threads)
@@ -506,6 +558,7 @@ def main():
         # command): HBM bytes per launch (FETCH_SIZE / WRITE_SIZE passes) and the parse's SQ counters
         traffic, issue = None, None
         same_cfg = lambda j: (j.get("batch", j.get("batch_images")) == args.batch and not tiles_split and not c5
+                              and not c4u
                               and j.get("parse_mode", "lanes") == geom["mode"])
         try:
             tj = json.loads((PROFILES / "pmc_traffic.json").read_text())
@@ -513,7 +566,7 @@ def main():
                 traffic = tj.get("k_parse_hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
-        bins = args.batch * BINS_PER_IMAGE if not c5 and not tiles_split else None
+        bins = args.batch * BINS_PER_IMAGE if not c5 and not c4u and not tiles_split else None
         if bins:
             issue = {"bins_per_launch": bins, "bins_per_s": round(bins / (parse_ms / 1e3), 1)}
             try:
@@ -548,10 +601,15 @@ def main():
             "vs_baseline": None,
             "dtype": "u16" if c5 else "u8",
             "data": ("synthetic: 135 generated 10-bit tiles (heif_amd/synth_encoder.py) permuted per image" if c5 else
+                     "synthetic: 48 distinct generated 8-bit tiles per image, no tile repeated in the batch "
+                     "(heif_amd/synth_encoder.py CONFIG4U)" if c4u else
                      "synthetic: halfmoonbay.heic tiles permuted per image (mt19937_64 Fisher-Yates)"),
             "config": {
                 "workload": f"config5 shard: {args.batch} x 7680x4320 10-bit 4:2:0 intra HEIC grids per GPU "
-                            f"(135 tiles of 512x512, WPP)" if c5 else f"config4 shard: {args.batch} x 4032x3024 8-bit 4:2:0 intra HEIC grid stills per GPU "
+                            f"(135 tiles of 512x512, WPP)" if c5 else
+                            f"config4 geometry, distinct tiles (control): {args.batch} x 4032x3024 8-bit 4:2:0 intra "
+                            f"HEIC grid stills per GPU (48 tiles of 512x512, WPP)" if c4u else
+                            f"config4 shard: {args.batch} x 4032x3024 8-bit 4:2:0 intra HEIC grid stills per GPU "
                             f"(48 tiles of 512x512, WPP)",
                 "images_per_gpu": args.batch,
                 "global_batch": total_images,
@@ -598,7 +656,7 @@ def main():
         if with_cpu:
             build = cpu_build
             threads = effective_cpus()
-            label = "synthetic 10-bit" if c5 else "halfmoonbay"
+            label = "synthetic 10-bit" if c5 else "synthetic distinct 8-bit" if c4u else "halfmoonbay"
             cb = cpu_baseline(src, args.cpu_seconds, threads, label)
             one = cpu_baseline(src, min(args.cpu_seconds, 4.0), 1, label)
             cb["value_1core"] = one["value"]

@@ -618,24 +618,16 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     std::vector<uint32_t> order;
     const int mode = parse_mode_for(int(mode_req), int(hb.pics.size()));
     const int solo_waves = solo_waves_for(hb.lane_rows);
-    int parse_group = 1;
+    int parse_group = 1, rows_lanes = 64;
     if (mode == PARSE_SPREAD) {
         if (spread_parse_order(hb.pics.data(), int(hb.pics.size()), order) < 0)
             return fail(HEIFGPU_E_UNSUPPORTED, "spread parse: over 2^20 pictures or 4096 substreams per picture");
     } else if (mode == PARSE_ROWS) {
-        parse_group = rows_parse_order(hb.pics.data(), int(hb.pics.size()), order);
-    } else {
-        // deal pictures by payload size; HEIFGPU_PARSE_COST=chain deals by their WPP critical
-        // path instead (A/B r03, 128 images: 16,911 / 16,863 vs 17,002 / 16,950 Mpix/s by bytes)
-        static const bool by_bytes = [] {
-            const char *e = std::getenv("HEIFGPU_PARSE_COST");
-            return !(e && std::string(e) == "chain");
-        }();
-        std::vector<float> cost;
-        if (!by_bytes) parse_chain_cost(hb.pics.data(), int(hb.pics.size()), hb.subs.data(), hb.seqs.data(), cost);
+        rows_lanes = rows_lanes_for(int(hb.pics.size()));
+        parse_group = rows_parse_order(hb.pics.data(), int(hb.pics.size()), rows_lanes, order);
+    } else {  // pictures dealt by payload size (r03: dealing by WPP critical path lost, 16.9 vs 17.0 Gpix/s)
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows,
-                                        mode == PARSE_SOLO ? 1 : ppw_req, order, by_bytes ? nullptr : cost.data(),
-                                        mode == PARSE_LANES && lanes_jobs_default());
+                                        mode == PARSE_SOLO ? 1 : ppw_req, order);
     }
     // spread and rows parses: WPP neighbours in other waves (progress words,
     // context hand-off blocks, the job counter after the progress words)
@@ -756,6 +748,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.parse_order = b->porder.p;
     a.n_slots = int(order.size());
     a.parse_group = parse_group;
+    a.rows_lanes = rows_lanes;
     a.seqs = G.seqs.p;
     a.sf = G.sf.p;
     a.outs = G.outs.p;
@@ -768,14 +761,11 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.lane_rows = hb.lane_rows;
     a.parse_mode = mode;
     a.solo_waves = solo_waves;
-    a.lane_jobs = mode == PARSE_LANES && lanes_jobs_default() ? 1 : 0;
-    a.lf_tiles = lf_tiles_for(hb.pics.data(), int(hb.pics.size()), hb.seqs.data());
     a.xprog = nullptr;  // (per parse set: heifgpu_batch_decode)
     a.xctx = cross_rows ? b->xctx.p : nullptr;
     a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
     a.xntu = nullptr;
     a.stream_patience_us = stream_patience_us();
-    a.intra_fused = !a.intra_stream && intra_fused_default() ? 1 : 0;
     // rows wrap round the lanes (waves) of a picture: the WPP context staging
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
@@ -908,13 +898,6 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
             HIP_TRY(hipEventRecord(ev[3], r));
             HIP_TRY(hipEventRecord(ev[4], r));
         }
-    } else if (a.intra_fused) {
-        // fused: no k_transform; k_intra_fused transforms each TB itself after the parse
-        HIP_TRY(hipStreamWaitEvent(r, ps.parsed, 0));
-        if (t) {
-            HIP_TRY(hipEventRecord(ev[3], r));
-            HIP_TRY(hipEventRecord(ev[4], r));
-        }
     } else {
         // transform stream (the recon stream with two sets): this set's parse
         hipStream_t x = b->n_sets >= 3 ? ctx->xform : r;
@@ -957,7 +940,7 @@ int heifgpu_batch_parse_geometry(const heifgpu_batch *b, uint32_t *mode, uint32_
     if (!b || !b->loaded) return fail(HEIFGPU_E_INVALID, "invalid batch");
     const BatchArgs &a = b->args;
     const bool solo = a.parse_mode == PARSE_SOLO, lanes = a.parse_mode == PARSE_LANES, rows = a.parse_mode == PARSE_ROWS;
-    const uint32_t ppw = lanes ? uint32_t(std::max(1, a.parse_group)) : rows ? 64u : 1u;
+    const uint32_t ppw = lanes ? uint32_t(std::max(1, a.parse_group)) : rows ? uint32_t(a.rows_lanes) : 1u;
     if (mode) *mode = uint32_t(a.parse_mode);
     if (workgroups) *workgroups = rows ? uint32_t(a.parse_group) * uint32_t(a.max_rows) : (uint32_t(a.n_slots) + ppw - 1) / ppw;
     if (pics_per_wave) *pics_per_wave = ppw;

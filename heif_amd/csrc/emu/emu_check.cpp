@@ -76,15 +76,17 @@ int main(int argc, char **argv) {
     const int solo_waves = solo_waves_for(hb.lane_rows);
     int parse_group = 1;
     if (mode == PARSE_SPREAD) spread_parse_order(hb.pics.data(), int(hb.pics.size()), order);
-    else if (mode == PARSE_ROWS) parse_group = rows_parse_order(hb.pics.data(), int(hb.pics.size()), order);
+    else if (mode == PARSE_ROWS)
+        parse_group = rows_parse_order(hb.pics.data(), int(hb.pics.size()), rows_lanes_for(int(hb.pics.size())), order);
     else
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0,
-                                        order, nullptr, mode == PARSE_LANES && lanes_jobs_default());
+                                        order);
     std::vector<uint32_t> xprog(hb.rows + 1), xntu(hb.rows + hb.pics.size() + 1, 0);  // (+ the job counter)
     std::vector<uint8_t> xctx((hb.rows + 1) * size_t(CTX_PAD));
     a.parse_order = order.data();
     a.n_slots = int(order.size());
     a.parse_group = parse_group;
+    a.rows_lanes = rows_lanes_for(int(hb.pics.size()));
     a.seqs = hb.seqs.data();
     a.sf = hb.sf.data();
     a.outs = &out;
@@ -104,15 +106,12 @@ int main(int argc, char **argv) {
     a.lane_rows = hb.lane_rows;
     a.parse_mode = mode;
     a.solo_waves = solo_waves;
-    a.lane_jobs = mode == PARSE_LANES && lanes_jobs_default() ? 1 : 0;
-    a.lf_tiles = lf_tiles_for(hb.pics.data(), int(hb.pics.size()), hb.seqs.data());
     a.xprog = xprog.data();
     a.xctx = xctx.data();
     a.xjob = xprog.data() + hb.rows;
     a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
     a.xntu = a.intra_stream ? xntu.data() : nullptr;
     a.stream_patience_us = stream_patience_us();
-    a.intra_fused = !a.intra_stream && intra_fused_default() ? 1 : 0;
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);
@@ -156,7 +155,7 @@ int main(int argc, char **argv) {
                                : mode == PARSE_ROWS   ? "rows"
                                                       : "lanes");
     printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);
-    if (stages >= 2 && !a.intra_stream && !a.intra_fused) emu_transform(a);  // (streaming: k_intra_stream transforms each TB)
+    if (stages >= 2 && !a.intra_stream) emu_transform(a);  // (streaming: k_intra_stream transforms each TB)
     if (stages >= 3) {
         emu_intra(a);
         if (a.intra_stream) {  // the second launch: the pictures the first gave up on

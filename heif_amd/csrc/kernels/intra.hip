@@ -22,6 +22,10 @@
 // finished CTU is written to the picture once.
 #include "kernels.hpp"
 #include "xform.hpp"
+#if defined(HG_HOST_EMU)
+#include <cstdio>
+#include <cstdlib>
+#endif
 
 namespace hg {
 
@@ -153,11 +157,37 @@ struct Win {
     int rx0, ry0;        // the sample res[0] holds (plane: 0, 0; streaming: the TB's origin)
     int csx, csy;        // CTB width, height in component samples (4:2:2 chroma: csy = 2 csx)
     int cx0, cy0;        // CTB origin in component samples
+#if defined(HG_HOST_EMU)
+    // emulation only: the LDS objects the pointers must stay inside (the r04
+    // gain-map fault was a residual pointer moved before its LDS buffer, which
+    // the host build could not see): the wave's window block, and the residual's
+    // object when it is an LDS tile (null: a residual plane in global memory)
+    const unsigned char *blk_lo = nullptr, *blk_hi = nullptr;
+    const int16_t *res_lo = nullptr, *res_hi = nullptr;
+    void check_blk(const void *p, size_t bytes) const {
+        const unsigned char *q = static_cast<const unsigned char *>(p);
+        if (blk_lo && (q < blk_lo || q + bytes > blk_hi)) {
+            fprintf(stderr, "k_intra: window access %td bytes outside the wave's LDS block\n",
+                    q < blk_lo ? q - blk_lo : q + bytes - blk_hi);
+            abort();
+        }
+    }
+    void check_res(const int16_t *p, size_t elems) const {
+        if (res_lo && (p < res_lo || p + elems > res_hi)) {
+            fprintf(stderr, "k_intra: residual access %td elements outside its LDS tile\n",
+                    p < res_lo ? p - res_lo : p + elems - res_hi);
+            abort();
+        }
+    }
+#endif
     // a decoded neighbour (xn, yn) in picture coordinates; only called for
     // available samples, which lie in the row above, the column to the left
     // or the current CTU
     __device__ __forceinline__ int fetch(int xn, int yn) const {
         const int lx = xn - cx0, ly = yn - cy0;
+#if defined(HG_HOST_EMU)
+        check_blk(ly < 0 ? above + lx + 1 : lx < 0 ? left + ly : cur + ly * csx + lx, sizeof(Pel));
+#endif
         if (ly < 0) return above[lx + 1];
         if (lx < 0) return left[ly];
         return cur[ly * csx + lx];
@@ -182,6 +212,10 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     // (the TB's first residual, formed only where it is in bounds: a pointer moved
     // before an LDS buffer is out of the object, and its flat address lost the aperture on the GPU)
     const int16_t *rt = cbf ? w.res + ((ptrdiff_t)(y0 - w.ry0) * w.rp + (x0 - w.rx0)) : w.res;
+#if defined(HG_HOST_EMU)
+    if (cbf) w.check_res(rt, (size_t)(n - 1) * w.rp + n);
+    w.check_blk(w.cur + ((y0 - w.cy0) * w.csx + (x0 - w.cx0)), ((size_t)(n - 1) * w.csx + n) * sizeof(Pel));
+#endif
     const int r0 = (cbf && n <= 8 && lane < n * n) ? rt[(lane >> log2n) * w.rp + (lane & (n - 1))] : 0;
     // 1. gather neighbours in search order (8.4.4.2.2): s < 2n left column bottom-up,
     //    s == 2n corner, s > 2n top row left-to-right
@@ -556,7 +590,7 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 // LDS of k_intra's streaming mode beyond the windows: the transform tables
 // (workgroup) and per wave the transform tiles (transform_tb, xform.hpp)
 constexpr size_t kXfTablesBytes = 1088, kXfWaveBytes = 2 * 32 * 32 * sizeof(int16_t) + 16;
-constexpr int kIntraPlanes = 0, kIntraStream = 1, kIntraFused = 2;
+constexpr int kIntraPlanes = 0, kIntraStream = 1;
 constexpr uint32_t kGaveUp = ~0u;                 // a wave's progress word: it gave its rows up
 constexpr uint64_t kRedoPatience = 200000000ull;  // 2 s (10 ns ticks): the parse is over by then
 
@@ -567,12 +601,13 @@ constexpr uint64_t kRedoPatience = 200000000ull;  // 2 s (10 ns ticks): the pars
 // transformed by the wave itself (transform_tb into LDS) right before its
 // prediction, so no k_transform pass and no residual planes; the
 // reconstruction trails the parse by a CTU instead of starting after it.
-// Mode kIntraFused: k_intra_fused, after the parse like k_intra but with the
-// TBs transformed in-line as in the streaming mode (no k_transform stage).
+// (r04's third mode, k_intra_fused: the in-line transform after the parse
+// instead of k_transform + k_intra, lost beside the next parse, 12.2-12.9
+// against 18.6 Gpix/s; removed in r05)
 template <typename Pel, int CF, int Mode>
 __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs &a, unsigned char *smem) {
     constexpr bool Poll = Mode == kIntraStream;       // rows consumed while the parse writes them
-    constexpr bool XfInline = Mode != kIntraPlanes;   // each TB transformed by the wave (no k_transform)
+    constexpr bool XfInline = Poll;                   // each TB transformed by the wave (no k_transform)
     const int nw = (int)HG_UNI(blockDim.x >> 6);
     const int pic = a.pic0 + blockIdx.x;
     const int wave = (int)HG_UNI(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -616,6 +651,10 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
         win[k].rx0 = win[k].ry0 = 0;
         win[k].csx = lay.csx[k];
         win[k].csy = lay.csy[k];
+#if defined(HG_HOST_EMU)
+        win[k].blk_lo = blk;
+        win[k].blk_hi = blk + lay.bytes;
+#endif
     }
     progress[wave] = 0;  // every lane writes the same value
     __syncthreads();
@@ -688,6 +727,9 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                         HG_STREAM_SLEEP();
                     }
                     if (gave_up) break;
+                    // the records behind the count / progress word: formally ordered
+                    // after the poll (the parse published them with an agent release)
+                    HG_ACQ_AGENT();
                     reload = true;
                 }
             }
@@ -802,6 +844,10 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
             w.csy = cidx == 0 ? win[0].csy : (cidx == 1 ? win[1].csy : win[2].csy);
             w.cx0 = cidx == 0 ? win[0].cx0 : (cidx == 1 ? win[1].cx0 : win[2].cx0);
             w.cy0 = cidx == 0 ? win[0].cy0 : (cidx == 1 ? win[1].cy0 : win[2].cy0);
+#if defined(HG_HOST_EMU)
+            w.blk_lo = win[0].blk_lo;
+            w.blk_hi = win[0].blk_hi;
+#endif
             const int PW = cidx ? cw : W, PH = cidx ? ch : H;
             // a TB must lie inside the picture and inside its CTU window, with a mode
             // of 8.4.2 (the parse keeps it so; the check keeps the tables in range)
@@ -818,6 +864,10 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                     w.rp = n;
                     w.rx0 = tu.x;
                     w.ry0 = tu.y;
+#if defined(HG_HOST_EMU)
+                    w.res_lo = X.d;
+                    w.res_hi = X.d + 32 * 32;  // (the 2 KB residual tile of XfScratch)
+#endif
                 }
             }
 #if !defined(HG_HOST_EMU) && !defined(HG_INTRA_NO_PAIR)
@@ -880,16 +930,6 @@ __global__ void __launch_bounds__(kMaxWaves * 64) k_intra_stream(BatchArgs a) {
     intra_body<Pel, CF, kIntraStream>(a, smem);
 }
 
-template <typename Pel, int CF>
-__global__ void __launch_bounds__(kMaxWaves * 64) k_intra_fused(BatchArgs a) {
-#if defined(HG_HOST_EMU)
-    unsigned char *smem = g_emu.smem;
-#else
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-#endif
-    intra_body<Pel, CF, kIntraFused>(a, smem);
-}
-
 // luma / chroma wave pairs (k_intra's split): for batches of few pictures,
 // where the per-picture TB chain is the latency (HEIFGPU_INTRA_SPLIT=0/1 forces it)
 static bool intra_split_for(const BatchArgs &a, int nw) {
@@ -944,7 +984,7 @@ static int stream_waves(int nw) {
 
 static size_t intra_lds_bytes(const BatchArgs &a, int nw) {
     size_t b = 64 + (size_t)nw * win_layout(a.max_log2ctb, a.chroma_format, a.bytes_per_sample).bytes;
-    if (a.intra_stream || a.intra_fused) b += kXfTablesBytes + (size_t)nw * kXfWaveBytes;
+    if (a.intra_stream) b += kXfTablesBytes + (size_t)nw * kXfWaveBytes;
     return b;
 }
 
@@ -961,11 +1001,6 @@ static void emu_intra_cf(const BatchArgs &a, int nw) {
     if (a.intra_stream) {
         if (a.bytes_per_sample == 1) emu_launch(k_intra_stream<uint8_t, CF>, a.n_pics, 1, nw, a, false, lds);
         else emu_launch(k_intra_stream<uint16_t, CF>, a.n_pics, 1, nw, a, false, lds);
-        return;
-    }
-    if (a.intra_fused) {
-        if (a.bytes_per_sample == 1) emu_launch(k_intra_fused<uint8_t, CF>, a.n_pics, 1, nw, a, false, lds);
-        else emu_launch(k_intra_fused<uint16_t, CF>, a.n_pics, 1, nw, a, false, lds);
         return;
     }
     if (a.bytes_per_sample == 1) emu_launch(k_intra<uint8_t, CF>, a.n_pics, 1, nw, a, false, lds);
@@ -993,13 +1028,6 @@ static void launch_intra_cf(const BatchArgs &a, int nw, size_t lds, hipStream_t 
             hipLaunchKernelGGL((k_intra_stream<uint8_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
         else
             hipLaunchKernelGGL((k_intra_stream<uint16_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
-        return;
-    }
-    if (a.intra_fused) {
-        if (a.bytes_per_sample == 1)
-            hipLaunchKernelGGL((k_intra_fused<uint8_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
-        else
-            hipLaunchKernelGGL((k_intra_fused<uint16_t, CF>), dim3(a.n_pics), dim3(nw * 64), lds, s, a);
         return;
     }
     if (a.bytes_per_sample == 1)
@@ -1031,13 +1059,6 @@ hipError_t launch_intra(const BatchArgs &a0, hipStream_t s) {
 uint32_t stream_patience_us() {
     const char *e = std::getenv("HEIFGPU_STREAM_PATIENCE_US");
     return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 200000u;
-}
-
-// k_intra_fused (the transform folded into the reconstruction after the parse)
-// instead of k_transform + k_intra: HEIFGPU_FUSED=1 (read per prepare)
-bool intra_fused_default() {
-    const char *e = std::getenv("HEIFGPU_FUSED");
-    return e && std::atoi(e) != 0;
 }
 
 // Streaming reconstruction (k_intra_stream beside the spread parse) for the

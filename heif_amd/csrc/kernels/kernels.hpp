@@ -50,20 +50,19 @@ struct BatchArgs {
     int total_rows;            // sum of CTB rows over pictures
     int bytes_per_sample;      // 1 or 2
     int chroma_format;         // chroma_format_idc, shared by the batch's pictures
-    int parse_group;           // k_parse_lanes pictures per wave (lanes_parse_order's choice; launch_parse otherwise)
+    int parse_group;           // k_parse_lanes pictures per wave (lanes_parse_order's choice; launch_parse otherwise);
+                               // k_parse_rows: groups (row waves per CTB row)
+    int rows_lanes;            // k_parse_rows: pictures per group (lanes of a row wave, <= 64)
     int max_log2ctb;           // largest CTB size in the batch (sizes k_intra's LDS)
     int lane_rows;             // k_parse_lanes lanes per picture: max over pictures of (WPP ? min(rows, 64) : 1)
     int wpp_ring;              // some WPP picture has more CTB rows than lanes (its rows wrap round its lanes)
     int parse_mode;            // PARSE_LANES (k_parse_lanes) or PARSE_SOLO (k_parse_solo)
     int solo_waves;            // k_parse_solo waves per workgroup (solo_waves_for(lane_rows))
-    int lane_jobs;             // lanes mode: k_parse_jobs (lanes take substreams from a per-wave job list)
-    int lf_tiles;              // k_loopfilter workgroups per picture (lf_tiles_for: the largest picture, assemblies included)
     uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
     uint32_t *xntu;            // streaming mode: per-row TU records written so far (null otherwise)
     uint32_t *xjob;            // spread / rows parse: the job counter each workgroup dequeues its substream job from
     int intra_stream;          // k_intra transforms and reconstructs each row behind the spread parse (same launch window)
-    int intra_fused;           // k_intra_fused after the parse: TBs transformed in-line, no k_transform stage
     int stream_redo;           // k_intra_stream's second launch (after the parse): the pictures the first gave up on
     uint32_t stream_patience_us;  // first launch: give a picture up after this long without parse progress (0: at once)
     int has_assembly;          // some picture is PD_ASSEMBLY (launch_deblock runs k_assemble first)
@@ -116,8 +115,7 @@ constexpr int kSoloMaxWaves = 16;
 // first); returns the pictures per wave it dealt for (BatchArgs::parse_group).
 // ppw_force = 0: the adaptive choice.
 // cost (optional): per-picture parse cost to deal by (default: payload bytes)
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
-                      const float *cost = nullptr, bool jobs = false);
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order);
 // k_intra_stream (reconstruction behind the spread parse, k_transform folded in) for this batch
 // (same box, spread, one-decode latency: 4 images 28.3 vs 33.7 ms streamed; 8
 // images 44.4 vs 40.5, the reconstruction no longer keeps up with the parse)
@@ -125,23 +123,15 @@ constexpr int kStreamMaxPics = 192;
 bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly);
 // k_intra_stream's patience (us) before its first launch gives a picture up to the second
 uint32_t stream_patience_us();
-// k_intra_fused in place of k_transform + k_intra (HEIFGPU_FUSED)
-bool intra_fused_default();
-// k_loopfilter tiles of the largest picture of a batch (assembly pictures included)
-int lf_tiles_for(const PicDesc *pics, int n, const SeqParams *seqs);
-// lanes mode runs k_parse_jobs (substreams from a per-wave job list) with HEIFGPU_LANES_JOBS=1
-bool lanes_jobs_default();
-constexpr int kJobsMaxPics = 16;  // k_parse_jobs pictures per wave at most
-// per-picture WPP critical path in payload bytes (the rows' bytes spread evenly
-// over their CTUs, row r's CTU c after row r-1's CTU c+1); non-WPP: all bytes
-void parse_chain_cost(const PicDesc *pics, int n, const uint32_t *subs, const SeqParams *seqs, std::vector<float> &cost);
 // the parse mode a batch of n_pics pictures runs in (requested: PARSE_*)
 int parse_mode_for(int requested, int n_pics);
 // spread mode's wave slots (row << 20 | picture); -1 if the batch exceeds the encoding
 int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order);
-// rows mode (k_parse_rows): groups of 64 pictures by payload size, slot g * 64 + lane
-// (~0u: empty); returns the number of groups (BatchArgs::parse_group)
-int rows_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order);
+// rows mode (k_parse_rows): groups of `lanes` (rows_lanes_for) pictures by payload size,
+// slot g * lanes + lane (~0u: empty); returns the number of groups (BatchArgs::parse_group)
+int rows_parse_order(const PicDesc *pics, int n, int lanes, std::vector<uint32_t> &order);
+// pictures per k_parse_rows group (HEIFGPU_ROWS_LANES, default 64)
+int rows_lanes_for(int n_pics);
 int solo_waves_for(int lane_rows);
 
 #if defined(HG_HOST_EMU)

@@ -326,260 +326,10 @@ __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
     }
 }
 
-// ---------------------------------------------------------------- fused
-// k_loopfilter: deblocking (both directions), SAO, crop and grid placement of
-// one 64x64 luma tile (and its chroma tiles) per workgroup, in LDS.  The tile
-// and a halo (luma 8, chroma 4 samples) are loaded once; the vertical edges
-// of every halo row are filtered, then the horizontal edges of every halo
-// column, then SAO reads the 3x3 neighbourhoods and the visible samples go to
-// the caller's planes.  Why the halo suffices: an edge modifies at most 3
-// samples on each side and reads 4 (luma; chroma 1 and 2), edges of one
-// direction never share a modified sample, and SAO reads one sample around
-// each output sample, so the final deblocked values of the tile plus a
-// one-sample ring depend only on edges inside the tile's range and on
-// unfiltered samples at most 4 outside it.  Replaces k_deblock<V>,
-// k_deblock<H> and k_sao_out (three passes over the picture in HBM) with one
-// read of the reconstruction and one write of the output.
-constexpr int kLfT = 64, kLfHaloY = 8, kLfHaloC = 4, kLfWaves = 4;
-
-struct LfDims {
-    int ly_w, ly_h, lc_w, lc_h;  // LDS region sizes (samples)
-};
-__host__ __device__ inline LfDims lf_dims(int chroma_format) {
-    const int sx = chroma_sx(chroma_format), sy = chroma_sy(chroma_format);
-    LfDims d;
-    d.ly_w = d.ly_h = kLfT + 2 * kLfHaloY;
-    d.lc_w = chroma_format ? (kLfT >> sx) + 2 * kLfHaloC : 0;
-    d.lc_h = chroma_format ? (kLfT >> sy) + 2 * kLfHaloC : 0;
-    return d;
-}
-inline size_t lf_lds_bytes(int bytes_per_sample, int chroma_format) {
-    const LfDims d = lf_dims(chroma_format);
-    return (size_t)bytes_per_sample * ((size_t)d.ly_w * d.ly_h + 2 * (size_t)d.lc_w * d.lc_h);
-}
-
-// f(t) for t in [0, n) over the workgroup's kLfWaves waves (host emulation:
-// one thread per wave walks its wave's 64 lanes)
-template <class F>
-__device__ __forceinline__ void lf_for(int n, F f) {
-    const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-    for (int b = wave * 64; b < n; b += 64 * kLfWaves)
-        for (int l = lane; l < 64 && b + l < n; l += kWave) f(b + l);
-}
-
-template <typename Pel>
-__global__ void __launch_bounds__(kLfWaves * 64) k_loopfilter(BatchArgs a) {
-#if defined(HG_HOST_EMU)
-    unsigned char *smem = g_emu.smem;
-#else
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-#endif
-    const int pic = a.pic0 + blockIdx.y;
-    const PicDesc pd = a.pics[pic];
-    if (pd.flags & PD_CHILD) return;  // filtered and output through its assembly
-    const SeqParams sp = a.seqs[pd.seq];
-    const int W = sp.width, H = sp.height, log2ctb = sp.log2_ctb;
-    const int tiles_x = (W + kLfT - 1) / kLfT;
-    const int x0 = (int)(blockIdx.x % (unsigned)tiles_x) * kLfT, y0 = (int)(blockIdx.x / (unsigned)tiles_x) * kLfT;
-    if (y0 >= H) return;
-    const OutImage oi = a.outs[pd.image];
-    // visible region of this picture in the output image (luma, window coordinates)
-    const int vw = min(sp.out_w, oi.width - pd.out_x), vh = min(sp.out_h, oi.height - pd.out_y);
-    if (vw <= 0 || vh <= 0) return;
-    if (x0 >= sp.conf_l + vw || x0 + kLfT <= sp.conf_l || y0 >= sp.conf_t + vh || y0 + kLfT <= sp.conf_t) return;
-    const int cf = sp.chroma_format, sx = chroma_sx(cf), sy = chroma_sy(cf);
-    const int cw = cf ? W >> sx : 0, ch = cf ? H >> sy : 0;
-    const int w4 = (W + 3) >> 2, h4 = (H + 3) >> 2;
-    const int wctb = (W + (1 << log2ctb) - 1) >> log2ctb;
-    const int8_t *qpy = reinterpret_cast<const int8_t *>(a.maps + pd.map_off);
-    const uint8_t *flg = a.maps + pd.map_off + (size_t)w4 * h4;
-    const Pel *gY = reinterpret_cast<const Pel *>(a.recon + pd.recon_off);
-    const LfDims d = lf_dims(cf);
-    Pel *sY = reinterpret_cast<Pel *>(smem);
-    Pel *sC[2] = {sY + d.ly_w * d.ly_h, sY + d.ly_w * d.ly_h + d.lc_w * d.lc_h};
-    const int ry0 = y0 - kLfHaloY, rx0 = x0 - kLfHaloY;
-    const int cx0 = x0 >> sx, cy0 = y0 >> sy, ctw = kLfT >> sx, cth = kLfT >> sy;
-    const int cry0 = cy0 - kLfHaloC, crx0 = cx0 - kLfHaloC;
-    const int ncomp = cf ? 3 : 1;
-
-    // 1. the region, in dwords (region origins and plane widths are multiples
-    //    of 4 samples, so no dword straddles a plane's edge); samples outside
-    //    the picture are never read as filter or SAO inputs
-    {
-        constexpr int per = 4 / (int)sizeof(Pel);  // samples per dword
-        const int ny = d.ly_h * (d.ly_w / per), nc = d.lc_h * (d.lc_w / per);
-        lf_for(ny + 2 * nc, [&](int t) {
-            int comp = 0, u = t;
-            if (u >= ny) {
-                u -= ny;
-                comp = 1 + u / nc;
-                u %= nc;
-            }
-            const int rw = comp ? d.lc_w : d.ly_w, PW = comp ? cw : W, PH = comp ? ch : H;
-            const int r = u / (rw / per), xq = (u % (rw / per)) * per;
-            const int gy = (comp ? cry0 : ry0) + r, gx = (comp ? crx0 : rx0) + xq;
-            if (gy < 0 || gy >= PH || gx < 0 || gx >= PW) return;
-            const Pel *src = comp ? gY + (size_t)W * H + (size_t)(comp - 1) * cw * ch : gY;
-            Pel *dst = comp ? sC[comp - 1] : sY;
-            *reinterpret_cast<uint32_t *>(dst + r * rw + xq) =
-                *reinterpret_cast<const uint32_t *>(src + (size_t)gy * PW + gx);
-        });
-    }
-    __syncthreads();
-
-    // 2-3. deblocking: vertical edges on every halo row, then horizontal edges on every halo column
-    if (!pd.dbk_disabled) {
-        const int ne_y = kLfT / 8 + 1, ns_y = (kLfT + 8) / 4;  // edges x0 .. x0+64, segments y0-4 .. y0+68
-        const int ne_cx = ctw / 8 + 1, ne_cy = cth / 8 + 1;
-        for (int dir = 0; dir < 2; ++dir) {
-            const bool vert = dir == 0;
-            const int lc = vert ? 4 >> sy : 4 >> sx;                       // chroma lines per segment
-            const int ne_c = vert ? ne_cx : ne_cy;
-            const int ns_c = cf ? ((vert ? cth : ctw) + 2 * kLfHaloC) / lc : 0;
-            const int nl = ne_y * ns_y, nc = cf ? ne_c * ns_c : 0;
-            lf_for(nl + 2 * nc, [&](int t) {
-                if (t < nl) {
-                    const int e = t % ne_y, sgm = t / ne_y;
-                    const int x = vert ? x0 + 8 * e : x0 - 4 + 4 * sgm, y = vert ? y0 - 4 + 4 * sgm : y0 + 8 * e;
-                    if (vert ? (x <= 0 || x >= W || y < 0 || y >= H) : (y <= 0 || y >= H || x < 0 || x >= W)) return;
-                    const int fq = flg[(y >> 2) * w4 + (x >> 2)];
-                    if (!(fq & (vert ? MF_EDGE_V : MF_EDGE_H))) return;
-                    const int xp = vert ? x - 1 : x, yp = vert ? y : y - 1;
-                    const int fp = flg[(yp >> 2) * w4 + (xp >> 2)];
-                    luma_segment<Pel>(sY + (y - ry0) * d.ly_w + (x - rx0), vert ? 1 : d.ly_w, vert ? d.ly_w : 1,
-                                      qpy[(yp >> 2) * w4 + (xp >> 2)], qpy[(y >> 2) * w4 + (x >> 2)], fp & MF_NOFILT,
-                                      fq & MF_NOFILT, pd.beta_off, pd.tc_off, sp.bit_depth_y);
-                    return;
-                }
-                const int u = t - nl, cidx = 1 + u / nc, v = u % nc;
-                const int e = v % ne_c, sgm = v / ne_c;
-                const int xc = vert ? cx0 + 8 * e : crx0 + lc * sgm, yc = vert ? cry0 + lc * sgm : cy0 + 8 * e;
-                if (vert ? (xc <= 0 || xc >= cw || yc < 0 || yc >= ch) : (yc <= 0 || yc >= ch || xc < 0 || xc >= cw))
-                    return;
-                const int xl = xc << sx, yl = yc << sy;
-                const int fq = flg[(yl >> 2) * w4 + (xl >> 2)];
-                if (!(fq & (vert ? MF_EDGE_V : MF_EDGE_H))) return;
-                const int xlp = vert ? xl - 1 : xl, ylp = vert ? yl : yl - 1;
-                const int fp = flg[(ylp >> 2) * w4 + (xlp >> 2)];
-                const int qpP = qpy[(ylp >> 2) * w4 + (xlp >> 2)], qpQ = qpy[(yl >> 2) * w4 + (xl >> 2)];
-                const int off = cidx == 1 ? sp.cb_qp_offset : sp.cr_qp_offset;
-                const int qpc = chroma_qp_map(((qpQ + qpP + 1) >> 1) + off, cf);
-                const int bd = sp.bit_depth_c;
-                const int tc = c_tc[clip3(0, 53, qpc + 2 + (pd.tc_off << 1))] * (1 << (bd - 8));
-                const int maxv = (1 << bd) - 1;
-                Pel *q = sC[cidx - 1] + (yc - cry0) * d.lc_w + (xc - crx0);
-                const int sa = vert ? 1 : d.lc_w, sk = vert ? d.lc_w : 1;  // across / along the edge
-                for (int k = 0; k < lc; ++k) {
-                    const int p0 = q[k * sk - sa], p1 = q[k * sk - 2 * sa], q0 = q[k * sk], q1 = q[k * sk + sa];
-                    const int delta = clip3(-tc, tc, ((((q0 - p0) * 4) + p1 - q1 + 4) >> 3));
-                    if (!(fp & MF_NOFILT)) q[k * sk - sa] = (Pel)clip3(0, maxv, p0 + delta);
-                    if (!(fq & MF_NOFILT)) q[k * sk] = (Pel)clip3(0, maxv, q0 - delta);
-                }
-            });
-            __syncthreads();
-        }
-    }
-
-    // 4. SAO + crop + placement of the tile's visible samples, four output
-    //    samples per task (one 4- or 8-byte store when whole and aligned)
-    const bool on = pd.sao_luma || pd.sao_chroma;  // SaoTypeIdx is 0 for a component whose flag is off
-    const SaoParams *sao = a.sao + pd.sao_off;
-    int nq[3] = {0, 0, 0}, qlo[3] = {0, 0, 0}, rlo[3] = {0, 0, 0}, nr[3] = {0, 0, 0};
-    for (int c = 0; c < ncomp; ++c) {
-        const int subx = c ? sx : 0, suby = c ? sy : 0;
-        const int tx0 = c ? cx0 : x0, ty0 = c ? cy0 : y0, tw = c ? ctw : kLfT, th = c ? cth : kLfT;
-        const int cl = sp.conf_l >> subx, ct = sp.conf_t >> suby;
-        const int vwc = c ? (vw + (1 << sx) - 1) >> sx : vw, vhc = c ? (vh + (1 << sy) - 1) >> sy : vh;
-        // window rows / quads whose samples lie in the tile
-        const int ya = max(ty0 - ct, 0), yb = min(ty0 + th - ct, vhc);
-        const int xa = max(tx0 - cl, 0), xb = min(tx0 + tw - cl, vwc);
-        if (ya >= yb || xa >= xb) continue;
-        rlo[c] = ya;
-        nr[c] = yb - ya;
-        qlo[c] = xa >> 2;
-        nq[c] = ((xb + 3) >> 2) - qlo[c];
-    }
-    const int n0 = nr[0] * nq[0], n1 = nr[1] * nq[1], n2 = nr[2] * nq[2];
-    lf_for(n0 + n1 + n2, [&](int t) {
-        const int c = t < n0 ? 0 : (t < n0 + n1 ? 1 : 2);
-        const int u = c == 0 ? t : (c == 1 ? t - n0 : t - n0 - n1);
-        const int subx = c ? sx : 0, suby = c ? sy : 0;
-        const int tx0 = c ? cx0 : x0, tw = c ? ctw : kLfT;
-        const int cl = sp.conf_l >> subx, ct = sp.conf_t >> suby;
-        const int vwc = c ? (vw + (1 << sx) - 1) >> sx : vw;
-        const int y = rlo[c] + u / nq[c], xw = (qlo[c] + u % nq[c]) * 4;  // window coordinates
-        const int ys = y + ct;
-        const Pel *R = c ? sC[c - 1] : sY;
-        const int RW = c ? d.lc_w : d.ly_w, rxo = c ? crx0 : rx0, ryo = c ? cry0 : ry0;
-        const int PW = c ? cw : W, PH = c ? ch : H, bd = c ? sp.bit_depth_c : sp.bit_depth_y;
-        int v[4];
-        bool own[4];
-        int n_own = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int xs = xw + j + cl;
-            own[j] = xw + j < vwc && xs >= tx0 && xs < tx0 + tw;
-            v[j] = 0;
-            if (!own[j]) continue;
-            ++n_own;
-            const Pel *pp = R + (ys - ryo) * RW + (xs - rxo);
-            int s = *pp;
-            if (on) {
-                const SaoParams &sv = sao[(ys >> (log2ctb - suby)) * wctb + (xs >> (log2ctb - subx))];
-                const int type = sv.type[c];
-                if (type && !(flg[((ys << suby) >> 2) * w4 + ((xs << subx) >> 2)] & MF_NOFILT)) {
-                    int o = 0;
-                    if (type == 2) {
-                        const int cls = sv.band_eo[c];
-                        const int hx = cls == 0 ? 1 : (cls == 1 ? 0 : (cls == 2 ? 1 : -1));
-                        const int vy = cls == 0 ? 0 : 1;
-                        const int ax = xs - hx, ay = ys - vy, bx = xs + hx, by = ys + vy;
-                        if (ax >= 0 && ay >= 0 && ax < PW && ay < PH && bx >= 0 && by >= 0 && bx < PW && by < PH) {
-                            const int na = pp[-vy * RW - hx], nb = pp[vy * RW + hx];
-                            int e = 2 + (s > na) - (s < na) + (s > nb) - (s < nb);
-                            if (e <= 2) e = e == 2 ? 0 : e + 1;
-                            o = e ? sv.off[c][e - 1] : 0;
-                        }
-                    } else {
-                        const int k = ((s >> (bd - 5)) - sv.band_eo[c]) & 31;
-                        o = k < 4 ? sv.off[c][k] : 0;
-                    }
-                    s = clip3(0, (1 << bd) - 1, s + o);
-                }
-            }
-            v[j] = s;
-        }
-        const uint64_t plane = c == 0 ? oi.plane[0] : (c == 1 ? oi.plane[1] : oi.plane[2]);
-        const int pitch = c == 0 ? oi.pitch[0] : (c == 1 ? oi.pitch[1] : oi.pitch[2]);
-        const int ox = (pd.out_x >> subx) + xw, oy = (pd.out_y >> suby) + y;
-        Pel *dst = reinterpret_cast<Pel *>(plane + (size_t)oy * pitch) + ox;
-        if (n_own == 4 && (reinterpret_cast<uintptr_t>(dst) & (4 * sizeof(Pel) - 1)) == 0) {
-            if (sizeof(Pel) == 1)
-                *reinterpret_cast<uint32_t *>(dst) = (uint32_t)v[0] | (uint32_t)v[1] << 8 | (uint32_t)v[2] << 16 |
-                                                     (uint32_t)v[3] << 24;
-            else
-                *reinterpret_cast<uint64_t *>(dst) = (uint64_t)v[0] | (uint64_t)v[1] << 16 | (uint64_t)v[2] << 32 |
-                                                     (uint64_t)v[3] << 48;
-        } else {
-            for (int j = 0; j < 4; ++j)
-                if (own[j]) dst[j] = (Pel)v[j];
-        }
-    });
-}
-
-// The fused loop filter only with HEIFGPU_LF=fused.  r04 A/B (same box, 128
-// images): alone 9.2 ms against 2.9 + 4.1 for the three split kernels, and
-// beside the next decode's parse 53 ms against ~33, with k_transform (on its
-// own stream) 60 ms against 29.  Its 9.6 KB of LDS per workgroup competes with
-// the parse waves and k_transform for the LDS the parse leaves free, which is
-// what decides the reconstruction kernels' residency in the pipeline (a parse
-// padded by 4 KB of LDS per wave took 129 ms instead of 81 beside them).
-// (read at every launch, so a test can switch it within one process)
-inline bool lf_fused() {
-    const char *e = std::getenv("HEIFGPU_LF");
-    return e && std::string(e) == "fused";
-}
-inline int lf_tiles(const BatchArgs &a) { return a.lf_tiles; }
+// (r04 also had k_loopfilter: both deblocking directions, SAO and output per
+// 64x64 tile in LDS, bit-exact, but 9.2 ms alone against 7.0 for the three
+// kernels here and 53 against ~33 ms beside the next parse, whose residency its
+// 9.6 KB of LDS per workgroup took; removed in r05)
 
 #if defined(HG_HOST_EMU)
 void emu_deblock(const BatchArgs &a) {
@@ -587,7 +337,6 @@ void emu_deblock(const BatchArgs &a) {
         if (a.bytes_per_sample == 1) emu_launch(k_assemble<uint8_t>, 1, a.n_pics, 1, a, true);
         else emu_launch(k_assemble<uint16_t>, 1, a.n_pics, 1, a, true);
     }
-    if (lf_fused()) return;  // deblocking runs inside k_loopfilter (emu_sao_out)
     if (a.bytes_per_sample == 1) {
         emu_launch(k_deblock<uint8_t, true>, 1, a.n_pics, 1, a, true);
         emu_launch(k_deblock<uint8_t, false>, 1, a.n_pics, 1, a, true);
@@ -597,12 +346,6 @@ void emu_deblock(const BatchArgs &a) {
     }
 }
 void emu_sao_out(const BatchArgs &a) {
-    if (lf_fused()) {
-        const size_t lds = lf_lds_bytes(a.bytes_per_sample, a.chroma_format);
-        if (a.bytes_per_sample == 1) emu_launch(k_loopfilter<uint8_t>, lf_tiles(a), a.n_pics, kLfWaves, a, false, lds);
-        else emu_launch(k_loopfilter<uint16_t>, lf_tiles(a), a.n_pics, kLfWaves, a, false, lds);
-        return;
-    }
     if (a.bytes_per_sample == 1) emu_launch(k_sao_out<uint8_t>, 1, a.n_pics, 1, a, true);
     else emu_launch(k_sao_out<uint16_t>, 1, a.n_pics, 1, a, true);
 }
@@ -612,21 +355,24 @@ void emu_sao_out(const BatchArgs &a) {
 // (128 images) gets few long-lived workgroups per picture: beside the next
 // decode's parse, 2 / 4 instead of 64 / 256 took deblocking 21 -> 7.7 ms and
 // the step 85.9 -> 85.6 ms (r04 A/B); small batches keep many, for latency.
-// HEIFGPU_DBK_BLOCKS / HEIFGPU_SAO_BLOCKS force a count.
-static int lf_blocks(const char *var, int n_pics, int total, int lo, int hi) {
-    const char *e = std::getenv(var);
-    int v = e ? std::atoi(e) : total / (n_pics > 0 ? n_pics : 1);
-    if (!e) v = v < lo ? lo : (v > hi ? hi : v);
+// HEIFGPU_DBK_BLOCKS / HEIFGPU_SAO_BLOCKS force a count (read once).
+static int lf_blocks(int forced, int n_pics, int total, int lo, int hi) {
+    int v = forced > 0 ? forced : total / (n_pics > 0 ? n_pics : 1);
+    if (forced <= 0) v = v < lo ? lo : (v > hi ? hi : v);
     return v < 1 ? 1 : (v > 1024 ? 1024 : v);
+}
+static int env_int(const char *var) {
+    const char *e = std::getenv(var);
+    return e ? std::atoi(e) : 0;
 }
 
 hipError_t launch_deblock(const BatchArgs &a, hipStream_t s) {
-    dim3 grid(lf_blocks("HEIFGPU_DBK_BLOCKS", a.n_pics, 8192, 2, 64), a.n_pics), block(256);
+    static const int forced = env_int("HEIFGPU_DBK_BLOCKS");
+    dim3 grid(lf_blocks(forced, a.n_pics, 8192, 2, 64), a.n_pics), block(256);
     if (a.has_assembly) {  // the assemblies' children are reconstructed: put them together first
         if (a.bytes_per_sample == 1) hipLaunchKernelGGL(k_assemble<uint8_t>, grid, block, 0, s, a);
         else hipLaunchKernelGGL(k_assemble<uint16_t>, grid, block, 0, s, a);
     }
-    if (lf_fused()) return hipGetLastError();  // deblocking runs inside k_loopfilter (launch_sao_out)
     if (a.bytes_per_sample == 1) {
         hipLaunchKernelGGL((k_deblock<uint8_t, true>), grid, block, 0, s, a);
         hipLaunchKernelGGL((k_deblock<uint8_t, false>), grid, block, 0, s, a);
@@ -638,14 +384,8 @@ hipError_t launch_deblock(const BatchArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_sao_out(const BatchArgs &a, hipStream_t s) {
-    if (lf_fused()) {
-        const size_t lds = lf_lds_bytes(a.bytes_per_sample, a.chroma_format);
-        const dim3 g(lf_tiles(a), a.n_pics), b(kLfWaves * 64);
-        if (a.bytes_per_sample == 1) hipLaunchKernelGGL(k_loopfilter<uint8_t>, g, b, lds, s, a);
-        else hipLaunchKernelGGL(k_loopfilter<uint16_t>, g, b, lds, s, a);
-        return hipGetLastError();
-    }
-    dim3 grid(lf_blocks("HEIFGPU_SAO_BLOCKS", a.n_pics, 24576, 4, 256), a.n_pics), block(256);
+    static const int forced = env_int("HEIFGPU_SAO_BLOCKS");
+    dim3 grid(lf_blocks(forced, a.n_pics, 24576, 4, 256), a.n_pics), block(256);
     if (a.bytes_per_sample == 1) hipLaunchKernelGGL(k_sao_out<uint8_t>, grid, block, 0, s, a);
     else hipLaunchKernelGGL(k_sao_out<uint16_t>, grid, block, 0, s, a);
     return hipGetLastError();
@@ -669,14 +409,5 @@ hipError_t launch_status_fold(const uint32_t *status, uint32_t *sticky, int n, h
     return hipGetLastError();
 }
 #endif
-
-int lf_tiles_for(const PicDesc *pics, int n, const SeqParams *seqs) {
-    int t = 0;
-    for (int i = 0; i < n; ++i) {
-        const SeqParams &sp = seqs[pics[i].seq];
-        t = std::max(t, ((sp.width + kLfT - 1) / kLfT) * ((sp.height + kLfT - 1) / kLfT));
-    }
-    return t;
-}
 
 }  // namespace hg

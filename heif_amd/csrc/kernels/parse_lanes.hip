@@ -93,21 +93,13 @@ constexpr uint32_t kProgDone = 0x7fffffffu;
 // and coefficient records while the parse writes them (agent-scope stores)
 constexpr uint32_t PF_COHERENT = 1u << 31;
 
-// per-lane LDS block.  HG_LANE_LDS_ODD: 212 bytes (53 dwords, odd), so the
-// 64 lanes' copies of one context byte fall in 64 different LDS banks (at 208
-// bytes = 52 dwords lanes l and l + 16 share a bank: 4-way conflicts)
-#if defined(HG_LANE_LDS_ODD)
-struct alignas(4) LaneLds {
-#else
+// per-lane LDS block (208 bytes: lanes l and l + 16 share a bank for one
+// context byte; an odd 212-byte block, 64 banks, measured 76.8 vs 76.3 ms, r04)
 struct alignas(16) LaneLds {
-#endif
     uint8_t ctx[CTX_PAD];
     uint8_t ipmL[16], ipmA[16];  // IntraPredModeY (4x4 units): last written per row / per column
     uint8_t dL[8], dA[8];        // CtDepth (8x8 units)
     int8_t qL[8], qA[8];         // QpY (8x8 units)
-#if defined(HG_LANE_LDS_ODD)
-    uint8_t pad_odd[4];
-#endif
 };
 
 // picture constants and output pointers (LDS, one per picture of the wave)
@@ -117,7 +109,6 @@ struct LanePic {
     int subx, suby;  // log2 SubWidthC, SubHeightC (Table 6-1)
     int w4, h4, w8, saoL, saoC;
     int R, lane0, ring;  // lanes of the picture, its first lane, rows wrap round the lanes (WPP rows > R)
-    int stage;           // the picture's WPP context staging block (job lanes), or -1: one per row slot
     uint32_t flags, bits_off, bits_end, sub_first, row_off, tu_cap, coef_cap, pic;
     // global memory, said so in the type: a generic pointer loaded from LDS
     // would make every store through it a flat store, and flat stores count in
@@ -312,6 +303,11 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 }
 __device__ __forceinline__ void uni_state(Lane &L) {
 #define HG_U(f) L.f = uni32(L.f)
+#if defined(HG_SOLO_UNI_ENGINE)  // tuning: only the engine and the unit kind made scalar
+    HG_U(range); HG_U(value); HG_U(k); HG_U(cn); HG_U(lb); HG_U(budget); HG_U(st);
+    L.cur = uni64(L.cur);
+    return;
+#endif
     HG_U(range); HG_U(value); HG_U(k); HG_U(cn); HG_U(lb); HG_U(budget); HG_U(status); HG_U(st); HG_U(fl);
     HG_U(row); HG_U(c); HG_U(ctbx); HG_U(ctby); HG_U(qx); HG_U(qy); HG_U(ql); HG_U(qd); HG_U(tx); HG_U(ty);
     HG_U(tl); HG_U(td); HG_U(tcbf); HG_U(qp_prev_last); HG_U(qp_pred); HG_U(cu_qp_delta_val); HG_U(qpy_cur);
@@ -952,7 +948,7 @@ struct Env {
 // row r + 1 writes it only after its own start, and row r + 2 cannot start
 // before that), else per row slot (lane / wave / spread row)
 HG_HD inline uint8_t *wpp_stage(const Env &E, const LanePic &P, int row) {
-    return E.wctx + (size_t)(P.stage >= 0 ? P.stage : P.lane0 + row % P.R) * CTX_PAD;
+    return E.wctx + (size_t)(P.lane0 + row % P.R) * CTX_PAD;
 }
 // progress word of substream `row` (monotone row * wctb + CTUs done, so a
 // slot shared by rows r and r + R never runs backwards)
@@ -963,15 +959,10 @@ HG_HD inline uint32_t *prog_word(const Env &E, const LanePic &P, int row) { retu
 // CTU above it (split_cu_flag's CtDepth, sao_merge_up_flag; intra modes and
 // QP prediction stay inside the CTB row), so one CTU ahead is enough.  The
 // 2-CTU lag of the reconstruction (above-right neighbours) is k_intra's.
-// (HG_WPP_LAG2: two CTUs ahead throughout, as before r03.)
 template <class EG>
 HG_HD inline bool wpp_ready(const Lane &L, const LanePic &P, const Env &E) {
     if (!(L.fl & F_WPP) || L.row == 0) return true;
-#if defined(HG_WPP_LAG2)
-    const int ahead = L.c + 2;
-#else
     const int ahead = L.c == 0 ? 2 : L.c + 1;
-#endif
     const uint32_t need = (uint32_t)(L.row - 1) * (uint32_t)P.wctb + (uint32_t)(ahead < P.wctb ? ahead : P.wctb);
     const uint32_t *pw = prog_word(E, P, L.row - 1);
     return (EG::kSpread ? load_agent(pw) : prog_load(pw)) >= need;
@@ -1000,13 +991,8 @@ HG_HD inline void row_outputs(Lane &L, const LanePic &P) {
 // through registers measured 5 % slower: the selects run on every lane of
 // every coefficient step, the saved stores were cheap.)
 HG_HD inline void coef_push(Lane &L, const LanePic &P, uint32_t w) {
-#if defined(HG_NO_COEF_STORE)  // timing experiment only: the stores' share of the parse
-    ++L.ncoef;
-    (void)w;
-#else
     if (P.flags & PF_COHERENT) store_word_agent((uint32_t *)(P.coef_base + L.coef_row + L.ncoef++), w);
     else P.coef_base[L.coef_row + L.ncoef++] = w;
-#endif
 }
 
 // ------------------------------------------------------------------ units
@@ -1609,13 +1595,9 @@ HG_HD inline void sb_store(L_ &L, const P_ &P, uint32_t sig, uint32_t signs, uin
     const uint32_t w3 = (uint32_t)xS | ((uint32_t)yS << 3) | ((uint32_t)L.rc_scan << 6) | (hide ? 1u << 8 : 0u) |
                         (esc0 << 9);
     if (L.ncoef + L.nesc + 4 <= P.coef_cap) {
-#if defined(HG_NO_COEF_STORE)  // timing experiment only
-        (void)w0, (void)w3;
-#else
         TuRec *d = (TuRec *)(P.coef_base + L.coef_row + L.ncoef);
         if (P.flags & PF_COHERENT) store_tu_agent(d, w0, (uint32_t)nib, (uint32_t)(nib >> 32), w3);
         else store_tu(d, w0, (uint32_t)nib, (uint32_t)(nib >> 32), w3);
-#endif
         L.ncoef += 4;
     } else {
         L.status |= ST_CAPACITY;
@@ -1892,10 +1874,9 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     const uint32_t pv = (L.fl & F_STOP) ? kProgDone : (uint32_t)L.row * (uint32_t)P.wctb + (uint32_t)L.c;
     if constexpr (EG::kSpread) {
         if (E.a->xntu) {  // k_intra's streaming mode reads this row's records as they appear
-#if defined(HG_REC_WBL2) && !defined(HG_HOST_EMU)  // tuning variant: plain record stores, then an L2 write-back
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
-            stores_done();  // (the records went out as agent-scope stores: PF_COHERENT)
+            // the records (agent-scope stores: PF_COHERENT) before the count: an
+            // agent release, which k_intra_stream's acquire after its poll pairs with
+            HG_REL_AGENT();
             store_agent(E.a->xntu + P.row_off + L.row, L.ntu);
         }
         stores_done();
@@ -1962,7 +1943,6 @@ HG_HD inline bool pic_init(LanePic &P, const BatchArgs &a, int pic, int lane0, i
     const bool wpp = (sp.flags & SP_WPP) != 0;
     const int R = wpp ? (hctb < cap ? hctb : cap) : 1;
     P.R = R;
-    P.stage = -1;
     P.lane0 = lane0;
     P.ring = wpp && hctb > R;
     P.W = sp.width;
@@ -1994,11 +1974,7 @@ HG_HD inline bool pic_init(LanePic &P, const BatchArgs &a, int pic, int lane0, i
     P.w8 = (sp.width + 7) >> 3;
     P.saoL = pd.sao_luma;
     P.saoC = pd.sao_chroma;
-#if defined(HG_REC_WBL2)
-    P.flags = sp.flags;
-#else
     P.flags = sp.flags | (a.xntu ? PF_COHERENT : 0u);
-#endif
     P.bits_off = (uint32_t)pd.bits_off;
     P.bits_end = (uint32_t)pd.bits_off + a.rsubs[pd.sub_first + pd.n_sub];  // RBSP end (k_rbsp)
     P.sub_first = pd.sub_first;
@@ -2085,57 +2061,22 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
     return full;
 }
 
-// Job lanes (k_parse_jobs): about two substreams per lane, so each wave's WPP
-// ramps fill with other pictures' rows; fewer pictures per wave only while
-// that would leave under 3/4 of the SIMDs a wave (small batches).
-// HEIFGPU_LANES_PPW forces a value.
-inline int jobs_pics_per_wave(int lane_rows, int n_pics) {
-    const char *fe = std::getenv("HEIFGPU_LANES_PPW");
-    const int forced = fe ? std::atoi(fe) : 0;
-    if (forced > 0) return forced < kJobsMaxPics ? forced : kJobsMaxPics;
-    const int rows = lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows);
-    int p = std::max(1, std::min(kJobsMaxPics, 128 / rows));
-    const long floor_waves = lanes_simds() * 3L / 4;
-    while (p > 1 && (n_pics + p - 1) / p < floor_waves) --p;
-    return p;
-}
-
 }  // namespace
-
-// k_parse_jobs only with HEIFGPU_LANES_JOBS=1: measured slower than the
-// static mapping at the bench's batch (r04 A/B, same box: parse alone 75.7 ms
-// static vs 91.5 / 102.3 / 110.1 / 120.6 at 6 / 8 / 12 / 16 pictures per
-// wave).  Twice the lanes busy per pass, but the wave's passes get longer
-// (each divergent loop runs to its slowest busy lane) and a wave alone on a
-// SIMD hides less latency than the static 1.5 waves per SIMD.  Beside the
-// parse the reconstruction stream was much faster (47 vs 74 ms at 6 per wave).
-bool lanes_jobs_default() {  // (read at every prepare: tests switch it within one process)
-    const char *e = std::getenv("HEIFGPU_LANES_JOBS");
-    return e && std::atoi(e) != 0;
-}
 
 // Wave slot -> picture.  A wave runs until its heaviest picture is parsed,
 // and every extra busy picture in it adds divergent units to each pass, so
 // the critical path is the wave holding the most work.  Pictures are sorted
-// by payload size; the `heavy` largest each get a wave to themselves (their
-// WPP chain is the kernel's critical path, and a pass over one picture's
-// lanes is cheaper than over four), the rest are dealt snake-wise (wave w of
-// W gets ranks w, 2W-1-w, 2W+w, 4W-1-w, ...): heavy beside light.  Empty
-// slots are ~0u.  HEIFGPU_PARSE_ORDER=0: batch order; HEIFGPU_PARSE_HEAVY
-// overrides the heavy count.
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
-                      const float *cost, bool jobs) {
+// by payload size and dealt snake-wise (wave w of W gets ranks w, 2W-1-w,
+// 2W+w, 4W-1-w, ...): heavy beside light.  Empty slots are ~0u.
+// HEIFGPU_PARSE_ORDER=0: batch order (kept for the emulation test of an
+// unsorted dealing).
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
         return e ? std::atoi(e) : 1;
     }();
-    static const int heavy_env = [] {
-        const char *e = std::getenv("HEIFGPU_PARSE_HEAVY");
-        return e ? std::atoi(e) : -1;
-    }();
-    const int full = jobs ? kJobsMaxPics : 64 / (lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows));
-    const int ppw = ppw_force > 0 ? std::min(ppw_force, full)
-                                  : (jobs ? jobs_pics_per_wave(lane_rows, n) : lanes_pics_per_wave(lane_rows, n));
+    const int full = 64 / (lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows));
+    const int ppw = ppw_force > 0 ? std::min(ppw_force, full) : lanes_pics_per_wave(lane_rows, n);
     if (!on || n <= 0) {
         order.resize((size_t)n);
         for (int i = 0; i < n; ++i) order[(size_t)i] = (uint32_t)i;
@@ -2146,20 +2087,14 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
     for (int i = 0; i < n; ++i)
         if (!(pics[i].flags & PD_ASSEMBLY)) by_size.push_back((uint32_t)i);
     n = (int)by_size.size();
-    if (cost)
-        std::stable_sort(by_size.begin(), by_size.end(), [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
-    else
-        std::stable_sort(by_size.begin(), by_size.end(),
-                         [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
-    int heavy = heavy_env >= 0 ? heavy_env : 0;
-    heavy = ppw > 1 ? std::min(heavy, n) : 0;
-    const int rest = n - heavy, W = (rest + ppw - 1) / ppw;
-    order.assign((size_t)(heavy + W) * ppw, ~0u);
-    for (int h = 0; h < heavy; ++h) order[(size_t)h * ppw] = by_size[(size_t)h];
-    for (int r = 0; r < rest; ++r) {
+    std::stable_sort(by_size.begin(), by_size.end(),
+                     [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
+    const int W = (n + ppw - 1) / ppw;
+    order.assign((size_t)W * ppw, ~0u);
+    for (int r = 0; r < n; ++r) {
         const int band = r / W, pos = r % W;
         const int w = (band & 1) ? W - 1 - pos : pos;
-        order[(size_t)(heavy + w) * ppw + band] = by_size[(size_t)(heavy + r)];
+        order[(size_t)w * ppw + band] = by_size[(size_t)r];
     }
     return ppw;
 }
@@ -2224,7 +2159,16 @@ int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order)
 // payload size (copies of one tile there) are spread so that each group holds
 // copies of K different sizes, the K adjacent ones; "copies": of all of them.
 // A batch of distinct photos (no two payloads of equal size) is unaffected.
-int rows_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order) {
+int rows_lanes_for(int n_pics) {
+    static const int forced = [] {
+        const char *e = std::getenv("HEIFGPU_ROWS_LANES");
+        return e ? std::atoi(e) : 0;
+    }();
+    (void)n_pics;
+    return forced > 0 && forced < 64 ? forced : 64;
+}
+
+int rows_parse_order(const PicDesc *pics, int n, int lanes, std::vector<uint32_t> &order) {
     static const long band = [] {
         const char *e = std::getenv("HEIFGPU_ROWS_DEAL");
         if (!e) return 1L;
@@ -2252,8 +2196,8 @@ int rows_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order) {
         for (size_t i = 0; i < idx.size(); ++i) t[i] = by_size[idx[i]];
         by_size.swap(t);
     }
-    const int groups = ((int)by_size.size() + 63) / 64;
-    order.assign((size_t)groups * 64, ~0u);
+    const int groups = ((int)by_size.size() + lanes - 1) / lanes;
+    order.assign((size_t)groups * lanes, ~0u);
     std::copy(by_size.begin(), by_size.end(), order.begin());
     return groups;
 }
@@ -2314,91 +2258,6 @@ void emu_parse_lanes(const BatchArgs &a) {
                         lanes[l].status |= ST_SUBSTREAM_END;
                         atomicOr(&a.status[pics[l / a.lane_rows].pic], lanes[l].status);
                         lanes[l].st = U_DONE;
-                    }
-                break;
-            }
-        }
-        if (stats)
-            printf("wave %d: %ld passes, %.1f units per pass\n", w, passes, (double)units / passes);
-    }
-}
-
-// job lanes (k_parse_jobs): the same pass structure, idle lanes taking the
-// next substream of the wave's job list (row order across its pictures) at
-// each pass start, in lane order
-void emu_parse_jobs(const BatchArgs &a) {
-    const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : jobs_pics_per_wave(a.lane_rows, a.n_pics);
-    const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
-    const int waves = (n_slots + ppw - 1) / ppw;
-    uint64_t tab[64], seq[15];
-    for (int i = 0; i < 64; ++i) tab[i] = state_row(i);
-    for (int i = 0; i < 15; ++i) seq[i] = sig_seq(i);
-    std::vector<LaneLds> lds(64);
-    std::vector<LanePic> pics((size_t)ppw);
-    std::vector<Lane> lanes(64);
-    std::vector<int> ps(64, 0);
-    std::vector<uint8_t> wctx((size_t)ppw * CTX_PAD);
-    std::vector<uint32_t> prog((size_t)ppw * a.max_rows), nsub((size_t)ppw);
-    static const bool stats = std::getenv("HEIFGPU_LANES_STATS") != nullptr;
-    for (int w = 0; w < waves; ++w) {
-        std::fill(prog.begin(), prog.end(), 0u);
-        uint32_t n_jobs = 0, next = 0;
-        for (int s = 0; s < ppw; ++s) {
-            const int slot = w * ppw + s;
-            const bool in = slot < n_slots && (!a.parse_order || a.parse_order[slot] != ~0u);
-            const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
-            LanePic &P = pics[(size_t)s];
-            nsub[(size_t)s] = 0;
-            if (in && pic_init(P, a, pic, s * a.max_rows, 1 << 20)) {
-                P.ring = 1;
-                P.stage = s;
-                nsub[(size_t)s] = (P.flags & SP_WPP) ? (uint32_t)P.hctb : 1u;
-            }
-            n_jobs = std::max(n_jobs, nsub[(size_t)s] * (uint32_t)ppw);
-        }
-        for (int l = 0; l < 64; ++l) lanes[(size_t)l].st = U_DONE;
-        Env E{&a, lds.data(), prog.data(), wctx.data(), 0};
-        long passes = 0, units = 0;
-        for (;; ++passes) {
-            for (int l = 0; l < 64 && next < n_jobs; ++l) {
-                if (lanes[(size_t)l].st != U_DONE) continue;
-                while (next < n_jobs) {
-                    const uint32_t j = next++;
-                    const int s = (int)(j % (uint32_t)ppw), row = (int)(j / (uint32_t)ppw);
-                    if ((uint32_t)row < nsub[(size_t)s]) {
-                        ps[(size_t)l] = s;
-                        lane_start(lanes[(size_t)l], pics[(size_t)s], lds[(size_t)l], row);
-                        break;
-                    }
-                }
-            }
-            bool any = false, progressed = false;
-            for (int l = 0; l < 64; ++l) any |= lanes[(size_t)l].st != U_DONE;
-            if (!any) break;
-            for (int l = 0; l < 64; ++l)
-                if (lanes[(size_t)l].st != U_DONE) {
-                    const LanePic &P = pics[(size_t)ps[(size_t)l]];
-                    const Eng G{lds[(size_t)l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
-                    q_refill(lanes[(size_t)l], G);
-                }
-            for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
-                for (int l = 0; l < 64; ++l) {
-                    Lane &L = lanes[(size_t)l];
-                    E.lane = l;
-                    LanePic &P = pics[(size_t)ps[(size_t)l]];
-                    if (L.st != kind || (kind == U_CTU && !ctu_ready(L, P, E))) continue;
-                    progressed = true;
-                    ++units;
-                    const Eng G{lds[(size_t)l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
-                    run_unit(kind, L, lds[(size_t)l], P, E, G);
-                }
-            }
-            if (!progressed) {  // cannot happen: a row's job follows the row above's
-                for (int l = 0; l < 64; ++l)
-                    if (lanes[(size_t)l].st != U_DONE) {
-                        lanes[(size_t)l].status |= ST_SUBSTREAM_END;
-                        atomicOr(&a.status[pics[(size_t)ps[(size_t)l]].pic], lanes[(size_t)l].status);
-                        lanes[(size_t)l].st = U_DONE;
                     }
                 break;
             }
@@ -2488,8 +2347,8 @@ void emu_parse_rows(const BatchArgs &a) {
         for (int r = 0; r < R; ++r)
             for (int l = 0; l < 64; ++l) {
                 const size_t i = (size_t)r * 64 + (size_t)l;
-                const int slot = g * 64 + l;
-                const bool in = slot < a.n_slots && a.parse_order[slot] != ~0u;
+                const int slot = g * a.rows_lanes + l;
+                const bool in = l < a.rows_lanes && slot < a.n_slots && a.parse_order[slot] != ~0u;
                 live[i] = in && pic_init(pics[i], a, a.pic0 + (int)a.parse_order[slot], 0, 1 << 20) && r < pics[i].R;
                 if (live[i]) lane_start(lanes[i], pics[i], lds[i], r);
                 else lanes[i].st = U_DONE;
@@ -2546,7 +2405,6 @@ void emu_parse(const BatchArgs &a) {
     }
     if (a.parse_mode == PARSE_SOLO) emu_parse_solo<false>(a);
     else if (a.parse_mode == PARSE_SPREAD) emu_parse_solo<true>(a);
-    else if (a.lane_jobs) emu_parse_jobs(a);
     else emu_parse_lanes(a);
 }
 #else
@@ -2638,122 +2496,6 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
 #endif
 }
 
-// Job lanes (BatchArgs::lane_jobs): the lanes of a wave are not tied to
-// pictures.  The wave holds `ppw` pictures (more rows than lanes, e.g. 8
-// pictures x 16 WPP rows = 128 substreams on 64 lanes), and a lane that
-// finishes a substream takes the next one from the wave's job list, in row
-// order across the pictures (row 0 of every picture, then row 1, ...).  The
-// WPP ramp of one picture (row r starts ~2r CTU-times late) then fills with
-// the early rows of the others: with equal CTUs, 8 pictures per wave take the
-// same 46 CTU-times as 4 pictures on statically assigned lanes, at twice the
-// lanes busy per pass (r03: 22.4 of 64).  A row's job comes after the row
-// above's, so every wait is on a substream some lane holds.  Progress words
-// are per (picture, row) in LDS; the WPP context hand-off goes through one
-// staging block per picture (wpp_stage).
-inline size_t jobs_lds_bytes(int ppw, int max_rows) {
-    return lane_blocks_bytes(64) + sizeof(LanePic) * (size_t)ppw + sizeof(uint32_t) * (size_t)ppw * max_rows +
-           (64 + 16) * sizeof(uint64_t) + (size_t)ppw * CTX_PAD + sizeof(uint32_t) * ((size_t)ppw + 4);
-}
-
-__global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_jobs(BatchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int ppw = a.parse_group;
-    LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
-    LanePic *s_pic = reinterpret_cast<LanePic *>(smem + lane_blocks_bytes(64));
-    uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_pic + ppw);
-    uint64_t *s_seq = s_tab + 64;
-    uint8_t *s_wctx = reinterpret_cast<uint8_t *>(s_seq + 16);
-    uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_wctx + (size_t)ppw * CTX_PAD);
-    uint32_t *s_nsub = s_prog + (size_t)ppw * a.max_rows;  // [ppw] substreams of the picture (0: none)
-    uint32_t *s_next = s_nsub + ppw;                        // [0] next job, [1] jobs (ppw * max substreams)
-    const int lane = threadIdx.x;
-    s_tab[lane] = state_row(lane);
-    if (lane < 15) s_seq[lane] = sig_seq(lane);
-    for (int i = lane; i < ppw * a.max_rows; i += 64) s_prog[i] = 0;
-    if (lane == 0) s_next[0] = s_next[1] = 0;
-    __syncthreads();
-    if (lane < ppw) {  // lane s sets up picture s of the wave
-        const int slot = (int)blockIdx.x * ppw + lane;
-        const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
-        const bool in = slot < n_slots && (!a.parse_order || a.parse_order[slot] != ~0u);
-        const int pic = a.pic0 + (in && a.parse_order ? (int)a.parse_order[slot] : slot);
-        LanePic &P = s_pic[lane];
-        uint32_t nsub = 0;
-        if (in && pic_init(P, a, pic, lane * a.max_rows, 1 << 20)) {
-            P.ring = 1;
-            P.stage = lane;
-            nsub = (P.flags & SP_WPP) ? (uint32_t)P.hctb : 1u;
-        }
-        s_nsub[lane] = nsub;
-        atomicMax(&s_next[1], nsub * (uint32_t)ppw);
-    }
-    __syncthreads();
-    const uint32_t n_jobs = s_next[1];
-    const Env E{&a, s_lds, s_prog, s_wctx, lane};
-    LaneLds &ld = s_lds[lane];
-    Lane L;
-    L.st = U_DONE;
-    int ps = 0;  // picture slot of the lane's substream
-    bool more = n_jobs > 0;
-#if defined(HG_PARSE_PROF)
-    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const uint64_t t_start = __builtin_amdgcn_s_memtime();
-#endif
-    for (uint32_t pass = 0;; ++pass) {
-        if (more && __any(L.st == U_DONE)) {  // idle lanes take the next substreams
-            bool got = false;
-            if (L.st == U_DONE) {
-                for (uint32_t j; (j = atomicAdd(&s_next[0], 1u)) < n_jobs;) {
-                    const int s = (int)(j % (uint32_t)ppw), row = (int)(j / (uint32_t)ppw);
-                    if ((uint32_t)row < s_nsub[s]) {
-                        ps = s;
-                        lane_start(L, s_pic[s], ld, row);
-                        got = true;
-                        break;
-                    }
-                }
-            }
-            more = !__any(L.st == U_DONE && !got);
-        }
-        if (!__any(L.st != U_DONE)) break;
-        pass_wait();
-        LanePic &P = s_pic[ps];
-        const Eng G{ld.ctx, s_tab, s_seq, a.rbsp, (P.bits_end + 64u) & ~3u};
-        if (L.st != U_DONE) q_refill(L, G);
-        bool progressed = false;
-#pragma unroll
-        for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
-            const bool mine = L.st == kind && (kind != U_CTU || ctu_ready(L, P, E));
-            if (!__any(mine)) continue;
-            progressed = true;
-#if defined(HG_PARSE_PROF)
-            const uint64_t t1 = __builtin_amdgcn_s_memtime();
-            pf[7] += (uint64_t)__popcll(__ballot(mine));  // lanes running a unit
-#endif
-            if (mine) run_unit(kind, L, ld, P, E, G);
-#if defined(HG_PARSE_PROF)
-            const uint64_t t2 = __builtin_amdgcn_s_memtime();
-            pf[kind <= U_CTU ? 2 : kind <= U_TT ? 3 : kind - 1] += t2 - t1;
-#endif
-        }
-#if defined(HG_PARSE_PROF)
-        ++pf[1];
-#endif
-        if (!progressed || pass > (1u << 30)) {  // every live lane waits: cannot happen (a row's job follows the row above's)
-            if (L.st != U_DONE) {
-                L.status |= ST_SUBSTREAM_END;
-                atomicOr(&a.status[P.pic], L.status);
-            }
-            break;
-        }
-    }
-#if defined(HG_PARSE_PROF)
-    pf[0] = __builtin_amdgcn_s_memtime() - t_start;
-    if (lane == 0)
-        for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[k], (unsigned long long)pf[k]);
-#endif
-}
-
 // Row waves (k_parse_rows, PARSE_ROWS): lane = picture, wave = one WPP CTB
 // row of a group of up to 64 pictures of similar payload (rows_parse_order).
 // In k_parse_lanes a picture's 16 rows share a wave, and the WPP ramp (row r
@@ -2796,8 +2538,8 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_rows(BatchArgs a) {
     if (lane < 15) s_seq[lane] = sig_seq(lane);
     const uint32_t groups = (uint32_t)a.parse_group;
     const uint32_t j = dequeue_job(a.xjob);
-    const int row = (int)(j / groups), slot = (int)(j % groups) * 64 + lane;
-    const bool in = row < a.max_rows && slot < a.n_slots && a.parse_order[slot] != ~0u;
+    const int row = (int)(j / groups), slot = (int)(j % groups) * a.rows_lanes + lane;
+    const bool in = lane < a.rows_lanes && row < a.max_rows && slot < a.n_slots && a.parse_order[slot] != ~0u;
     Lane L;
     LaneLds &ld = s_lds[lane];
     LanePic &P = s_pic[lane];
@@ -2823,7 +2565,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_rows(BatchArgs a) {
             if (!__any(mine)) continue;
             progressed = true;
             // the rows above (contexts, SAO parameters, depth line) after their progress words
-            if (kind == U_CTU) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (kind == U_CTU) HG_ACQ_AGENT();
 #if defined(HG_PARSE_PROF)
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
             pf[7] += (uint64_t)__popcll(__ballot(mine));
@@ -2973,8 +2715,12 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
         start = (uint32_t)__builtin_amdgcn_readfirstlane((int)start);
         if (start != ~0u) sw.restart(a.rbsp, start, lim, lane);
         else sw.advance(a.rbsp, (uint32_t)__builtin_amdgcn_readfirstlane((int)rd), lim, lane);
-        // the rows above (contexts, SAO parameters, depth line) before their readers
-        if (st == U_CTU) HG_FENCE_ACQ();
+        // the rows above (contexts, SAO parameters, depth line: other workgroups'
+        // agent-scope stores) after their progress words, before their readers
+        if (st == U_CTU) {
+            if (Spread) HG_ACQ_AGENT();
+            else HG_FENCE_ACQ();
+        }
 #if defined(HG_PARSE_PROF)
         const uint64_t t1 = __builtin_amdgcn_s_memtime();
         ++pf[7];
@@ -3032,7 +2778,9 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
         return hipGetLastError();
     }
     if (a.parse_mode == PARSE_ROWS) {
-        if (!a.parse_order || !a.xprog || !a.xctx || !a.xjob || a.parse_group < 1) return hipErrorInvalidValue;
+        if (!a.parse_order || !a.xprog || !a.xctx || !a.xjob || a.parse_group < 1 || a.rows_lanes < 1 ||
+            a.rows_lanes > 64)
+            return hipErrorInvalidValue;
         const long jobs = (long)a.parse_group * a.max_rows;
         if (jobs <= 0) return hipSuccess;
         if (jobs >= (1L << 31)) return hipErrorInvalidValue;
@@ -3040,20 +2788,10 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
         return hipGetLastError();
     }
     // the dealing of parse_order fixed the pictures per wave (lanes_parse_order)
-    const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group
-                    : (a.lane_jobs ? jobs_pics_per_wave(a.lane_rows, a.n_pics) : lanes_pics_per_wave(a.lane_rows, a.n_pics));
+    const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : lanes_pics_per_wave(a.lane_rows, a.n_pics);
     a.parse_group = ppw;
     const int waves = ((a.parse_order ? a.n_slots : a.n_pics) + ppw - 1) / ppw;
-    // HEIFGPU_PARSE_LDS_PAD: extra (unused) LDS per wave (tuning: residency beside the reconstruction kernels)
-    static const size_t pad = [] {
-        const char *e = std::getenv("HEIFGPU_PARSE_LDS_PAD");
-        return e ? (size_t)std::atoi(e) : (size_t)0;
-    }();
-    if (a.lane_jobs)
-        hipLaunchKernelGGL(k_parse_jobs, dim3(waves), dim3(64), jobs_lds_bytes(ppw, a.max_rows) + pad, s, a);
-    else
-        hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64),
-                           lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0) + pad, s, a);
+    hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0), s, a);
     return hipGetLastError();
 }
 #endif

@@ -61,6 +61,8 @@ inline void emu_syncthreads() {
 #define HG_GAS
 #define HG_FENCE_ACQ() std::atomic_thread_fence(std::memory_order_acquire)
 #define HG_FENCE_REL() std::atomic_thread_fence(std::memory_order_release)
+#define HG_ACQ_AGENT() std::atomic_thread_fence(std::memory_order_acquire)
+#define HG_REL_AGENT() std::atomic_thread_fence(std::memory_order_release)
 #define HG_WAVE_SYNC() ((void)0)
 #define HG_SLEEP() std::this_thread::yield()
 template <class T>
@@ -102,6 +104,23 @@ constexpr int kWave = 64;
 #endif
 #define HG_FENCE_ACQ() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup")
 #define HG_FENCE_REL() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup")
+// Cross-CU hand-offs (another workgroup, possibly on another XCD: MI355X_MICROARCH.md
+// "inter-workgroup visibility").  Consumer: after the relaxed poll has matched,
+// an agent acquire (s_waitcnt vmcnt(0); buffer_inv sc1: this CU's L1 dropped)
+// before the handed-off bytes are read.  Producer: an agent release (buffer_wbl2
+// sc1; s_waitcnt vmcnt(0)), then the explicit wait the guide prescribes (the
+// compiler may drop its own after the write-back), then the relaxed flag store.
+#if defined(HG_HANDOFF_RELAXED)  // A/B only: the r04 forms (vmcnt(0) + sc1 flag; no acquire)
+#define HG_ACQ_AGENT() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup")
+#define HG_REL_AGENT() __builtin_amdgcn_s_waitcnt(0x0f70)
+#else
+#define HG_ACQ_AGENT() __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent")
+#define HG_REL_AGENT()                                  \
+    do {                                                \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  \
+    } while (0)
+#endif
 // Orders one wave's own LDS traffic across lanes (write by lane i, read by
 // lane j).  A wave's LDS instructions execute in order, so wavefront scope is
 // enough; workgroup scope would also drain the wave's outstanding global

@@ -325,3 +325,27 @@ def single_heic(p: SynthParams, seed: int = 0, layout: Optional[BoxLayout] = Non
 
 # BASELINE config 5: 8K 10-bit Main-10 grid, 15 x 9 tiles of 512x512
 CONFIG5 = dict(out_w=7680, out_h=4320, params=SynthParams(bit_depth=10))
+# Control workload of config-4 geometry whose 48 grid tiles are all distinct
+# bitstreams (the bench's halfmoonbay permutations repeat 48 tiles): 8-bit
+# 4:2:0 512x512 WPP tiles, sig_coeff_flag density cycling over 0..100 % so the
+# payloads run from ~8 to ~45 KB (halfmoonbay's tiles: 1.4 to 76 KB)
+CONFIG4U = dict(out_w=4032, out_h=3024, params=SynthParams(bit_depth=8))
+
+
+def config4u_tile(j: int) -> bytes:
+    """Distinct tile j of the CONFIG4U workload (seed and density from j)."""
+    p = dataclasses.replace(CONFIG4U["params"], density=(j * 37 + 11) % 101)
+    return picture(p, (1 << 24) + j)
+
+
+def config4u_image(seed: int, threads: int = 1) -> bytes:
+    """Image `seed` of the CONFIG4U workload: tiles 48*seed .. 48*seed+47."""
+    import concurrent.futures as cf
+
+    js = range(48 * seed, 48 * seed + 48)
+    if threads > 1:  # (ctypes releases the GIL inside the generator)
+        with cf.ThreadPoolExecutor(threads) as ex:
+            pics = list(ex.map(config4u_tile, js))
+    else:
+        pics = [config4u_tile(j) for j in js]
+    return grid_heic(CONFIG4U["out_w"], CONFIG4U["out_h"], CONFIG4U["params"], pictures=pics)

@@ -34,28 +34,22 @@ def _run(exe, path, env_extra=None):
 # unsplit kernel.)
 # k_parse_solo (one substream per wave), k_parse_solo<true> (spread: the
 # automatic choice for a single image), k_parse_lanes (one substream per lane)
-# with its adaptive geometry (one picture per wave for a single image) and the
-# full 64-lane packing of large batches (four 16-row pictures per wave),
-# k_parse_jobs (lanes take substreams from the wave's job list: adaptive, 8
-# pictures = 128 substreams on 64 lanes, and an odd 5), and batch (unsorted)
-# wave order; k_parse_rows (lane = picture, wave = one CTB row of the group,
-# WPP through coherent global memory) in size-sorted and copies-apart dealing
+# with its adaptive geometry (one picture per wave for a single image), the
+# full 64-lane packing of large batches (four 16-row pictures per wave) and
+# batch (unsorted) wave order; k_parse_rows (lane = picture, wave = one CTB
+# row of the group, WPP through coherent global memory) in size-sorted and
+# copies-apart dealing, and with 32-picture groups
 LANES = {"HEIFGPU_PARSE": "lanes"}
-JOBS = {**LANES, "HEIFGPU_LANES_JOBS": "1"}
 PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "spread"}, "lanes": LANES,
            "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0"},
-           "jobs": JOBS, "jobs8": {**JOBS, "HEIFGPU_LANES_PPW": "8"}, "jobs5": {**JOBS, "HEIFGPU_LANES_PPW": "5"},
            "ppw1": {**LANES, "HEIFGPU_LANES_PPW": "1", "HEIFGPU_INTRA_SPLIT": "0"},
-           "lf_fused": {"HEIFGPU_LF": "fused"},
            # spread with k_intra_stream giving every picture up to its second launch, and without streaming
            "spread_redo": {"HEIFGPU_PARSE": "spread", "HEIFGPU_STREAM_PATIENCE_US": "0"},
            "spread_nostream": {"HEIFGPU_PARSE": "spread", "HEIFGPU_STREAM": "0"},
-           # k_intra_fused: the transform folded into the reconstruction after the parse
-           "fused": {**LANES, "HEIFGPU_FUSED": "1"},
-           "fused_solo": {"HEIFGPU_PARSE": "solo", "HEIFGPU_FUSED": "1"},
            "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"},
            "rows": {"HEIFGPU_PARSE": "rows"},
-           "rows_copies": {"HEIFGPU_PARSE": "rows", "HEIFGPU_ROWS_DEAL": "copies"}}
+           "rows_copies": {"HEIFGPU_PARSE": "rows", "HEIFGPU_ROWS_DEAL": "copies"},
+           "rows32": {"HEIFGPU_PARSE": "rows", "HEIFGPU_ROWS_LANES": "32"}}
 
 
 @pytest.mark.parametrize("parser", list(PARSERS))
@@ -64,7 +58,7 @@ def test_emulated_kernels_match_oracle(emu_check, parser):
     assert rc == 0 and "EMU PARITY OK" in out, out[-2000:]
 
 
-@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "jobs8", "rows"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "rows"])
 def test_emulated_kernels_permuted_image(emu_check, tmp_path, halfmoonbay, parser):
     p = tmp_path / "perm.heic"
     p.write_bytes(permuted_heic(halfmoonbay, 42))
@@ -91,7 +85,7 @@ def _corrupt(data: bytes, mode: str) -> bytes:
     return bytes(d)
 
 
-@pytest.mark.parametrize("parser", ["solo", "spread", "spread_redo", "lanes", "packed", "jobs8", "rows"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "spread_redo", "lanes", "packed", "rows"])
 @pytest.mark.parametrize("mode", ["random", "zeroed"])
 def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode, parser):
     """Corrupt slice data must end in status bits, never in a crash (the same

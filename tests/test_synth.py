@@ -232,29 +232,19 @@ def test_gpu_synthetic_bit_exact(H, gctx, oracle_mod, name, over, parse):
         _assert_equal(_planes(outs[0]), oracle_mod.decode_heic(data, with_checks=False), (name, seed))
 
 
-VARIANTS = {
-    "lf_fused": {"HEIFGPU_LF": "fused"},  # k_loopfilter: deblocking + SAO + output in one LDS-tiled kernel
-    "jobs": {"HEIFGPU_LANES_JOBS": "1"},  # k_parse_jobs, adaptive pictures per wave
-    "jobs3": {"HEIFGPU_LANES_JOBS": "1", "HEIFGPU_LANES_PPW": "3"},
-}
-
-
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", list(VARIANTS))
-def test_gpu_synthetic_variants_bit_exact(H, gctx, oracle_mod, monkeypatch, variant):
-    """The optional kernels (selected by environment, read at every prepare /
-    launch) on every tool / geometry case, several pictures per batch so the
-    job lanes mix pictures: k_loopfilter (HEIFGPU_LF=fused) and k_parse_jobs
-    (HEIFGPU_LANES_JOBS=1)."""
-    for k, v in VARIANTS[variant].items():
-        monkeypatch.setenv(k, v)
+def test_gpu_synthetic_rows_bit_exact(H, gctx, oracle_mod):
+    """k_parse_rows (lane = picture, one wave per CTB row of the batch's
+    pictures, WPP hand-offs through coherent global memory) on every tool /
+    geometry case, three pictures per batch (non-WPP cases: the row-0 wave
+    walks every row)."""
     for name, over in CASES:
         p = params(over)
         datas = [S.single_heic(p, seed=s) for s in range(3)]
-        outs, st = _decode(H, gctx, datas, "lanes")
-        assert st == [0, 0, 0], (variant, name)
+        outs, st = _decode(H, gctx, datas, "rows")
+        assert st == [0, 0, 0], name
         for o, d in zip(outs, datas):
-            _assert_equal(_planes(o), oracle_mod.decode_heic(d, with_checks=False), (variant, name))
+            _assert_equal(_planes(o), oracle_mod.decode_heic(d, with_checks=False), ("rows", name))
 
 
 @pytest.mark.gpu
