@@ -55,7 +55,7 @@ sys.path.insert(0, str(ROOT))
 
 SAMPLE = ROOT / "tests" / "golden" / "halfmoonbay.heic"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-ROUND = "r04"
+ROUND = "r05"
 PROFILES = ROOT / "profiles" / ROUND
 BINS_PER_IMAGE = 15358022  # CABAC bins of one halfmoonbay image (oracle count; every permutation has the same)
 

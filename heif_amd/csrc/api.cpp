@@ -61,6 +61,7 @@ struct heifgpu_ctx {
     // running parse instead of in front of the next one on the parse stream
     hipStream_t prep = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    StreamKnobs stream;  // the streaming knobs, read once at heifgpu_create
     // timing ring, one slot per timed decode call: rbsp start, rbsp end, parse
     // end, transform start, transform end, recon start, 3 stage ends, parse
     // start.  heifgpu_stage_times folds every call since the previous query (a
@@ -480,6 +481,7 @@ int heifgpu_create(int device, heifgpu_ctx **out) {
     HIP_TRY(hipSetDevice(device));
     auto c = std::make_unique<heifgpu_ctx>();
     c->device = device;
+    c->stream = stream_knobs_from_env();
     // parse and reconstruction streams at the same priority: with the parse
     // stream at the highest priority (HEIFGPU_PARSE_PRIORITY=1) k_transform
     // starves beside it and the bench measured 1 % lower (two A/B pairs,
@@ -763,9 +765,9 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.solo_waves = solo_waves;
     a.xprog = nullptr;  // (per parse set: heifgpu_batch_decode)
     a.xctx = cross_rows ? b->xctx.p : nullptr;
-    a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
+    a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly, ctx->stream) ? 1 : 0;
     a.xntu = nullptr;
-    a.stream_patience_us = stream_patience_us();
+    a.stream_patience_us = ctx->stream.patience_us;
     // rows wrap round the lanes (waves) of a picture: the WPP context staging
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;

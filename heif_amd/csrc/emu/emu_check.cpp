@@ -109,9 +109,10 @@ int main(int argc, char **argv) {
     a.xprog = xprog.data();
     a.xctx = xctx.data();
     a.xjob = xprog.data() + hb.rows;
-    a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly) ? 1 : 0;
+    const StreamKnobs knobs = stream_knobs_from_env();
+    a.intra_stream = intra_stream_for(mode, int(hb.pics.size()), hb.has_assembly, knobs) ? 1 : 0;
     a.xntu = a.intra_stream ? xntu.data() : nullptr;
-    a.stream_patience_us = stream_patience_us();
+    a.stream_patience_us = knobs.patience_us;
     a.wpp_ring = mode == PARSE_SOLO ? (hb.max_wpp_rows > solo_waves ? 1 : 0) : hb.wpp_ring;
     a.has_assembly = hb.has_assembly ? 1 : 0;
     a.total_rows = int(hb.rows);

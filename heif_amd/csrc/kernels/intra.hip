@@ -1053,23 +1053,27 @@ hipError_t launch_intra(const BatchArgs &a0, hipStream_t s) {
 }
 #endif
 
-// k_intra_stream's patience: how long (us) the first launch waits without
-// parse progress before it gives a picture up to the second launch.
-// HEIFGPU_STREAM_PATIENCE_US overrides (0: give every picture up, a test knob).
-uint32_t stream_patience_us() {
-    const char *e = std::getenv("HEIFGPU_STREAM_PATIENCE_US");
-    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 200000u;
+// The streaming knobs, read from the environment when a context is created
+// (heifgpu_create; the emulation driver reads them once per run):
+// HEIFGPU_STREAM=0 turns k_intra_stream off, HEIFGPU_STREAM_MAX_PICS moves its
+// batch limit (tuning), HEIFGPU_STREAM_PATIENCE_US is how long the first
+// launch waits without parse progress before it gives a picture up to the
+// second launch (0: every picture, a test knob).
+StreamKnobs stream_knobs_from_env() {
+    StreamKnobs k;
+    const char *e = std::getenv("HEIFGPU_STREAM");
+    k.enabled = !(e && std::atoi(e) == 0);
+    const char *m = std::getenv("HEIFGPU_STREAM_MAX_PICS");
+    k.max_pics = m && *m ? std::atoi(m) : kStreamMaxPics;
+    const char *p = std::getenv("HEIFGPU_STREAM_PATIENCE_US");
+    k.patience_us = p && *p ? (uint32_t)std::strtoul(p, nullptr, 10) : 200000u;
+    return k;
 }
 
 // Streaming reconstruction (k_intra_stream beside the spread parse) for the
-// small batches (up to 192 pictures: four 4032x3024 images, kStreamMaxPics);
-// HEIFGPU_STREAM=0 turns it off.
-bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly) {
-    const char *e = std::getenv("HEIFGPU_STREAM");
-    if (e && std::atoi(e) == 0) return false;
-    const char *m = std::getenv("HEIFGPU_STREAM_MAX_PICS");  // (tuning)
-    const int max_pics = m && *m ? std::atoi(m) : kStreamMaxPics;
-    return parse_mode == PARSE_SPREAD && !has_assembly && n_pics > 0 && n_pics <= max_pics;
+// small batches (up to 192 pictures: four 4032x3024 images, kStreamMaxPics)
+bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly, const StreamKnobs &k) {
+    return k.enabled && parse_mode == PARSE_SPREAD && !has_assembly && n_pics > 0 && n_pics <= k.max_pics;
 }
 
 }  // namespace hg

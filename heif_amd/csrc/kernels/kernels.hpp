@@ -120,9 +120,13 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
 // (same box, spread, one-decode latency: 4 images 28.3 vs 33.7 ms streamed; 8
 // images 44.4 vs 40.5, the reconstruction no longer keeps up with the parse)
 constexpr int kStreamMaxPics = 192;
-bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly);
-// k_intra_stream's patience (us) before its first launch gives a picture up to the second
-uint32_t stream_patience_us();
+struct StreamKnobs {
+    bool enabled = true;
+    int max_pics = kStreamMaxPics;
+    uint32_t patience_us = 200000;  // first launch: give a picture up after this long without parse progress
+};
+StreamKnobs stream_knobs_from_env();
+bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly, const StreamKnobs &k);
 // the parse mode a batch of n_pics pictures runs in (requested: PARSE_*)
 int parse_mode_for(int requested, int n_pics);
 // spread mode's wave slots (row << 20 | picture); -1 if the batch exceeds the encoding

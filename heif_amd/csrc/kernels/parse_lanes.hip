@@ -229,6 +229,7 @@ struct EngLanesT {
     const uint8_t *rbsp;  // BatchArgs::rbsp (emulation prevention removed by k_rbsp)
     uint32_t lim;         // no loads at or past this offset (the picture's RBSP end + 64)
     HG_HD uint64_t row(uint32_t st) const { return tab[st]; }
+    HG_HD uint64_t seqw(int idx) const { return seq[idx]; }
 };
 using Eng = EngLanesT<false>;
 using EngRows = EngLanesT<true>;
@@ -274,13 +275,23 @@ struct EngSoloT {
 #endif
     uint8_t *ctx;
     uint32_t tlo, thi;    // lane s: state_row(s) (GPU); unused under emulation
-    const uint64_t *seq;
+    const uint64_t *seq;  // (emulation; the GPU reads sqlo / sqhi)
     const uint8_t *rbsp;
     uint32_t lim;
     Win win;
+    uint32_t sqlo, sqhi;  // lane i < 15: sig_seq(i) (GPU: a v_readlane, no LDS round trip in the chain)
 #if defined(HG_HOST_EMU)
     uint64_t row(uint32_t st) const { return state_row((int)st); }
+    uint64_t seqw(int idx) const { return seq[idx]; }
 #else
+    __device__ __forceinline__ uint64_t seqw(int idx) const {
+#if defined(HG_SOLO_SEQ_LDS)  // A/B only: the LDS table, as before r05
+        return seq[idx];
+#endif
+        const int i = __builtin_amdgcn_readfirstlane(idx);
+        return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sqlo, i) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sqhi, i) << 32);
+    }
     __device__ __forceinline__ uint64_t row(uint32_t st) const {
         const int s = __builtin_amdgcn_readfirstlane((int)st);
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)tlo, s);
@@ -303,17 +314,33 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 }
 __device__ __forceinline__ void uni_state(Lane &L) {
 #define HG_U(f) L.f = uni32(L.f)
-#if defined(HG_SOLO_UNI_ENGINE)  // tuning: only the engine and the unit kind made scalar
-    HG_U(range); HG_U(value); HG_U(k); HG_U(cn); HG_U(lb); HG_U(budget); HG_U(st);
-    L.cur = uni64(L.cur);
-    return;
-#endif
+#if defined(HG_SOLO_UNI_ALL)  // A/B only: r04's list, every field (134 SGPRs spilled into VGPR lanes)
     HG_U(range); HG_U(value); HG_U(k); HG_U(cn); HG_U(lb); HG_U(budget); HG_U(status); HG_U(st); HG_U(fl);
     HG_U(row); HG_U(c); HG_U(ctbx); HG_U(ctby); HG_U(qx); HG_U(qy); HG_U(ql); HG_U(qd); HG_U(tx); HG_U(ty);
     HG_U(tl); HG_U(td); HG_U(tcbf); HG_U(qp_prev_last); HG_U(qp_pred); HG_U(cu_qp_delta_val); HG_U(qpy_cur);
     HG_U(qg_x); HG_U(qg_y); HG_U(cu_modes); HG_U(cu_chroma); HG_U(tb_t); HG_U(tb_n); HG_U(tb_cidx); HG_U(tb_x);
     HG_U(tb_y); HG_U(tb_log2); HG_U(tb_mode); HG_U(tb_coef0); HG_U(rc_scan); HG_U(rc_last_sub); HG_U(rc_last_pos);
     HG_U(rc_i); HG_U(rc_prev_c1); HG_U(ntu); HG_U(ncoef); HG_U(nesc); HG_U(tu_row); HG_U(coef_row);
+#elif defined(HG_SOLO_UNI_TB)  // A/B: the default set and the TB unit's fields
+    HG_U(range); HG_U(value); HG_U(k); HG_U(cn); HG_U(lb); HG_U(budget); HG_U(st); HG_U(fl);
+    HG_U(qx); HG_U(qy); HG_U(ql); HG_U(qd); HG_U(tx); HG_U(ty); HG_U(tl); HG_U(td); HG_U(tcbf);
+    HG_U(ctbx); HG_U(ctby); HG_U(tb_log2); HG_U(tb_cidx); HG_U(rc_i); HG_U(rc_scan); HG_U(rc_last_sub);
+    HG_U(rc_last_pos); HG_U(rc_prev_c1); HG_U(tb_t); HG_U(tb_n); HG_U(tb_mode); HG_U(tb_x); HG_U(tb_y);
+#elif defined(HG_SOLO_UNI_LEAN)  // A/B: the default set without the tree positions
+    HG_U(range); HG_U(value); HG_U(k); HG_U(cn); HG_U(lb); HG_U(budget); HG_U(st); HG_U(fl);
+    HG_U(ql); HG_U(qd); HG_U(tl); HG_U(td); HG_U(tcbf);
+    HG_U(tb_log2); HG_U(tb_cidx); HG_U(rc_i); HG_U(rc_scan); HG_U(rc_last_sub); HG_U(rc_last_pos); HG_U(rc_prev_c1);
+#else
+    // the engine and the tree / residual state the units branch on; the other
+    // fields stay in VGPRs (all 64 lanes alike) and are read where used.  r05
+    // A/B, one image, same box: 27.2 ms against 28.1 with every field scalar
+    // (r04; that list left 134 SGPRs spilled into VGPR lanes, reloaded at
+    // every unit) and 29.5 with the engine alone (profiles/r05/ab/b1_engine_select_uni.txt)
+    HG_U(range); HG_U(value); HG_U(k); HG_U(cn); HG_U(lb); HG_U(budget); HG_U(st); HG_U(fl);
+    HG_U(qx); HG_U(qy); HG_U(ql); HG_U(qd); HG_U(tx); HG_U(ty); HG_U(tl); HG_U(td); HG_U(tcbf);
+    HG_U(ctbx); HG_U(ctby); HG_U(tb_log2); HG_U(tb_cidx); HG_U(rc_i); HG_U(rc_scan); HG_U(rc_last_sub);
+    HG_U(rc_last_pos); HG_U(rc_prev_c1);
+#endif
 #undef HG_U
     L.cur = uni64(L.cur);
     L.rc_csbf = uni64(L.rc_csbf);
@@ -629,6 +656,7 @@ HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
         // through a VALU select and v_readfirstlane), then mask arithmetic.
         // (uni32: the lanes are identical, but where the compiler cannot
         // prove it, e.g. at engine start, the operands must be made scalar)
+#if defined(HG_SOLO_OLD_SELECT)  // A/B only: the r04 form (the bin from SCC, then mask arithmetic)
         uint32_t lp;
         asm("s_cmp_ge_u32 %1, %2\n\ts_cselect_b32 %0, 1, 0" : "=s"(lp) : "s"(uni32(L.value)), "s"(uni32(sr)) : "scc");
         const uint32_t m = 0u - lp;
@@ -636,6 +664,22 @@ HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
         L.value -= sr & m;
         const uint32_t rn = (lps & m) | (rm & ~m);
         const int nb = __builtin_clz(rn) - 23;
+#else
+        // one compare, every choice an s_cselect on its SCC: the bin, the new
+        // range, what leaves the offset and the shift that picks the next state
+        uint32_t lp, rn, d, sh;
+        asm("s_cmp_ge_u32 %4, %5\n\t"
+            "s_cselect_b32 %0, 1, 0\n\t"
+            "s_cselect_b32 %1, %6, %7\n\t"
+            "s_cselect_b32 %2, %5, 0\n\t"
+            "s_cselect_b32 %3, 0, 8"
+            : "=&s"(lp), "=&s"(rn), "=&s"(d), "=&s"(sh)
+            : "s"(uni32(L.value)), "s"(uni32(sr)), "s"(uni32(lps)), "s"(uni32(rm))
+            : "scc");
+        s = ((hi >> sh) & 0xffu) ^ mps;
+        L.value -= d;
+        const int nb = __builtin_clz(rn) - 23;
+#endif
         L.range = rn << nb;
         L.k -= nb;
         if (L.k < 8) vfill(L, G);
@@ -694,6 +738,15 @@ HG_HD inline int dec(Lane &L, const EG &G, int ci) {
     const int bin = dec_s(L, G, s);
     G.ctx[ci] = (uint8_t)s;
     return bin;
+}
+
+// A/B switch (HG_SB_GENERIC): the 9-slot sig_coeff_flag loop for every TB size
+HG_HD constexpr bool sb_generic_loop() {
+#if defined(HG_SB_GENERIC)
+    return true;
+#else
+    return false;
+#endif
 }
 
 // byte `slot` (0..11) of a 3-word register cache of context states
@@ -1635,7 +1688,7 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         // use sigCtx 0 at the TB's DC (slot 0) and off + 0..2 (slots 1..3)
         const int cbase = CTX_SIG + (cidx ? 27 : 0);
         auto cb = [&](int i) { return ctx_ld(L, G, cbase + i); };
-        uint64_t seq = G.seq[L.rc_scan * 5 + (l2 == 2 ? 4 : pcs)];  // slot per scan position
+        uint64_t seq = G.seqw(L.rc_scan * 5 + (l2 == 2 ? 4 : pcs));  // slot per scan position
         uint32_t c0, c1 = 0, c2 = 0;
         int off = 0;
         if (l2 == 2) {
@@ -1649,6 +1702,21 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         }
         HG_SB_T(L, 0, tsb);
         if constexpr (EG::kSolo) {
+          if (l2 > 2 && !sb_generic_loop()) {
+            // scalar engine, TBs above 4x4: the four slots in one 32-bit word
+            // (a byte shift reads or writes a slot), no slot 8 to select
+            auto dec_slot4 = [&](uint32_t slot) -> uint32_t {
+                const uint32_t sh = slot * 8u;
+                uint32_t cs = (c0 >> sh) & 0xffu;
+                const uint32_t bin = (uint32_t)dec_s(L, G, cs);
+                c0 = (c0 & ~(0xffu << sh)) | (cs << sh);
+                return bin;
+            };
+            uint32_t sg = sig;
+            for (int nn = nstart; nn > 0; --nn) sg |= dec_slot4((uint32_t)(seq >> (4 * nn)) & 3u) << nn;
+            if (nstart >= 0) sg |= (infer_dc && sg == 0) ? 1u : dec_slot4((uint32_t)seq & 3u);
+            sig = sg;
+          } else {
             // scalar engine: slots 0..7 as one 64-bit word (a shift reads or
             // writes a slot), slot 8 apart; every select branch-free, the bin
             // an integer, so an iteration is one scalar chain
@@ -1671,6 +1739,7 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             sig = sg;
             c0 = (uint32_t)cc;
             c1 = (uint32_t)(cc >> 32);
+          }
         } else {
             for (int nn = nstart; nn >= 0; --nn) {
                 if (nn > 0 || !infer_dc) {
@@ -1729,9 +1798,10 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
                 const uint32_t f = (uint32_t)dec_s(L, G, cs);
                 gc = (gc & ~(0xffu << gs)) | (cs << gs);
                 g1 |= f << nn;
-                last_g1 = (last_g1 < 0 && f) ? nn : last_g1;
                 c1 = (c1 > 0 && !f) ? c1 + 1 : 0;
             }
+            // the first greater1 flag set in decoding order: positions decode from the highest down
+            last_g1 = g1 ? msb32(g1) : -1;
         } else {
             for (uint32_t m = sig; m && num_g1 < 8;) {
                 const int nn = msb32(m);
@@ -2315,7 +2385,7 @@ void emu_parse_solo(const BatchArgs &a) {
                 const uint32_t start = L.st == U_CTU ? substream_start(L, P, a) : ~0u;
                 if (start != ~0u) sw.restart(a.rbsp, start, lim, 0);
                 else sw.advance(a.rbsp, L.lb, lim, 0);
-                const EG G{lds[(size_t)w].ctx, 0u, 0u, seq, a.rbsp, lim, sw.view()};
+                const EG G{lds[(size_t)w].ctx, 0u, 0u, seq, a.rbsp, lim, sw.view(), 0u, 0u};
                 run_unit(L.st, L, lds[(size_t)w], P, E, G);
             }
             if (!any) break;
@@ -2635,6 +2705,8 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
     if (threadIdx.x < 64) s_prog[threadIdx.x] = 0;
     const uint64_t trow = state_row(lane);
     const uint32_t tlo = (uint32_t)trow, thi = (uint32_t)(trow >> 32);
+    const uint64_t sq = lane < 15 ? sig_seq(lane) : 0;
+    const uint32_t sqlo = (uint32_t)sq, sqhi = (uint32_t)(sq >> 32);
     // spread: the slot from the job counter (a row's predecessor is the slot
     // before it, so it is already held by a running wave whatever order the
     // workgroups are dispatched in); solo: the workgroup's own picture
@@ -2729,7 +2801,7 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
 #if !defined(HG_SOLO_NO_UNI)
             uni_state(L);
 #endif
-            const EG G{ld.ctx, tlo, thi, s_seq, a.rbsp, lim, sw.view()};
+            const EG G{ld.ctx, tlo, thi, s_seq, a.rbsp, lim, sw.view(), sqlo, sqhi};
 #if defined(HG_PARSE_PROF)
             const int eix = (P.row_off + L.row) * 128 + L.c;
 #endif

@@ -96,23 +96,28 @@ def test_halfmoonbay_parse_modes(H, ctx, oracle_halfmoonbay, halfmoonbay, parse,
 
 
 @pytest.mark.parametrize("stream", ["0", "patience0", "default"])
-def test_halfmoonbay_streaming_modes(H, ctx, oracle_halfmoonbay, halfmoonbay, monkeypatch, stream):
+def test_halfmoonbay_streaming_modes(H, oracle_halfmoonbay, halfmoonbay, monkeypatch, stream):
     """Spread parse with k_intra_stream (the default for one image), without it
     (k_transform + k_intra after the parse), and with a first launch that gives
     every picture up at once (HEIFGPU_STREAM_PATIENCE_US=0: what a profiler that
     serialises dispatches does to it), so the second launch after the parse
-    reconstructs all of them.  Bit-exact with status 0 in every case."""
+    reconstructs all of them.  Bit-exact with status 0 in every case.  (The
+    knobs are read when a context is created: each case makes its own.)"""
     if stream == "0":
         monkeypatch.setenv("HEIFGPU_STREAM", "0")
     elif stream == "patience0":
         monkeypatch.setenv("HEIFGPU_STREAM_PATIENCE_US", "0")
-    img = H.HeifImage.parse(halfmoonbay)
-    b = ctx.prepare([img], parse="spread")
-    out = ctx.alloc_outputs([img])
-    for _ in range(2):  # the second decode reuses the set's progress / done words
-        b.decode_async(out)
-    assert b.status() == [0]
-    b.free()
+    c = H.DecodeContext(0)
+    try:
+        img = H.HeifImage.parse(halfmoonbay)
+        b = c.prepare([img], parse="spread")
+        out = c.alloc_outputs([img])
+        for _ in range(2):  # the second decode reuses the set's progress / done words
+            b.decode_async(out)
+        assert b.status() == [0]
+        b.free()
+    finally:
+        c.close()
     for got, want in zip(planes_np(out[0]), (oracle_halfmoonbay.y, oracle_halfmoonbay.cb, oracle_halfmoonbay.cr)):
         assert np.array_equal(got, want)
 
