@@ -279,13 +279,18 @@ struct EngSoloT {
     const uint8_t *rbsp;
     uint32_t lim;
     Win win;
-    uint32_t sqlo, sqhi;  // lane i < 15: sig_seq(i) (GPU: a v_readlane, no LDS round trip in the chain)
+    // lane i < 15: sig_seq(i).  Read from LDS (`seq`) by default: the
+    // v_readlane form (HG_SOLO_SEQ_VGPR) measured 26.7 against 25.7 ms for
+    // one image (r05 same-box A/B, profiles/r05/ab/b1_engine_variants.txt);
+    // the two builds differ mostly in where the register allocator put its
+    // SGPR spills (89 here against 138)
+    uint32_t sqlo, sqhi;
 #if defined(HG_HOST_EMU)
     uint64_t row(uint32_t st) const { return state_row((int)st); }
     uint64_t seqw(int idx) const { return seq[idx]; }
 #else
     __device__ __forceinline__ uint64_t seqw(int idx) const {
-#if defined(HG_SOLO_SEQ_LDS)  // A/B only: the LDS table, as before r05
+#if !defined(HG_SOLO_SEQ_VGPR)
         return seq[idx];
 #endif
         const int i = __builtin_amdgcn_readfirstlane(idx);
