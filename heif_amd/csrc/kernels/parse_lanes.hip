@@ -1633,8 +1633,19 @@ HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     L.st = U_SB;
 }
 
-// bit n of a 16-bit mask to bit 4n (a nibble per scan position)
+// bit n of a 16-bit mask to bit 4n (a nibble per scan position).  Scalar
+// engine: two s_bitreplicate_b64_b32 (each bit doubled) and a mask, three
+// SALU ops instead of the twelve of the shift-and-mask ladder
+template <bool Scalar = false>
 HG_HD inline uint64_t spread16_nib(uint32_t m) {
+#if !defined(HG_HOST_EMU) && defined(__HIP_DEVICE_COMPILE__) && !defined(HG_NO_BITREPLICATE)
+    if constexpr (Scalar) {
+        uint64_t x2, x4;
+        asm("s_bitreplicate_b64_b32 %0, %1" : "=s"(x2) : "s"(uni32(m & 0xffffu)));
+        asm("s_bitreplicate_b64_b32 %0, %1" : "=s"(x4) : "s"((uint32_t)x2));
+        return x4 & 0x1111111111111111ull;
+    }
+#endif
     uint64_t x = m & 0xffffu;
     x = (x | (x << 24)) & 0x000000ff000000ffull;
     x = (x | (x << 12)) & 0x000f000f000f000full;
@@ -1791,10 +1802,11 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         const int first_sig = 31 - __builtin_clz(sig & (0u - sig));
         const int last_sig = msb32(sig);
         int num_g1 = 0, last_g1 = -1;
+        uint32_t beyond8 = sig;  // after the greater1 loop: the significant positions past the first eight
         if constexpr (EG::kSolo) {
             // scalar engine: the first 8 significant positions, every update a
             // select on integers (no boolean carried across the engine's refill branch)
-            uint32_t m = sig;
+            uint32_t &m = beyond8;
             for (int j = 0; j < 8 && m; ++j) {
                 const int nn = msb32(m);
                 m ^= 1u << nn;
@@ -1808,7 +1820,7 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             // the first greater1 flag set in decoding order: positions decode from the highest down
             last_g1 = g1 ? msb32(g1) : -1;
         } else {
-            for (uint32_t m = sig; m && num_g1 < 8;) {
+            for (uint32_t &m = beyond8; m && num_g1 < 8;) {
                 const int nn = msb32(m);
                 m &= ~(1u << nn);
                 const int gs = (c1 < 3 ? c1 : 3) * 8;
@@ -1816,12 +1828,10 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
                 const int f = dec_s(L, G, cs);
                 gc = (gc & ~(0xffu << gs)) | (cs << gs);
                 ++num_g1;
-                if (f) {
-                    g1 |= 1u << nn;
-                    if (last_g1 < 0) last_g1 = nn;
-                }
+                g1 |= (uint32_t)f << nn;
                 if (c1 > 0) c1 = f ? 0 : c1 + 1;
             }
+            last_g1 = g1 ? msb32(g1) : -1;  // the first set in decoding order (positions decode downwards)
         }
         L.rc_prev_c1 = c1;
         for (int k = 0; k < 4; ++k) ctx_st(L, G, gbase + k, (gc >> (8 * k)) & 0xffu);
@@ -1840,13 +1850,23 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         // coeff_abs_level_remaining where one is coded, so only those levels
         // are visited, one at a time (their Rice parameters chain); the r03
         // layout stored every coefficient with its own 4-byte store.
+#if defined(HG_R05_BASE)
         uint64_t nib = spread16_nib(g1) + spread16_nib(g2);
+#else
+        uint64_t nib = spread16_nib<EG::kSolo>(g1) + (g2 ? 1ull << (4 * last_g1) : 0ull);  // (g2: at most the one bit)
+#endif
         {
-            uint32_t m8 = sig;  // the first eight significant positions (scan order = highest first)
+            // the levels with a coded remainder: greater1 set but not the one with a
+            // greater2 flag, greater2 set, and every position past the first eight
+            const uint32_t lastb = last_g1 >= 0 ? 1u << last_g1 : 0u;
+#if defined(HG_R05_BASE)  // A/B only: the first-eight mask recomputed (as before)
+            uint32_t m8 = sig;
             for (int j = 0; j < 8 && m8; ++j) m8 &= ~(1u << msb32(m8));
             m8 = sig & ~m8;
-            const uint32_t lastb = last_g1 >= 0 ? 1u << last_g1 : 0u;
             uint32_t need = (g1 & ~lastb) | g2 | (sig & ~m8);
+#else
+            uint32_t need = (g1 & ~lastb) | g2 | beyond8;
+#endif
             int last_abs = 0, last_rice = 0;
             bool first_rem = true;
             while (need) {

@@ -1,14 +1,14 @@
 #!/bin/bash
 # SQ counters of k_parse_lanes (one rocprofv3 --pmc pass per counter set,
 # each within the 8-SQ-counter limit), reduced to per-launch and per-bin
-# figures in gpurun_out/pmc_parse/parse_counters_<mode>.json.
+# figures in gpurun_out/pmc_parse_<mode>/parse_counters_<mode>.json.
 # usage: [PARSE=lanes|solo] tools/pmc_parse.sh [library-suffix]   (on the GPU box, repo root)
 V=$1
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 LIB=$R/heif_amd/libheifgpu${V:+_$V}.so
-OUT=$R/gpurun_out/pmc_parse${V:+_$V}
 BATCH=${PMC_BATCH:-128}
 MODE=${PARSE:-lanes}
+OUT=$R/gpurun_out/pmc_parse_${MODE}${V:+_$V}
 cd /tmp && export TMPDIR=/tmp
 mkdir -p "$OUT"
 i=0
