@@ -854,6 +854,17 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         HIP_TRY(launch_status_fold(ps.status.p, G.sticky.p, b->n_pics, s));
         return HEIFGPU_OK;
     }
+#if defined(HG_ABLATE)
+    // measurement builds only (make variant VDEFS=-DHG_ABLATE): HEIFGPU_ABLATE bit i
+    // drops reconstruction stage i (1 transform, 2 intra, 4 deblock, 8 sao): wrong
+    // pixels, the co-run cost of each stage on the parse
+    static const int ablate = [] {
+        const char *e = std::getenv("HEIFGPU_ABLATE");
+        return e ? std::atoi(e) : 0;
+    }();
+#else
+    constexpr int ablate = 0;
+#endif
     hipStream_t p = ctx->parse, r = ctx->recon;
     if (b->n_pics == 0) {  // a tile subset without pictures: nothing to decode
         return HEIFGPU_OK;
@@ -905,14 +916,14 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         hipStream_t x = b->n_sets >= 3 ? ctx->xform : r;
         HIP_TRY(hipStreamWaitEvent(x, ps.parsed, 0));
         if (t) HIP_TRY(hipEventRecord(ev[3], x));
-        HIP_TRY(launch_transform(a, x));
+        if (!(ablate & 1)) HIP_TRY(launch_transform(a, x));
         if (t) HIP_TRY(hipEventRecord(ev[4], x));
         HIP_TRY(hipEventRecord(ps.transformed, x));
         // recon stream: this set's transform, and the caller's prior work before the planes are written
         HIP_TRY(hipStreamWaitEvent(r, ps.transformed, 0));
     }
     if (t) HIP_TRY(hipEventRecord(ev[5], r));
-    HIP_TRY(launch_intra(a, r));
+    if (!(ablate & 2)) HIP_TRY(launch_intra(a, r));
     if (a.intra_stream) {
         // the second launch, after the parse: the pictures the first one gave up
         // on (none, unless the parse did not run beside it); the rest exit at once
@@ -922,10 +933,10 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
         HIP_TRY(launch_intra(a2, r));
     }
     if (t) HIP_TRY(hipEventRecord(ev[6], r));
-    HIP_TRY(launch_deblock(a, r));
+    if (!(ablate & 4)) HIP_TRY(launch_deblock(a, r));
     if (t) HIP_TRY(hipEventRecord(ev[7], r));
     HIP_TRY(hipStreamWaitEvent(r, ctx->fork, 0));
-    HIP_TRY(launch_sao_out(a, r));
+    if (!(ablate & 8)) HIP_TRY(launch_sao_out(a, r));
     if (t) HIP_TRY(hipEventRecord(ev[8], r));
     HIP_TRY(launch_status_fold(ps.status.p, G.sticky.p, b->n_pics, r));
     HIP_TRY(hipEventRecord(ps.recon_done, r));

@@ -82,6 +82,20 @@ HG_HD inline uint64_t state_row(int st) {
     return r | (lps_next << 32) | (mps_next << 40);
 }
 
+// Vector engines (lanes, rows): one row per context byte s = pStateIdx << 1 |
+// valMps, valMps folded in: rangeTabLps[4], the next context byte after an LPS
+// and after an MPS, then the bin an LPS and an MPS decode to (bits 48 / 56).
+// A decision indexes it by the byte itself and reads the new byte and the bin
+// from one shift (no valMps extraction, XOR or row-index masking; r05 A/B at
+// 128 images: 18,770 vs 18,590 Mpix/s)
+constexpr int kTabRows = 128;
+HG_HD inline uint64_t state_row_ctx(int s) {
+    const uint64_t r = state_row(s >> 1);
+    const uint64_t mps = (uint64_t)(s & 1);
+    return (r & 0xffffffffull) | ((((r >> 32) & 0xffu) ^ mps) << 32) | ((((r >> 40) & 0xffu) ^ mps) << 40) |
+           ((mps ^ 1u) << 48) | (mps << 56);
+}
+
 constexpr uint32_t kProgDone = 0x7fffffffu;
 // Parse waves at the highest issue priority (s_setprio 3; 0 turns it off).
 // Same-box pairs, r04: 128 images 83.5-83.8 vs 84.4 ms per step, one image
@@ -223,13 +237,20 @@ struct EngLanesT {
     static constexpr bool kSolo = false;
     static constexpr bool kSpread = Spread;
     static constexpr bool kCtxReg = false;  // contexts in LDS (ctx)
+    static constexpr bool kRowCtx = true;
     uint8_t *ctx;
-    const uint64_t *tab;  // per pStateIdx: rangeTabLps[4] | transIdxLps << 32 | transIdxMps << 40 (LDS)
+    const uint64_t *tab;  // engine_row of every context byte (LDS)
     const uint64_t *seq;  // sig_seq(scan, pattern): slot of every scan position of a sub-block (LDS)
     const uint8_t *rbsp;  // BatchArgs::rbsp (emulation prevention removed by k_rbsp)
     uint32_t lim;         // no loads at or past this offset (the picture's RBSP end + 64)
+    // the 8x8 up-right diagonal scan of 32x32 TBs' sub-blocks and its inverse in
+    // LDS (null: the constant tables).  A lane-varying index into constant memory
+    // is a vector load, and its wait would drain the wave's record stores too
+    const uint8_t *sp8 = nullptr, *inv8 = nullptr;
     HG_HD uint64_t row(uint32_t st) const { return tab[st]; }
     HG_HD uint64_t seqw(int idx) const { return seq[idx]; }
+    HG_HD int scan8(int scan, int i) const { return sp8 && scan == 0 ? sp8[i] : kScanPos[3][scan][i]; }
+    HG_HD int scan8_inv(int scan, int r) const { return inv8 && scan == 0 ? inv8[r] : kScanInv[3][scan][r]; }
 };
 using Eng = EngLanesT<false>;
 using EngRows = EngLanesT<true>;
@@ -265,6 +286,7 @@ struct Win {
 template <bool Spread>
 struct EngSoloT {
     static constexpr bool kSolo = true;
+    static constexpr bool kRowCtx = false;  // rows per pStateIdx (tlo / thi)
     // one wave per workgroup: the rows of a picture on different CUs, their
     // WPP progress, context hand-off, SAO and depth lines in coherent global memory
     static constexpr bool kSpread = Spread;
@@ -285,6 +307,28 @@ struct EngSoloT {
     // the two builds differ mostly in where the register allocator put its
     // SGPR spills (89 here against 138)
     uint32_t sqlo, sqhi;
+    // lane i: kScanPos[3][0][i] | kScanInv[3][0][i] << 8 (a byte of constant memory
+    // is a vector load even at a uniform index: v_readlane instead)
+    uint32_t scan8v;
+#if defined(HG_HOST_EMU)
+    int scan8(int scan, int i) const { return kScanPos[3][scan][i]; }
+    int scan8_inv(int scan, int r) const { return kScanInv[3][scan][r]; }
+#else
+    __device__ __forceinline__ int scan8(int scan, int i) const {
+#if defined(HG_NO_SCAN8)  // A/B only: the constant tables
+        return kScanPos[3][scan][i];
+#endif
+        if (scan != 0) return kScanPos[3][scan][i];
+        return __builtin_amdgcn_readlane((int)scan8v, __builtin_amdgcn_readfirstlane(i)) & 0xff;
+    }
+    __device__ __forceinline__ int scan8_inv(int scan, int r) const {
+#if defined(HG_NO_SCAN8)
+        return kScanInv[3][scan][r];
+#endif
+        if (scan != 0) return kScanInv[3][scan][r];
+        return (__builtin_amdgcn_readlane((int)scan8v, __builtin_amdgcn_readfirstlane(r)) >> 8) & 0xff;
+    }
+#endif
 #if defined(HG_HOST_EMU)
     uint64_t row(uint32_t st) const { return state_row((int)st); }
     uint64_t seqw(int idx) const { return seq[idx]; }
@@ -543,6 +587,8 @@ HG_HD inline uint32_t bswap32(uint32_t w) {
 template <class EG>
 HG_HD inline uint32_t q_pop(Lane &L, const EG &G) {
     if constexpr (EG::kSolo) return G.win.get(L.lb++);
+    // (A/B r05: two bit tests and three selects instead of the compare chain,
+    // which compiles to nested exec-mask branches: 17,520 vs 18,590 Mpix/s)
     const uint32_t w = L.ai == 0 ? L.a0 : (L.ai == 1 ? L.a1 : (L.ai == 2 ? L.a2 : L.a3));
     if (++L.ai == 4) {
         L.ai = 0;
@@ -648,6 +694,22 @@ HG_HD inline void engine_init(Lane &L, const EG &G, uint32_t start, uint32_t end
 // is a shift by clz and lowers k.
 template <class EG>
 HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
+    if constexpr (EG::kRowCtx) {
+        const uint64_t row = G.row(s);
+        const uint32_t lps = ((uint32_t)row >> ((L.range >> 3) & 24u)) & 0xffu;
+        const uint32_t rm = L.range - lps;
+        const uint32_t sr = rm << L.k;
+        const bool isl = L.value >= sr;
+        L.value -= isl ? sr : 0u;
+        const uint32_t rn = isl ? lps : rm;
+        const int nb = __builtin_clz(rn) - 23;
+        L.range = rn << nb;
+        L.k -= nb;
+        const uint32_t t = (uint32_t)(row >> (isl ? 32 : 40));
+        s = t & 0xffu;
+        if (L.k < 8) vfill(L, G);
+        return (int)((t >> 16) & 1u);
+    }
     const uint32_t st = s >> 1, mps = s & 1u;
     const uint64_t row = G.row(st);
     const uint32_t hi = (uint32_t)(row >> 32);  // next byte after an LPS | after an MPS << 8
@@ -945,15 +1007,17 @@ HG_HD inline int derive_luma_mode(const Lane &L, const LaneLds &ld, int xPb, int
 // selected, not indexed, so they stay immediates; the 8x8 sub-block scan of
 // 32x32 TBs comes from the table.  scan_pos returns x | (y << 4).
 HG_HD inline uint64_t scan4_word(int scan) { return scan == 0 ? kScan4Pos[0] : (scan == 1 ? kScan4Pos[1] : kScan4Pos[2]); }
-HG_HD inline int scan_pos(int l, int scan, int i) {
-    if (l == 3) return kScanPos[3][scan][i];
+template <class EG>
+HG_HD inline int scan_pos(const EG &G, int l, int scan, int i) {
+    if (l == 3) return G.scan8(scan, i);
     if (l == 0) return 0;
     const uint64_t t = l == 2 ? scan4_word(scan) : (scan == 0 ? kScan2Pos[0] : (scan == 1 ? kScan2Pos[1] : kScan2Pos[2]));
     const uint32_t e = (uint32_t)(t >> (4 * i)) & 15u;
     return (int)((e & 3) | ((e >> 2) << 4));
 }
-HG_HD inline int scan_inv(int l, int scan, int raster) {
-    if (l == 3) return kScanInv[3][scan][raster];
+template <class EG>
+HG_HD inline int scan_inv(const EG &G, int l, int scan, int raster) {
+    if (l == 3) return G.scan8_inv(scan, raster);
     if (l == 0) return 0;
     const uint64_t t = l == 2 ? (scan == 0 ? kScan4Inv[0] : (scan == 1 ? kScan4Inv[1] : kScan4Inv[2]))
                               : (scan == 0 ? kScan2Inv[0] : (scan == 1 ? kScan2Inv[1] : kScan2Inv[2]));
@@ -991,6 +1055,12 @@ HG_HD inline uint64_t sig_seq(int idx) {
         q |= ((slots >> (4 * e)) & 15u) << (4 * n);
     }
     return q;
+}
+
+// the 8x8 diagonal scan of 32x32 TBs (kScanPos[3][0]) and its inverse into LDS, one entry per lane
+HG_HD inline void scan8_tables(uint8_t *t, int lane) {
+    t[lane] = kScanPos[3][0][lane];
+    t[64 + lane] = kScanInv[3][0][lane];
 }
 
 struct Env {
@@ -1624,8 +1694,8 @@ HG_HD inline void unit_tb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
     }
     const int sbl = l2 - 2, sbw = 1 << sbl;
     L.rc_scan = scan;
-    L.rc_last_sub = scan_inv(sbl, scan, (ly >> 2) * sbw + (lx >> 2));
-    L.rc_last_pos = scan_inv(2, scan, (ly & 3) * 4 + (lx & 3));
+    L.rc_last_sub = scan_inv(G, sbl, scan, (ly >> 2) * sbw + (lx >> 2));
+    L.rc_last_pos = scan_inv(G, 2, scan, (ly & 3) * 4 + (lx & 3));
     L.rc_csbf = 0;
     L.rc_prev_c1 = 1;
     L.fl &= ~F_ANY_SB;
@@ -1681,7 +1751,7 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
 #endif
     const int l2 = L.tb_log2, cidx = L.tb_cidx, i = L.rc_i;
     const int sbl = l2 - 2, sbw = 1 << sbl;
-    const int sp = scan_pos(sbl, L.rc_scan, i);
+    const int sp = scan_pos(G, sbl, L.rc_scan, i);
     const int xS = sp & 15, yS = sp >> 4;
     int pcs = 0;  // prevCsbf
     if (xS < sbw - 1) pcs |= (int)((L.rc_csbf >> (yS * 8 + xS + 1)) & 1);
@@ -1757,19 +1827,21 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             c1 = (uint32_t)(cc >> 32);
           }
         } else {
-            for (int nn = nstart; nn >= 0; --nn) {
-                if (nn > 0 || !infer_dc) {
-                    const int slot = (int)((seq >> (4 * nn)) & 15u);
-                    uint32_t cs = cache_get(c0, c1, c2, slot);
-                    const int bin = dec_s(L, G, cs);
-                    cache_put(c0, c1, c2, slot, cs);
-                    if (bin) {
-                        sig |= 1u << nn;
-                        infer_dc = false;
-                    }
-                } else {
-                    sig |= 1u;  // inferred DC of a coded sub-block
-                }
+            // positions nstart .. 1 without a per-position branch (the bin is or-ed
+            // in), position 0 apart: inferred in a coded sub-block with no other
+            // significant coefficient (r05 A/B against the r04 loop, which tested
+            // for the inferred DC at every position: parse alone 63.1 -> 59.9 ms,
+            // 18,770 -> 19,260 Mpix/s at 128 images)
+            auto dec_slot = [&](int slot) -> uint32_t {
+                uint32_t cs = cache_get(c0, c1, c2, slot);
+                const uint32_t bin = (uint32_t)dec_s(L, G, cs);
+                cache_put(c0, c1, c2, slot, cs);
+                return bin;
+            };
+            for (int nn = nstart; nn > 0; --nn) sig |= dec_slot((int)((seq >> (4 * nn)) & 15u)) << nn;
+            if (nstart >= 0) {
+                if (infer_dc && sig == 0) sig |= 1u;
+                else sig |= dec_slot((int)(seq & 15u));
             }
         }
         auto cw = [&](int i, uint32_t v) { ctx_st(L, G, cbase + i, v & 0xffu); };
@@ -2303,8 +2375,10 @@ void emu_parse_lanes(const BatchArgs &a) {
     const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : lanes_pics_per_wave(a.lane_rows, a.n_pics);
     const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
     const int waves = (n_slots + ppw - 1) / ppw;
-    uint64_t tab[64], seq[15];
-    for (int i = 0; i < 64; ++i) tab[i] = state_row(i);
+    uint64_t tab[kTabRows], seq[15];
+    uint8_t scan8[128];
+    for (int i = 0; i < 64; ++i) scan8_tables(scan8, i);
+    for (int i = 0; i < kTabRows; ++i) tab[i] = state_row_ctx(i);
     for (int i = 0; i < 15; ++i) seq[i] = sig_seq(i);
     std::vector<LaneLds> lds(64);
     std::vector<LanePic> pics(64);
@@ -2331,7 +2405,7 @@ void emu_parse_lanes(const BatchArgs &a) {
             for (int l = 0; l < 64; ++l)
                 if (lanes[l].st != U_DONE) {
                     const LanePic &P = pics[l / a.lane_rows];
-                    const Eng G{lds[l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
+                    const Eng G{lds[l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u, scan8, scan8 + 64};
                     q_refill(lanes[l], G);
                 }
             // the kernel's pass: every unit kind in syntax order, each on the lanes in it
@@ -2343,7 +2417,7 @@ void emu_parse_lanes(const BatchArgs &a) {
                     if (L.st != kind || (kind == U_CTU && !ctu_ready(L, P, E))) continue;
                     progressed = true;
                     ++units;
-                    const Eng G{lds[l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
+                    const Eng G{lds[l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u, scan8, scan8 + 64};
                     run_unit(kind, L, lds[l], P, E, G);
                 }
             }
@@ -2410,7 +2484,7 @@ void emu_parse_solo(const BatchArgs &a) {
                 const uint32_t start = L.st == U_CTU ? substream_start(L, P, a) : ~0u;
                 if (start != ~0u) sw.restart(a.rbsp, start, lim, 0);
                 else sw.advance(a.rbsp, L.lb, lim, 0);
-                const EG G{lds[(size_t)w].ctx, 0u, 0u, seq, a.rbsp, lim, sw.view(), 0u, 0u};
+                const EG G{lds[(size_t)w].ctx, 0u, 0u, seq, a.rbsp, lim, sw.view(), 0u, 0u, 0u};
                 run_unit(L.st, L, lds[(size_t)w], P, E, G);
             }
             if (!any) break;
@@ -2430,8 +2504,10 @@ void emu_parse_solo(const BatchArgs &a) {
 // rows mode: a group's row waves round-robin, one pass per wave per round
 void emu_parse_rows(const BatchArgs &a) {
     const int groups = a.parse_group, R = a.max_rows;
-    uint64_t tab[64], seq[15];
-    for (int i = 0; i < 64; ++i) tab[i] = state_row(i);
+    uint64_t tab[kTabRows], seq[15];
+    uint8_t scan8[128];
+    for (int i = 0; i < 64; ++i) scan8_tables(scan8, i);
+    for (int i = 0; i < kTabRows; ++i) tab[i] = state_row_ctx(i);
     for (int i = 0; i < 15; ++i) seq[i] = sig_seq(i);
     std::vector<LaneLds> lds((size_t)R * 64);
     std::vector<LanePic> pics((size_t)R * 64);
@@ -2460,7 +2536,7 @@ void emu_parse_rows(const BatchArgs &a) {
                 for (int l = 0; l < 64; ++l) {
                     const size_t i = (size_t)r * 64 + (size_t)l;
                     if (lanes[i].st == U_DONE) continue;
-                    const EngRows G{lds[i].ctx, tab, seq, a.rbsp, (pics[i].bits_end + 64u) & ~3u};
+                    const EngRows G{lds[i].ctx, tab, seq, a.rbsp, (pics[i].bits_end + 64u) & ~3u, scan8, scan8 + 64};
                     q_refill(lanes[i], G);
                 }
                 for (int kind = U_CTU; kind <= U_CTU_END; ++kind)
@@ -2473,7 +2549,7 @@ void emu_parse_rows(const BatchArgs &a) {
                         if (kind == U_CTU && !ctu_ready<EngRows>(L, P, E)) continue;
                         progressed = true;
                         ++units;
-                        const EngRows G{lds[i].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u};
+                        const EngRows G{lds[i].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u, scan8, scan8 + 64};
                         run_unit(kind, L, lds[i], P, E, G);
                     }
                 passes += units != units0;  // (a pass without progress is a sleep on the GPU)
@@ -2505,9 +2581,11 @@ void emu_parse(const BatchArgs &a) {
 #else
 // LDS of one wave: LaneLds per used lane, LanePic per picture, progress words,
 // engine tables, and the WPP context staging when rows wrap
+// kTabRows + 16 engine-table words, then the 8x8 scan and its inverse (128 bytes)
+constexpr size_t kLaneTablesBytes = (kTabRows + 16) * sizeof(uint64_t) + 128;
 inline size_t lanes_lds_bytes(int ppw, int lane_rows, bool ring) {
     return lane_blocks_bytes(ppw * lane_rows) + sizeof(LanePic) * (size_t)ppw + 64 * sizeof(uint32_t) +
-           (64 + 16) * sizeof(uint64_t) + (ring ? 64 * (size_t)CTX_PAD : 0);
+           kLaneTablesBytes + (ring ? 64 * (size_t)CTX_PAD : 0);
 }
 
 #if defined(HG_PARSE_WPE)
@@ -2523,16 +2601,18 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     LanePic *s_pic = reinterpret_cast<LanePic *>(smem + lane_blocks_bytes(nl));
     uint32_t *s_prog = reinterpret_cast<uint32_t *>(s_pic + ppw);
     uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_prog + 64);
-    uint64_t *s_seq = s_tab + 64;
-    uint8_t *s_wctx = a.wpp_ring ? reinterpret_cast<uint8_t *>(s_seq + 16) : nullptr;
+    uint64_t *s_seq = s_tab + kTabRows;
+    uint8_t *s_scan = reinterpret_cast<uint8_t *>(s_seq + 16);
+    uint8_t *s_wctx = a.wpp_ring ? s_scan + 128 : nullptr;
     const int lane = threadIdx.x;
 #if HG_PARSE_SETPRIO > 0
     // the parse is the latency-critical stream: win issue arbitration against
     // the reconstruction kernels of the previous decode sharing the SIMD
     __builtin_amdgcn_s_setprio(HG_PARSE_SETPRIO);
 #endif
-    s_tab[lane] = state_row(lane);
+    for (int i = lane; i < kTabRows; i += 64) s_tab[i] = state_row_ctx(i);
     if (lane < 15) s_seq[lane] = sig_seq(lane);
+    scan8_tables(s_scan, lane);
     const int pl = lane / a.lane_rows, row = lane % a.lane_rows;
     const int slot = (int)blockIdx.x * ppw + pl;
     const int n_slots = a.parse_order ? a.n_slots : a.n_pics;
@@ -2546,7 +2626,11 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     if (!live) L.st = U_DONE;
     __syncthreads();
     const Env E{&a, s_lds, s_prog, s_wctx, lane};
+#if defined(HG_NO_SCAN8)
     const Eng G{ld.ctx, s_tab, s_seq, a.rbsp, live ? (P.bits_end + 64u) & ~3u : 0u};
+#else
+    const Eng G{ld.ctx, s_tab, s_seq, a.rbsp, live ? (P.bits_end + 64u) & ~3u : 0u, s_scan, s_scan + 64};
+#endif
 #if defined(HG_PARSE_PROF)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
@@ -2608,9 +2692,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
 // than taking blockIdx.x: a job's predecessor (g, r - 1) has a lower number,
 // so it is held by a wave that is already running, whatever order the
 // hardware dispatches the workgroups in.
-inline size_t rows_lds_bytes() {
-    return lane_blocks_bytes(64) + sizeof(LanePic) * 64 + (64 + 16) * sizeof(uint64_t);
-}
+inline size_t rows_lds_bytes() { return lane_blocks_bytes(64) + sizeof(LanePic) * 64 + kLaneTablesBytes; }
 
 // the job counter: lane 0 takes the next number, the wave shares it
 __device__ __forceinline__ uint32_t dequeue_job(uint32_t *ctr) {
@@ -2624,13 +2706,15 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_rows(BatchArgs a) {
     LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
     LanePic *s_pic = reinterpret_cast<LanePic *>(smem + lane_blocks_bytes(64));
     uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_pic + 64);
-    uint64_t *s_seq = s_tab + 64;
+    uint64_t *s_seq = s_tab + kTabRows;
+    uint8_t *s_scan = reinterpret_cast<uint8_t *>(s_seq + 16);
     const int lane = threadIdx.x;
 #if HG_PARSE_SETPRIO > 0
     __builtin_amdgcn_s_setprio(HG_PARSE_SETPRIO);
 #endif
-    s_tab[lane] = state_row(lane);
+    for (int i = lane; i < kTabRows; i += 64) s_tab[i] = state_row_ctx(i);
     if (lane < 15) s_seq[lane] = sig_seq(lane);
+    scan8_tables(s_scan, lane);
     const uint32_t groups = (uint32_t)a.parse_group;
     const uint32_t j = dequeue_job(a.xjob);
     const int row = (int)(j / groups), slot = (int)(j % groups) * a.rows_lanes + lane;
@@ -2643,7 +2727,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_rows(BatchArgs a) {
     else L.st = U_DONE;
     __syncthreads();
     const Env E{&a, s_lds, a.xprog + (live ? P.row_off : 0u), a.xctx + (live ? (size_t)P.row_off * CTX_PAD : 0), lane};
-    const EngRows G{ld.ctx, s_tab, s_seq, a.rbsp, live ? (P.bits_end + 64u) & ~3u : 0u};
+    const EngRows G{ld.ctx, s_tab, s_seq, a.rbsp, live ? (P.bits_end + 64u) & ~3u : 0u, s_scan, s_scan + 64};
 #if defined(HG_PARSE_PROF)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
@@ -2730,6 +2814,7 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
     if (threadIdx.x < 64) s_prog[threadIdx.x] = 0;
     const uint64_t trow = state_row(lane);
     const uint32_t tlo = (uint32_t)trow, thi = (uint32_t)(trow >> 32);
+    const uint32_t scan8v = (uint32_t)kScanPos[3][0][lane] | ((uint32_t)kScanInv[3][0][lane] << 8);
     const uint64_t sq = lane < 15 ? sig_seq(lane) : 0;
     const uint32_t sqlo = (uint32_t)sq, sqhi = (uint32_t)(sq >> 32);
     // spread: the slot from the job counter (a row's predecessor is the slot
@@ -2826,7 +2911,7 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
 #if !defined(HG_SOLO_NO_UNI)
             uni_state(L);
 #endif
-            const EG G{ld.ctx, tlo, thi, s_seq, a.rbsp, lim, sw.view(), sqlo, sqhi};
+            const EG G{ld.ctx, tlo, thi, s_seq, a.rbsp, lim, sw.view(), sqlo, sqhi, scan8v};
 #if defined(HG_PARSE_PROF)
             const int eix = (P.row_off + L.row) * 128 + L.c;
 #endif
