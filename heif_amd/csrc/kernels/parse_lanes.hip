@@ -88,6 +88,8 @@ HG_HD inline uint64_t state_row(int st) {
 // A decision indexes it by the byte itself and reads the new byte and the bin
 // from one shift (no valMps extraction, XOR or row-index masking; r05 A/B at
 // 128 images: 18,770 vs 18,590 Mpix/s)
+// (A/B r05: the decoded bin in bit 7 of the context byte, 256 rows, one shift
+// less per decision: 19,020 vs 19,200 Mpix/s, rejected)
 constexpr int kTabRows = 128;
 HG_HD inline uint64_t state_row_ctx(int s) {
     const uint64_t r = state_row(s >> 1);
@@ -134,6 +136,13 @@ struct LanePic {
     TuRec HG_GAS *tu_base;
     Coef HG_GAS *coef_base;
 };
+
+// sub-block slots per pass of the lanes parse (A/B: HG_SB_SLOTS)
+#if defined(HG_SB_SLOTS)
+constexpr int kSbSlots = HG_SB_SLOTS;
+#else
+constexpr int kSbSlots = 1;
+#endif
 
 // syntax units (Lane.st)
 enum Unit : int {
@@ -587,9 +596,25 @@ HG_HD inline uint32_t bswap32(uint32_t w) {
 template <class EG>
 HG_HD inline uint32_t q_pop(Lane &L, const EG &G) {
     if constexpr (EG::kSolo) return G.win.get(L.lb++);
-    // (A/B r05: two bit tests and three selects instead of the compare chain,
-    // which compiles to nested exec-mask branches: 17,520 vs 18,590 Mpix/s)
+#if !defined(HG_HOST_EMU) && defined(__HIP_DEVICE_COMPILE__)
+    // the dword at index ai as three v_cndmask.  Written in C++ the selection
+    // compiles to nested exec-mask branches (a dozen SALU instructions at every
+    // refill site), and as bit tests into a dynamically indexed scratch array;
+    // r05 A/B at 128 images: 19,490 against 19,200 (branches) and 17,520
+    // (scratch) Mpix/s; 17 % fewer static instructions in k_parse_lanes
+    uint32_t w;
+    asm("v_cmp_eq_u32 vcc, 1, %1\n\t"
+        "v_cndmask_b32 %0, %2, %3, vcc\n\t"
+        "v_cmp_eq_u32 vcc, 2, %1\n\t"
+        "v_cndmask_b32 %0, %0, %4, vcc\n\t"
+        "v_cmp_eq_u32 vcc, 3, %1\n\t"
+        "v_cndmask_b32 %0, %0, %5, vcc"
+        : "=&v"(w)
+        : "v"(L.ai), "v"(L.a0), "v"(L.a1), "v"(L.a2), "v"(L.a3)
+        : "vcc");
+#else
     const uint32_t w = L.ai == 0 ? L.a0 : (L.ai == 1 ? L.a1 : (L.ai == 2 ? L.a2 : L.a3));
+#endif
     if (++L.ai == 4) {
         L.ai = 0;
         if (L.bv) {
@@ -2397,7 +2422,13 @@ void emu_parse_lanes(const BatchArgs &a) {
             if (!live) lanes[l].st = U_DONE;
         }
         Env E{&a, lds.data(), prog, a.wpp_ring ? wctx.data() : nullptr, 0};
-        long passes = 0, units = 0;
+        long passes = 0, units = 0, kruns = 0, kr[8] = {}, ku[8] = {};
+#if defined(HG_DEFER_MIN)
+        uint32_t deferred[64] = {};
+#endif
+#if defined(HG_SBDEFER_MIN)
+        uint32_t sbwait[64] = {};
+#endif
         for (;; ++passes) {
             bool any = false, progressed = false;
             for (int l = 0; l < 64; ++l) any |= lanes[l].st != U_DONE;
@@ -2409,12 +2440,53 @@ void emu_parse_lanes(const BatchArgs &a) {
                     q_refill(lanes[l], G);
                 }
             // the kernel's pass: every unit kind in syntax order, each on the lanes in it
-            for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
+#if defined(HG_DEFER_MIN)
+            bool sb_any = false;
+            for (int l = 0; l < 64; ++l) sb_any |= lanes[l].st == U_SB;
+#endif
+            for (int kk = U_CTU; kk <= U_CTU_END + kSbSlots - 1; ++kk) {
+                const int kind = kk <= U_SB ? kk : (kk < U_SB + kSbSlots ? (int)U_SB : kk - kSbSlots + 1);
+                bool mine[64], anym = false;
+                int cnt = 0;
+                for (int l = 0; l < 64; ++l) {
+                    E.lane = l;
+                    mine[l] = lanes[l].st == kind && (kind != U_CTU || ctu_ready(lanes[l], pics[l / a.lane_rows], E));
+                    anym |= mine[l];
+                    cnt += mine[l] ? 1 : 0;
+                }
+                if (!anym) continue;
+#if defined(HG_DEFER_MIN)
+                if (kind >= HG_DEFER_LO && kind <= U_TB && sb_any) {
+                    bool urgent = false;
+                    for (int l = 0; l < 64; ++l) urgent |= mine[l] && deferred[l] >= HG_DEFER_MAX;
+                    if (cnt < HG_DEFER_MIN && !urgent) {
+                        for (int l = 0; l < 64; ++l) deferred[l] += mine[l] ? 1 : 0;
+                        continue;
+                    }
+                    for (int l = 0; l < 64; ++l)
+                        if (mine[l]) deferred[l] = 0;
+                }
+#endif
+#if defined(HG_SBDEFER_MIN)
+                if (kind == U_SB && progressed) {
+                    bool urgent = false;
+                    for (int l = 0; l < 64; ++l) urgent |= mine[l] && sbwait[l] >= HG_SBDEFER_MAX;
+                    if (cnt < HG_SBDEFER_MIN && !urgent) {
+                        for (int l = 0; l < 64; ++l) sbwait[l] += mine[l] ? 1 : 0;
+                        continue;
+                    }
+                    for (int l = 0; l < 64; ++l)
+                        if (mine[l]) sbwait[l] = 0;
+                }
+#endif
+                ++kruns;
+                ++kr[kind];
+                ku[kind] += cnt;
                 for (int l = 0; l < 64; ++l) {
                     Lane &L = lanes[l];
                     E.lane = l;
                     LanePic &P = pics[l / a.lane_rows];
-                    if (L.st != kind || (kind == U_CTU && !ctu_ready(L, P, E))) continue;
+                    if (!mine[l]) continue;
                     progressed = true;
                     ++units;
                     const Eng G{lds[l].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u, scan8, scan8 + 64};
@@ -2432,7 +2504,10 @@ void emu_parse_lanes(const BatchArgs &a) {
             }
         }
         if (stats)
-            printf("wave %d: %ld passes, %.1f units per pass\n", w, passes, (double)units / passes);
+            printf("wave %d: %ld passes, %.1f units per pass, %ld kind runs, %.2f units per kind run\n", w, passes,
+                   (double)units / passes, kruns, (double)units / kruns);
+        if (stats)
+            for (int k = U_CTU; k <= U_CTU_END; ++k) printf("  kind %d: %ld runs, %ld units\n", k, kr[k], ku[k]);
     }
 }
 
@@ -2635,6 +2710,9 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
+#if defined(HG_DEFER_MIN)
+    uint32_t deferred = 0;  // passes this lane's tree / TB unit has been held back
+#endif
     for (uint32_t pass = 0;; ++pass) {
         if (!__any(L.st != U_DONE)) break;
         pass_wait();
@@ -2642,10 +2720,25 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
         // one pass: every unit kind in syntax order, each run by the lanes in it
         // (a uniform loop: the units are never linearised into one divergent region)
         bool progressed = false;
+#if defined(HG_DEFER_MIN)
+        const bool sb_any = __any(L.st == U_SB);
+#endif
 #pragma unroll
-        for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
+        for (int kk = U_CTU; kk <= U_CTU_END + kSbSlots - 1; ++kk) {
+            const int kind = kk <= U_SB ? kk : (kk < U_SB + kSbSlots ? (int)U_SB : kk - kSbSlots + 1);
             const bool mine = L.st == kind && (kind != U_CTU || ctu_ready(L, P, E));
             if (!__any(mine)) continue;
+#if defined(HG_DEFER_MIN)
+            // A/B: a tree / TB unit wanted by fewer than HG_DEFER_MIN lanes waits (at
+            // most HG_DEFER_MAX passes) while sub-blocks run, so that more lanes share it
+            if (kind >= HG_DEFER_LO && kind <= U_TB && sb_any) {
+                if (__popcll(__ballot(mine)) < HG_DEFER_MIN && !__any(mine && deferred >= HG_DEFER_MAX)) {
+                    if (mine) ++deferred;
+                    continue;
+                }
+                if (mine) deferred = 0;
+            }
+#endif
             progressed = true;
 #if defined(HG_PARSE_PROF)
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
