@@ -137,13 +137,6 @@ struct LanePic {
     Coef HG_GAS *coef_base;
 };
 
-// sub-block slots per pass of the lanes parse (A/B: HG_SB_SLOTS)
-#if defined(HG_SB_SLOTS)
-constexpr int kSbSlots = HG_SB_SLOTS;
-#else
-constexpr int kSbSlots = 1;
-#endif
-
 // syntax units (Lane.st)
 enum Unit : int {
     U_DONE = 0,
@@ -2423,12 +2416,6 @@ void emu_parse_lanes(const BatchArgs &a) {
         }
         Env E{&a, lds.data(), prog, a.wpp_ring ? wctx.data() : nullptr, 0};
         long passes = 0, units = 0, kruns = 0, kr[8] = {}, ku[8] = {};
-#if defined(HG_DEFER_MIN)
-        uint32_t deferred[64] = {};
-#endif
-#if defined(HG_SBDEFER_MIN)
-        uint32_t sbwait[64] = {};
-#endif
         for (;; ++passes) {
             bool any = false, progressed = false;
             for (int l = 0; l < 64; ++l) any |= lanes[l].st != U_DONE;
@@ -2440,12 +2427,7 @@ void emu_parse_lanes(const BatchArgs &a) {
                     q_refill(lanes[l], G);
                 }
             // the kernel's pass: every unit kind in syntax order, each on the lanes in it
-#if defined(HG_DEFER_MIN)
-            bool sb_any = false;
-            for (int l = 0; l < 64; ++l) sb_any |= lanes[l].st == U_SB;
-#endif
-            for (int kk = U_CTU; kk <= U_CTU_END + kSbSlots - 1; ++kk) {
-                const int kind = kk <= U_SB ? kk : (kk < U_SB + kSbSlots ? (int)U_SB : kk - kSbSlots + 1);
+            for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
                 bool mine[64], anym = false;
                 int cnt = 0;
                 for (int l = 0; l < 64; ++l) {
@@ -2455,30 +2437,6 @@ void emu_parse_lanes(const BatchArgs &a) {
                     cnt += mine[l] ? 1 : 0;
                 }
                 if (!anym) continue;
-#if defined(HG_DEFER_MIN)
-                if (kind >= HG_DEFER_LO && kind <= U_TB && sb_any) {
-                    bool urgent = false;
-                    for (int l = 0; l < 64; ++l) urgent |= mine[l] && deferred[l] >= HG_DEFER_MAX;
-                    if (cnt < HG_DEFER_MIN && !urgent) {
-                        for (int l = 0; l < 64; ++l) deferred[l] += mine[l] ? 1 : 0;
-                        continue;
-                    }
-                    for (int l = 0; l < 64; ++l)
-                        if (mine[l]) deferred[l] = 0;
-                }
-#endif
-#if defined(HG_SBDEFER_MIN)
-                if (kind == U_SB && progressed) {
-                    bool urgent = false;
-                    for (int l = 0; l < 64; ++l) urgent |= mine[l] && sbwait[l] >= HG_SBDEFER_MAX;
-                    if (cnt < HG_SBDEFER_MIN && !urgent) {
-                        for (int l = 0; l < 64; ++l) sbwait[l] += mine[l] ? 1 : 0;
-                        continue;
-                    }
-                    for (int l = 0; l < 64; ++l)
-                        if (mine[l]) sbwait[l] = 0;
-                }
-#endif
                 ++kruns;
                 ++kr[kind];
                 ku[kind] += cnt;
@@ -2710,9 +2668,6 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
 #endif
-#if defined(HG_DEFER_MIN)
-    uint32_t deferred = 0;  // passes this lane's tree / TB unit has been held back
-#endif
     for (uint32_t pass = 0;; ++pass) {
         if (!__any(L.st != U_DONE)) break;
         pass_wait();
@@ -2720,25 +2675,10 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
         // one pass: every unit kind in syntax order, each run by the lanes in it
         // (a uniform loop: the units are never linearised into one divergent region)
         bool progressed = false;
-#if defined(HG_DEFER_MIN)
-        const bool sb_any = __any(L.st == U_SB);
-#endif
 #pragma unroll
-        for (int kk = U_CTU; kk <= U_CTU_END + kSbSlots - 1; ++kk) {
-            const int kind = kk <= U_SB ? kk : (kk < U_SB + kSbSlots ? (int)U_SB : kk - kSbSlots + 1);
+        for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
             const bool mine = L.st == kind && (kind != U_CTU || ctu_ready(L, P, E));
             if (!__any(mine)) continue;
-#if defined(HG_DEFER_MIN)
-            // A/B: a tree / TB unit wanted by fewer than HG_DEFER_MIN lanes waits (at
-            // most HG_DEFER_MAX passes) while sub-blocks run, so that more lanes share it
-            if (kind >= HG_DEFER_LO && kind <= U_TB && sb_any) {
-                if (__popcll(__ballot(mine)) < HG_DEFER_MIN && !__any(mine && deferred >= HG_DEFER_MAX)) {
-                    if (mine) ++deferred;
-                    continue;
-                }
-                if (mine) deferred = 0;
-            }
-#endif
             progressed = true;
 #if defined(HG_PARSE_PROF)
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
