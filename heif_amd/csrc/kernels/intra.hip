@@ -589,7 +589,11 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 // carries no per-format arithmetic)
 // LDS of k_intra's streaming mode beyond the windows: the transform tables
 // (workgroup) and per wave the transform tiles (transform_tb, xform.hpp)
-constexpr size_t kXfTablesBytes = 1088, kXfWaveBytes = 2 * 32 * 32 * sizeof(int16_t) + 16;
+// (s_tm 1024 B, s_dst 16 B, s_mt; per wave the d tile 32 x 34, the g tile 32 x 32, the extent pair)
+constexpr size_t kXfTablesBytes = 1040 + kMtElems * sizeof(int16_t);
+constexpr size_t kXfDBytes = 32 * kXfDStride32 * sizeof(int16_t), kXfGBytes = 32 * 32 * sizeof(int16_t);
+constexpr size_t kXfWaveBytes = kXfDBytes + kXfGBytes + 16;
+static_assert(kXfTablesBytes % 16 == 0 && kXfWaveBytes % 16 == 0, "transform scratch alignment");
 constexpr int kIntraPlanes = 0, kIntraStream = 1;
 constexpr uint32_t kGaveUp = ~0u;                 // a wave's progress word: it gave its rows up
 constexpr uint64_t kRedoPatience = 200000000ull;  // 2 s (10 ns ticks): the parse is over by then
@@ -635,10 +639,11 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
     if constexpr (XfInline) {
         unsigned char *tab = smem + 64 + (size_t)nw * lay.bytes;
         unsigned char *xw = tab + kXfTablesBytes + (size_t)wave * kXfWaveBytes;
-        X = XfScratch{reinterpret_cast<int16_t *>(xw), reinterpret_cast<int16_t *>(xw + 2048),
-                      reinterpret_cast<int32_t *>(xw + 4096), reinterpret_cast<int8_t *>(tab),
-                      reinterpret_cast<int8_t *>(tab + 1024)};
-        xf_tables(reinterpret_cast<int8_t *>(tab), reinterpret_cast<int8_t *>(tab + 1024), lane);
+        X = XfScratch{reinterpret_cast<int16_t *>(xw), reinterpret_cast<int16_t *>(xw + kXfDBytes),
+                      reinterpret_cast<int32_t *>(xw + kXfDBytes + kXfGBytes), reinterpret_cast<int8_t *>(tab),
+                      reinterpret_cast<int8_t *>(tab + 1024), reinterpret_cast<int16_t *>(tab + 1040)};
+        xf_tables(reinterpret_cast<int8_t *>(tab), reinterpret_cast<int8_t *>(tab + 1024),
+                  reinterpret_cast<int16_t *>(tab + 1040), lane);
     }
     IntraScratch *S = reinterpret_cast<IntraScratch *>(blk);
     Win<Pel> win[3];

@@ -36,13 +36,14 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     // the 32x32 DCT matrix in LDS (lane-varying rows: LDS, not constant loads).
     // (Computing g in place of d through registers halves the LDS but raised
     // VGPRs 34 -> 70 and measured 14.6 -> 18.6 ms.)
-    HG_BLOCK_SHARED int16_t tile[kWaves][2][32 * 32];
+    HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t dtile[kWaves][32 * kXfDStride32];
+    HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t gtile[kWaves][32 * 32];
     HG_BLOCK_SHARED int32_t extent[kWaves][2];  // last nonzero row / column of d
     HG_BLOCK_SHARED int8_t s_tm[32 * 32];
     HG_BLOCK_SHARED int8_t s_dst[16];
+    HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t s_mt[kMtElems];
     // every wave fills the tables (same values; the host emulation runs one lane per wave)
-    for (int i = (int)(threadIdx.x & 63); i < 32 * 32; i += kWave) s_tm[i] = c_tm.m[i >> 5][i & 31];
-    for (int i = (int)(threadIdx.x & 63); i < 16; i += kWave) s_dst[i] = c_dst[i >> 2][i & 3];
+    xf_tables(s_tm, s_dst, s_mt, (int)(threadIdx.x & 63));
     __syncthreads();
     const int pic = a.pic0 + blockIdx.y, row = blockIdx.x;
     const PicDesc pd = a.pics[pic];
@@ -63,8 +64,8 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     int16_t HG_GAS *res_plane[3] = {res0, res0 + (size_t)W * H, res0 + (size_t)W * H + (size_t)cw * ch};
     const int pitch[3] = {W, cw, cw};
     const bool scaling = (sp.flags & SP_SCALING_LIST) != 0;
-    int16_t *d = tile[wave][0];
-    int16_t *g = tile[wave][1];
+    int16_t *d = dtile[wave];
+    int16_t *g = gtile[wave];
 
     // Pass A: 4x4 TBs, four at a time, 16 lanes each (sub-tile q of d / g).
     // A 4x4 TB has 16 outputs; run one per wave it left 48 lanes idle and paid
@@ -177,7 +178,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         const int cidx = tu.flags & TU_CIDX_MASK;
         const int n = 1 << tu.log2;
         if (tu.log2 > 5 || cidx > 2 || tu.x + n > pitch[cidx] || tu.y + n > (cidx ? ch : H)) continue;
-        transform_tb(tu, coefs, sp, a.sf, XfScratch{d, g, extent[wave], s_tm, s_dst},
+        transform_tb(tu, coefs, sp, a.sf, XfScratch{d, g, extent[wave], s_tm, s_dst, s_mt},
                      res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x, pitch[cidx], lane);
     }
 }

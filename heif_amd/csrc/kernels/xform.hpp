@@ -121,18 +121,50 @@ __device__ __forceinline__ SbRec load_rec(const CoefSrc<Coherent> &src, uint32_t
 }
 
 
-// a wave's transform scratch: d and g tiles (int16, 32x32 each), the extent
-// pair, and the workgroup's matrix tables (filled by xf_tables)
+// 8x8 .. 32x32 TBs: both stages as dot products of packed int16 pairs
+// (v_dot2c_i32_i16: two multiply-adds per instruction, four per pair of
+// 8-byte LDS reads).  The first stage reads d column-wise, so d is scattered
+// transposed (dT[x][y], row stride n + 2: columns of a 32-wide tile in
+// distinct banks); the matrix is kept transposed per size, mtT_n[y][j] =
+// transMatrix[j * 32 / n][y], same stride, so both operands of every dot run
+// along j.  (r04's loops: one int8 matrix load, one int16 load and a
+// multiply-add per term, ~7 instructions per term.)
+constexpr int kXfDStride32 = 32 + 2;
+constexpr int kMtElems = 8 * 10 + 16 * 18 + 32 * 34;  // int16
+__device__ __forceinline__ int mt_off(int log2n) { return log2n == 3 ? 0 : (log2n == 4 ? 8 * 10 : 8 * 10 + 16 * 18); }
+
+// a wave's transform scratch: d (int16, 32 x 34: the transposed layout's
+// padding) and g (32x32) tiles, the extent pair, and the workgroup's matrix
+// tables (filled by xf_tables)
 struct XfScratch {
     int16_t *d, *g;
     int32_t *extent;
     const int8_t *tm, *dst;
+    const int16_t *mt;  // kMtElems: mtT_n of n = 8, 16, 32
 };
 
-// s_tm[32 * 32] and s_dst[16] from the constant tables, by the lanes of one wave
-__device__ __forceinline__ void xf_tables(int8_t *s_tm, int8_t *s_dst, int lane) {
+// s_tm[32 * 32], s_dst[16] and s_mt[kMtElems] from the constant tables, by the lanes of one wave
+__device__ __forceinline__ void xf_tables(int8_t *s_tm, int8_t *s_dst, int16_t *s_mt, int lane) {
     for (int i = lane; i < 32 * 32; i += kWave) s_tm[i] = c_tm.m[i >> 5][i & 31];
     for (int i = lane; i < 16; i += kWave) s_dst[i] = c_dst[i >> 2][i & 3];
+    for (int i = lane; i < kMtElems; i += kWave) {
+        const int l2 = i < 80 ? 3 : (i < 80 + 288 ? 4 : 5), n = 1 << l2, sn = n + 2, k = i - mt_off(l2);
+        const int y = k / sn, j = k % sn;
+        s_mt[i] = (int16_t)(j < n ? c_tm.m[j << (5 - l2)][y] : 0);
+    }
+}
+
+// s + a.lo * b.lo + a.hi * b.hi (signed 16-bit halves)
+__device__ __forceinline__ int dot2_i16(uint32_t a, uint32_t b, int s) {
+#if defined(HG_HOST_EMU)
+    return s + (int)(int16_t)(a & 0xffffu) * (int)(int16_t)(b & 0xffffu) + (int)(int16_t)(a >> 16) * (int)(int16_t)(b >> 16);
+#else
+    typedef short short2_t __attribute__((ext_vector_type(2)));
+    short2_t va, vb;
+    __builtin_memcpy(&va, &a, 4);
+    __builtin_memcpy(&vb, &b, 4);
+    return __builtin_amdgcn_sdot2(va, vb, s, false);
+#endif
 }
 
 // Residual of coded TB `tu` into dst (row pitch `pitch` samples) by one wave.
@@ -150,8 +182,10 @@ __device__ __forceinline__ void transform_tb(const TuRec &tu, const CoefSrc<Cohe
     if (log2n < 2 || log2n > 5 || cidx > 2) return;
     const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
     const bool bypass = (tu.flags & TU_BYPASS) != 0, ts = (tu.flags & TU_TSKIP) != 0;
-    // 1. zero the tile, scatter d[y][x] (scaled unless bypass)
-    for (int i = lane; i < n * n / 2; i += kWave) reinterpret_cast<int32_t *>(d)[i] = 0;
+    // 1. zero the tile, scatter d[y][x] (scaled unless bypass; transposed for the dot-product stages)
+    const bool dots = !bypass && !ts && log2n >= 3 && X.mt != nullptr;
+    const int sn = n + 2;
+    for (int i = lane; i < (dots ? n * sn : n * n) / 2; i += kWave) reinterpret_cast<int32_t *>(d)[i] = 0;
     if (lane == 0) X.extent[0] = X.extent[1] = 0;
     xf_sync();
     const int qp = tu.qp;
@@ -170,7 +204,7 @@ __device__ __forceinline__ void transform_tb(const TuRec &tu, const CoefSrc<Cohe
             const int m = use_m ? mtab[pos] : 16;
             dv = clip16(((int64_t)v * m * ls + rnd) >> bd_shift);
         }
-        d[pos] = (int16_t)dv;
+        d[dots ? (pos & (n - 1)) * sn + (pos >> log2n) : pos] = (int16_t)dv;
         my_row = max(my_row, pos >> log2n);
         my_col = max(my_col, pos & (n - 1));
     };
@@ -212,6 +246,42 @@ __device__ __forceinline__ void transform_tb(const TuRec &tu, const CoefSrc<Cohe
         const int g0 = clip16(((int64_t)64 * d[0] + 64) >> 7);
         const int16_t r = (int16_t)clip16(((int64_t)64 * g0 + (1 << (bd2 - 1))) >> bd2);
         for (int i = lane; i < n * n; i += kWave) dst[(i >> log2n) * pitch + (i & (n - 1))] = r;
+        xf_sync();
+        return;
+    }
+    if (dots) {
+        // 2. e[y][x] = sum_{j < rows} M[j][y] dT[x][j] over the nonzero columns, rounded up to a
+        //    multiple of four (d is zero there, so g is too): the row pass's dots read whole quads
+        const int16_t *mt = X.mt + mt_off(log2n);
+        const int rows4 = (rows + 3) & ~3, cols4 = (cols + 3) & ~3;
+        const int lc = cols4 > 4 ? 32 - __builtin_clz((unsigned)(cols4 - 1)) : 2;
+        for (int o = lane; o < (n << lc); o += kWave) {
+            const int y = o >> lc, x = o & ((1 << lc) - 1);
+            if (x >= cols4) continue;
+            const uint32_t *pa = reinterpret_cast<const uint32_t *>(mt + y * sn);
+            const uint32_t *pb = reinterpret_cast<const uint32_t *>(d + x * sn);
+            int s = 0;
+#pragma unroll 2
+            for (int j = 0; j < rows4 / 2; j += 2) {
+                s = dot2_i16(pa[j], pb[j], s);
+                s = dot2_i16(pa[j + 1], pb[j + 1], s);
+            }
+            g[y * n + x] = (int16_t)min(max((s + 64) >> 7, -32768), 32767);  // (|s| < 2^27: 32-bit)
+        }
+        xf_sync();
+        // 3. r[y][x] = sum_{j < cols} M[j][x] g[y][j]: (r + rnd) >> (20 - bitDepth)
+        for (int o = lane; o < n * n; o += kWave) {
+            const int y = o >> log2n, x = o & (n - 1);
+            const uint32_t *pa = reinterpret_cast<const uint32_t *>(mt + x * sn);
+            const uint32_t *pb = reinterpret_cast<const uint32_t *>(g + y * n);
+            int s = 0;
+#pragma unroll 2
+            for (int j = 0; j < cols4 / 2; j += 2) {
+                s = dot2_i16(pa[j], pb[j], s);
+                s = dot2_i16(pa[j + 1], pb[j + 1], s);
+            }
+            dst[y * pitch + x] = (int16_t)min(max((s + (1 << (bd2 - 1))) >> bd2, -32768), 32767);
+        }
         xf_sync();
         return;
     }
