@@ -573,12 +573,14 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 
 }  // namespace
 
-// Register budget: at 7 waves per SIMD (<= 72 VGPRs) more reconstruction waves
-// fit beside the next decode's k_parse_lanes (176 VGPRs per wave) than at the
-// compiler's own 84; 8 (64 VGPRs) and the unconstrained build measured slower
-// (DESIGN.md section 5).  HG_INTRA_WPE=0 leaves it to the compiler.
+// Register budget: at most 5 waves per SIMD (<= 102 VGPRs, 76 used).  r04
+// measured 7 (72 VGPRs) best against 8 and the compiler's own; with r05's
+// lighter parse and transform, same-box pairs at 128 images gave 7: 19,690,
+// 5: 20,210, 4: 20,020 Mpix/s (profiles/r05/ab/ab_b128_dot4.txt): fewer
+// resident k_intra waves take less issue from the parse beside them.
+// HG_INTRA_WPE=0 leaves it to the compiler.
 #ifndef HG_INTRA_WPE
-#define HG_INTRA_WPE 7
+#define HG_INTRA_WPE 5
 #endif
 #if HG_INTRA_WPE > 0
 #define HG_INTRA_ATTR __attribute__((amdgpu_waves_per_eu(HG_INTRA_WPE)))
@@ -589,8 +591,8 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 // carries no per-format arithmetic)
 // LDS of k_intra's streaming mode beyond the windows: the transform tables
 // (workgroup) and per wave the transform tiles (transform_tb, xform.hpp)
-// (s_tm 1024 B, s_dst 16 B, s_mt; per wave the d tile 32 x 34, the g tile 32 x 32, the extent pair)
-constexpr size_t kXfTablesBytes = 1040 + kMtElems * sizeof(int16_t);
+// (the transposed matrices s_mt; per wave the d tile 32 x 34, the g tile 32 x 32, the extent pair)
+constexpr size_t kXfTablesBytes = kMtElems * sizeof(int16_t);
 constexpr size_t kXfDBytes = 32 * kXfDStride32 * sizeof(int16_t), kXfGBytes = 32 * 32 * sizeof(int16_t);
 constexpr size_t kXfWaveBytes = kXfDBytes + kXfGBytes + 16;
 static_assert(kXfTablesBytes % 16 == 0 && kXfWaveBytes % 16 == 0, "transform scratch alignment");
@@ -640,10 +642,8 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
         unsigned char *tab = smem + 64 + (size_t)nw * lay.bytes;
         unsigned char *xw = tab + kXfTablesBytes + (size_t)wave * kXfWaveBytes;
         X = XfScratch{reinterpret_cast<int16_t *>(xw), reinterpret_cast<int16_t *>(xw + kXfDBytes),
-                      reinterpret_cast<int32_t *>(xw + kXfDBytes + kXfGBytes), reinterpret_cast<int8_t *>(tab),
-                      reinterpret_cast<int8_t *>(tab + 1024), reinterpret_cast<int16_t *>(tab + 1040)};
-        xf_tables(reinterpret_cast<int8_t *>(tab), reinterpret_cast<int8_t *>(tab + 1024),
-                  reinterpret_cast<int16_t *>(tab + 1040), lane);
+                      reinterpret_cast<int32_t *>(xw + kXfDBytes + kXfGBytes), reinterpret_cast<int16_t *>(tab)};
+        xf_tables(reinterpret_cast<int16_t *>(tab), lane);
     }
     IntraScratch *S = reinterpret_cast<IntraScratch *>(blk);
     Win<Pel> win[3];

@@ -39,11 +39,9 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t dtile[kWaves][32 * kXfDStride32];
     HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t gtile[kWaves][32 * 32];
     HG_BLOCK_SHARED int32_t extent[kWaves][2];  // last nonzero row / column of d
-    HG_BLOCK_SHARED int8_t s_tm[32 * 32];
-    HG_BLOCK_SHARED int8_t s_dst[16];
     HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t s_mt[kMtElems];
     // every wave fills the tables (same values; the host emulation runs one lane per wave)
-    xf_tables(s_tm, s_dst, s_mt, (int)(threadIdx.x & 63));
+    xf_tables(s_mt, (int)(threadIdx.x & 63));
     __syncthreads();
     const int pic = a.pic0 + blockIdx.y, row = blockIdx.x;
     const PicDesc pd = a.pics[pic];
@@ -128,20 +126,18 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                         scaling ? a.sf[sp.sf_off + sf_size_offset(0) + (uint32_t)cidx * 16u + (uint32_t)pos] : 16;
                     dv = clip16(((int64_t)dv * m * ls + ((int64_t)1 << (bd_shift - 1))) >> bd_shift);
                 }
-                d[(vl & 48) + pos] = (int16_t)dv;
+                d[(vl & 48) + ((pos & 3) << 2) + (pos >> 2)] = (int16_t)dv;  // transposed: dT[x][y]
             }
             wave_sync();
-            // first stage: g[y][x] = clip16((sum_k M[k][y] d[k][x] + 64) >> 7)
+            // first stage: g[y][x] = clip16((sum_k M[k][y] dT[x][k] + 64) >> 7), two dot products
             for (int vl = lane; vl < 64; vl += kWave) {
                 TuRec tu;
                 if (!grp(vl, tu) || (tu.flags & (TU_BYPASS | TU_TSKIP))) continue;
-                const int16_t *dq = d + (vl & 48);
                 const int y = (vl & 15) >> 2, x = vl & 3;
-                const bool dst_tr = (tu.flags & TU_DST) != 0;
-                int32_t s = 0;
-                for (int k = 0; k < 4; ++k)
-                    s += (int32_t)(dst_tr ? s_dst[k * 4 + y] : s_tm[(k * 8) * 32 + y]) * dq[k * 4 + x];
-                g[vl] = (int16_t)clip16(((int64_t)s + 64) >> 7);
+                const uint32_t *pa = reinterpret_cast<const uint32_t *>(mt_of(s_mt, 2, (tu.flags & TU_DST) != 0) + y * 4);
+                const uint32_t *pb = reinterpret_cast<const uint32_t *>(d + (vl & 48) + x * 4);
+                const int s = dot2_i16(pa[1], pb[1], dot2_i16(pa[0], pb[0], 0));
+                g[vl] = (int16_t)min(max((s + 64) >> 7, -32768), 32767);
             }
             wave_sync();
             // second stage (or bypass / transform skip) and the residual store
@@ -154,15 +150,14 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                 const int16_t *dq = d + (vl & 48), *gq = g + (vl & 48);
                 int r;
                 if (tu.flags & TU_BYPASS) {
-                    r = dq[vl & 15];
+                    r = dq[x * 4 + y];
                 } else if (tu.flags & TU_TSKIP) {
-                    r = (dq[vl & 15] * (1 << 7) + (1 << (bd2 - 1))) >> bd2;  // tsShift = 5 + log2(4)
-                } else {
-                    const bool dst_tr = (tu.flags & TU_DST) != 0;
-                    int32_t s = 0;  // 4 terms of |g| <= 2^15 times |M| <= 90
-                    for (int k = 0; k < 4; ++k)
-                        s += (int32_t)(dst_tr ? s_dst[k * 4 + x] : s_tm[(k * 8) * 32 + x]) * gq[y * 4 + k];
-                    r = (int)((s + (1 << (bd2 - 1))) >> bd2);
+                    r = (dq[x * 4 + y] * (1 << 7) + (1 << (bd2 - 1))) >> bd2;  // tsShift = 5 + log2(4)
+                } else {  // 4 terms of |g| <= 2^15 times |M| <= 90
+                    const uint32_t *pa = reinterpret_cast<const uint32_t *>(mt_of(s_mt, 2, (tu.flags & TU_DST) != 0) + x * 4);
+                    const uint32_t *pb = reinterpret_cast<const uint32_t *>(gq + y * 4);
+                    const int s = dot2_i16(pa[1], pb[1], dot2_i16(pa[0], pb[0], 0));
+                    r = (s + (1 << (bd2 - 1))) >> bd2;
                 }
                 res_plane[cidx][(size_t)(tu.y + y) * pitch[cidx] + tu.x + x] = (int16_t)clip16(r);
             }
@@ -178,7 +173,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
         const int cidx = tu.flags & TU_CIDX_MASK;
         const int n = 1 << tu.log2;
         if (tu.log2 > 5 || cidx > 2 || tu.x + n > pitch[cidx] || tu.y + n > (cidx ? ch : H)) continue;
-        transform_tb(tu, coefs, sp, a.sf, XfScratch{d, g, extent[wave], s_tm, s_dst, s_mt},
+        transform_tb(tu, coefs, sp, a.sf, XfScratch{d, g, extent[wave], s_mt},
                      res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x, pitch[cidx], lane);
     }
 }

@@ -129,8 +129,11 @@ __device__ __forceinline__ SbRec load_rec(const CoefSrc<Coherent> &src, uint32_t
 // transMatrix[j * 32 / n][y], same stride, so both operands of every dot run
 // along j.  (r04's loops: one int8 matrix load, one int16 load and a
 // multiply-add per term, ~7 instructions per term.)
+// 4x4: the DCT and the DST (luma) matrices, transposed the same way, row
+// stride 4 (an 8-byte read per row, four lanes per TB column).
 constexpr int kXfDStride32 = 32 + 2;
-constexpr int kMtElems = 8 * 10 + 16 * 18 + 32 * 34;  // int16
+constexpr int kMt4Dct = 8 * 10 + 16 * 18 + 32 * 34, kMt4Dst = kMt4Dct + 16;
+constexpr int kMtElems = kMt4Dst + 16;  // int16
 __device__ __forceinline__ int mt_off(int log2n) { return log2n == 3 ? 0 : (log2n == 4 ? 8 * 10 : 8 * 10 + 16 * 18); }
 
 // a wave's transform scratch: d (int16, 32 x 34: the transposed layout's
@@ -139,20 +142,28 @@ __device__ __forceinline__ int mt_off(int log2n) { return log2n == 3 ? 0 : (log2
 struct XfScratch {
     int16_t *d, *g;
     int32_t *extent;
-    const int8_t *tm, *dst;
-    const int16_t *mt;  // kMtElems: mtT_n of n = 8, 16, 32
+    const int16_t *mt;  // kMtElems: mtT_n of n = 8, 16, 32, then the 4x4 DCT and DST
 };
 
-// s_tm[32 * 32], s_dst[16] and s_mt[kMtElems] from the constant tables, by the lanes of one wave
-__device__ __forceinline__ void xf_tables(int8_t *s_tm, int8_t *s_dst, int16_t *s_mt, int lane) {
-    for (int i = lane; i < 32 * 32; i += kWave) s_tm[i] = c_tm.m[i >> 5][i & 31];
-    for (int i = lane; i < 16; i += kWave) s_dst[i] = c_dst[i >> 2][i & 3];
+// s_mt[kMtElems] from the constant tables, by the lanes of one wave
+__device__ __forceinline__ void xf_tables(int16_t *s_mt, int lane) {
     for (int i = lane; i < kMtElems; i += kWave) {
+        if (i >= kMt4Dct) {  // 4x4: mtT[y][k] = M[k][y]
+            const int k = i & 3, y = (i >> 2) & 3;
+            s_mt[i] = (int16_t)(i >= kMt4Dst ? c_dst[k][y] : c_tm.m[k * 8][y]);
+            continue;
+        }
         const int l2 = i < 80 ? 3 : (i < 80 + 288 ? 4 : 5), n = 1 << l2, sn = n + 2, k = i - mt_off(l2);
         const int y = k / sn, j = k % sn;
         s_mt[i] = (int16_t)(j < n ? c_tm.m[j << (5 - l2)][y] : 0);
     }
 }
+
+// the transposed matrix of a TB of size 1 << log2n (DST: 4x4 luma), and its row stride
+__device__ __forceinline__ const int16_t *mt_of(const int16_t *mt, int log2n, bool dst_tr) {
+    return log2n == 2 ? mt + (dst_tr ? kMt4Dst : kMt4Dct) : mt + mt_off(log2n);
+}
+__device__ __forceinline__ int mt_stride(int log2n) { return log2n == 2 ? 4 : (1 << log2n) + 2; }
 
 // s + a.lo * b.lo + a.hi * b.hi (signed 16-bit halves)
 __device__ __forceinline__ int dot2_i16(uint32_t a, uint32_t b, int s) {
@@ -175,7 +186,6 @@ template <bool Coherent, class DstPtr>
 __device__ __forceinline__ void transform_tb(const TuRec &tu, const CoefSrc<Coherent> &coefs, const SeqParams &sp,
                                              const uint8_t *sf, const XfScratch &X, DstPtr dst, int pitch, int lane) {
     int16_t *d = X.d, *g = X.g;
-    const int8_t *s_tm = X.tm, *s_dst = X.dst;
     const bool scaling = (sp.flags & SP_SCALING_LIST) != 0;
     const int cidx = tu.flags & TU_CIDX_MASK;
     const int log2n = tu.log2, n = 1 << log2n;
@@ -183,8 +193,8 @@ __device__ __forceinline__ void transform_tb(const TuRec &tu, const CoefSrc<Cohe
     const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
     const bool bypass = (tu.flags & TU_BYPASS) != 0, ts = (tu.flags & TU_TSKIP) != 0;
     // 1. zero the tile, scatter d[y][x] (scaled unless bypass; transposed for the dot-product stages)
-    const bool dots = !bypass && !ts && log2n >= 3 && X.mt != nullptr;
-    const int sn = n + 2;
+    const bool dots = !bypass && !ts;
+    const int sn = mt_stride(log2n);
     for (int i = lane; i < (dots ? n * sn : n * n) / 2; i += kWave) reinterpret_cast<int32_t *>(d)[i] = 0;
     if (lane == 0) X.extent[0] = X.extent[1] = 0;
     xf_sync();
@@ -240,7 +250,6 @@ __device__ __forceinline__ void transform_tb(const TuRec &tu, const CoefSrc<Cohe
         return;
     }
     const bool dst_tr = (tu.flags & TU_DST) != 0;
-    const int kstep = 32 >> log2n;
     if (!dst_tr && rows == 1 && cols == 1) {
         // DC only: both stages are constant (transMatrix[0][*] = 64)
         const int g0 = clip16(((int64_t)64 * d[0] + 64) >> 7);
@@ -249,69 +258,37 @@ __device__ __forceinline__ void transform_tb(const TuRec &tu, const CoefSrc<Cohe
         xf_sync();
         return;
     }
-    if (dots) {
-        // 2. e[y][x] = sum_{j < rows} M[j][y] dT[x][j] over the nonzero columns, rounded up to a
-        //    multiple of four (d is zero there, so g is too): the row pass's dots read whole quads
-        const int16_t *mt = X.mt + mt_off(log2n);
-        const int rows4 = (rows + 3) & ~3, cols4 = (cols + 3) & ~3;
-        const int lc = cols4 > 4 ? 32 - __builtin_clz((unsigned)(cols4 - 1)) : 2;
-        for (int o = lane; o < (n << lc); o += kWave) {
-            const int y = o >> lc, x = o & ((1 << lc) - 1);
-            if (x >= cols4) continue;
-            const uint32_t *pa = reinterpret_cast<const uint32_t *>(mt + y * sn);
-            const uint32_t *pb = reinterpret_cast<const uint32_t *>(d + x * sn);
-            int s = 0;
-#pragma unroll 2
-            for (int j = 0; j < rows4 / 2; j += 2) {
-                s = dot2_i16(pa[j], pb[j], s);
-                s = dot2_i16(pa[j + 1], pb[j + 1], s);
-            }
-            g[y * n + x] = (int16_t)min(max((s + 64) >> 7, -32768), 32767);  // (|s| < 2^27: 32-bit)
-        }
-        xf_sync();
-        // 3. r[y][x] = sum_{j < cols} M[j][x] g[y][j]: (r + rnd) >> (20 - bitDepth)
-        for (int o = lane; o < n * n; o += kWave) {
-            const int y = o >> log2n, x = o & (n - 1);
-            const uint32_t *pa = reinterpret_cast<const uint32_t *>(mt + x * sn);
-            const uint32_t *pb = reinterpret_cast<const uint32_t *>(g + y * n);
-            int s = 0;
-#pragma unroll 2
-            for (int j = 0; j < cols4 / 2; j += 2) {
-                s = dot2_i16(pa[j], pb[j], s);
-                s = dot2_i16(pa[j + 1], pb[j + 1], s);
-            }
-            dst[y * pitch + x] = (int16_t)min(max((s + (1 << (bd2 - 1))) >> bd2, -32768), 32767);
-        }
-        xf_sync();
-        return;
-    }
-    // 2. vertical (column) pass over the nonzero columns:
-    //    e[y][x] = sum_{j < rows} M[j][y] d[j][x]; g = clip16((e + 64) >> 7)
-    // columns padded to a power of two: shifts instead of a division per output
-    const int lc = cols > 1 ? 32 - __builtin_clz((unsigned)(cols - 1)) : 0;
+    // 2. e[y][x] = sum_{j < rows} M[j][y] dT[x][j] over the nonzero columns, rounded up to a
+    //    multiple of four (d is zero there, so g is too): the row pass's dots read whole quads
+    const int16_t *mt = mt_of(X.mt, log2n, dst_tr);
+    const int rows4 = (rows + 3) & ~3, cols4 = (cols + 3) & ~3;
+    const int lc = cols4 > 4 ? 32 - __builtin_clz((unsigned)(cols4 - 1)) : 2;
     for (int o = lane; o < (n << lc); o += kWave) {
         const int y = o >> lc, x = o & ((1 << lc) - 1);
-        if (x >= cols) continue;
-        int32_t s = 0;
-        if (dst_tr) {
-            for (int j = 0; j < rows; ++j) s += (int32_t)s_dst[j * 4 + y] * d[j * n + x];
-        } else {
-            for (int j = 0; j < rows; ++j) s += (int32_t)s_tm[(j * kstep) * 32 + y] * d[j * n + x];
+        if (x >= cols4) continue;
+        const uint32_t *pa = reinterpret_cast<const uint32_t *>(mt + y * sn);
+        const uint32_t *pb = reinterpret_cast<const uint32_t *>(d + x * sn);
+        int s = 0;
+#pragma unroll 2
+        for (int j = 0; j < rows4 / 2; j += 2) {
+            s = dot2_i16(pa[j], pb[j], s);
+            s = dot2_i16(pa[j + 1], pb[j + 1], s);
         }
-        g[y * n + x] = (int16_t)clip16(((int64_t)s + 64) >> 7);
+        g[y * n + x] = (int16_t)min(max((s + 64) >> 7, -32768), 32767);  // (|s| < 2^27: 32-bit)
     }
     xf_sync();
-    // 3. horizontal (row) pass: r[y][x] = sum_{j < cols} M[j][x] g[y][j]; (r + rnd) >> (20 - bitDepth)
-    //    (|g| <= 2^15 after clipping and |M| <= 90, so |sum| < 32 * 90 * 2^15 < 2^31: 32-bit)
+    // 3. r[y][x] = sum_{j < cols} M[j][x] g[y][j]: (r + rnd) >> (20 - bitDepth)
     for (int o = lane; o < n * n; o += kWave) {
         const int y = o >> log2n, x = o & (n - 1);
-        int32_t s = 0;
-        if (dst_tr) {
-            for (int j = 0; j < cols; ++j) s += (int32_t)s_dst[j * 4 + x] * g[y * n + j];
-        } else {
-            for (int j = 0; j < cols; ++j) s += (int32_t)s_tm[(j * kstep) * 32 + x] * g[y * n + j];
+        const uint32_t *pa = reinterpret_cast<const uint32_t *>(mt + x * sn);
+        const uint32_t *pb = reinterpret_cast<const uint32_t *>(g + y * n);
+        int s = 0;
+#pragma unroll 2
+        for (int j = 0; j < cols4 / 2; j += 2) {
+            s = dot2_i16(pa[j], pb[j], s);
+            s = dot2_i16(pa[j + 1], pb[j + 1], s);
         }
-        dst[y * pitch + x] = (int16_t)clip16((s + (1 << (bd2 - 1))) >> bd2);
+        dst[y * pitch + x] = (int16_t)min(max((s + (1 << (bd2 - 1))) >> bd2, -32768), 32767);
     }
     xf_sync();
 }
