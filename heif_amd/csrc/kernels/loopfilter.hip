@@ -253,6 +253,82 @@ __device__ __forceinline__ int sao_sample(const Pel *P, int PW, int PH, int xs, 
     return clip3(0, (1 << bd) - 1, v + o);
 }
 
+// Four samples in one load: 4 x 8 bits in a dword, 4 x 16 bits in a qword
+template <typename Pel>
+struct QuadLoad;
+template <>
+struct QuadLoad<uint8_t> {
+    using W = uint32_t;
+    static __device__ __forceinline__ int at(W w, int j) { return (int)((w >> (8 * j)) & 0xffu); }
+};
+template <>
+struct QuadLoad<uint16_t> {
+    using W = uint64_t;
+    static __device__ __forceinline__ int at(W w, int j) { return (int)((w >> (16 * j)) & 0xffffu); }
+};
+
+// SAO (8.7.3) of the four samples (xs0 .. xs0 + 3, ys) of component cidx when
+// xs0 is a multiple of 4 and the four are one aligned load (then they share a
+// CTB, and the neighbour rows are aligned loads too): the CTB's parameters
+// read once, the neighbours of every edge class from two quads and two
+// samples, no per-sample branches.  False: not applicable (sao_sample per
+// sample).
+template <typename Pel>
+__device__ __forceinline__ bool sao_quad(const Pel *P, int PW, int PH, int xs0, int ys, int cidx, int subx, int suby,
+                                         const SaoParams *sao, int wctb, int log2ctb, const uint8_t *flg, int w4,
+                                         int bd, int v[4]) {
+    using Q = QuadLoad<Pel>;
+    using W = typename Q::W;
+    const Pel *row = P + (size_t)ys * PW;
+    if ((xs0 & 3) || (PW & 3) || (reinterpret_cast<uintptr_t>(row + xs0) & (sizeof(W) - 1))) return false;
+    const W c = *reinterpret_cast<const W *>(row + xs0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = Q::at(c, j);
+    const SaoParams &s = sao[(ys >> (log2ctb - suby)) * wctb + (xs0 >> (log2ctb - subx))];
+    const int type = s.type[cidx];
+    if (!type) return true;
+    // MF_NOFILT of each sample's 4x4 luma block: at most two blocks per quad
+    const uint8_t *fr = flg + (size_t)((ys << suby) >> 2) * w4;
+    const int b0 = (xs0 << subx) >> 2, b3 = ((xs0 + 3) << subx) >> 2;
+    const int f0 = fr[b0], f3 = fr[b3];
+    const int cl = s.band_eo[cidx];
+    const int maxv = (1 << bd) - 1;
+    int o[4] = {0, 0, 0, 0};
+    if (type == 2) {
+        const int hx = cl == 0 ? 1 : (cl == 1 ? 0 : (cl == 2 ? 1 : -1)), vy = cl == 0 ? 0 : 1;
+        const int ya = ys - vy, yb = ys + vy;
+        const bool va = ya >= 0, vb = yb < PH;
+        const Pel *ra = P + (size_t)(va ? ya : ys) * PW, *rb = P + (size_t)(vb ? yb : ys) * PW;
+        const W qa = *reinterpret_cast<const W *>(ra + xs0), qb = *reinterpret_cast<const W *>(rb + xs0);
+        // the one sample of each neighbour row outside the quad: a at x - hx, b at x + hx
+        const int xa_out = hx > 0 ? xs0 - 1 : xs0 + 4, xb_out = hx > 0 ? xs0 + 4 : xs0 - 1;
+        const int ea = hx != 0 && xa_out >= 0 && xa_out < PW ? (int)ra[xa_out] : 0;
+        const int eb = hx != 0 && xb_out >= 0 && xb_out < PW ? (int)rb[xb_out] : 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ja = j - hx, jb = j + hx;  // quad positions of the neighbours (-1 or 4: outside)
+            const int na = ja < 0 || ja > 3 ? ea : Q::at(qa, ja < 0 ? 0 : (ja > 3 ? 3 : ja));
+            const int nb = jb < 0 || jb > 3 ? eb : Q::at(qb, jb < 0 ? 0 : (jb > 3 ? 3 : jb));
+            const bool in = va && vb && xs0 + ja >= 0 && xs0 + ja < PW && xs0 + jb >= 0 && xs0 + jb < PW;
+            int e = 2 + (v[j] > na) - (v[j] < na) + (v[j] > nb) - (v[j] < nb);
+            e = e <= 2 ? (e == 2 ? 0 : e + 1) : e;
+            o[j] = in && e ? s.off[cidx][e - 1] : 0;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = ((v[j] >> (bd - 5)) - cl) & 31;
+            o[j] = k < 4 ? s.off[cidx][k] : 0;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool nf = ((((xs0 + j) << subx) >> 2) == b0 ? f0 : f3) & MF_NOFILT;
+        if (!nf) v[j] = clip3(0, maxv, v[j] + o[j]);
+    }
+    return true;
+}
+
 // SAO + crop + grid placement: one thread per four consecutive output samples
 // of a row (one 4- or 8-byte store; per sample at a row's ragged end or an
 // unaligned caller plane)
@@ -300,12 +376,14 @@ __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
         const bool on = pd.sao_luma || pd.sao_chroma;  // SaoTypeIdx is 0 for a component whose flag is off
         const int bd = cidx ? sp.bit_depth_c : sp.bit_depth_y;
         int v[4];
+        if (!(n == 4 && on && sao_quad(P, PW, PH, xs0, ys, cidx, subx, suby, sao, wctb, log2ctb, flg, w4, bd, v))) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            v[j] = 0;
-            if (j < n)
-                v[j] = on ? sao_sample(P, PW, PH, xs0 + j, ys, cidx, subx, suby, sao, wctb, log2ctb, flg, w4, bd)
-                          : (int)P[(size_t)ys * PW + xs0 + j];
+            for (int j = 0; j < 4; ++j) {
+                v[j] = 0;
+                if (j < n)
+                    v[j] = on ? sao_sample(P, PW, PH, xs0 + j, ys, cidx, subx, suby, sao, wctb, log2ctb, flg, w4, bd)
+                              : (int)P[(size_t)ys * PW + xs0 + j];
+            }
         }
         // component fields by select: a lane-varying index into the OutImage copy made
         // the compiler keep it in LDS (12 KB per workgroup, 519 M bank-conflict cycles per launch)
