@@ -194,6 +194,21 @@ struct Win {
     }
 };
 
+#if !defined(HG_HOST_EMU)
+// the sum over the lanes of each aligned group of m (2 <= m <= 64, a power of
+// two) lanes, in every lane of the group: ds_swizzle xor steps inside 32-lane
+// halves (one LDS-crossbar instruction each, against __shfl_xor's address
+// arithmetic and bounds select), ds_bpermute across them
+__device__ __forceinline__ int group_sum(int v, int m) {
+    if (m >= 64) v += __builtin_amdgcn_ds_bpermute(((int)__lane_id() ^ 32) << 2, v);
+    if (m >= 32) v += __builtin_amdgcn_ds_swizzle(v, 0x1f | (16 << 10));
+    if (m >= 16) v += __builtin_amdgcn_ds_swizzle(v, 0x1f | (8 << 10));
+    if (m >= 8) v += __builtin_amdgcn_ds_swizzle(v, 0x1f | (4 << 10));
+    if (m >= 4) v += __builtin_amdgcn_ds_swizzle(v, 0x1f | (2 << 10));
+    return v + __builtin_amdgcn_ds_swizzle(v, 0x1f | (1 << 10));
+}
+#endif
+
 template <typename Pel, int CF>
 __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L, const TuRec &tu, const Win<Pel> &w,
                                                                  int PW, int PH, int cidx, int bd, bool strong,
@@ -257,6 +272,26 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
 #else
     if (ns <= 64) {  // 4x4 and 8x8 TBs (most of them): one chunk of 4n + 1 <= 33 samples
         const int s = lane;
+#if !defined(HG_INTRA_GATHER_R04)
+        // every step formed for all lanes with selects (the branchy form
+        // split the wave into three exec regions per step): the column left
+        // of the TB bottom-up, the corner, the row above left to right
+        const int xn = s <= 2 * n ? x0 - 1 : x0 + s - 2 * n - 1;
+        const int yn = s < 2 * n ? y0 + 2 * n - 1 - s : y0 - 1;
+        const bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
+                        nb_avail(zc, xn << subx, yn << suby, bx0, by0, csl);
+        const int lx = xn - w.cx0, ly = yn - w.cy0;
+        const Pel *src = ly < 0 ? w.above + lx + 1 : (lx < 0 ? w.left + ly : w.cur + ly * w.csx + lx);
+        const int val = (int)*(av ? src : w.cur);  // (an unavailable lane reads the window's first sample)
+        const uint64_t msk = __ballot(av);
+        const uint64_t below = msk & ((1ull << lane) - 1ull);
+        const int sub = below ? 63 - __clzll(below) : __ffsll((unsigned long long)msk) - 1;
+        const int sv = __shfl(val, av ? lane : sub, 64);
+        const int v = msk ? sv : (1 << (bd - 1));
+        int16_t *dp = s < 2 * n ? L->left + (2 * n - s) : L->top + (s - 2 * n);
+        if (s < ns) *dp = (int16_t)v;
+        if (s == 2 * n) L->left[0] = (int16_t)v;
+#else
         int xn, yn;
         if (s < 2 * n) {
             xn = x0 - 1;
@@ -286,6 +321,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         } else if (s < ns) {
             L->top[s - 2 * n] = (int16_t)v;
         }
+#endif
     } else {
     // 16x16 (65 samples) needs two chunks, 32x32 (129) three
     const int nch = ns <= 128 ? 2 : 3;
@@ -389,16 +425,18 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     const int maxv = (1 << bd) - 1;
     // 4. prediction (+ residual)
     int dc = 0;
-    if (mode == 1) {  // DC: wave reduction of the 2n references (every lane ends with the sum)
+    if (mode == 1) {  // DC: the 2n <= 64 references summed over lanes 0 .. 2n - 1, then broadcast
+#if !defined(HG_HOST_EMU)
+        int sum = lane < 2 * n ? (lane < n ? tp[1 + lane] : lf[1 + lane - n]) : 0;
+        sum = __builtin_amdgcn_readlane(group_sum(sum, 2 * n), 0);
+#else
         int sum = 0;
         for (int i = lane; i < 2 * n; i += kWave) sum += i < n ? tp[1 + i] : lf[1 + i - n];
-#if !defined(HG_HOST_EMU)
-        for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
 #endif
         dc = (sum + n) >> (log2n + 1);
     }
     const int lx0 = x0 - w.cx0, ly0 = y0 - w.cy0;
-    for (int o = lane; o < n * n; o += kWave) {
+    auto predict_sample = [&](int o) {
         const int x = o & (n - 1), y = o >> log2n;
         int pv;
         if (mode == 0) {
@@ -428,6 +466,14 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         if (cbf) pv += (n <= 8 && o == lane) ? r0 : rt[y * w.rp + x];
         pv = min(max(pv, 0), maxv);
         w.cur[li] = (Pel)pv;
+    };
+#if !defined(HG_HOST_EMU)
+    if (n <= 8) {  // one sample per lane: no loop
+        if (lane < n * n) predict_sample(lane);
+    } else
+#endif
+    {
+        for (int o = lane; o < n * n; o += kWave) predict_sample(o);
     }
     wave_sync();
 }
@@ -539,10 +585,10 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     int dc = 0;
     const int ang = c_angle[mode], inv = c_inv_angle[mode];
     const int16_t *main_ = mode >= 18 ? tp : lf, *side = mode >= 18 ? lf : tp;
-    if (mode == 1) {
-        int sum = sl < 2 * n ? (sl < n ? tp[1 + sl] : lf[1 + sl - n]) : 0;
-        for (int off = 16; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
-        dc = (sum + n) >> (log2n + 1);
+    if (mode == 1) {  // each half sums its 2n <= 16 references in its lanes 0 .. 2n - 1
+        const int sum = group_sum(sl < 2 * n ? (sl < n ? tp[1 + sl] : lf[1 + sl - n]) : 0, 2 * n);
+        const int s0 = __builtin_amdgcn_readlane(sum, 0), s1 = __builtin_amdgcn_readlane(sum, 32);
+        dc = ((h ? s1 : s0) + n) >> (log2n + 1);
     }
     const int lx0 = x0 - w.cx0, ly0 = y0 - w.cy0;
     for (int it = 0; it < nch; ++it) {
