@@ -40,8 +40,12 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t gtile[kWaves][32 * 32];
     HG_BLOCK_SHARED int32_t extent[kWaves][2];  // last nonzero row / column of d
     HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t s_mt[kMtElems];
-    // every wave fills the tables (same values; the host emulation runs one lane per wave)
-    xf_tables(s_mt, (int)(threadIdx.x & 63));
+    // the workgroup's threads copy the table (the host emulation runs one thread per wave)
+#if defined(HG_HOST_EMU)
+    xf_tables(s_mt, 0, 1);
+#else
+    xf_tables(s_mt, (int)threadIdx.x, (int)blockDim.x);
+#endif
     __syncthreads();
     const int pic = a.pic0 + blockIdx.y, row = blockIdx.x;
     const PicDesc pd = a.pics[pic];
@@ -72,30 +76,14 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     // the host emulation runs one lane per wave).
     {
         const uint32_t mine = ntu > (uint32_t)wave ? (ntu - (uint32_t)wave + kWaves - 1) / kWaves : 0;
-        for (uint32_t j = 0; j < mine; j += 4) {
-            // TB of group q = vl >> 4 in this round, if it is a coded 4x4 TB
-            auto group_tb = [&](int vl, TuRec &tu) -> bool {
-                const uint32_t jq = j + (uint32_t)(vl >> 4);
-                if (jq >= mine) return false;
-                tu = tus[(uint32_t)wave + kWaves * jq];
-                const int cidx = tu.flags & TU_CIDX_MASK;
-                return (tu.flags & TU_CBF) && tu.log2 == 2 && cidx <= 2 && tu.x + 4 <= pitch[cidx] &&
-                       tu.y + 4 <= (cidx ? ch : H);
-            };
-            // the lane's record, loaded once per round (each phase below would
-            // otherwise re-load it after the wave syncs)
-#if defined(HG_HOST_EMU)
-            auto grp = group_tb;
-#else
-            // one record per lane: each `vl` loop below runs once per lane (vl == lane)
-            static_assert(kWave == 64, "the cached record assumes vl == lane");
-            TuRec tu_c;
-            const bool ok_c = group_tb(lane, tu_c);
-            auto grp = [&](int, TuRec &tu) -> bool {
-                tu = tu_c;
-                return ok_c;
-            };
-#endif
+        // the wave's j-th record: a coded 4x4 TB inside its plane?
+        auto want4 = [&](const TuRec &tu) -> bool {
+            const int cidx = tu.flags & TU_CIDX_MASK;
+            return (tu.flags & TU_CBF) && tu.log2 == 2 && cidx <= 2 && tu.x + 4 <= pitch[cidx] &&
+                   tu.y + 4 <= (cidx ? ch : H);
+        };
+        // one round: up to four TBs, group q = vl >> 4 runs TB q (grp(vl, tu))
+        auto round4 = [&](auto &&grp) {
             for (int vl = lane; vl < 64; vl += kWave) d[vl] = 0;
             wave_sync();
             for (int vl = lane; vl < 64; vl += kWave) {
@@ -162,20 +150,88 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
                 res_plane[cidx][(size_t)(tu.y + y) * pitch[cidx] + tu.x + x] = (int16_t)clip16(r);
             }
             wave_sync();
+        };
+#if defined(HG_HOST_EMU)
+        for (uint32_t j = 0; j < mine; j += 4) {
+            round4([&](int vl, TuRec &tu) -> bool {
+                const uint32_t jq = j + (uint32_t)(vl >> 4);
+                if (jq >= mine) return false;
+                tu = tus[(uint32_t)wave + kWaves * jq];
+                return want4(tu);
+            });
         }
+#else
+        // the rounds take the coded 4x4 TBs only: 64 of the wave's records per
+        // coalesced load, a ballot of the wanted ones, four set bits per round
+        // (rounds over consecutive records, coded or not, ran mostly empty groups)
+        static_assert(kWave == 64, "one record per lane");
+        for (uint32_t c0 = 0; c0 < mine; c0 += 64) {
+            const uint32_t jl = c0 + (uint32_t)lane;
+            uint4 rec = make_uint4(0, 0, 0, 0);
+            if (jl < mine) rec = *reinterpret_cast<const uint4 *>(tus + (uint32_t)wave + kWaves * jl);
+            TuRec rl;
+            __builtin_memcpy(&rl, &rec, sizeof(rl));
+            uint64_t todo = __ballot(jl < mine && want4(rl));
+            while (todo) {
+                int src = -1;
+                for (int q = 0; q < 4 && todo; ++q) {
+                    const int jq = __builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    if (q == (lane >> 4)) src = jq;
+                }
+                const int sl = src < 0 ? 0 : src;
+                const uint4 r = make_uint4((uint32_t)__shfl((int)rec.x, sl, 64), (uint32_t)__shfl((int)rec.y, sl, 64),
+                                           (uint32_t)__shfl((int)rec.z, sl, 64), (uint32_t)__shfl((int)rec.w, sl, 64));
+                TuRec tu_c;
+                __builtin_memcpy(&tu_c, &r, sizeof(tu_c));
+                const bool ok_c = src >= 0;
+                round4([&](int, TuRec &tu) -> bool {
+                    tu = tu_c;
+                    return ok_c;
+                });
+            }
+        }
+#endif
     }
 
     // Pass B: every larger TB, one per wave
-    for (uint32_t t = wave; t < ntu; t += kWaves) {
-        const TuRec tu = tus[t];
-        if (!(tu.flags & TU_CBF)) continue;
-        if (tu.log2 == 2) continue;  // pass A
+    auto pass_b = [&](const TuRec &tu) {
         const int cidx = tu.flags & TU_CIDX_MASK;
-        const int n = 1 << tu.log2;
-        if (tu.log2 > 5 || cidx > 2 || tu.x + n > pitch[cidx] || tu.y + n > (cidx ? ch : H)) continue;
         transform_tb(tu, coefs, sp, a.sf, XfScratch{d, g, extent[wave], s_mt},
                      res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x, pitch[cidx], lane);
+    };
+    auto wanted = [&](const TuRec &tu) {
+        const int cidx = tu.flags & TU_CIDX_MASK, n = 1 << tu.log2;
+        return (tu.flags & TU_CBF) && tu.log2 != 2 && tu.log2 <= 5 && cidx <= 2 && tu.x + n <= pitch[cidx] &&
+               tu.y + n <= (cidx ? ch : H);
+    };
+#if defined(HG_HOST_EMU)
+    for (uint32_t t = wave; t < ntu; t += kWaves)
+        if (wanted(tus[t])) pass_b(tus[t]);
+#else
+    // the wave's next 64 records in one coalesced load, one per lane; the TBs it
+    // transforms are the set bits of a ballot (a scalar load and its wait per
+    // record, coded or not, before)
+    for (uint32_t t0 = wave; t0 < ntu; t0 += 64u * kWaves) {
+        const uint32_t t = t0 + (uint32_t)lane * kWaves;
+        uint4 rec = make_uint4(0, 0, 0, 0);
+        if (t < ntu) rec = *reinterpret_cast<const uint4 *>(tus + t);
+        TuRec mine;
+        __builtin_memcpy(&mine, &rec, sizeof(mine));
+        uint64_t todo = __ballot(t < ntu && wanted(mine));
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint4 r = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)rec.x, j),
+                                       (uint32_t)__builtin_amdgcn_readlane((int)rec.y, j),
+                                       (uint32_t)__builtin_amdgcn_readlane((int)rec.z, j),
+                                       (uint32_t)__builtin_amdgcn_readlane((int)rec.w, j));
+            TuRec tu;
+            __builtin_memcpy(&tu, &r, sizeof(tu));
+            pass_b(tu);
+        }
     }
+#endif
 }
 
 #if defined(HG_HOST_EMU)

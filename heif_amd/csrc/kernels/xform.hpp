@@ -145,18 +145,35 @@ struct XfScratch {
     const int16_t *mt;  // kMtElems: mtT_n of n = 8, 16, 32, then the 4x4 DCT and DST
 };
 
-// s_mt[kMtElems] from the constant tables, by the lanes of one wave
-__device__ __forceinline__ void xf_tables(int16_t *s_mt, int lane) {
-    for (int i = lane; i < kMtElems; i += kWave) {
+// the transposed tables, built at compile time (filling them per workgroup
+// with an integer division per entry cost k_transform 7 % of its VALU)
+struct alignas(16) MtTables {
+    int16_t v[kMtElems];
+};
+constexpr MtTables make_mt_tables() {
+    MtTables t{};
+    const TransMatrix m = make_matrix();
+    constexpr int dst4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
+    for (int i = 0; i < kMtElems; ++i) {
         if (i >= kMt4Dct) {  // 4x4: mtT[y][k] = M[k][y]
             const int k = i & 3, y = (i >> 2) & 3;
-            s_mt[i] = (int16_t)(i >= kMt4Dst ? c_dst[k][y] : c_tm.m[k * 8][y]);
+            t.v[i] = (int16_t)(i >= kMt4Dst ? dst4[k][y] : m.m[k * 8][y]);
             continue;
         }
-        const int l2 = i < 80 ? 3 : (i < 80 + 288 ? 4 : 5), n = 1 << l2, sn = n + 2, k = i - mt_off(l2);
+        const int l2 = i < 80 ? 3 : (i < 80 + 288 ? 4 : 5), n = 1 << l2, sn = n + 2;
+        const int k = i - (l2 == 3 ? 0 : (l2 == 4 ? 80 : 80 + 288));
         const int y = k / sn, j = k % sn;
-        s_mt[i] = (int16_t)(j < n ? c_tm.m[j << (5 - l2)][y] : 0);
+        t.v[i] = (int16_t)(j < n ? m.m[j << (5 - l2)][y] : 0);
     }
+    return t;
+}
+__constant__ MtTables c_mt = make_mt_tables();
+
+// s_mt[kMtElems] from the constant table, thread `tid` of `nth` (as dwords)
+__device__ __forceinline__ void xf_tables(int16_t *s_mt, int tid, int nth = kWave) {
+    static_assert(kMtElems % 2 == 0, "dword copy");
+    for (int i = tid; i < kMtElems / 2; i += nth)
+        reinterpret_cast<uint32_t *>(s_mt)[i] = reinterpret_cast<const uint32_t *>(c_mt.v)[i];
 }
 
 // the transposed matrix of a TB of size 1 << log2n (DST: 4x4 luma), and its row stride
