@@ -644,6 +644,15 @@ HG_HD inline void q_refill(Lane &L, const EG &G) {
         L.lb += 16;
         L.fp = 1;
     }
+#if !defined(HG_NO_TOPUP)
+    // top the bit window up to more than 32 bits once per pass, so that inside
+    // the pass vfill's pop (the queue select and its reload branches, run by
+    // the whole wave whenever one lane needs it) is rarely reached
+    if (L.cn <= 32) {
+        L.cur |= (uint64_t)be_pop(L, G) << (32 - L.cn);
+        L.cn += 32;
+    }
+#endif
 }
 
 // value += 16 more look-ahead bits (k < 8 on entry, so k <= 23 and value < 2^32 after).
