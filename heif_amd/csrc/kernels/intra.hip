@@ -232,6 +232,9 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     w.check_blk(w.cur + ((y0 - w.cy0) * w.csx + (x0 - w.cx0)), ((size_t)(n - 1) * w.csx + n) * sizeof(Pel));
 #endif
     const int r0 = (cbf && n <= 8 && lane < n * n) ? rt[(lane >> log2n) * w.rp + (lane & (n - 1))] : 0;
+#if defined(HG_IABL_TB)  // measurement builds only (wrong pixels): the TB's work dropped
+    if (r0 != 12345) return;
+#endif
     // 1. gather neighbours in search order (8.4.4.2.2): s < 2n left column bottom-up,
     //    s == 2n corner, s > 2n top row left-to-right
 #if defined(HG_HOST_EMU)
@@ -269,6 +272,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             else L->top[s - 2 * n] = (int16_t)v;
         }
     }
+#elif defined(HG_IABL_GATHER)  // measurement builds only: no neighbour gather
 #else
     if (ns <= 64) {  // 4x4 and 8x8 TBs (most of them): one chunk of 4n + 1 <= 33 samples
         const int s = lane;
@@ -467,7 +471,10 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         pv = min(max(pv, 0), maxv);
         w.cur[li] = (Pel)pv;
     };
-#if !defined(HG_HOST_EMU)
+#if defined(HG_IABL_PRED)  // measurement builds only: no prediction
+    if (lane == 1000) predict_sample(0);
+    if (false)
+#elif !defined(HG_HOST_EMU)
     if (n <= 8) {  // one sample per lane: no loop
         if (lane < n * n) predict_sample(lane);
     } else

@@ -32,6 +32,27 @@ __constant__ uint8_t c_tc[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
 
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// t / d and t % d for 0 <= t < 2^24 and a divisor d >= 1 the wave shares, through
+// its f32 reciprocal (computed once by the caller) and one correction each way:
+// a handful of VALU instead of the ~40 of an integer division
+struct FastDiv {
+    int d;
+    float r;
+    __device__ __forceinline__ explicit FastDiv(int d_) : d(d_ > 0 ? d_ : 1), r(1.0f / (float)(d_ > 0 ? d_ : 1)) {}
+    __device__ __forceinline__ int div(int t, int &rem) const {
+        int q = (int)((float)t * r);
+        rem = t - q * d;
+        if (rem < 0) {
+            --q;
+            rem += d;
+        } else if (rem >= d) {
+            ++q;
+            rem -= d;
+        }
+        return q;
+    }
+};
+
 __device__ __forceinline__ int chroma_qp_map(int qpi, int chroma) {
     if (chroma != 1) return qpi < 51 ? qpi : 51;
     if (qpi < 30) return qpi;
@@ -172,15 +193,17 @@ __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
     const int ns_c = VERT ? ch / lc : cw / lc;
     const int nc = sp.chroma_format ? ne_c * ns_c : 0;
     const int total = nl + 2 * nc;
+    const FastDiv dl(VERT ? ne_l : ns_l), dc(nc), dce(VERT ? ne_c : ns_c);
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
         if (t < nl) {
-            int x, y;
+            int x, y, tr;
+            const int tq = dl.div(t, tr);
             if (VERT) {
-                x = 8 * (t % ne_l + 1);
-                y = 4 * (t / ne_l);
+                x = 8 * (tr + 1);
+                y = 4 * tq;
             } else {
-                x = 4 * (t % ns_l);
-                y = 8 * (t / ns_l + 1);
+                x = 4 * tr;
+                y = 8 * (tq + 1);
             }
             const int fq = flg[(y >> 2) * w4 + (x >> 2)];
             if (!(fq & (VERT ? MF_EDGE_V : MF_EDGE_H))) continue;
@@ -191,14 +214,16 @@ __global__ void __launch_bounds__(256) k_deblock(BatchArgs a) {
                               sp.bit_depth_y);
         } else {
             const int u = t - nl;
-            const int cidx = 1 + u / nc, v = u % nc;
+            int v, vr;
+            const int cidx = 1 + dc.div(u, v);
+            const int vq = dce.div(v, vr);
             int xc, yc;
             if (VERT) {
-                xc = 8 * (v % ne_c + 1);
-                yc = lc * (v / ne_c);
+                xc = 8 * (vr + 1);
+                yc = lc * vq;
             } else {
-                xc = lc * (v % ns_c);
-                yc = 8 * (v / ns_c + 1);
+                xc = lc * vr;
+                yc = 8 * (vq + 1);
             }
             const int xl = xc << sx, yl = yc << sy;
             const int fq = flg[(yl >> 2) * w4 + (xl >> 2)];
@@ -355,17 +380,17 @@ __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
     const int qw = (vw + 3) >> 2, qcw = (vcw + 3) >> 2;  // quads per row
     const int nl = qw * vh, nc = qcw * vch;
     const int total = nl + 2 * nc;
+    const FastDiv dq(qw), dn(nc), dqc(qcw);
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
         int cidx, q, y;
         if (t < nl) {
             cidx = 0;
-            q = t % qw;
-            y = t / qw;
+            y = dq.div(t, q);
         } else {
             const int u = t - nl;
-            cidx = 1 + u / nc;
-            q = (u % nc) % qcw;
-            y = (u % nc) / qcw;
+            int v;
+            cidx = 1 + dn.div(u, v);
+            y = dqc.div(v, q);
         }
         const int subx = cidx ? sx : 0, suby = cidx ? sy : 0;
         const int PW = cidx ? cw : W, PH = cidx ? ch : H;
