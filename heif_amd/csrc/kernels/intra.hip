@@ -645,7 +645,7 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
 // LDS of k_intra's streaming mode beyond the windows: the transform tables
 // (workgroup) and per wave the transform tiles (transform_tb, xform.hpp)
 // (the transposed matrices s_mt; per wave the d tile 32 x 34, the g tile 32 x 32, the extent pair)
-constexpr size_t kXfTablesBytes = kMtElems * sizeof(int16_t);
+constexpr size_t kXfTablesBytes = sizeof(XfTab);
 constexpr size_t kXfDBytes = 32 * kXfDStride32 * sizeof(int16_t), kXfGBytes = 32 * 32 * sizeof(int16_t);
 constexpr size_t kXfWaveBytes = kXfDBytes + kXfGBytes + 16;
 static_assert(kXfTablesBytes % 16 == 0 && kXfWaveBytes % 16 == 0, "transform scratch alignment");
@@ -695,8 +695,8 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
         unsigned char *tab = smem + 64 + (size_t)nw * lay.bytes;
         unsigned char *xw = tab + kXfTablesBytes + (size_t)wave * kXfWaveBytes;
         X = XfScratch{reinterpret_cast<int16_t *>(xw), reinterpret_cast<int16_t *>(xw + kXfDBytes),
-                      reinterpret_cast<int32_t *>(xw + kXfDBytes + kXfGBytes), reinterpret_cast<int16_t *>(tab)};
-        xf_tables(reinterpret_cast<int16_t *>(tab), lane);
+                      reinterpret_cast<int32_t *>(xw + kXfDBytes + kXfGBytes), reinterpret_cast<const XfTab *>(tab)};
+        xf_tables(reinterpret_cast<XfTab *>(tab), lane);
     }
     IntraScratch *S = reinterpret_cast<IntraScratch *>(blk);
     Win<Pel> win[3];

@@ -30,7 +30,13 @@ constexpr int kWaves = HG_XF_WAVES;
 
 }  // namespace
 
-__global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
+// 7 waves per SIMD (72 VGPRs, one of them spilled): the MFMA path of transform_tb
+// alone takes the kernel to 112 (4 waves); at 6 waves k_transform alone is 8.0 ms,
+// at 7 7.5 ms (A/B in DESIGN 5.11)
+#if !defined(HG_XF_WPE)
+#define HG_XF_WPE 7
+#endif
+__global__ void __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(HG_XF_WPE))) k_transform(BatchArgs a) {
     // per wave: the scaled coefficients d and the first-stage output g, both
     // clipped to 16 bits by 8.6.2 / 8.6.4.2, so int16 tiles (4 KiB per wave);
     // the 32x32 DCT matrix in LDS (lane-varying rows: LDS, not constant loads).
@@ -39,13 +45,14 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t dtile[kWaves][32 * kXfDStride32];
     HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t gtile[kWaves][32 * 32];
     HG_BLOCK_SHARED int32_t extent[kWaves][2];  // last nonzero row / column of d
-    HG_BLOCK_SHARED __attribute__((aligned(16))) int16_t s_mt[kMtElems];
-    // the workgroup's threads copy the table (the host emulation runs one thread per wave)
+    HG_BLOCK_SHARED XfTab s_tab;
+    // the workgroup's threads copy the tables (the host emulation runs one thread per wave)
 #if defined(HG_HOST_EMU)
-    xf_tables(s_mt, 0, 1);
+    xf_tables(&s_tab, 0, 1);
 #else
-    xf_tables(s_mt, (int)threadIdx.x, (int)blockDim.x);
+    xf_tables(&s_tab, (int)threadIdx.x, (int)blockDim.x);
 #endif
+    const int16_t *s_mt = s_tab.mt;
     __syncthreads();
     const int pic = a.pic0 + blockIdx.y, row = blockIdx.x;
     const PicDesc pd = a.pics[pic];
@@ -197,7 +204,7 @@ __global__ void __launch_bounds__(kWaves * 64) k_transform(BatchArgs a) {
     // Pass B: every larger TB, one per wave
     auto pass_b = [&](const TuRec &tu) {
         const int cidx = tu.flags & TU_CIDX_MASK;
-        transform_tb(tu, coefs, sp, a.sf, XfScratch{d, g, extent[wave], s_mt},
+        transform_tb(tu, coefs, sp, a.sf, XfScratch{d, g, extent[wave], &s_tab},
                      res_plane[cidx] + (size_t)tu.y * pitch[cidx] + tu.x, pitch[cidx], lane);
     };
     auto wanted = [&](const TuRec &tu) {

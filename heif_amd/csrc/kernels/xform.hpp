@@ -1,6 +1,8 @@
 // xform.hpp — scaling + inverse transform of one TB by one wave (8.6.2-8.6.4),
 // shared by k_transform (pass B) and k_intra's streaming mode, which
-// transforms each TB just before predicting it.
+// transforms each TB just before predicting it.  The two matrix stages run as
+// packed int16 dot products (4x4, 8x8 and the host emulation) or as int8
+// MFMAs on split operands (16x16, 32x32; transform_mfma), bit-exact either way.
 #pragma once
 #include "kernels.hpp"
 #include "tables.hpp"
@@ -136,45 +138,132 @@ constexpr int kMt4Dct = 8 * 10 + 16 * 18 + 32 * 34, kMt4Dst = kMt4Dct + 16;
 constexpr int kMtElems = kMt4Dst + 16;  // int16
 __device__ __forceinline__ int mt_off(int log2n) { return log2n == 3 ? 0 : (log2n == 4 ? 8 * 10 : 8 * 10 + 16 * 18); }
 
+// The workgroup's transform tables (LDS copy of c_xf, built at compile time:
+// filling them per workgroup with an integer division per entry cost
+// k_transform 7 % of its VALU): the transposed matrices of the dot products,
+// which the MFMA path's operands are packed from as well.
+struct alignas(16) XfTab {
+    int16_t mt[kMtElems];
+};
+static_assert(sizeof(XfTab) % 16 == 0 && (sizeof(int16_t) * kMtElems) % 16 == 0, "XfTab layout");
+
 // a wave's transform scratch: d (int16, 32 x 34: the transposed layout's
-// padding) and g (32x32) tiles, the extent pair, and the workgroup's matrix
-// tables (filled by xf_tables)
+// padding) and g (32x32) tiles, the extent pair, and the workgroup's tables
 struct XfScratch {
     int16_t *d, *g;
     int32_t *extent;
-    const int16_t *mt;  // kMtElems: mtT_n of n = 8, 16, 32, then the 4x4 DCT and DST
+    const XfTab *tab;
 };
 
-// the transposed tables, built at compile time (filling them per workgroup
-// with an integer division per entry cost k_transform 7 % of its VALU)
-struct alignas(16) MtTables {
-    int16_t v[kMtElems];
-};
-constexpr MtTables make_mt_tables() {
-    MtTables t{};
+constexpr XfTab make_xf_tab() {
+    XfTab t{};
     const TransMatrix m = make_matrix();
     constexpr int dst4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
     for (int i = 0; i < kMtElems; ++i) {
         if (i >= kMt4Dct) {  // 4x4: mtT[y][k] = M[k][y]
             const int k = i & 3, y = (i >> 2) & 3;
-            t.v[i] = (int16_t)(i >= kMt4Dst ? dst4[k][y] : m.m[k * 8][y]);
+            t.mt[i] = (int16_t)(i >= kMt4Dst ? dst4[k][y] : m.m[k * 8][y]);
             continue;
         }
         const int l2 = i < 80 ? 3 : (i < 80 + 288 ? 4 : 5), n = 1 << l2, sn = n + 2;
         const int k = i - (l2 == 3 ? 0 : (l2 == 4 ? 80 : 80 + 288));
         const int y = k / sn, j = k % sn;
-        t.v[i] = (int16_t)(j < n ? m.m[j << (5 - l2)][y] : 0);
+        t.mt[i] = (int16_t)(j < n ? m.m[j << (5 - l2)][y] : 0);
     }
     return t;
 }
-__constant__ MtTables c_mt = make_mt_tables();
+__constant__ XfTab c_xf = make_xf_tab();
 
-// s_mt[kMtElems] from the constant table, thread `tid` of `nth` (as dwords)
-__device__ __forceinline__ void xf_tables(int16_t *s_mt, int tid, int nth = kWave) {
-    static_assert(kMtElems % 2 == 0, "dword copy");
-    for (int i = tid; i < kMtElems / 2; i += nth)
-        reinterpret_cast<uint32_t *>(s_mt)[i] = reinterpret_cast<const uint32_t *>(c_mt.v)[i];
+// the tables from the constant copy, thread `tid` of `nth` (as dwords)
+__device__ __forceinline__ void xf_tables(XfTab *dst, int tid, int nth = kWave) {
+    for (int i = tid; i < (int)(sizeof(XfTab) / 4); i += nth)
+        reinterpret_cast<uint32_t *>(dst)[i] = reinterpret_cast<const uint32_t *>(&c_xf)[i];
 }
+
+#if !defined(HG_HOST_EMU) && !defined(HG_XF_NO_MFMA)
+// 16x16 and 32x32 TBs on the int8 MFMA (v_mfma_i32_32x32x32_i8, 16x16 zero
+// padded), bit-exact: an int16 operand v is split as v = 256 hi + lo' + 128
+// with hi = v >> 8 and lo' = (v & 255) - 128 both int8, so a product is
+// 256 (hi . B) + (lo' . B) + 128 colsum(B), the last term the accumulator's
+// start value (corr, the column sums by dot products of the packed B).  Stage 1 computes G^T = D^T M with D^T rows from the
+// transposed tile (lane = TB column x, k = 16h .. 16h + 15); its result holds
+// G[y][x] with y on the lane and x = (i & 3) + 8 (i >> 2) + 4h in register i,
+// which is stage 2's A operand (R = G M) as it stands, with B's rows permuted
+// to match (b2).  Both B operands are packed per TB from the int16 table mt
+// (mtT_n, row y = M_n[.][y] at stride sn): an LDS copy of int8 tables took
+// the workgroup below 7 per CU (A/B: 0.6 ms of k_transform).  Operand maps checked on the hardware
+// (tools/probe/mfma_i8_probe.cpp).  Four MFMAs and ~150 VALU per TB against
+// ~2,400 instructions of dot products for a 32x32 TB.
+typedef int xf_v4i __attribute__((ext_vector_type(4)));
+typedef int xf_v16i __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ int xf_hi(uint32_t w0, uint32_t w1) {
+    return (int)__builtin_amdgcn_perm(w1, w0, 0x07050301u);
+}
+__device__ __forceinline__ int xf_lo(uint32_t w0, uint32_t w1) {
+    return (int)(__builtin_amdgcn_perm(w1, w0, 0x06040200u) ^ 0x80808080u);
+}
+// four int16 values held in int32 registers to their packed high bytes / low bytes ^ 0x80
+__device__ __forceinline__ int xf_hi4(int g0, int g1, int g2, int g3) {
+    return (int)(__builtin_amdgcn_perm((uint32_t)g1, (uint32_t)g0, 0x0c0c0501u) |
+                 (__builtin_amdgcn_perm((uint32_t)g3, (uint32_t)g2, 0x0c0c0501u) << 16));
+}
+__device__ __forceinline__ int xf_lo4(int g0, int g1, int g2, int g3) {
+    return (int)((__builtin_amdgcn_perm((uint32_t)g1, (uint32_t)g0, 0x0c0c0400u) |
+                  (__builtin_amdgcn_perm((uint32_t)g3, (uint32_t)g2, 0x0c0c0400u) << 16)) ^ 0x80808080u);
+}
+// the low bytes of the int16 pairs (w0, w1): four int8 values
+__device__ __forceinline__ int xf_b8(uint32_t w0, uint32_t w1) {
+    return (int)__builtin_amdgcn_perm(w1, w0, 0x06040200u);
+}
+template <class DstPtr>
+__device__ __forceinline__ void transform_mfma(const int16_t *dT, int sn, int log2n, const int16_t *mt, DstPtr dst,
+                                               int pitch, int bd2, int lane) {
+    const int n = 1 << log2n, r = lane & 31, h = lane >> 5;
+    // lane (r, h): b1 = M[16h + jj][r], b2 = M[8q + 4h + (jj & 3)][r] in register q (zero past n)
+    const bool live = r < n, live1 = live && 16 * h < n;
+    const uint32_t *pm = reinterpret_cast<const uint32_t *>(mt + (live ? r : 0) * sn);
+    const uint32_t *pm1 = pm + (live1 ? 8 * h : 0);
+    const xf_v4i b1 = {live1 ? xf_b8(pm1[0], pm1[1]) : 0, live1 ? xf_b8(pm1[2], pm1[3]) : 0,
+                       live1 ? xf_b8(pm1[4], pm1[5]) : 0, live1 ? xf_b8(pm1[6], pm1[7]) : 0};
+    const uint32_t *pm2 = pm + 2 * h;
+    const bool live2 = live && n == 32;  // (registers 2, 3 hold k >= 16)
+    const xf_v4i b2 = {live ? xf_b8(pm2[0], pm2[1]) : 0, live ? xf_b8(pm2[4], pm2[5]) : 0,
+                       live2 ? xf_b8(pm2[8], pm2[9]) : 0, live2 ? xf_b8(pm2[12], pm2[13]) : 0};
+    // 128 colsum_r(M): this lane's 16 entries of b1 and its partner's (lane ^ 32)
+    int cs = __builtin_amdgcn_sdot4(b1.x, 0x01010101, 0, false);
+    cs = __builtin_amdgcn_sdot4(b1.y, 0x01010101, cs, false);
+    cs = __builtin_amdgcn_sdot4(b1.z, 0x01010101, cs, false);
+    cs = __builtin_amdgcn_sdot4(b1.w, 0x01010101, cs, false);
+    const int corr = 128 * (cs + __shfl_xor(cs, 32, 64));
+    const uint32_t *pa = reinterpret_cast<const uint32_t *>(dT + r * sn + 16 * h);
+    const xf_v4i ah = {xf_hi(pa[0], pa[1]), xf_hi(pa[2], pa[3]), xf_hi(pa[4], pa[5]), xf_hi(pa[6], pa[7])};
+    const xf_v4i al = {xf_lo(pa[0], pa[1]), xf_lo(pa[2], pa[3]), xf_lo(pa[4], pa[5]), xf_lo(pa[6], pa[7])};
+    // the high bytes' product, scaled and corrected, starts the low bytes' one
+    xf_v16i acc = {};
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(ah, b1, acc, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = (acc[i] << 8) + corr;
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(al, b1, acc, 0, 0, 0);
+    int g[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) g[i] = min(max((acc[i] + 64) >> 7, -32768), 32767);
+    const xf_v4i gh = {xf_hi4(g[0], g[1], g[2], g[3]), xf_hi4(g[4], g[5], g[6], g[7]),
+                       xf_hi4(g[8], g[9], g[10], g[11]), xf_hi4(g[12], g[13], g[14], g[15])};
+    const xf_v4i gl = {xf_lo4(g[0], g[1], g[2], g[3]), xf_lo4(g[4], g[5], g[6], g[7]),
+                       xf_lo4(g[8], g[9], g[10], g[11]), xf_lo4(g[12], g[13], g[14], g[15])};
+    acc = xf_v16i{};
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(gh, b2, acc, 0, 0, 0);
+    const int rnd = 1 << (bd2 - 1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = (acc[i] << 8) + corr + rnd;
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(gl, b2, acc, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int y = (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (y < n && r < n) dst[y * pitch + r] = (int16_t)min(max(acc[i] >> bd2, -32768), 32767);
+    }
+}
+#endif
 
 // the transposed matrix of a TB of size 1 << log2n (DST: 4x4 luma), and its row stride
 __device__ __forceinline__ const int16_t *mt_of(const int16_t *mt, int log2n, bool dst_tr) {
@@ -275,9 +364,19 @@ __device__ __forceinline__ void transform_tb(const TuRec &tu, const CoefSrc<Cohe
         xf_sync();
         return;
     }
+#if !defined(HG_HOST_EMU) && !defined(HG_XF_NO_MFMA)
+    // 16x16 / 32x32 on the int8 MFMA, every such TB past the DC shortcut (A/B in DESIGN
+    // 5.11, also against sparse TBs left on the dot products); the host emulation and
+    // the smaller TBs take the dot products below, which the MFMA path matches bit for bit
+    if (log2n >= 4) {
+        transform_mfma(d, sn, log2n, mt_of(X.tab->mt, log2n, false), dst, pitch, bd2, lane);
+        xf_sync();
+        return;
+    }
+#endif
     // 2. e[y][x] = sum_{j < rows} M[j][y] dT[x][j] over the nonzero columns, rounded up to a
     //    multiple of four (d is zero there, so g is too): the row pass's dots read whole quads
-    const int16_t *mt = mt_of(X.mt, log2n, dst_tr);
+    const int16_t *mt = mt_of(X.tab->mt, log2n, dst_tr);
     const int rows4 = (rows + 3) & ~3, cols4 = (cols + 3) & ~3;
     const int lc = cols4 > 4 ? 32 - __builtin_clz((unsigned)(cols4 - 1)) : 2;
     for (int o = lane; o < (n << lc); o += kWave) {
