@@ -52,11 +52,31 @@
 extern "C" __device__ int hg_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 #endif
 
+// HG_PARSE_TU (library build, Makefile): 1 compiles the lanes / rows kernels and
+// launch_parse, 2 (kernels/parse_solo.hip) the solo / spread kernels, so each
+// translation unit gets its own code-generation flags; unset, everything (the
+// host emulation and the counter builds)
+#if defined(HG_PARSE_TU) && HG_PARSE_TU != 1 && HG_PARSE_TU != 2
+#error "HG_PARSE_TU is 1 or 2"
+#endif
+#if !defined(HG_PARSE_TU) || HG_PARSE_TU == 1
+#define HG_PARSE_WANT_LANES 1
+#else
+#define HG_PARSE_WANT_LANES 0
+#endif
+#if !defined(HG_PARSE_TU) || HG_PARSE_TU == 2
+#define HG_PARSE_WANT_SOLO 1
+#else
+#define HG_PARSE_WANT_SOLO 0
+#endif
+
 namespace hg {
 
+namespace {
 __constant__ uint8_t c_lps_l[256] = {HG_LPS_TABLE};
 __constant__ uint8_t c_trans_l[64] = {HG_TRANS_LPS};
 __constant__ uint8_t c_ctx_init_l[CTX_NUM] = {HG_CTX_INIT_VALUES};
+}  // namespace
 #if defined(HG_PARSE_PROF) && !defined(HG_HOST_EMU)
 // s_memtime cycles per wave: [0] kernel, [1] passes, [2..6] unit kinds CTU, tree (CQT+CU+TT), TB, SB,
 // CTU_END; [7] units run (lanes x unit executions) (tuning build only; heifgpu_debug_counters slots 8..15)
@@ -363,7 +383,7 @@ __device__ __forceinline__ int uni32(int v) { return __builtin_amdgcn_readfirstl
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
     return (uint64_t)uni32((uint32_t)v) | ((uint64_t)uni32((uint32_t)(v >> 32)) << 32);
 }
-__device__ __forceinline__ void uni_state(Lane &L) {
+[[maybe_unused]] __device__ __forceinline__ void uni_state(Lane &L) {
 #define HG_U(f) L.f = uni32(L.f)
 #if defined(HG_SOLO_UNI_ALL)  // A/B only: r04's list, every field (134 SGPRs spilled into VGPR lanes)
     HG_U(range); HG_U(value); HG_U(k); HG_U(cn); HG_U(lb); HG_U(budget); HG_U(status); HG_U(st); HG_U(fl);
@@ -835,7 +855,7 @@ HG_HD inline int dec(Lane &L, const EG &G, int ci) {
 }
 
 // A/B switch (HG_SB_GENERIC): the 9-slot sig_coeff_flag loop for every TB size
-HG_HD constexpr bool sb_generic_loop() {
+[[maybe_unused]] HG_HD constexpr bool sb_generic_loop() {
 #if defined(HG_SB_GENERIC)
     return true;
 #else
@@ -2257,6 +2277,7 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
 
 }  // namespace
 
+#if HG_PARSE_WANT_LANES  // (the host-side choices live in the lanes translation unit)
 // Wave slot -> picture.  A wave runs until its heaviest picture is parsed,
 // and every extra busy picture in it adds divergent units to each pass, so
 // the critical path is the wave holding the most work.  Pictures are sorted
@@ -2395,6 +2416,7 @@ int rows_parse_order(const PicDesc *pics, int n, int lanes, std::vector<uint32_t
     std::copy(by_size.begin(), by_size.end(), order.begin());
     return groups;
 }
+#endif  // HG_PARSE_WANT_LANES
 
 #if defined(HG_HOST_EMU)
 // one wave at a time, one unit per live lane per pass, lanes in order
@@ -2630,7 +2652,20 @@ inline size_t lanes_lds_bytes(int ppw, int lane_rows, bool ring) {
            kLaneTablesBytes + (ring ? 64 * (size_t)CTX_PAD : 0);
 }
 
-#if defined(HG_PARSE_WPE)
+// the job counter: lane 0 takes the next number, the wave shares it
+__device__ __forceinline__ uint32_t dequeue_job(uint32_t *ctr) {
+    uint32_t j = 0;
+    if (__lane_id() == 0) j = atomicAdd(ctr, 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+}
+
+#if HG_PARSE_WANT_LANES
+// a register budget of 256 (2 waves per SIMD, the occupancy the VGPR floor
+// below fixes anyway); 0 leaves it to the compiler
+#if !defined(HG_PARSE_WPE)
+#define HG_PARSE_WPE 2
+#endif
+#if HG_PARSE_WPE > 0
 #define HG_PARSE_ATTR __attribute__((amdgpu_waves_per_eu(HG_PARSE_WPE)))
 #else
 #define HG_PARSE_ATTR
@@ -2651,6 +2686,12 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     // the parse is the latency-critical stream: win issue arbitration against
     // the reconstruction kernels of the previous decode sharing the SIMD
     __builtin_amdgcn_s_setprio(HG_PARSE_SETPRIO);
+#endif
+#if !defined(HG_PARSE_NO_VGPR_FLOOR)
+    // at least 176 VGPRs, so at most 2 parse waves per SIMD whatever the allocator
+    // needs: at <= 168 a SIMD takes 3, the reconstruction kernels beside them find no
+    // room and the step loses 7 % (A/B in DESIGN 5.11)
+    asm volatile("" ::: "v175");
 #endif
     for (int i = lane; i < kTabRows; i += 64) s_tab[i] = state_row_ctx(i);
     if (lane < 15) s_seq[lane] = sig_seq(lane);
@@ -2735,13 +2776,6 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
 // so it is held by a wave that is already running, whatever order the
 // hardware dispatches the workgroups in.
 inline size_t rows_lds_bytes() { return lane_blocks_bytes(64) + sizeof(LanePic) * 64 + kLaneTablesBytes; }
-
-// the job counter: lane 0 takes the next number, the wave shares it
-__device__ __forceinline__ uint32_t dequeue_job(uint32_t *ctr) {
-    uint32_t j = 0;
-    if (__lane_id() == 0) j = atomicAdd(ctr, 1u);
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
-}
 
 __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_rows(BatchArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2830,6 +2864,9 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_rows(BatchArgs a) {
 // progress words and the row-to-row context copies are in the workgroup's
 // LDS, so the 2-CTU lag needs no memory traffic; waves waiting for the row
 // above sleep.
+#endif  // HG_PARSE_WANT_LANES
+
+#if HG_PARSE_WANT_SOLO
 inline size_t solo_lds_bytes(int nw, bool ring) {
     return lane_blocks_bytes(nw) + sizeof(LanePic) + 64 * sizeof(uint32_t) + 16 * sizeof(uint64_t) +
            (ring ? (size_t)nw * CTX_PAD : 0);
@@ -2983,9 +3020,8 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
 #endif
 }
 
-hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
-    BatchArgs a = a0;
-    if (a.lane_rows < 1 || a.lane_rows > 64) return hipErrorInvalidValue;
+// the solo and spread modes (launch_parse)
+hipError_t launch_parse_solo(const BatchArgs &a, hipStream_t s) {
     if (a.parse_mode == PARSE_SOLO) {
         if (a.solo_waves < 1 || a.solo_waves > kSoloMaxWaves) return hipErrorInvalidValue;
         const int n = a.parse_order ? a.n_slots : a.n_pics;
@@ -2994,13 +3030,21 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
                            solo_lds_bytes(a.solo_waves, a.wpp_ring != 0), s, a);
         return hipGetLastError();
     }
-    if (a.parse_mode == PARSE_SPREAD) {
-        if (!a.parse_order || !a.xprog || !a.xctx || !a.xjob) return hipErrorInvalidValue;
-        if (a.n_slots <= 0) return hipSuccess;
-        // (the progress words start at 0: k_rbsp of this decode cleared them)
-        hipLaunchKernelGGL(k_parse_solo<true>, dim3(a.n_slots), dim3(64), solo_lds_bytes(1, false), s, a);
-        return hipGetLastError();
-    }
+    if (!a.parse_order || !a.xprog || !a.xctx || !a.xjob) return hipErrorInvalidValue;
+    if (a.n_slots <= 0) return hipSuccess;
+    // (the progress words start at 0: k_rbsp of this decode cleared them)
+    hipLaunchKernelGGL(k_parse_solo<true>, dim3(a.n_slots), dim3(64), solo_lds_bytes(1, false), s, a);
+    return hipGetLastError();
+}
+#endif  // HG_PARSE_WANT_SOLO
+
+#if HG_PARSE_WANT_LANES
+hipError_t launch_parse_solo(const BatchArgs &a, hipStream_t s);
+
+hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
+    BatchArgs a = a0;
+    if (a.lane_rows < 1 || a.lane_rows > 64) return hipErrorInvalidValue;
+    if (a.parse_mode == PARSE_SOLO || a.parse_mode == PARSE_SPREAD) return launch_parse_solo(a, s);
     if (a.parse_mode == PARSE_ROWS) {
         if (!a.parse_order || !a.xprog || !a.xctx || !a.xjob || a.parse_group < 1 || a.rows_lanes < 1 ||
             a.rows_lanes > 64)
@@ -3018,11 +3062,12 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
     hipLaunchKernelGGL(k_parse_lanes, dim3(waves), dim3(64), lanes_lds_bytes(ppw, a.lane_rows, a.wpp_ring != 0), s, a);
     return hipGetLastError();
 }
+#endif  // HG_PARSE_WANT_LANES
 #endif
 
 }  // namespace hg
 
-#if !defined(HG_HOST_EMU)
+#if !defined(HG_HOST_EMU) && HG_PARSE_WANT_LANES
 // Tuning hook (include/heifgpu.h): copies out and zeroes k_parse_lanes'
 // per-wave s_memtime counters.  Returns the number of counters written, or 0
 // for the product library (counters compiled out; `make prof` has them).
