@@ -364,7 +364,7 @@ def main():
     ap.add_argument("--split", choices=["images", "tiles"], default="images",
                     help="images: each rank its own shard (weak); tiles: every rank the same images, "
                          "tiles k %% world == rank (strong)")
-    ap.add_argument("--parse", choices=["auto", "lanes", "solo", "spread", "rows"], default="auto",
+    ap.add_argument("--parse", choices=["auto", "lanes", "solo", "spread"], default="auto",
                     help="CABAC parse mode (auto: solo for small batches, lanes otherwise)")
     ap.add_argument("--ppw", type=int, default=0, help="lanes mode: pictures per wave (0 = adaptive)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-parse + upload + decode leg")
@@ -552,7 +552,7 @@ def main():
         launch_bytes = args.batch * algo_per_image * len(range(offset, info.num_tiles, stride)) // info.num_tiles
         achieved = launch_bytes / (parse_ms / 1e3) / 1e9
         geom = batch.parse_geometry()
-        kname = {"solo": "k_parse_solo<false>", "spread": "k_parse_solo<true>", "rows": "k_parse_rows"}.get(
+        kname = {"solo": "k_parse_solo<false>", "spread": "k_parse_solo<true>"}.get(
             geom["mode"], "k_parse_lanes")
         # counter evidence of this round (profiles/<round>/, written by tools/pmc_*.sh on the same
         # command): HBM bytes per launch (FETCH_SIZE / WRITE_SIZE passes) and the parse's SQ counters

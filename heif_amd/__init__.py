@@ -338,8 +338,7 @@ class DeviceBatch:
         """The CABAC parse launch of this batch (heifgpu_batch_parse_geometry)."""
         v = [ctypes.c_uint32() for _ in range(4)]
         _lib.check(lib.heifgpu_batch_parse_geometry(self._h, *[ctypes.byref(x) for x in v]))
-        mode = {_lib.PARSE_LANES: "lanes", _lib.PARSE_SOLO: "solo", _lib.PARSE_SPREAD: "spread",
-                _lib.PARSE_ROWS: "rows"}[v[0].value]
+        mode = {_lib.PARSE_LANES: "lanes", _lib.PARSE_SOLO: "solo", _lib.PARSE_SPREAD: "spread"}[v[0].value]
         return {"mode": mode, "workgroups": v[1].value, "pics_per_wave": v[2].value,
                 "waves_per_workgroup": v[3].value}
 

@@ -121,9 +121,10 @@ class IpcHandle(ctypes.Structure):
     _fields_ = [("handle", ctypes.c_uint8 * 64), ("offset", ctypes.c_uint64)]
 
 
-PARSE_AUTO, PARSE_LANES, PARSE_SOLO, PARSE_SPREAD, PARSE_ROWS = 0, 1, 2, 3, 4
-PARSE_MODES = {"auto": PARSE_AUTO, "lanes": PARSE_LANES, "solo": PARSE_SOLO, "spread": PARSE_SPREAD,
-               "rows": PARSE_ROWS}
+PARSE_AUTO, PARSE_LANES, PARSE_SOLO, PARSE_SPREAD = 0, 1, 2, 3
+PARSE_ROWS = 4  # ABI 5 only; removed in ABI 6 (prepare answers HEIFGPU_E_UNSUPPORTED)
+PARSE_MODES = {"auto": PARSE_AUTO, "lanes": PARSE_LANES, "solo": PARSE_SOLO, "spread": PARSE_SPREAD}
+ABI_VERSION = 6  # HEIFGPU_ABI_VERSION of include/heifgpu.h these declarations follow
 
 
 # every symbol include/heifgpu.h declares (checked by tests/test_abi.py)
@@ -212,6 +213,10 @@ def _load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # the structs above follow ABI_VERSION: a library of another version must not be called
+    got = lib.heifgpu_abi_version()
+    if got != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: library ABI {got}, these bindings expect {ABI_VERSION} (rebuild it)")
     return lib
 
 

@@ -31,7 +31,7 @@ static_assert(sizeof(heifgpu_planes) == 40, "heifgpu_planes: 3 pointers + 3 int3
 static_assert(sizeof(heifgpu_batch_opts) == 20, "heifgpu_batch_opts: 5 x uint32");
 static_assert(sizeof(heifgpu_ipc_handle) == 72, "heifgpu_ipc_handle: 64-byte HIP handle + uint64 offset");
 static_assert(HEIFGPU_PARSE_AUTO == PARSE_AUTO && HEIFGPU_PARSE_LANES == PARSE_LANES && HEIFGPU_PARSE_SOLO == PARSE_SOLO &&
-                  HEIFGPU_PARSE_SPREAD == PARSE_SPREAD && HEIFGPU_PARSE_ROWS == PARSE_ROWS,
+                  HEIFGPU_PARSE_SPREAD == PARSE_SPREAD,
               "parse modes");
 static_assert(sizeof(heifgpu_tile_params) == 55 * 4 + 64 * 4, "heifgpu_tile_params: 55 int32 + 64 uint32");
 
@@ -110,6 +110,14 @@ thread_local std::string g_err;
 int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
+}
+
+// Test hook: HEIFGPU_FAULT_INJECT names a failure to inject ("prepare": a
+// reload fails after it has begun to overwrite its descriptor generation).
+// Read at every call, so one test process can switch it on and off.
+bool fault_injected(const char *what) {
+    const char *e = std::getenv("HEIFGPU_FAULT_INJECT");
+    return e && std::strcmp(e, what) == 0;
 }
 
 #define HIP_TRY(expr)                                                                             \
@@ -559,6 +567,8 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     if (offset >= stride) return fail(HEIFGPU_E_INVALID, "tile_offset must be below tile_stride");
     const uint32_t mode_req = opts ? opts->parse_mode : 0u;
     if (mode_req > HEIFGPU_PARSE_ROWS) return fail(HEIFGPU_E_INVALID, "parse_mode");
+    if (mode_req == HEIFGPU_PARSE_ROWS)
+        return fail(HEIFGPU_E_UNSUPPORTED, "HEIFGPU_PARSE_ROWS was removed in ABI 6 (DESIGN.md 5.9)");
     const int ppw_req = opts ? int(std::min<uint32_t>(opts->pics_per_wave, 64u)) : 0;
     if (*inout && (*inout)->device != ctx->device) return fail(HEIFGPU_E_INVALID, "batch belongs to another device");
     HIP_TRY(hipSetDevice(ctx->device));
@@ -611,8 +621,12 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     // not for the in-flight decodes' transform and reconstruction, which read
     // only their parse set, the other generation and the sample arena (that
     // one is ordered by the recon stream).
-    if (b->loaded) HIP_TRY(hipEventSynchronize(b->uploaded));
-    const int gi = b->loaded ? b->cur ^ 1 : b->cur;
+    // (unconditionally: a reload that failed may have issued copies from staging)
+    HIP_TRY(hipEventSynchronize(b->uploaded));
+    // The generation the last successful load did not use (not the
+    // one of b->loaded, which a failed reload clears while gen[cur] still holds
+    // the last good load, its in-flight decodes and their sticky status)
+    const int gi = b->gen[b->cur].loaded ? b->cur ^ 1 : b->cur;
     DescGen &G = b->gen[gi];
     for (int k = 0; k < b->n_sets; ++k)
         if (b->set[k].pending) HIP_TRY(hipStreamWaitEvent(ctx->upload, b->set[k].parsed, 0));
@@ -620,20 +634,17 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     std::vector<uint32_t> order;
     const int mode = parse_mode_for(int(mode_req), int(hb.pics.size()));
     const int solo_waves = solo_waves_for(hb.lane_rows);
-    int parse_group = 1, rows_lanes = 64;
+    int parse_group = 1;
     if (mode == PARSE_SPREAD) {
         if (spread_parse_order(hb.pics.data(), int(hb.pics.size()), order) < 0)
             return fail(HEIFGPU_E_UNSUPPORTED, "spread parse: over 2^20 pictures or 4096 substreams per picture");
-    } else if (mode == PARSE_ROWS) {
-        rows_lanes = rows_lanes_for(int(hb.pics.size()));
-        parse_group = rows_parse_order(hb.pics.data(), int(hb.pics.size()), rows_lanes, order);
     } else {  // pictures dealt by payload size (r03: dealing by WPP critical path lost, 16.9 vs 17.0 Gpix/s)
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows,
-                                        mode == PARSE_SOLO ? 1 : ppw_req, order);
+                                        mode == PARSE_SOLO ? 1 : ppw_req, order, hb.subs.data(), hb.seqs.data());
     }
-    // spread and rows parses: WPP neighbours in other waves (progress words,
+    // spread parse: WPP neighbours in other waves (progress words,
     // context hand-off blocks, the job counter after the progress words)
-    const bool cross_rows = mode == PARSE_SPREAD || mode == PARSE_ROWS;
+    const bool cross_rows = mode == PARSE_SPREAD;
     const bool grows = (order.size() > b->porder.cap || hb.bits_size > b->bits.cap || hb.bits_size > b->set[0].rbsp.cap || hb.pics.size() > G.pics.cap ||
                                      hb.subs.size() > b->subs.cap || hb.seqs.size() > G.seqs.cap ||
                                      hb.sf.size() > G.sf.cap || n > G.outs.cap || hb.recon_bytes > b->recon.cap ||
@@ -651,6 +662,11 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     // A failure from here on leaves the batch unusable until a reload succeeds
     // (its arguments may point at freed arenas): `loaded` is set again last.
     b->loaded = false;
+    G.loaded = false;  // its previous contents (two loads back) are overwritten from here on
+    G.pic_image.clear();
+    G.n_images = 0;
+    if (fault_injected("prepare"))  // test hook: a reload that fails after touching the generation
+        return fail(HEIFGPU_E_INVALID, "injected prepare failure (HEIFGPU_FAULT_INJECT=prepare)");
     // ---- device arenas (reused when large enough)
     HIP_TRY(b->bits.alloc(hb.bits_size));
     HIP_TRY(G.pics.alloc(hb.pics.size()));
@@ -750,7 +766,6 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
     a.parse_order = b->porder.p;
     a.n_slots = int(order.size());
     a.parse_group = parse_group;
-    a.rows_lanes = rows_lanes;
     a.seqs = G.seqs.p;
     a.sf = G.sf.p;
     a.outs = G.outs.p;
@@ -828,7 +843,7 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     a.resid = ps.resid.p;
     a.rbsp = ps.rbsp.p;
     a.rsubs = ps.rsubs.p;
-    if (a.parse_mode == PARSE_SPREAD || a.parse_mode == PARSE_ROWS) {
+    if (a.parse_mode == PARSE_SPREAD) {
         a.xprog = ps.xprog.p;
         a.xjob = ps.xprog.p + a.total_rows;
         a.xntu = a.intra_stream ? ps.xntu.p : nullptr;
@@ -952,10 +967,10 @@ int heifgpu_batch_parse_geometry(const heifgpu_batch *b, uint32_t *mode, uint32_
                                  uint32_t *pics_per_wave, uint32_t *waves_per_workgroup) {
     if (!b || !b->loaded) return fail(HEIFGPU_E_INVALID, "invalid batch");
     const BatchArgs &a = b->args;
-    const bool solo = a.parse_mode == PARSE_SOLO, lanes = a.parse_mode == PARSE_LANES, rows = a.parse_mode == PARSE_ROWS;
-    const uint32_t ppw = lanes ? uint32_t(std::max(1, a.parse_group)) : rows ? uint32_t(a.rows_lanes) : 1u;
+    const bool solo = a.parse_mode == PARSE_SOLO, lanes = a.parse_mode == PARSE_LANES;
+    const uint32_t ppw = lanes ? uint32_t(std::max(1, a.parse_group)) : 1u;
     if (mode) *mode = uint32_t(a.parse_mode);
-    if (workgroups) *workgroups = rows ? uint32_t(a.parse_group) * uint32_t(a.max_rows) : (uint32_t(a.n_slots) + ppw - 1) / ppw;
+    if (workgroups) *workgroups = (uint32_t(a.n_slots) + ppw - 1) / ppw;
     if (pics_per_wave) *pics_per_wave = ppw;
     if (waves_per_workgroup) *waves_per_workgroup = solo ? uint32_t(a.solo_waves) : 1u;
     return HEIFGPU_OK;

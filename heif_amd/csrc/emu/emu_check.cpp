@@ -76,17 +76,14 @@ int main(int argc, char **argv) {
     const int solo_waves = solo_waves_for(hb.lane_rows);
     int parse_group = 1;
     if (mode == PARSE_SPREAD) spread_parse_order(hb.pics.data(), int(hb.pics.size()), order);
-    else if (mode == PARSE_ROWS)
-        parse_group = rows_parse_order(hb.pics.data(), int(hb.pics.size()), rows_lanes_for(int(hb.pics.size())), order);
     else
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows, mode == PARSE_SOLO ? 1 : 0,
-                                        order);
+                                        order, hb.subs.data(), hb.seqs.data());
     std::vector<uint32_t> xprog(hb.rows + 1), xntu(hb.rows + hb.pics.size() + 1, 0);  // (+ the job counter)
     std::vector<uint8_t> xctx((hb.rows + 1) * size_t(CTX_PAD));
     a.parse_order = order.data();
     a.n_slots = int(order.size());
     a.parse_group = parse_group;
-    a.rows_lanes = rows_lanes_for(int(hb.pics.size()));
     a.seqs = hb.seqs.data();
     a.sf = hb.sf.data();
     a.outs = &out;
@@ -153,7 +150,6 @@ int main(int argc, char **argv) {
     }
     printf("parse mode: %s\n", mode == PARSE_SOLO     ? "solo"
                                : mode == PARSE_SPREAD ? "spread"
-                               : mode == PARSE_ROWS   ? "rows"
                                                       : "lanes");
     printf("parse: status 0x%x, %llu TBs, %llu coefficients\n", st, (unsigned long long)ntu, (unsigned long long)ncoef);
     if (stages >= 2 && !a.intra_stream) emu_transform(a);  // (streaming: k_intra_stream transforms each TB)

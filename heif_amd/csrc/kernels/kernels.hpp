@@ -50,9 +50,7 @@ struct BatchArgs {
     int total_rows;            // sum of CTB rows over pictures
     int bytes_per_sample;      // 1 or 2
     int chroma_format;         // chroma_format_idc, shared by the batch's pictures
-    int parse_group;           // k_parse_lanes pictures per wave (lanes_parse_order's choice; launch_parse otherwise);
-                               // k_parse_rows: groups (row waves per CTB row)
-    int rows_lanes;            // k_parse_rows: pictures per group (lanes of a row wave, <= 64)
+    int parse_group;           // k_parse_lanes pictures per wave (lanes_parse_order's choice; launch_parse otherwise)
     int max_log2ctb;           // largest CTB size in the batch (sizes k_intra's LDS)
     int lane_rows;             // k_parse_lanes lanes per picture: max over pictures of (WPP ? min(rows, 64) : 1)
     int wpp_ring;              // some WPP picture has more CTB rows than lanes (its rows wrap round its lanes)
@@ -61,7 +59,7 @@ struct BatchArgs {
     uint32_t *xprog;           // spread mode: per-row WPP progress words (total_rows)
     uint8_t *xctx;             // spread mode: per-row context hand-off blocks (total_rows * CTX_PAD)
     uint32_t *xntu;            // streaming mode: per-row TU records written so far (null otherwise)
-    uint32_t *xjob;            // spread / rows parse: the job counter each workgroup dequeues its substream job from
+    uint32_t *xjob;            // spread parse: the job counter each workgroup dequeues its substream job from
     int intra_stream;          // k_intra transforms and reconstructs each row behind the spread parse (same launch window)
     int stream_redo;           // k_intra_stream's second launch (after the parse): the pictures the first gave up on
     uint32_t stream_patience_us;  // first launch: give a picture up after this long without parse progress (0: at once)
@@ -108,14 +106,17 @@ inline void color_coefs(uint32_t matrix, bool full, ColorArgs &c) {
 }
 
 // parse modes (BatchArgs::parse_mode; heifgpu_batch_opts::parse_mode)
-enum : int { PARSE_AUTO = 0, PARSE_LANES = 1, PARSE_SOLO = 2, PARSE_SPREAD = 3, PARSE_ROWS = 4 };
+// (4 was r05's row waves, HEIFGPU_PARSE_ROWS: removed in ABI 6, prepare answers HEIFGPU_E_UNSUPPORTED)
+enum : int { PARSE_AUTO = 0, PARSE_LANES = 1, PARSE_SOLO = 2, PARSE_SPREAD = 3 };
 constexpr int kSoloMaxWaves = 16;
 // host: BatchArgs::parse_order for a batch (size-balanced k_parse_lanes waves,
 // or for solo mode with ppw_force = 1 one picture per workgroup, heaviest
 // first); returns the pictures per wave it dealt for (BatchArgs::parse_group).
 // ppw_force = 0: the adaptive choice.
-// cost (optional): per-picture parse cost to deal by (default: payload bytes)
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order);
+// subs / seqs (optional): the substream table and sequences, for dealing by
+// each picture's WPP critical path (HEIFGPU_LANES_DEAL=chain)
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
+                      const uint32_t *subs = nullptr, const SeqParams *seqs = nullptr);
 // k_intra_stream (reconstruction behind the spread parse, k_transform folded in) for this batch
 // (same box, spread, one-decode latency: 4 images 28.3 vs 33.7 ms streamed; 8
 // images 44.4 vs 40.5, the reconstruction no longer keeps up with the parse)
@@ -131,11 +132,6 @@ bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly, const Strea
 int parse_mode_for(int requested, int n_pics);
 // spread mode's wave slots (row << 20 | picture); -1 if the batch exceeds the encoding
 int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order);
-// rows mode (k_parse_rows): groups of `lanes` (rows_lanes_for) pictures by payload size,
-// slot g * lanes + lane (~0u: empty); returns the number of groups (BatchArgs::parse_group)
-int rows_parse_order(const PicDesc *pics, int n, int lanes, std::vector<uint32_t> &order);
-// pictures per k_parse_rows group (HEIFGPU_ROWS_LANES, default 64)
-int rows_lanes_for(int n_pics);
 int solo_waves_for(int lane_rows);
 
 #if defined(HG_HOST_EMU)

@@ -119,12 +119,7 @@ HG_HD inline uint64_t state_row_ctx(int s) {
 }
 
 constexpr uint32_t kProgDone = 0x7fffffffu;
-// Parse waves at the highest issue priority (s_setprio 3; 0 turns it off).
-// Same-box pairs, r04: 128 images 83.5-83.8 vs 84.4 ms per step, one image
-// 27.8 vs 28.05 ms
-#if !defined(HG_PARSE_SETPRIO)
-#define HG_PARSE_SETPRIO 3
-#endif
+// (parse waves at issue priority HG_PARSE_SETPRIO: wave.hpp)
 // LanePic.flags bit above the SP_ flags: k_intra_stream reads this picture's TU
 // and coefficient records while the parse writes them (agent-scope stores)
 constexpr uint32_t PF_COHERENT = 1u << 31;
@@ -250,14 +245,13 @@ struct Lane {
 // bytes of n lane blocks, rounded up so the LanePic after them stays 16-byte aligned
 HG_HD inline size_t lane_blocks_bytes(int n) { return (sizeof(LaneLds) * (size_t)n + 15) & ~(size_t)15; }
 
-// engine context of one lane (lanes mode: every lane its own substream).
-// Spread = true: the row waves of k_parse_rows, whose WPP neighbours are other
-// waves (progress, context hand-off, SAO and depth lines through coherent
-// global memory, as in spread mode)
-template <bool Spread>
-struct EngLanesT {
+// engine context of one lane (lanes mode: every lane its own substream; a
+// picture's WPP rows are lanes of one wave, so no hand-off leaves the wave).
+// (r05's row waves, k_parse_rows, were this engine with spread mode's
+// hand-offs; removed in r06, their A/B record is DESIGN 5.9)
+struct Eng {
     static constexpr bool kSolo = false;
-    static constexpr bool kSpread = Spread;
+    static constexpr bool kSpread = false;
     static constexpr bool kCtxReg = false;  // contexts in LDS (ctx)
     static constexpr bool kRowCtx = true;
     uint8_t *ctx;
@@ -274,8 +268,6 @@ struct EngLanesT {
     HG_HD int scan8(int scan, int i) const { return sp8 && scan == 0 ? sp8[i] : kScanPos[3][scan][i]; }
     HG_HD int scan8_inv(int scan, int r) const { return inv8 && scan == 0 ? inv8[r] : kScanInv[3][scan][r]; }
 };
-using Eng = EngLanesT<false>;
-using EngRows = EngLanesT<true>;
 
 // Solo mode (k_parse_solo): one substream per WAVE, run by its lane 0 alone,
 // so the engine state is wave-uniform.  The state rows live in two VGPRs
@@ -310,7 +302,9 @@ struct EngSoloT {
     static constexpr bool kSolo = true;
     static constexpr bool kRowCtx = false;  // rows per pStateIdx (tlo / thi)
     // one wave per workgroup: the rows of a picture on different CUs, their
-    // WPP progress, context hand-off, SAO and depth lines in coherent global memory
+    // WPP progress, context hand-off, SAO and depth lines in coherent global
+    // memory.  Rule: hand-off data goes out only through store_agent, so the
+    // progress word needs vmcnt(0) only, not an L2 write-back (unit_ctu_end)
     static constexpr bool kSpread = Spread;
 #if defined(HG_HOST_EMU)
     static constexpr bool kCtxReg = false;  // one lane per wave: contexts stay in the LDS block
@@ -2093,6 +2087,11 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
             HG_REL_AGENT();
             store_agent(E.a->xntu + P.row_off + L.row, L.ntu);
         }
+        // The rule that makes vmcnt(0) enough here: every word the row below
+        // reads after this progress word (the context hand-off, SAO parameters,
+        // the depth line) went out above as an agent-scope store (store_agent,
+        // coherent at L2 across XCDs), so completing them orders them.  A plain
+        // store into hand-off data would need HG_REL_AGENT() (L2 write-back) here.
         stores_done();
         store_agent(prog_word(E, P, L.row), pv);
     } else {
@@ -2278,18 +2277,50 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
 }  // namespace
 
 #if HG_PARSE_WANT_LANES  // (the host-side choices live in the lanes translation unit)
+// WPP critical path of a picture in payload bytes: row r's bytes (from the
+// entry points) spread evenly over its CTUs; CTU (r, c) starts after (r, c - 1)
+// and after (r - 1, c), or (r - 1, 1) at c = 0 (the context hand-off after CTU
+// 1, 9.3.1).  Without WPP the picture is one substream: its bytes.
+double wpp_chain_bytes(const PicDesc &pd, const uint32_t *subs, int wctb) {
+    const int R = (int)pd.n_sub;
+    if (R <= 1 || wctb <= 0) return (double)pd.bits_len;
+    std::vector<double> done((size_t)wctb, 0.0);  // finish time of CTU c in the row above
+    for (int r = 0; r < R; ++r) {
+        const uint32_t b0 = subs[pd.sub_first + r] & SUB_OFFSET;
+        const uint32_t b1 = r + 1 < R ? subs[pd.sub_first + r + 1] & SUB_OFFSET : pd.bits_len;
+        const double w = (double)(b1 > b0 ? b1 - b0 : 0u) / wctb;
+        double t = 0.0;
+        for (int c = 0; c < wctb; ++c) {
+            const double above = r == 0 ? 0.0 : done[(size_t)(c == 0 ? std::min(1, wctb - 1) : c)];
+            t = std::max(t, above) + w;
+            done[(size_t)c] = t;
+        }
+    }
+    return done[(size_t)wctb - 1];
+}
+
 // Wave slot -> picture.  A wave runs until its heaviest picture is parsed,
 // and every extra busy picture in it adds divergent units to each pass, so
 // the critical path is the wave holding the most work.  Pictures are sorted
 // by payload size and dealt snake-wise (wave w of W gets ranks w, 2W-1-w,
 // 2W+w, 4W-1-w, ...): heavy beside light.  Empty slots are ~0u.
 // HEIFGPU_PARSE_ORDER=0: batch order (kept for the emulation test of an
-// unsorted dealing).
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order) {
+// unsorted dealing).  HEIFGPU_LANES_DEAL (read at every prepare; tuning):
+// "chain" sorts by wpp_chain_bytes instead of payload bytes (needs subs and
+// seqs), "light" / "chain_light" give wave w of the W leads (ranks 0..W-1)
+// the lightest remaining pictures in order (the heaviest lead the two
+// lightest), so the waves that set the kernel time carry the fewest busy
+// companions.
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
+                      const uint32_t *subs, const SeqParams *seqs) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
         return e ? std::atoi(e) : 1;
     }();
+    const char *deal_env = std::getenv("HEIFGPU_LANES_DEAL");
+    const std::string deal = deal_env ? deal_env : "";
+    const bool by_chain = (deal == "chain" || deal == "chain_light") && subs && seqs;
+    const bool light = deal == "light" || deal == "chain_light";
     const int full = 64 / (lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows));
     const int ppw = ppw_force > 0 ? std::min(ppw_force, full) : lanes_pics_per_wave(lane_rows, n);
     if (!on || n <= 0) {
@@ -2302,10 +2333,34 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
     for (int i = 0; i < n; ++i)
         if (!(pics[i].flags & PD_ASSEMBLY)) by_size.push_back((uint32_t)i);
     n = (int)by_size.size();
-    std::stable_sort(by_size.begin(), by_size.end(),
-                     [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
+    std::vector<double> cost((size_t)(by_chain ? n : 0));
+    if (by_chain) {
+        for (int i = 0; i < n; ++i) {
+            const PicDesc &pd = pics[by_size[(size_t)i]];
+            const SeqParams &sp = seqs[pd.seq];
+            const int ctb = 1 << sp.log2_ctb;
+            cost[(size_t)i] = (sp.flags & SP_WPP) ? wpp_chain_bytes(pd, subs, (sp.width + ctb - 1) >> sp.log2_ctb)
+                                                  : (double)pd.bits_len;
+        }
+        std::vector<size_t> idx((size_t)n);
+        for (int i = 0; i < n; ++i) idx[(size_t)i] = (size_t)i;
+        std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return cost[x] > cost[y]; });
+        std::vector<uint32_t> t((size_t)n);
+        for (int i = 0; i < n; ++i) t[(size_t)i] = by_size[idx[(size_t)i]];
+        by_size.swap(t);
+    } else {
+        std::stable_sort(by_size.begin(), by_size.end(),
+                         [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
+    }
     const int W = (n + ppw - 1) / ppw;
     order.assign((size_t)W * ppw, ~0u);
+    if (light) {
+        for (int w = 0; w < W && w < n; ++w) order[(size_t)w * ppw] = by_size[(size_t)w];
+        int r = n - 1;  // the lightest remaining picture
+        for (int w = 0; w < W; ++w)
+            for (int k = 1; k < ppw && r >= W; ++k) order[(size_t)w * ppw + k] = by_size[(size_t)r--];
+        return ppw;
+    }
     for (int r = 0; r < n; ++r) {
         const int band = r / W, pos = r % W;
         const int w = (band & 1) ? W - 1 - pos : pos;
@@ -2332,7 +2387,6 @@ int parse_mode_for(int requested, int n_pics) {
         return v == "solo"     ? PARSE_SOLO
                : v == "spread" ? PARSE_SPREAD
                : v == "lanes"  ? PARSE_LANES
-               : v == "rows"   ? PARSE_ROWS
                                : PARSE_AUTO;
     }();
     static const int max_pics = [] {
@@ -2340,7 +2394,7 @@ int parse_mode_for(int requested, int n_pics) {
         return e ? std::atoi(e) : 768;
     }();
     if (env != PARSE_AUTO) return env;
-    if (requested == PARSE_LANES || requested == PARSE_SOLO || requested == PARSE_SPREAD || requested == PARSE_ROWS)
+    if (requested == PARSE_LANES || requested == PARSE_SOLO || requested == PARSE_SPREAD)
         return requested;
     return n_pics <= max_pics ? PARSE_SPREAD : PARSE_LANES;
 }
@@ -2367,55 +2421,6 @@ int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order)
     return 1;
 }
 
-// rows mode: the pictures by payload size (heaviest first), 64 consecutive
-// ranks per group, so a row wave's lanes carry similar work.
-// HEIFGPU_ROWS_DEAL=K (measurement control for batches with repeated
-// bitstreams, such as the bench's tile permutations): pictures of equal
-// payload size (copies of one tile there) are spread so that each group holds
-// copies of K different sizes, the K adjacent ones; "copies": of all of them.
-// A batch of distinct photos (no two payloads of equal size) is unaffected.
-int rows_lanes_for(int n_pics) {
-    static const int forced = [] {
-        const char *e = std::getenv("HEIFGPU_ROWS_LANES");
-        return e ? std::atoi(e) : 0;
-    }();
-    (void)n_pics;
-    return forced > 0 && forced < 64 ? forced : 64;
-}
-
-int rows_parse_order(const PicDesc *pics, int n, int lanes, std::vector<uint32_t> &order) {
-    static const long band = [] {
-        const char *e = std::getenv("HEIFGPU_ROWS_DEAL");
-        if (!e) return 1L;
-        return std::string(e) == "copies" ? (1L << 30) : std::max(1L, std::atol(e));
-    }();
-    std::vector<uint32_t> by_size;
-    for (int i = 0; i < n; ++i)
-        if (!(pics[i].flags & PD_ASSEMBLY)) by_size.push_back((uint32_t)i);
-    std::stable_sort(by_size.begin(), by_size.end(),
-                     [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
-    if (band > 1) {  // key: (band of K sizes, copy number within its size, size rank)
-        std::vector<uint32_t> nth(by_size.size()), cls(by_size.size());
-        for (size_t i = 0; i < by_size.size(); ++i) {
-            const bool same = i && pics[by_size[i]].bits_len == pics[by_size[i - 1]].bits_len;
-            nth[i] = same ? nth[i - 1] + 1 : 0;
-            cls[i] = i == 0 ? 0 : cls[i - 1] + (same ? 0 : 1);
-        }
-        std::vector<size_t> idx(by_size.size());
-        for (size_t i = 0; i < idx.size(); ++i) idx[i] = i;
-        std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) {
-            const long bx = cls[x] / band, by = cls[y] / band;
-            return bx != by ? bx < by : nth[x] < nth[y];
-        });
-        std::vector<uint32_t> t(by_size.size());
-        for (size_t i = 0; i < idx.size(); ++i) t[i] = by_size[idx[i]];
-        by_size.swap(t);
-    }
-    const int groups = ((int)by_size.size() + lanes - 1) / lanes;
-    order.assign((size_t)groups * lanes, ~0u);
-    std::copy(by_size.begin(), by_size.end(), order.begin());
-    return groups;
-}
 #endif  // HG_PARSE_WANT_LANES
 
 #if defined(HG_HOST_EMU)
@@ -2565,79 +2570,7 @@ void emu_parse_solo(const BatchArgs &a) {
     }
 }
 
-// rows mode: a group's row waves round-robin, one pass per wave per round
-void emu_parse_rows(const BatchArgs &a) {
-    const int groups = a.parse_group, R = a.max_rows;
-    uint64_t tab[kTabRows], seq[15];
-    uint8_t scan8[128];
-    for (int i = 0; i < 64; ++i) scan8_tables(scan8, i);
-    for (int i = 0; i < kTabRows; ++i) tab[i] = state_row_ctx(i);
-    for (int i = 0; i < 15; ++i) seq[i] = sig_seq(i);
-    std::vector<LaneLds> lds((size_t)R * 64);
-    std::vector<LanePic> pics((size_t)R * 64);
-    std::vector<Lane> lanes((size_t)R * 64);
-    std::vector<uint8_t> live((size_t)R * 64);
-    static const bool stats = std::getenv("HEIFGPU_LANES_STATS") != nullptr;
-    for (int g = 0; g < groups; ++g) {
-        for (int r = 0; r < R; ++r)
-            for (int l = 0; l < 64; ++l) {
-                const size_t i = (size_t)r * 64 + (size_t)l;
-                const int slot = g * a.rows_lanes + l;
-                const bool in = l < a.rows_lanes && slot < a.n_slots && a.parse_order[slot] != ~0u;
-                live[i] = in && pic_init(pics[i], a, a.pic0 + (int)a.parse_order[slot], 0, 1 << 20) && r < pics[i].R;
-                if (live[i]) lane_start(lanes[i], pics[i], lds[i], r);
-                else lanes[i].st = U_DONE;
-            }
-        long passes = 0, units = 0;
-        for (;;) {
-            bool any = false, progressed = false;
-            for (int r = 0; r < R; ++r) {
-                bool wave_any = false;
-                for (int l = 0; l < 64; ++l) wave_any |= lanes[(size_t)r * 64 + (size_t)l].st != U_DONE;
-                if (!wave_any) continue;
-                any = true;
-                const long units0 = units;
-                for (int l = 0; l < 64; ++l) {
-                    const size_t i = (size_t)r * 64 + (size_t)l;
-                    if (lanes[i].st == U_DONE) continue;
-                    const EngRows G{lds[i].ctx, tab, seq, a.rbsp, (pics[i].bits_end + 64u) & ~3u, scan8, scan8 + 64};
-                    q_refill(lanes[i], G);
-                }
-                for (int kind = U_CTU; kind <= U_CTU_END; ++kind)
-                    for (int l = 0; l < 64; ++l) {
-                        const size_t i = (size_t)r * 64 + (size_t)l;
-                        Lane &L = lanes[i];
-                        LanePic &P = pics[i];
-                        if (L.st != kind) continue;
-                        const Env E{&a, nullptr, a.xprog + P.row_off, a.xctx + (size_t)P.row_off * CTX_PAD, l};
-                        if (kind == U_CTU && !ctu_ready<EngRows>(L, P, E)) continue;
-                        progressed = true;
-                        ++units;
-                        const EngRows G{lds[i].ctx, tab, seq, a.rbsp, (P.bits_end + 64u) & ~3u, scan8, scan8 + 64};
-                        run_unit(kind, L, lds[i], P, E, G);
-                    }
-                passes += units != units0;  // (a pass without progress is a sleep on the GPU)
-            }
-            if (!any) break;
-            if (!progressed) {  // every live lane of the group waits: cannot happen (row 0 never waits)
-                for (size_t i = 0; i < lanes.size(); ++i)
-                    if (lanes[i].st != U_DONE) {
-                        lanes[i].status |= ST_SUBSTREAM_END;
-                        atomicOr(&a.status[pics[i].pic], lanes[i].status);
-                        lanes[i].st = U_DONE;
-                    }
-                break;
-            }
-        }
-        if (stats) printf("group %d: %ld wave passes, %.1f units per pass\n", g, passes, (double)units / passes);
-    }
-}
-
 void emu_parse(const BatchArgs &a) {
-    if (a.parse_mode == PARSE_ROWS) {
-        emu_parse_rows(a);
-        return;
-    }
     if (a.parse_mode == PARSE_SOLO) emu_parse_solo<false>(a);
     else if (a.parse_mode == PARSE_SPREAD) emu_parse_solo<true>(a);
     else emu_parse_lanes(a);
@@ -2717,6 +2650,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
 #if defined(HG_PARSE_PROF)
     uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
     for (uint32_t pass = 0;; ++pass) {
         if (!__any(L.st != U_DONE)) break;
@@ -2755,103 +2689,25 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     pf[0] = __builtin_amdgcn_s_memtime() - t_start;
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[k], (unsigned long long)pf[k]);
-#endif
-}
-
-// Row waves (k_parse_rows, PARSE_ROWS): lane = picture, wave = one WPP CTB
-// row of a group of up to 64 pictures of similar payload (rows_parse_order).
-// In k_parse_lanes a picture's 16 rows share a wave, and the WPP ramp (row r
-// starts about 2r CTU-times after row 0) leaves two thirds of the lanes of an
-// issuing wave masked off (r04: 17.5 of 48 per pass).  Here every lane of a
-// wave is at the same row, so the lanes wait together: a wave whose row above
-// is not far enough ahead in any lane sleeps (s_sleep) and gives its SIMD's
-// issue to the other waves, instead of issuing masked passes.  The row above
-// is another wave, possibly on another XCD: progress words, the context
-// hand-off after CTU 1, SAO parameters and the CtDepth line go through
-// coherent (agent-scope) global memory, as in spread mode (EngRows).
-//
-// Jobs (group g, row r) are numbered row-major, j = r * groups + g, and each
-// workgroup dequeues its job from a counter (a.xjob, zeroed by k_rbsp) rather
-// than taking blockIdx.x: a job's predecessor (g, r - 1) has a lower number,
-// so it is held by a wave that is already running, whatever order the
-// hardware dispatches the workgroups in.
-inline size_t rows_lds_bytes() { return lane_blocks_bytes(64) + sizeof(LanePic) * 64 + kLaneTablesBytes; }
-
-__global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_rows(BatchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    LaneLds *s_lds = reinterpret_cast<LaneLds *>(smem);
-    LanePic *s_pic = reinterpret_cast<LanePic *>(smem + lane_blocks_bytes(64));
-    uint64_t *s_tab = reinterpret_cast<uint64_t *>(s_pic + 64);
-    uint64_t *s_seq = s_tab + kTabRows;
-    uint8_t *s_scan = reinterpret_cast<uint8_t *>(s_seq + 16);
-    const int lane = threadIdx.x;
-#if HG_PARSE_SETPRIO > 0
-    __builtin_amdgcn_s_setprio(HG_PARSE_SETPRIO);
-#endif
-    for (int i = lane; i < kTabRows; i += 64) s_tab[i] = state_row_ctx(i);
-    if (lane < 15) s_seq[lane] = sig_seq(lane);
-    scan8_tables(s_scan, lane);
-    const uint32_t groups = (uint32_t)a.parse_group;
-    const uint32_t j = dequeue_job(a.xjob);
-    const int row = (int)(j / groups), slot = (int)(j % groups) * a.rows_lanes + lane;
-    const bool in = lane < a.rows_lanes && row < a.max_rows && slot < a.n_slots && a.parse_order[slot] != ~0u;
-    Lane L;
-    LaneLds &ld = s_lds[lane];
-    LanePic &P = s_pic[lane];
-    const bool live = in && pic_init(P, a, a.pic0 + (int)a.parse_order[slot], 0, 1 << 20) && row < P.R;
-    if (live) lane_start(L, P, ld, row);
-    else L.st = U_DONE;
-    __syncthreads();
-    const Env E{&a, s_lds, a.xprog + (live ? P.row_off : 0u), a.xctx + (live ? (size_t)P.row_off * CTX_PAD : 0), lane};
-    const EngRows G{ld.ctx, s_tab, s_seq, a.rbsp, live ? (P.bits_end + 64u) & ~3u : 0u, s_scan, s_scan + 64};
-#if defined(HG_PARSE_PROF)
-    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const uint64_t t_start = __builtin_amdgcn_s_memtime();
-#endif
-    uint32_t stalled = 0;  // consecutive passes without progress (bounded: never hang the device)
-    for (;;) {
-        if (!__any(L.st != U_DONE)) break;
-        pass_wait();
-        if (live) q_refill(L, G);
-        bool progressed = false;
-#pragma unroll
-        for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
-            const bool mine = L.st == kind && (kind != U_CTU || ctu_ready<EngRows>(L, P, E));
-            if (!__any(mine)) continue;
-            progressed = true;
-            // the rows above (contexts, SAO parameters, depth line) after their progress words
-            if (kind == U_CTU) HG_ACQ_AGENT();
-#if defined(HG_PARSE_PROF)
-            const uint64_t t1 = __builtin_amdgcn_s_memtime();
-            pf[7] += (uint64_t)__popcll(__ballot(mine));
-#endif
-            if (mine) run_unit(kind, L, ld, P, E, G);
-#if defined(HG_PARSE_PROF)
-            const uint64_t t2 = __builtin_amdgcn_s_memtime();
-            pf[kind <= U_CTU ? 2 : kind <= U_TT ? 3 : kind - 1] += t2 - t1;
-#endif
-        }
-#if defined(HG_PARSE_PROF)
-        ++pf[1];
-#endif
-        if (progressed) {
-            stalled = 0;
-            continue;
-        }
-        // every live lane waits for the row above: sleep, leaving the SIMD's issue to the busy waves
-        __builtin_amdgcn_s_sleep(HG_SOLO_SLEEP);
-        if (++stalled > (1u << 25)) {  // the row above never arrives (a corrupt picture stopped it)
-            if (L.st != U_DONE) {
-                atomicOr(&a.status[P.pic], L.status | ST_SUBSTREAM_END);
-                store_agent(prog_word(E, P, L.row), kProgDone);  // the rows below stop waiting too
-            }
-            break;
+    // per wave (the CTU-time slots, unused by this kernel): s_memrealtime at its start, its
+    // duration and place, then the passes and its first three pictures (16 bits each; 0xffff: none)
+    if (blockIdx.x < (unsigned)kCtuTimeCap) {
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readlane(in ? pic : 0xffff, 0);
+        const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane(in ? pic : 0xffff, a.lane_rows < 64 ? a.lane_rows : 0);
+        const uint32_t p2 =
+            (uint32_t)__builtin_amdgcn_readlane(in ? pic : 0xffff, 2 * a.lane_rows < 64 ? 2 * a.lane_rows : 0);
+        uint32_t hwid, xcc;  // where the wave ran: HW_ID (SIMD, CU, SH, SE) and the XCD
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (lane == 0) {
+            g_ctu_t[blockIdx.x][0] = rt_start;
+            // the wave's duration (low 32 bits), then HW_ID[15:0] and XCC_ID[3:0]
+            g_ctu_t[blockIdx.x][1] = ((__builtin_amdgcn_s_memrealtime() - rt_start) & 0xffffffffu) |
+                                     ((uint64_t)((hwid & 0xffffu) | ((xcc & 0xfu) << 16)) << 32);
+            g_ctu_t[blockIdx.x][2] = (pf[1] & 0xffffu) | ((uint64_t)(p0 & 0xffffu) << 16) |
+                                     ((uint64_t)(p1 & 0xffffu) << 32) | ((uint64_t)(p2 & 0xffffu) << 48);
         }
     }
-#if defined(HG_PARSE_PROF)
-    pf[0] = __builtin_amdgcn_s_memtime() - t_start;
-    if (lane == 0)
-        for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[k], (unsigned long long)pf[k]);
 #endif
 }
 
@@ -3045,16 +2901,6 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
     BatchArgs a = a0;
     if (a.lane_rows < 1 || a.lane_rows > 64) return hipErrorInvalidValue;
     if (a.parse_mode == PARSE_SOLO || a.parse_mode == PARSE_SPREAD) return launch_parse_solo(a, s);
-    if (a.parse_mode == PARSE_ROWS) {
-        if (!a.parse_order || !a.xprog || !a.xctx || !a.xjob || a.parse_group < 1 || a.rows_lanes < 1 ||
-            a.rows_lanes > 64)
-            return hipErrorInvalidValue;
-        const long jobs = (long)a.parse_group * a.max_rows;
-        if (jobs <= 0) return hipSuccess;
-        if (jobs >= (1L << 31)) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_parse_rows, dim3((unsigned)jobs), dim3(64), rows_lds_bytes(), s, a);
-        return hipGetLastError();
-    }
     // the dealing of parse_order fixed the pictures per wave (lanes_parse_order)
     const int ppw = a.parse_order && a.parse_group > 0 ? a.parse_group : lanes_pics_per_wave(a.lane_rows, a.n_pics);
     a.parse_group = ppw;

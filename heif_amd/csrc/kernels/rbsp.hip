@@ -99,11 +99,11 @@ __device__ __forceinline__ int wave_excl_sum(int v, int lane, int &total) {
 }  // namespace
 
 __global__ void __launch_bounds__(64) k_rbsp(BatchArgs a) {
-#if !defined(HG_HOST_EMU) && !defined(HG_RBSP_NOPRIO)
+#if !defined(HG_HOST_EMU) && HG_PARSE_SETPRIO > 0
     // on the parse stream right before k_parse, beside the previous decodes'
     // reconstruction: at the parse's issue priority, so the gap between two
     // parses is its own 0.25 ms and not 2 ms of issue lost to k_intra
-    __builtin_amdgcn_s_setprio(3);
+    __builtin_amdgcn_s_setprio(HG_PARSE_SETPRIO);
 #endif
     const int pic = a.pic0 + (int)blockIdx.x;
     const int lane = (int)threadIdx.x;

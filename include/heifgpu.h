@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define HEIFGPU_ABI_VERSION 5
+#define HEIFGPU_ABI_VERSION 6
 
 enum {
     HEIFGPU_OK = 0,
@@ -94,9 +94,10 @@ typedef struct {
      * HEIFGPU_PARSE_LANES packs one substream per lane (throughput);
      * HEIFGPU_PARSE_SOLO runs one substream per wavefront, a picture's rows in
      * one workgroup; HEIFGPU_PARSE_SPREAD one substream per wavefront, every
-     * row its own workgroup (latency of small batches); HEIFGPU_PARSE_ROWS
-     * (ABI 5) one picture per lane, one CTB row of up to 64 pictures per
-     * wavefront (throughput). */
+     * row its own workgroup (latency of small batches).  HEIFGPU_PARSE_ROWS
+     * (ABI 5 only: one picture per lane, one CTB row of up to 64 pictures per
+     * wavefront) was removed in ABI 6, as it won only on batches that repeat
+     * bitstreams; prepare answers HEIFGPU_E_UNSUPPORTED. */
     uint32_t parse_mode;
     /* lanes mode: pictures per wavefront (0 = adaptive; larger values are
      * capped at 64 / CTB rows) */
@@ -115,7 +116,7 @@ enum {
     HEIFGPU_PARSE_LANES = 1,
     HEIFGPU_PARSE_SOLO = 2,
     HEIFGPU_PARSE_SPREAD = 3,
-    HEIFGPU_PARSE_ROWS = 4
+    HEIFGPU_PARSE_ROWS = 4 /* removed in ABI 6: HEIFGPU_E_UNSUPPORTED */
 };
 
 /* ---- host: demux + parameter sets + slice headers ------------------- */
@@ -173,9 +174,11 @@ int heifgpu_batch_status(heifgpu_ctx *ctx, heifgpu_batch *batch, uint32_t *statu
  * reloaded again.  Returns HEIFGPU_E_DECODE if any is nonzero. */
 int heifgpu_batch_status_previous(heifgpu_ctx *ctx, heifgpu_batch *batch, uint32_t *status, size_t cap,
                                   size_t *n_prev, void *stream);
-/* HEIFGPU_ABI_VERSION of the library (a caller built against another
- * version's structs, e.g. the 16-byte ABI 3 heifgpu_batch_opts, must not
- * call it: check this first) */
+/* HEIFGPU_ABI_VERSION of the library.  Call this first: a caller built
+ * against another version (e.g. ABI 3's 16-byte heifgpu_batch_opts) must not
+ * call the other entry points.  ABI 6: HEIFGPU_PARSE_ROWS removed; a reload
+ * that fails no longer costs heifgpu_batch_status_previous the last good
+ * load's status. */
 int heifgpu_abi_version(void);
 void heifgpu_batch_free(heifgpu_batch *batch);
 /* stage timing (ms per decode call, from HIP events on the streams the

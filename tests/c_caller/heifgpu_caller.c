@@ -71,7 +71,7 @@ static void write_planes(FILE *f, const DevPlanes *p) {
 
 int main(int argc, char **argv) {
     CHECK(argc >= 2, "usage: heifgpu_caller FILE [--decode OUT]");
-    CHECK(HEIFGPU_ABI_VERSION == 5, "ABI version");
+    CHECK(HEIFGPU_ABI_VERSION == 6, "ABI version");
     CHECK(heifgpu_abi_version() == HEIFGPU_ABI_VERSION, "library ABI %d, header %d", heifgpu_abi_version(),
           HEIFGPU_ABI_VERSION);
     CHECK(sizeof(heifgpu_batch_opts) == 20, "heifgpu_batch_opts is %zu bytes", sizeof(heifgpu_batch_opts));

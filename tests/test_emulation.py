@@ -36,9 +36,7 @@ def _run(exe, path, env_extra=None):
 # automatic choice for a single image), k_parse_lanes (one substream per lane)
 # with its adaptive geometry (one picture per wave for a single image), the
 # full 64-lane packing of large batches (four 16-row pictures per wave) and
-# batch (unsorted) wave order; k_parse_rows (lane = picture, wave = one CTB
-# row of the group, WPP through coherent global memory) in size-sorted and
-# copies-apart dealing, and with 32-picture groups
+# batch (unsorted) wave order
 LANES = {"HEIFGPU_PARSE": "lanes"}
 PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "spread"}, "lanes": LANES,
            "packed": {**LANES, "HEIFGPU_PARSE_ADAPT": "0"},
@@ -46,10 +44,7 @@ PARSERS = {"solo": {"HEIFGPU_PARSE": "solo"}, "spread": {"HEIFGPU_PARSE": "sprea
            # spread with k_intra_stream giving every picture up to its second launch, and without streaming
            "spread_redo": {"HEIFGPU_PARSE": "spread", "HEIFGPU_STREAM_PATIENCE_US": "0"},
            "spread_nostream": {"HEIFGPU_PARSE": "spread", "HEIFGPU_STREAM": "0"},
-           "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"},
-           "rows": {"HEIFGPU_PARSE": "rows"},
-           "rows_copies": {"HEIFGPU_PARSE": "rows", "HEIFGPU_ROWS_DEAL": "copies"},
-           "rows32": {"HEIFGPU_PARSE": "rows", "HEIFGPU_ROWS_LANES": "32"}}
+           "order0": {**LANES, "HEIFGPU_PARSE_ORDER": "0"}}
 
 
 @pytest.mark.parametrize("parser", list(PARSERS))
@@ -58,7 +53,7 @@ def test_emulated_kernels_match_oracle(emu_check, parser):
     assert rc == 0 and "EMU PARITY OK" in out, out[-2000:]
 
 
-@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed", "rows"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "lanes", "packed"])
 def test_emulated_kernels_permuted_image(emu_check, tmp_path, halfmoonbay, parser):
     p = tmp_path / "perm.heic"
     p.write_bytes(permuted_heic(halfmoonbay, 42))
@@ -85,7 +80,7 @@ def _corrupt(data: bytes, mode: str) -> bytes:
     return bytes(d)
 
 
-@pytest.mark.parametrize("parser", ["solo", "spread", "spread_redo", "lanes", "packed", "rows"])
+@pytest.mark.parametrize("parser", ["solo", "spread", "spread_redo", "lanes", "packed"])
 @pytest.mark.parametrize("mode", ["random", "zeroed"])
 def test_emulated_kernels_survive_corrupt_streams(emu_check, tmp_path, halfmoonbay, mode, parser):
     """Corrupt slice data must end in status bits, never in a crash (the same

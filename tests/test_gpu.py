@@ -77,13 +77,12 @@ def test_halfmoonbay_bit_exact(H, oracle_halfmoonbay, halfmoonbay):
     ("spread", 0, {"mode": "spread", "workgroups": 768, "pics_per_wave": 1, "waves_per_workgroup": 1}),
     ("lanes", 0, {"mode": "lanes", "workgroups": 48, "pics_per_wave": 1, "waves_per_workgroup": 1}),
     ("lanes", 4, {"mode": "lanes", "workgroups": 12, "pics_per_wave": 4, "waves_per_workgroup": 1}),
-    ("rows", 0, {"mode": "rows", "workgroups": 16, "pics_per_wave": 64, "waves_per_workgroup": 1}),
 ])
 def test_halfmoonbay_parse_modes(H, ctx, oracle_halfmoonbay, halfmoonbay, parse, ppw, geom):
     """Config 3 in every parse geometry: solo (a workgroup of 16 waves per
     tile, one WPP row per wave), spread (one single-wave workgroup per WPP
     row: 768), lanes with one tile per wave, lanes packed four tiles per
-    wave, and rows (one wave per CTB row of all 48 tiles, lane = tile)."""
+    wave.  (r05's rows geometry is gone in ABI 6: test_rows_mode_removed.)"""
     img = H.HeifImage.parse(halfmoonbay)
     b = ctx.prepare([img], parse=parse, pics_per_wave=ppw)
     assert b.parse_geometry() == geom
@@ -167,7 +166,6 @@ def check_permuted(outs, seeds, oracle_tiles):
     ("solo", {"mode": "solo", "workgroups": 6144, "pics_per_wave": 1, "waves_per_workgroup": 16}),
     ("spread", {"mode": "spread", "workgroups": 98304, "pics_per_wave": 1, "waves_per_workgroup": 1}),
     ("lanes4", {"mode": "lanes", "workgroups": 1536, "pics_per_wave": 4, "waves_per_workgroup": 1}),
-    ("rows", {"mode": "rows", "workgroups": 1536, "pics_per_wave": 64, "waves_per_workgroup": 1}),
 ])
 def test_bench_shard_every_image(H, ctx, oracle_tiles, halfmoonbay, parse, geom):
     """The headline configuration itself (bench.py, config 4 shard): 128
@@ -203,7 +201,7 @@ def _damaged_halfmoonbay(oracle_mod, data, tile=5):
 
 
 @pytest.mark.parametrize("sets", [0, 2, 1])
-@pytest.mark.parametrize("parse", ["lanes", "spread", "rows"])
+@pytest.mark.parametrize("parse", ["lanes", "spread"])
 def test_status_sticky_over_pipelined_decodes(H, ctx, oracle_mod, oracle_tiles, halfmoonbay, parse, sets):
     """heifgpu_batch_status reports the OR over every decode since the last
     query (/root/reference/src/heic/decoder.rs:109-112: errors reach the
@@ -244,6 +242,45 @@ def test_status_sticky_over_pipelined_decodes(H, ctx, oracle_mod, oracle_tiles, 
     prev = b.status_previous()
     assert len(prev) == 3 and prev[0] == 0 and prev[2] == 0 and prev[1] != 0, prev
     assert b.status_previous() == [0, 0, 0]  # read and cleared
+    b.free()
+
+
+def test_status_previous_after_failed_reload(H, ctx, oracle_mod, halfmoonbay, monkeypatch):
+    """A reload that fails after it has begun to overwrite its descriptor
+    generation (injected: HEIFGPU_FAULT_INJECT=prepare) leaves the batch
+    unusable until a reload succeeds; that reload must not overwrite the last
+    good load's generation, so heifgpu_batch_status_previous still reports the
+    last good load's decode errors, sized for it."""
+    bad = _damaged_halfmoonbay(oracle_mod, halfmoonbay)
+    a_imgs = H.HeifImage.parse_many([halfmoonbay, bad, halfmoonbay], threads=4)
+    b = ctx.prepare(a_imgs)
+    outs = ctx.alloc_outputs(a_imgs)
+    b.decode_async(outs)  # load A, damaged image 1, status not read
+    clean = H.HeifImage.parse_many([halfmoonbay] * 2, threads=4)
+    monkeypatch.setenv("HEIFGPU_FAULT_INJECT", "prepare")
+    with pytest.raises(H.HeifGpuError, match="injected"):
+        ctx.prepare(clean, reuse=b, wait=False)
+    monkeypatch.delenv("HEIFGPU_FAULT_INJECT")
+    with pytest.raises(H.HeifGpuError, match="not loaded"):
+        b.decode_async(outs)
+    with pytest.raises(H.HeifGpuError, match="not loaded"):
+        b.status_previous()
+    ctx.prepare(clean, reuse=b)  # load B
+    outs_b = ctx.alloc_outputs(clean)
+    b.decode_async(outs_b)
+    assert b.status() == [0, 0]
+    prev = b.status_previous()  # A, three images, its damage kept
+    assert len(prev) == 3 and prev[0] == 0 and prev[2] == 0 and prev[1] != 0, prev
+    # a failure after a good reload: the next good reload's previous load is B
+    monkeypatch.setenv("HEIFGPU_FAULT_INJECT", "prepare")
+    with pytest.raises(H.HeifGpuError, match="injected"):
+        ctx.prepare(a_imgs, reuse=b)
+    monkeypatch.delenv("HEIFGPU_FAULT_INJECT")
+    ctx.prepare(a_imgs, reuse=b)
+    b.decode_async(outs)
+    st = b.status()
+    assert st[0] == 0 and st[2] == 0 and st[1] != 0, st
+    assert b.status_previous() == [0, 0]
     b.free()
 
 
@@ -464,3 +501,19 @@ def test_reloaded_batches_alternate(H, ctx, oracle_tiles, halfmoonbay):
     for b in batches:
         assert not any(b.status())
         b.free()
+
+
+def test_rows_mode_removed(H, ctx, halfmoonbay):
+    """HEIFGPU_PARSE_ROWS (ABI 5's row waves) is gone in ABI 6:
+    prepare answers HEIFGPU_E_UNSUPPORTED and the batch is not created."""
+    import ctypes
+
+    from heif_amd import _lib
+
+    img = H.HeifImage.parse(halfmoonbay)
+    arr = (ctypes.c_void_p * 1)(img._h.value)
+    opts = _lib.BatchOpts(1, 0, _lib.PARSE_ROWS, 0, 0)
+    b = ctypes.c_void_p()
+    rc = _lib.lib.heifgpu_batch_prepare_ex(ctx._h, arr, 1, ctypes.byref(opts), ctypes.byref(b))
+    assert rc == _lib.HEIFGPU_E_UNSUPPORTED and not b.value
+    assert "ABI 6" in _lib.last_error()

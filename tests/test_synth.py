@@ -233,21 +233,6 @@ def test_gpu_synthetic_bit_exact(H, gctx, oracle_mod, name, over, parse):
 
 
 @pytest.mark.gpu
-def test_gpu_synthetic_rows_bit_exact(H, gctx, oracle_mod):
-    """k_parse_rows (lane = picture, one wave per CTB row of the batch's
-    pictures, WPP hand-offs through coherent global memory) on every tool /
-    geometry case, three pictures per batch (non-WPP cases: the row-0 wave
-    walks every row)."""
-    for name, over in CASES:
-        p = params(over)
-        datas = [S.single_heic(p, seed=s) for s in range(3)]
-        outs, st = _decode(H, gctx, datas, "rows")
-        assert st == [0, 0, 0], name
-        for o, d in zip(outs, datas):
-            _assert_equal(_planes(o), oracle_mod.decode_heic(d, with_checks=False), ("rows", name))
-
-
-@pytest.mark.gpu
 @pytest.mark.parametrize("cf,bd", [(2, 8), (3, 10)])
 def test_gpu_chroma_format_grid_rgb_gather(H, oracle_mod, cf, bd):
     """A 4:2:2 / 4:4:4 grid (cropped last row and column): bit-exact planes of
