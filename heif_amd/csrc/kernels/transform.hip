@@ -65,8 +65,10 @@ __global__ void __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_e
     const TuRec *tus = a.tus + pd.tu_off + (uint64_t)row * pd.tu_cap_row;
     const CoefSrc<false> coefs{a.coefs + pd.coef_off + (uint64_t)row * pd.coef_cap_row};
     const int W = sp.width, H = sp.height;
-    const int cw = sp.chroma_format ? W >> chroma_sx(sp.chroma_format) : 0;
-    const int ch = sp.chroma_format ? H >> chroma_sy(sp.chroma_format) : 0;
+    // (made scalar: formed with VALU selects they took a VGPR each, and at the
+    // 72-VGPR budget one of them spilled to scratch)
+    const int cw = HG_UNI(sp.chroma_format ? W >> chroma_sx(sp.chroma_format) : 0);
+    const int ch = HG_UNI(sp.chroma_format ? H >> chroma_sy(sp.chroma_format) : 0);
     // global memory in the type: selected by cidx the pointers would be flat,
     // and flat stores count in lgkmcnt, so every LDS wait would wait for them
     int16_t HG_GAS *const res0 = (int16_t HG_GAS *)(a.resid + pd.resid_off);
