@@ -55,7 +55,7 @@ sys.path.insert(0, str(ROOT))
 
 SAMPLE = ROOT / "tests" / "golden" / "halfmoonbay.heic"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-ROUND = "r05"
+ROUND = "r06"
 PROFILES = ROOT / "profiles" / ROUND
 BINS_PER_IMAGE = 15358022  # CABAC bins of one halfmoonbay image (oracle count; every permutation has the same)
 
@@ -522,6 +522,41 @@ def main():
                               "k_gather_tiles launch per image and rank reading over xGMI (ms includes the exchange "
                               "and the closing barrier)"}
 
+    # --split tiles: every rank's own parse time, and the floor no tile split can
+    # go below: the heaviest tile's parse decoded alone (its WPP chain; tiles are
+    # independent pictures, /root/reference/src/heic/decoder.rs:114-119, so the
+    # split removes tiles from a rank but never shortens that chain)
+    split_parse = None
+    if tiles_split:
+        mine = {"rank": rank, "tiles": len(range(offset, info.num_tiles, stride)), "parse_ms": round(per_step[0], 3),
+                "parse_ms_alone": round(alone[0], 3)}
+        split_parse = [mine]
+        if world > 1:
+            split_parse = [None] * world
+            torch.distributed.all_gather_object(split_parse, mine)
+        if rank == 0:
+            heavy = max(range(info.num_tiles), key=lambda k: images[0].tile_params(k)["payload_bytes"])
+            fb = ctx.prepare(images[:1], tile_stride=info.num_tiles, tile_offset=heavy)
+            f_outs = ctx.alloc_outputs(images[:1])
+            ctx.set_timing(True)
+            lat = []
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t_f = time.perf_counter()
+                fb.decode_async(f_outs, stream.cuda_stream)
+                stream.synchronize()
+                lat.append((time.perf_counter() - t_f) * 1e3)
+            f_parse = ctx.stage_times()[0]
+            ctx.set_timing(False)
+            if any(fb.status(stream.cuda_stream)):
+                raise SystemExit("chain floor: decode status")
+            fb.free()
+            split_parse = {"per_rank": split_parse, "chain_floor": {
+                "tile": heavy, "payload_bytes": images[0].tile_params(heavy)["payload_bytes"],
+                "parse_ms": round(f_parse, 3), "latency_ms": round(min(lat), 3),
+                "what": "the image's heaviest tile (payload bytes) decoded alone, spread parse: its WPP chain, "
+                        "below which no rank's parse can go however the tiles are split"}}
+
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = end_to_end(H, ctx, files, outs, args.e2e_batches, host_threads, stream, info)
@@ -557,21 +592,31 @@ def main():
         # counter evidence of this round (profiles/<round>/, written by tools/pmc_*.sh on the same
         # command): HBM bytes per launch (FETCH_SIZE / WRITE_SIZE passes) and the parse's SQ counters
         traffic, issue = None, None
-        same_cfg = lambda j: (j.get("batch", j.get("batch_images")) == args.batch and not tiles_split and not c5
-                              and not c4u
+        # config 5 has its own counter files (suffix _config5); config4u and split runs have none
+        sfx = "_config5" if c5 else ""
+        same_cfg = lambda j: (j.get("batch", j.get("batch_images")) == args.batch and not tiles_split and not c4u
                               and j.get("parse_mode", "lanes") == geom["mode"])
         try:
-            tj = json.loads((PROFILES / "pmc_traffic.json").read_text())
+            tj = json.loads((PROFILES / f"pmc_traffic{sfx}.json").read_text())
             if same_cfg(tj):
                 traffic = tj.get("k_parse_hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
-        bins = args.batch * BINS_PER_IMAGE if not c5 and not c4u and not tiles_split else None
+        pj = None
+        try:
+            pj = json.loads((PROFILES / f"parse_counters_{geom['mode']}{sfx}.json").read_text())
+            if not same_cfg(pj):
+                pj = None
+        except (OSError, ValueError):
+            pj = None
+        # bins per image: the oracle's count for halfmoonbay (every permutation the same);
+        # config 5's from its counter file (tools/pmc_parse.sh counts them with the oracle)
+        bpi = BINS_PER_IMAGE if not c5 and not c4u else (pj or {}).get("bins_per_image")
+        bins = args.batch * bpi if bpi and not tiles_split else None
         if bins:
             issue = {"bins_per_launch": bins, "bins_per_s": round(bins / (parse_ms / 1e3), 1)}
             try:
-                pj = json.loads((PROFILES / f"parse_counters_{geom['mode']}.json").read_text())
-                if same_cfg(pj):
+                if pj:
                     pl, pw = pj["per_launch"], pj.get("per_wave", {})
                     valu, salu = pl["SQ_INSTS_VALU"] / bins, pl["SQ_INSTS_SALU"] / bins
                     issue.update({
@@ -583,9 +628,9 @@ def main():
                         "issue_floor_frac": round((4 * pw["SQ_INSTS_VALU"] + pw["SQ_INSTS_SALU"])
                                                   / (4 * pw["SQ_WAVE_CYCLES"]), 4),
                         "wait_frac": round(pl["SQ_WAIT_ANY"] / pl["SQ_WAVE_CYCLES"], 4),
-                        "source": f"profiles/{ROUND}/parse_counters_{geom['mode']}.json",
+                        "source": f"profiles/{ROUND}/parse_counters_{geom['mode']}{sfx}.json",
                     })
-            except (OSError, ValueError, KeyError, ZeroDivisionError):
+            except (ValueError, KeyError, ZeroDivisionError):
                 pass
         line = {
             "metric": ("Mpixels/s decoded (bit-exact) on 7680x4320 Main-10 HEIC batch" if c5 else
@@ -624,7 +669,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": traffic,
-                "traffic_source": f"profiles/{ROUND}/pmc_traffic.json" if traffic else None,
+                "traffic_source": f"profiles/{ROUND}/pmc_traffic{sfx}.json" if traffic else None,
                 "kernel": kname,
                 "parse_geometry": geom,
                 "kernel_ms_per_launch": round(parse_ms / chunks, 3),
@@ -653,6 +698,8 @@ def main():
             line["e2e"] = e2e
         if gather:
             line["tile_split_gather"] = gather
+        if split_parse:
+            line["tile_split_parse"] = split_parse
         if with_cpu:
             build = cpu_build
             threads = effective_cpus()

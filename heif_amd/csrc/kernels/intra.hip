@@ -194,6 +194,62 @@ struct Win {
     }
 };
 
+// One picture's CTU windows, from which a component's Win is formed where it
+// is used (a few scalar operations on the wave-uniform CTU and component)
+// instead of being held: three Win and six plane pointers live across the TB
+// loop kept k_intra at the 106-SGPR cap with 120-190 SGPRs spilled into VGPR
+// lanes, a v_writelane / v_readlane per use.  The block
+// layout is win_layout's: scratch, then per component the window, the left
+// column and the row above, each 16-byte aligned.
+template <typename Pel, int CF>
+struct Frame {
+    unsigned char *blk;    // the wave's window block (LDS)
+    Pel *recon;            // the picture's Y plane; Cb, Cr follow
+    const int16_t *resid;  // its Y residual plane (k_transform); Cb, Cr follow
+    int W, H, cw, ch, log2ctb;
+    uint32_t b0, b1;       // bytes of the Y and of one chroma component's part of the block
+    static constexpr uint32_t al16(uint32_t v) { return (v + 15u) & ~15u; }
+    static constexpr uint32_t kS0 = (uint32_t)((sizeof(IntraScratch) + 15) & ~size_t(15));
+    __device__ __forceinline__ int csx(int k) const { return k ? (1 << log2ctb) >> chroma_sx(CF) : 1 << log2ctb; }
+    __device__ __forceinline__ int csy(int k) const { return k ? (1 << log2ctb) >> chroma_sy(CF) : 1 << log2ctb; }
+    __device__ __forceinline__ int pw(int k) const { return k ? cw : W; }
+    __device__ __forceinline__ int ph(int k) const { return k ? ch : H; }
+    __device__ __forceinline__ size_t plane_off(int k) const {
+        return k ? (size_t)W * H + (k == 2 ? (size_t)cw * ch : 0) : 0;
+    }
+    __device__ __forceinline__ Pel *plane(int k) const { return recon + plane_off(k); }
+    __device__ __forceinline__ void init(int log2, int w_, int h_, int cw_, int ch_) {
+        log2ctb = log2, W = w_, H = h_, cw = cw_, ch = ch_;
+        const uint32_t bps = sizeof(Pel), c0 = 1u << log2;
+        b0 = al16(c0 * c0 * bps) + al16(c0 * bps) + al16((2 * c0 + 1) * bps);
+        const uint32_t cx = CF ? c0 >> chroma_sx(CF) : 0, cy = CF ? c0 >> chroma_sy(CF) : 0;
+        b1 = al16(cx * cy * bps) + al16(cy * bps) + al16((2 * cx + 1) * bps);
+    }
+    // component k's window at CTU column c of CTB row r
+    __device__ __forceinline__ Win<Pel> win(int k, int c, int r) const {
+        Win<Pel> w;
+        const int sx = csx(k), sy = csy(k);
+        const uint32_t cur = kS0 + (k ? b0 + (uint32_t)(k - 1) * b1 : 0u);
+        const uint32_t left = cur + al16((uint32_t)(sx * sy) * sizeof(Pel));
+        const uint32_t above = left + al16((uint32_t)sy * sizeof(Pel));
+        w.cur = reinterpret_cast<Pel *>(blk + cur);
+        w.left = reinterpret_cast<Pel *>(blk + left);
+        w.above = reinterpret_cast<Pel *>(blk + above);
+        w.res = resid + plane_off(k);
+        w.rp = pw(k);
+        w.rx0 = w.ry0 = 0;
+        w.csx = sx;
+        w.csy = sy;
+        w.cx0 = c * sx;
+        w.cy0 = r * sy;
+#if defined(HG_HOST_EMU)
+        w.blk_lo = blk;
+        w.blk_hi = blk + kS0 + b0 + (CF ? 2 * b1 : 0u);
+#endif
+        return w;
+    }
+};
+
 #if !defined(HG_HOST_EMU)
 // the sum over the lanes of each aligned group of m (2 <= m <= 64, a power of
 // two) lanes, in every lane of the group: ds_swizzle xor steps inside 32-lane
@@ -680,16 +736,14 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
     constexpr int chroma = CF;  // = sp.chroma_format (launch_intra picks the instantiation)
     const int cw = chroma ? W >> chroma_sx(chroma) : 0, ch = chroma ? H >> chroma_sy(chroma) : 0;
     const int ncomp = chroma ? 3 : 1;
-    Pel *planes[3];
-    planes[0] = reinterpret_cast<Pel *>(a.recon + pd.recon_off);
-    planes[1] = planes[0] + (size_t)W * H;
-    planes[2] = planes[1] + (size_t)cw * ch;
-    const int16_t *resp[3] = {a.resid + pd.resid_off, a.resid + pd.resid_off + (size_t)W * H,
-                              a.resid + pd.resid_off + (size_t)W * H + (size_t)cw * ch};
     const bool strong = (sp.flags & SP_STRONG_INTRA) != 0;
     const WinLayout lay = win_layout(log2ctb, chroma, (int)sizeof(Pel));
     uint32_t *progress = reinterpret_cast<uint32_t *>(smem);  // [nw], 64 B reserved
-    unsigned char *blk = smem + 64 + (size_t)wave * lay.bytes;
+    Frame<Pel, CF> F;
+    F.blk = smem + 64 + (size_t)wave * lay.bytes;
+    F.recon = reinterpret_cast<Pel *>(a.recon + pd.recon_off);
+    F.resid = a.resid + pd.resid_off;
+    F.init(log2ctb, W, H, cw, ch);
     XfScratch X{};
     if constexpr (XfInline) {
         unsigned char *tab = smem + 64 + (size_t)nw * lay.bytes;
@@ -698,22 +752,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                       reinterpret_cast<int32_t *>(xw + kXfDBytes + kXfGBytes), reinterpret_cast<const XfTab *>(tab)};
         xf_tables(reinterpret_cast<XfTab *>(tab), lane);
     }
-    IntraScratch *S = reinterpret_cast<IntraScratch *>(blk);
-    Win<Pel> win[3];
-    for (int k = 0; k < 3; ++k) {
-        win[k].cur = reinterpret_cast<Pel *>(blk + lay.cur[k]);
-        win[k].left = reinterpret_cast<Pel *>(blk + lay.left[k]);
-        win[k].above = reinterpret_cast<Pel *>(blk + lay.above[k]);
-        win[k].res = resp[k];
-        win[k].rp = k ? cw : W;
-        win[k].rx0 = win[k].ry0 = 0;
-        win[k].csx = lay.csx[k];
-        win[k].csy = lay.csy[k];
-#if defined(HG_HOST_EMU)
-        win[k].blk_lo = blk;
-        win[k].blk_hi = blk + lay.bytes;
-#endif
-    }
+    IntraScratch *S = reinterpret_cast<IntraScratch *>(F.blk);
     progress[wave] = 0;  // every lane writes the same value
     __syncthreads();
     const uint32_t stride = (uint32_t)wctb + 1;
@@ -823,25 +862,26 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
             if (c != cur) {
                 if (cur >= 0) {
                     // finish CTU `cur`: write the window back, keep its last column as `left`
-                    _Pragma("unroll") for (int k = 0; k < 3; ++k) {
+                    _Pragma("nounroll") for (int k = 0; k < 3; ++k) {
                         if (k >= ncomp) break;
                         if (k < k0 || k >= k1) continue;
-                        const Win<Pel> &w = win[k];
-                        const int PW = k ? cw : W, PH = k ? ch : H;
+                        const Win<Pel> w = F.win(k, cur, r);
+                        Pel *const plane = F.plane(k);
+                        const int PW = F.pw(k), PH = F.ph(k);
                         const int vw = min(w.csx, PW - w.cx0), vh = min(w.csy, PH - w.cy0);
                         if (vw == w.csx && !(PW & 3) &&
-                            !(reinterpret_cast<uintptr_t>(planes[k]) & (4 * sizeof(Pel) - 1))) {
+                            !(reinterpret_cast<uintptr_t>(plane) & (4 * sizeof(Pel) - 1))) {
                             // full-width CTU: four samples per lane, one 4- (8-) byte store
                             const int lq = __builtin_ctz((unsigned)w.csx) - 2;
                             for (int o = lane; o < (vh << lq); o += kWave) {
                                 const int x = (o & ((1 << lq) - 1)) << 2, y = o >> lq;
-                                *reinterpret_cast<Quad<Pel> *>(planes[k] + (size_t)(w.cy0 + y) * PW + w.cx0 + x) =
+                                *reinterpret_cast<Quad<Pel> *>(plane + (size_t)(w.cy0 + y) * PW + w.cx0 + x) =
                                     *reinterpret_cast<const Quad<Pel> *>(w.cur + y * w.csx + x);
                             }
                         } else {
                             for (int o = lane; o < vw * vh; o += kWave) {
                                 const int x = o % vw, y = o / vw;
-                                planes[k][(size_t)(w.cy0 + y) * PW + w.cx0 + x] = w.cur[y * w.csx + x];
+                                plane[(size_t)(w.cy0 + y) * PW + w.cx0 + x] = w.cur[y * w.csx + x];
                             }
                         }
                         for (int y = lane; y < w.csy; y += kWave) w.left[y] = w.cur[y * w.csx + w.csx - 1];
@@ -871,41 +911,24 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                     HG_FENCE_ACQ();
                 }
                 // start CTU c: the row above (corner .. above-right) and the residuals
-                _Pragma("unroll") for (int k = 0; k < 3; ++k) {
+                _Pragma("nounroll") for (int k = 0; k < 3; ++k) {
                     if (k >= ncomp) break;
                     if (k < k0 || k >= k1) continue;
-                    Win<Pel> &w = win[k];
-                    const int PW = k ? cw : W, PH = k ? ch : H;
-                    w.cx0 = c * w.csx;
-                    w.cy0 = r * w.csy;
+                    const Win<Pel> w = F.win(k, c, r);
+                    const Pel *const plane = F.plane(k);
+                    const int PW = F.pw(k);
                     const int yg = w.cy0 - 1;
                     for (int i = lane; i <= 2 * w.csx; i += kWave) {
                         const int xg = w.cx0 - 1 + i;
-                        w.above[i] = (yg >= 0 && xg >= 0 && xg < PW) ? planes[k][(size_t)yg * PW + xg] : (Pel)0;
+                        w.above[i] = (yg >= 0 && xg >= 0 && xg < PW) ? plane[(size_t)yg * PW + xg] : (Pel)0;
                     }
-                    (void)PH;
                 }
                 wave_sync();
             }
             const int cidx = tu.flags & TU_CIDX_MASK;
             if (cidx >= ncomp || cidx < k0 || cidx >= k1) continue;
-            // field-wise selects on the wave-uniform cidx: indexing win[] with it (or
-            // selecting one of its elements by reference) keeps the array in scratch memory
-            Win<Pel> w;
-            w.cur = cidx == 0 ? win[0].cur : (cidx == 1 ? win[1].cur : win[2].cur);
-            w.left = cidx == 0 ? win[0].left : (cidx == 1 ? win[1].left : win[2].left);
-            w.above = cidx == 0 ? win[0].above : (cidx == 1 ? win[1].above : win[2].above);
-            w.res = cidx == 0 ? win[0].res : (cidx == 1 ? win[1].res : win[2].res);
-            w.rp = cidx == 0 ? W : cw;
-            w.rx0 = w.ry0 = 0;
-            w.csx = cidx == 0 ? win[0].csx : (cidx == 1 ? win[1].csx : win[2].csx);
-            w.csy = cidx == 0 ? win[0].csy : (cidx == 1 ? win[1].csy : win[2].csy);
-            w.cx0 = cidx == 0 ? win[0].cx0 : (cidx == 1 ? win[1].cx0 : win[2].cx0);
-            w.cy0 = cidx == 0 ? win[0].cy0 : (cidx == 1 ? win[1].cy0 : win[2].cy0);
-#if defined(HG_HOST_EMU)
-            w.blk_lo = win[0].blk_lo;
-            w.blk_hi = win[0].blk_hi;
-#endif
+            // the TB's component window, formed here from the wave-uniform cidx and CTU
+            Win<Pel> w = F.win(cidx, cur, r);
             const int PW = cidx ? cw : W, PH = cidx ? ch : H;
             // a TB must lie inside the picture and inside its CTU window, with a mode
             // of 8.4.2 (the parse keeps it so; the check keeps the tables in range)
@@ -933,15 +956,15 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
             // both in one pass
             if (!XfInline && cidx == 1 && chroma == 1 && tu.log2 <= 3 && t + 1 < ntu && ((t + 1) & 63u) != 0) {
                 const int sel = (int)(t + 1 - t0);
-                const uint4 r = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)tblk.x, sel),
-                                           (uint32_t)__builtin_amdgcn_readlane((int)tblk.y, sel),
-                                           (uint32_t)__builtin_amdgcn_readlane((int)tblk.z, sel),
-                                           (uint32_t)__builtin_amdgcn_readlane((int)tblk.w, sel));
+                const uint4 rn = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)tblk.x, sel),
+                                            (uint32_t)__builtin_amdgcn_readlane((int)tblk.y, sel),
+                                            (uint32_t)__builtin_amdgcn_readlane((int)tblk.z, sel),
+                                            (uint32_t)__builtin_amdgcn_readlane((int)tblk.w, sel));
                 TuRec tr;
-                __builtin_memcpy(&tr, &r, sizeof(tr));
+                __builtin_memcpy(&tr, &rn, sizeof(tr));
                 if ((tr.flags & TU_CIDX_MASK) == 2 && tr.x == tu.x && tr.y == tu.y && tr.log2 == tu.log2 &&
                     tr.mode == tu.mode && tr.ctu == tu.ctu) {
-                    predict_pair<Pel>(S, tu, tr, win[1], win[2], PW, PH, sp.bit_depth_c, lane);
+                    predict_pair<Pel>(S, tu, tr, F.win(1, cur, r), F.win(2, cur, r), PW, PH, sp.bit_depth_c, lane);
                     ++t;
                     continue;
                 }

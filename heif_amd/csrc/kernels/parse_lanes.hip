@@ -2408,16 +2408,28 @@ int solo_waves_for(int lane_rows) { return lane_rows < 1 ? 1 : (lane_rows > kSol
 // first), a picture's rows consecutive and in order (a row waits only for a
 // lower slot, which a running wave holds: k_parse_solo<true> takes its slot
 // from the job counter)
+// HEIFGPU_SPREAD_ORDER=rows (read at every prepare; tuning): row-major
+// instead, row r of every picture before row r + 1 of any, so a row's wave
+// finds the row above long started instead of holding its slot while it waits
 int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order) {
     std::vector<uint32_t> by_size((size_t)n);
     for (int i = 0; i < n; ++i) by_size[(size_t)i] = (uint32_t)i;
     std::stable_sort(by_size.begin(), by_size.end(),
                      [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
+    const char *e = std::getenv("HEIFGPU_SPREAD_ORDER");
+    const bool row_major = e && std::string(e) == "rows";
     order.clear();
+    uint32_t max_sub = 0;
     for (uint32_t p : by_size) {
         if (p >= (1u << 20) || pics[p].n_sub >= (1u << 12)) return -1;
-        for (uint32_t r = 0; r < pics[p].n_sub; ++r) order.push_back(p | (r << 20));
+        max_sub = std::max(max_sub, pics[p].n_sub);
+        if (!row_major)
+            for (uint32_t r = 0; r < pics[p].n_sub; ++r) order.push_back(p | (r << 20));
     }
+    if (row_major)
+        for (uint32_t r = 0; r < max_sub; ++r)
+            for (uint32_t p : by_size)
+                if (r < pics[p].n_sub) order.push_back(p | (r << 20));
     return 1;
 }
 
@@ -2440,6 +2452,12 @@ void emu_parse_lanes(const BatchArgs &a) {
     std::vector<uint8_t> wctx(a.wpp_ring ? 64 * CTX_PAD : 0);
     uint32_t prog[64];
     static const bool stats = std::getenv("HEIFGPU_LANES_STATS") != nullptr;
+    // modelling knob (emulation only): the unit kinds of one pass, in order, as
+    // digits (default "1234567": U_CTU .. U_CTU_END once)
+    static const std::string order = [] {
+        const char *e = std::getenv("HEIFGPU_EMU_PASS_ORDER");
+        return std::string(e && *e ? e : "1234567");
+    }();
     for (int w = 0; w < waves; ++w) {
         for (int l = 0; l < 64; ++l) {
             prog[l] = 0;
@@ -2463,7 +2481,8 @@ void emu_parse_lanes(const BatchArgs &a) {
                     q_refill(lanes[l], G);
                 }
             // the kernel's pass: every unit kind in syntax order, each on the lanes in it
-            for (int kind = U_CTU; kind <= U_CTU_END; ++kind) {
+            for (const char ch : order) {
+                const int kind = ch - '0';
                 bool mine[64], anym = false;
                 int cnt = 0;
                 for (int l = 0; l < 64; ++l) {
@@ -2497,11 +2516,15 @@ void emu_parse_lanes(const BatchArgs &a) {
                 break;
             }
         }
-        if (stats)
+        if (stats) {
             printf("wave %d: %ld passes, %.1f units per pass, %ld kind runs, %.2f units per kind run\n", w, passes,
                    (double)units / passes, kruns, (double)units / kruns);
-        if (stats)
-            for (int k = U_CTU; k <= U_CTU_END; ++k) printf("  kind %d: %ld runs, %ld units\n", k, kr[k], ku[k]);
+            printf("  runs");
+            for (int k = U_CTU; k <= U_CTU_END; ++k) printf(" %ld", kr[k]);
+            printf("\n  units");
+            for (int k = U_CTU; k <= U_CTU_END; ++k) printf(" %ld", ku[k]);
+            printf("\n");
+        }
     }
 }
 

@@ -5,7 +5,8 @@ streamed reads — an upper-bound correction for k_parse's byte-wide loads,
 whose width the guide leaves uncalibrated).  Writes profiles/pmc_traffic.json,
 which bench.py reads for roofline.traffic.
 
-usage: python tools/summarize_profile.py r01
+usage: python tools/summarize_profile.py <tag> [round]
+  (profiles/<round>/ receives the files; a config-5 run's are suffixed _config5)
 """
 import collections
 import csv
@@ -28,11 +29,12 @@ def per_launch(path, counter):
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     src = ROOT / "gpurun_out" / f"prof_{tag}"
-    dst = ROOT / "profiles" / tag
+    dst = ROOT / "profiles" / (sys.argv[2] if len(sys.argv) > 2 else tag)
     dst.mkdir(parents=True, exist_ok=True)
-    shutil.copy(src / "kt" / "kt_kernel_stats.csv", dst / "kernel_stats.csv")
     bench = json.loads((src / "bench.json").read_text().strip().splitlines()[-1])
-    (dst / "bench.json").write_text(json.dumps(bench, indent=2) + "\n")
+    sfx = "_config5" if bench["config"]["workload"].startswith("config5") else ""
+    shutil.copy(src / "kt" / "kt_kernel_stats.csv", dst / f"kernel_stats{sfx}.csv")
+    (dst / f"bench{sfx}.json").write_text(json.dumps(bench, indent=2) + "\n")
     fetch = per_launch(src / "fetch" / "fetch_counter_collection.csv", "FETCH_SIZE")
     write = per_launch(src / "write" / "write_counter_collection.csv", "WRITE_SIZE")
     stats = {r["Name"]: float(r["AverageNs"]) for r in csv.DictReader(open(src / "kt" / "kt_kernel_stats.csv"))}
@@ -55,7 +57,7 @@ def main():
                   "`bench.py --steps 1 --warmup 1`; bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
         "kernels": kernels,
     }
-    (dst / "pmc_traffic.json").write_text(json.dumps(out, indent=2) + "\n")
+    (dst / f"pmc_traffic{sfx}.json").write_text(json.dumps(out, indent=2) + "\n")
     print(json.dumps(out, indent=2))
 
 
