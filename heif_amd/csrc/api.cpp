@@ -919,7 +919,7 @@ int heifgpu_batch_decode(heifgpu_ctx *ctx, heifgpu_batch *b, const heifgpu_plane
     HIP_TRY(hipEventRecord(ps.parsed, p));
     HIP_TRY(hipEventRecord(ctx->fork, s));
     if (a.intra_stream) {
-        // streaming (small batches, DESIGN.md §5.5): no k_transform; the
+        // streaming (small batches, DESIGN.md §5.4): no k_transform; the
         // reconstruction starts beside this decode's parse and trails it
         HIP_TRY(hipStreamWaitEvent(r, ps.progreset, 0));
         if (t) {

@@ -718,7 +718,7 @@ constexpr uint64_t kRedoPatience = 200000000ull;  // 2 s (10 ns ticks): the pars
 // reconstruction trails the parse by a CTU instead of starting after it.
 // (r04's third mode, k_intra_fused: the in-line transform after the parse
 // instead of k_transform + k_intra, lost beside the next parse, 12.2-12.9
-// against 18.6 Gpix/s; removed in r05, DESIGN 5.5.)
+// against 18.6 Gpix/s; removed in r05, DESIGN 5.4.)
 template <typename Pel, int CF, int Mode>
 __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs &a, unsigned char *smem) {
     constexpr bool Poll = Mode == kIntraStream;       // rows consumed while the parse writes them

@@ -432,7 +432,7 @@ __global__ void __launch_bounds__(256) k_sao_out(BatchArgs a) {
 // (r04 also had k_loopfilter: both deblocking directions, SAO and output per
 // 64x64 tile in LDS, bit-exact, but 9.2 ms alone against 7.0 for the three
 // kernels here and 53 against ~33 ms beside the next parse, whose residency its
-// 9.6 KB of LDS per workgroup took; removed in r05, DESIGN 5.5.)
+// 9.6 KB of LDS per workgroup took; removed in r05, DESIGN 5.4.)
 
 #if defined(HG_HOST_EMU)
 void emu_deblock(const BatchArgs &a) {

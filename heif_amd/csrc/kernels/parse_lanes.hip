@@ -248,7 +248,7 @@ HG_HD inline size_t lane_blocks_bytes(int n) { return (sizeof(LaneLds) * (size_t
 // engine context of one lane (lanes mode: every lane its own substream; a
 // picture's WPP rows are lanes of one wave, so no hand-off leaves the wave).
 // (r05's row waves, k_parse_rows, were this engine with spread mode's
-// hand-offs; removed in r06, their A/B record is DESIGN 5.9)
+// hand-offs; removed in r06, their A/B record is DESIGN 5.4)
 struct Eng {
     static constexpr bool kSolo = false;
     static constexpr bool kSpread = false;

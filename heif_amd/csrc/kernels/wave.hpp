@@ -135,7 +135,7 @@ constexpr int kWave = 64;
 // Issue priority of the parse stream's kernels (k_rbsp, k_parse_lanes,
 // k_parse_solo): s_setprio HG_PARSE_SETPRIO, 0 turns it off for all of them
 // (r04 A/B: 128 images 83.5-83.8 vs 84.4 ms per step, one image 27.8 vs
-// 28.05 ms; DESIGN 5.5, 5.11)
+// 28.05 ms; DESIGN 5.4, 5.11)
 #if !defined(HG_PARSE_SETPRIO)
 #define HG_PARSE_SETPRIO 3
 #endif

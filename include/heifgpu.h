@@ -97,7 +97,7 @@ typedef struct {
      * row its own workgroup (latency of small batches).  HEIFGPU_PARSE_ROWS
      * (ABI 5 only: one picture per lane, one CTB row of up to 64 pictures per
      * wavefront) was removed in ABI 6, as it won only on batches that repeat
-     * bitstreams (DESIGN.md §5.9); prepare answers HEIFGPU_E_UNSUPPORTED. */
+     * bitstreams (DESIGN.md §5.4); prepare answers HEIFGPU_E_UNSUPPORTED. */
     uint32_t parse_mode;
     /* lanes mode: pictures per wavefront (0 = adaptive; larger values are
      * capped at 64 / CTB rows) */
