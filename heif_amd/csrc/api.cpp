@@ -640,7 +640,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
             return fail(HEIFGPU_E_UNSUPPORTED, "spread parse: over 2^20 pictures or 4096 substreams per picture");
     } else {  // pictures dealt by payload size (r03: dealing by WPP critical path lost, 16.9 vs 17.0 Gpix/s)
         parse_group = lanes_parse_order(hb.pics.data(), int(hb.pics.size()), hb.lane_rows,
-                                        mode == PARSE_SOLO ? 1 : ppw_req, order, hb.subs.data(), hb.seqs.data());
+                                        mode == PARSE_SOLO ? 1 : ppw_req, order);
     }
     // spread parse: WPP neighbours in other waves (progress words,
     // context hand-off blocks, the job counter after the progress words)

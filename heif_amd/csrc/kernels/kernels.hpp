@@ -113,10 +113,7 @@ constexpr int kSoloMaxWaves = 16;
 // or for solo mode with ppw_force = 1 one picture per workgroup, heaviest
 // first); returns the pictures per wave it dealt for (BatchArgs::parse_group).
 // ppw_force = 0: the adaptive choice.
-// subs / seqs (optional): the substream table and sequences, for dealing by
-// each picture's WPP critical path (HEIFGPU_LANES_DEAL=chain)
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
-                      const uint32_t *subs = nullptr, const SeqParams *seqs = nullptr);
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order);
 // k_intra_stream (reconstruction behind the spread parse, k_transform folded in) for this batch
 // (same box, spread, one-decode latency: 4 images 28.3 vs 33.7 ms streamed; 8
 // images 44.4 vs 40.5, the reconstruction no longer keeps up with the parse)

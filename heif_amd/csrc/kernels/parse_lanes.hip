@@ -2277,50 +2277,21 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
 }  // namespace
 
 #if HG_PARSE_WANT_LANES  // (the host-side choices live in the lanes translation unit)
-// WPP critical path of a picture in payload bytes: row r's bytes (from the
-// entry points) spread evenly over its CTUs; CTU (r, c) starts after (r, c - 1)
-// and after (r - 1, c), or (r - 1, 1) at c = 0 (the context hand-off after CTU
-// 1, 9.3.1).  Without WPP the picture is one substream: its bytes.
-double wpp_chain_bytes(const PicDesc &pd, const uint32_t *subs, int wctb) {
-    const int R = (int)pd.n_sub;
-    if (R <= 1 || wctb <= 0) return (double)pd.bits_len;
-    std::vector<double> done((size_t)wctb, 0.0);  // finish time of CTU c in the row above
-    for (int r = 0; r < R; ++r) {
-        const uint32_t b0 = subs[pd.sub_first + r] & SUB_OFFSET;
-        const uint32_t b1 = r + 1 < R ? subs[pd.sub_first + r + 1] & SUB_OFFSET : pd.bits_len;
-        const double w = (double)(b1 > b0 ? b1 - b0 : 0u) / wctb;
-        double t = 0.0;
-        for (int c = 0; c < wctb; ++c) {
-            const double above = r == 0 ? 0.0 : done[(size_t)(c == 0 ? std::min(1, wctb - 1) : c)];
-            t = std::max(t, above) + w;
-            done[(size_t)c] = t;
-        }
-    }
-    return done[(size_t)wctb - 1];
-}
-
 // Wave slot -> picture.  A wave runs until its heaviest picture is parsed,
 // and every extra busy picture in it adds divergent units to each pass, so
 // the critical path is the wave holding the most work.  Pictures are sorted
 // by payload size and dealt snake-wise (wave w of W gets ranks w, 2W-1-w,
 // 2W+w, 4W-1-w, ...): heavy beside light.  Empty slots are ~0u.
 // HEIFGPU_PARSE_ORDER=0: batch order (kept for the emulation test of an
-// unsorted dealing).  HEIFGPU_LANES_DEAL (read at every prepare; tuning):
-// "chain" sorts by wpp_chain_bytes instead of payload bytes (needs subs and
-// seqs), "light" / "chain_light" give wave w of the W leads (ranks 0..W-1)
-// the lightest remaining pictures in order (the heaviest lead the two
-// lightest), so the waves that set the kernel time carry the fewest busy
-// companions.
-int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order,
-                      const uint32_t *subs, const SeqParams *seqs) {
+// unsorted dealing).  (r06 A/B, DESIGN 5.13: dealing by WPP critical path, or
+// the lightest pictures beside each wave's heaviest, won only where a wave's
+// companions repeat one bitstream, on the permuted halfmoonbay shard; on
+// distinct tiles both were neutral or worse, so snake dealing stays.)
+int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
         return e ? std::atoi(e) : 1;
     }();
-    const char *deal_env = std::getenv("HEIFGPU_LANES_DEAL");
-    const std::string deal = deal_env ? deal_env : "";
-    const bool by_chain = (deal == "chain" || deal == "chain_light") && subs && seqs;
-    const bool light = deal == "light" || deal == "chain_light";
     const int full = 64 / (lane_rows < 1 ? 1 : (lane_rows > 64 ? 64 : lane_rows));
     const int ppw = ppw_force > 0 ? std::min(ppw_force, full) : lanes_pics_per_wave(lane_rows, n);
     if (!on || n <= 0) {
@@ -2333,34 +2304,10 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
     for (int i = 0; i < n; ++i)
         if (!(pics[i].flags & PD_ASSEMBLY)) by_size.push_back((uint32_t)i);
     n = (int)by_size.size();
-    std::vector<double> cost((size_t)(by_chain ? n : 0));
-    if (by_chain) {
-        for (int i = 0; i < n; ++i) {
-            const PicDesc &pd = pics[by_size[(size_t)i]];
-            const SeqParams &sp = seqs[pd.seq];
-            const int ctb = 1 << sp.log2_ctb;
-            cost[(size_t)i] = (sp.flags & SP_WPP) ? wpp_chain_bytes(pd, subs, (sp.width + ctb - 1) >> sp.log2_ctb)
-                                                  : (double)pd.bits_len;
-        }
-        std::vector<size_t> idx((size_t)n);
-        for (int i = 0; i < n; ++i) idx[(size_t)i] = (size_t)i;
-        std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return cost[x] > cost[y]; });
-        std::vector<uint32_t> t((size_t)n);
-        for (int i = 0; i < n; ++i) t[(size_t)i] = by_size[idx[(size_t)i]];
-        by_size.swap(t);
-    } else {
-        std::stable_sort(by_size.begin(), by_size.end(),
-                         [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
-    }
+    std::stable_sort(by_size.begin(), by_size.end(),
+                     [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
     const int W = (n + ppw - 1) / ppw;
     order.assign((size_t)W * ppw, ~0u);
-    if (light) {
-        for (int w = 0; w < W && w < n; ++w) order[(size_t)w * ppw] = by_size[(size_t)w];
-        int r = n - 1;  // the lightest remaining picture
-        for (int w = 0; w < W; ++w)
-            for (int k = 1; k < ppw && r >= W; ++k) order[(size_t)w * ppw + k] = by_size[(size_t)r--];
-        return ppw;
-    }
     for (int r = 0; r < n; ++r) {
         const int band = r / W, pos = r % W;
         const int w = (band & 1) ? W - 1 - pos : pos;
