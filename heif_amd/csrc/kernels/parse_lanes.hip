@@ -2320,11 +2320,12 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
 // own (every lane alike, so one syntax unit at a time with nothing else in
 // the pass), one workgroup per substream so a picture's rows spread over CUs:
 // far faster per substream than a lane of a packed wave, but 64 lanes do one
-// substream's work, so it is the latency path of small batches, where packed
-// waves cannot fill the SIMDs anyway.  MI355X, halfmoonbay permutations
-// (tools/lat_modes.sh, profiles/r03/latency_modes.json): 1 image 37 vs 71 ms
-// parse, 16 images 70 vs 83 ms, 32 images 117 vs 91 ms; so batches up to 768
-// pictures (16 such images) take spread mode.  HEIFGPU_PARSE=lanes|solo|spread
+// substream's work, so it is the latency path of small and middle batches,
+// where packed waves cannot fill the SIMDs anyway.  MI355X, halfmoonbay
+// permutations, row-major spread against lanes (profiles/r06/ab/ab_mid.txt,
+// Mpix/s): 4 images 1,677 / 910, 16 4,711 / 2,864, 32 6,787 / 6,174, 64 7,819
+// / 11,135; distinct tiles at 32 images 7,683 / 7,768.  So batches up to 1536
+// pictures (32 such images) take spread mode.  HEIFGPU_PARSE=lanes|solo|spread
 // forces a mode for every batch, HEIFGPU_SOLO_MAX_PICS moves the switch-over.
 int parse_mode_for(int requested, int n_pics) {
     static const int env = [] {
@@ -2338,7 +2339,7 @@ int parse_mode_for(int requested, int n_pics) {
     }();
     static const int max_pics = [] {
         const char *e = std::getenv("HEIFGPU_SOLO_MAX_PICS");
-        return e ? std::atoi(e) : 768;
+        return e ? std::atoi(e) : 1536;
     }();
     if (env != PARSE_AUTO) return env;
     if (requested == PARSE_LANES || requested == PARSE_SOLO || requested == PARSE_SPREAD)
@@ -2350,33 +2351,30 @@ int parse_mode_for(int requested, int n_pics) {
 // (1024 threads); taller pictures wrap their rows round the waves
 int solo_waves_for(int lane_rows) { return lane_rows < 1 ? 1 : (lane_rows > kSoloMaxWaves ? kSoloMaxWaves : lane_rows); }
 
-// spread mode: one wave slot per substream, entry row << 20 | picture; the
-// pictures by payload size (heaviest first, so the longest WPP chains start
-// first), a picture's rows consecutive and in order (a row waits only for a
-// lower slot, which a running wave holds: k_parse_solo<true> takes its slot
-// from the job counter)
-// HEIFGPU_SPREAD_ORDER=rows (read at every prepare; tuning): row-major
-// instead, row r of every picture before row r + 1 of any, so a row's wave
-// finds the row above long started instead of holding its slot while it waits
+// spread mode: one wave slot per substream, entry row << 20 | picture, in
+// row-major order: row r of every picture (heaviest picture first) before row
+// r + 1 of any.  A row's wave holds its slot (and its SIMD residency) from the
+// dequeue until the row is parsed; picture-major order (a picture's rows in
+// consecutive slots) filled the resident waves with rows waiting on the WPP
+// ramp of their own picture, row-major order finds the row above long started.
+// r06 A/B: 16 images 3,474 -> 4,711 Mpix/s, 32 images 3,847 ->
+// 6,787 (distinct tiles: 3,709 -> 6,651 and 3,994 -> 7,683), one image equal.
+// A row's predecessor keeps a lower slot, held by a running wave
+// (k_parse_solo<true> takes its slot from the job counter).
 int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order) {
     std::vector<uint32_t> by_size((size_t)n);
     for (int i = 0; i < n; ++i) by_size[(size_t)i] = (uint32_t)i;
     std::stable_sort(by_size.begin(), by_size.end(),
                      [&](uint32_t x, uint32_t y) { return pics[x].bits_len > pics[y].bits_len; });
-    const char *e = std::getenv("HEIFGPU_SPREAD_ORDER");
-    const bool row_major = e && std::string(e) == "rows";
     order.clear();
     uint32_t max_sub = 0;
     for (uint32_t p : by_size) {
         if (p >= (1u << 20) || pics[p].n_sub >= (1u << 12)) return -1;
         max_sub = std::max(max_sub, pics[p].n_sub);
-        if (!row_major)
-            for (uint32_t r = 0; r < pics[p].n_sub; ++r) order.push_back(p | (r << 20));
     }
-    if (row_major)
-        for (uint32_t r = 0; r < max_sub; ++r)
-            for (uint32_t p : by_size)
-                if (r < pics[p].n_sub) order.push_back(p | (r << 20));
+    for (uint32_t r = 0; r < max_sub; ++r)
+        for (uint32_t p : by_size)
+            if (r < pics[p].n_sub) order.push_back(p | (r << 20));
     return 1;
 }
 

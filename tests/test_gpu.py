@@ -301,20 +301,28 @@ def test_permuted_batch_row_parallel(H, ctx, oracle_tiles, halfmoonbay):
 
 
 def test_large_batch_many_waves(H, ctx, oracle_tiles, halfmoonbay):
-    """22 images = 1056 pictures: the adaptive lanes packing takes the fewest
-    pictures per wave that fit one wave per SIMD, 2 here (528 waves on the
-    1024 SIMDs), size-sorted snake order across waves, every image checked."""
+    """22 images = 1056 pictures.  AUTO takes the spread parse (up to 1536
+    pictures, rows dequeued in row-major order: 16,896 single-wave jobs, far
+    more than the chip holds at once).  Forced to lanes, the adaptive packing
+    takes the fewest pictures per wave that fit one wave per SIMD, 2 here
+    (528 waves on the 1024 SIMDs), size-sorted snake order across waves.
+    Every image checked in both."""
     from heif_amd.synthetic import permuted_heic
 
     seeds = list(range(100, 122))
     imgs = [H.HeifImage.parse(permuted_heic(halfmoonbay, s)) for s in seeds]
     outs = ctx.alloc_outputs(imgs)
-    b = ctx.prepare(imgs)
-    assert b.parse_geometry() == {"mode": "lanes", "workgroups": 528, "pics_per_wave": 2, "waves_per_workgroup": 1}
-    b.decode_async(outs)
-    assert not any(b.status())
-    check_permuted(outs, seeds, oracle_tiles)
-    b.free()
+    for parse, geom in (("auto", {"mode": "spread", "workgroups": 16896, "pics_per_wave": 1, "waves_per_workgroup": 1}),
+                        ("lanes", {"mode": "lanes", "workgroups": 528, "pics_per_wave": 2, "waves_per_workgroup": 1})):
+        b = ctx.prepare(imgs, parse=parse)
+        assert b.parse_geometry() == geom
+        for o in outs:
+            for t in (o.y, o.cb, o.cr):
+                t.fill_(0)
+        b.decode_async(outs)
+        assert not any(b.status())
+        check_permuted(outs, seeds, oracle_tiles)
+        b.free()
 
 
 def test_repeat_decode_is_deterministic(H, ctx, halfmoonbay):
