@@ -250,6 +250,31 @@ struct Frame {
     }
 };
 
+// Facts of one TB record that depend on the record and the picture only:
+// formed for 64 records at once, one per lane, when the wave loads them (the
+// per-TB checks on the scalar unit were a large part of k_intra's scalar
+// instructions), read back with one v_readlane per TB.  Bit 0 (TBM_OK): the
+// TB is this wave's component (cidx in [k0, k1)), has a mode of 8.4.2, and
+// lies inside the picture and inside the window of CTB tu.ctu of row r (the
+// parse keeps it so; the check keeps the tables in range).  Bit 1 (TBM_PAIR,
+// set by the caller): a 4x4 / 8x8 Cb TB whose next record is its Cr TB.
+// Bits 8-15: zc, the z-order index of the TB's first luma 4x4 block in its
+// CTU (6.4.1 availability).
+enum : uint32_t { TBM_OK = 1u, TBM_PAIR = 2u };
+template <typename Pel, int CF>
+__device__ __forceinline__ uint32_t tb_meta(const TuRec &q, const Frame<Pel, CF> &F, int r, int k0, int k1) {
+    const int k = q.flags & TU_CIDX_MASK, n = 1 << q.log2;
+    const int subx = k ? chroma_sx(CF) : 0, suby = k ? chroma_sy(CF) : 0;
+    const int lcx = F.log2ctb - subx, lcy = F.log2ctb - suby;
+    const int cx0 = (int)q.ctu << lcx, cy0 = r << lcy;
+    const int PW = k ? F.cw : F.W, PH = k ? F.ch : F.H;
+    const bool ok = k < (CF ? 3 : 1) && k >= k0 && k < k1 && q.mode <= 34 && q.log2 >= 2 && q.log2 <= 5 &&
+                    q.x + n <= PW && q.y + n <= PH && q.x >= cx0 && q.y >= cy0 && q.x + n <= cx0 + (1 << lcx) &&
+                    q.y + n <= cy0 + (1 << lcy);
+    const int zc = ok ? zidx((((int)q.x - cx0) << subx) >> 2, (((int)q.y - cy0) << suby) >> 2) : 0;
+    return (ok ? TBM_OK : 0u) | ((uint32_t)zc << 8);
+}
+
 #if !defined(HG_HOST_EMU)
 // the sum over the lanes of each aligned group of m (2 <= m <= 64, a power of
 // two) lanes, in every lane of the group: ds_swizzle xor steps inside 32-lane
@@ -268,7 +293,7 @@ __device__ __forceinline__ int group_sum(int v, int m) {
 template <typename Pel, int CF>
 __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L, const TuRec &tu, const Win<Pel> &w,
                                                                  int PW, int PH, int cidx, int bd, bool strong,
-                                                                 int lane) {
+                                                                 int zc, int lane) {
     constexpr int chroma = CF;
     const int log2n = tu.log2, n = 1 << log2n, mode = tu.mode;
     const int x0 = tu.x, y0 = tu.y;
@@ -277,7 +302,6 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     const int bx0 = w.cx0 << subx, by0 = w.cy0 << suby, csl = w.csx << subx;
     const int ns = 4 * n + 1;
     const bool cbf = (tu.flags & TU_CBF) != 0;
-    const int zc = zidx(((x0 << subx) - bx0) >> 2, ((y0 << suby) - by0) >> 2);
     // residual of a 4x4 / 8x8 TB (one sample per lane): loaded now, used after
     // the neighbour and filter phases, so the load latency hides behind them
     // (the TB's first residual, formed only where it is in bounds: a pointer moved
@@ -553,7 +577,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
 template <typename Pel>
 __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch *L, const TuRec &tb, const TuRec &tr,
                                                                    const Win<Pel> &wb, const Win<Pel> &wr, int PW,
-                                                                   int PH, int bd, int lane) {
+                                                                   int PH, int bd, int zc, int lane) {
     // lanes 0-31 predict Cb and 32-63 Cr: the pairing needs a full 64-lane wave
     static_assert(kWave == 64, "predict_pair splits a 64-lane wave into two halves");
     const int log2n = tb.log2, n = 1 << log2n, mode = tb.mode;
@@ -574,7 +598,6 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     const bool pcm = ((h ? tr.flags : tb.flags) & TU_PCM) != 0;
     const int bx0 = w.cx0 << 1, by0 = w.cy0 << 1, csl = w.csx << 1;
     const int ns = 4 * n + 1, nch = n == 8 ? 2 : 1;
-    const int zc = zidx(((x0 << 1) - bx0) >> 2, ((y0 << 1) - by0) >> 2);
     // residuals (sample sl and sl + 32 of this half), used after the neighbour phase
     int r0 = 0, r1 = 0;
     if (cbf && sl < n * n) r0 = w.res[(ptrdiff_t)(y0 + (sl >> log2n)) * w.rp + x0 + (sl & (n - 1))];
@@ -774,6 +797,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
         int cur = -1;
 #if !defined(HG_HOST_EMU)
         uint4 tblk = make_uint4(0, 0, 0, 0);  // lane l: TuRec t0 + l (one coalesced load per 64 TBs)
+        uint32_t metav = 0;                   // lane l: tb_meta of that record
         uint32_t t0 = 0;
 #endif
         for (uint32_t t = 0;; ++t) {
@@ -849,6 +873,23 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                     } else {
                         tblk = i < ntu ? *reinterpret_cast<const uint4 *>(tus + i) : make_uint4(0, 0, 0, 0);
                     }
+                    TuRec q;
+                    __builtin_memcpy(&q, &tblk, sizeof(q));
+                    metav = i < ntu ? tb_meta(q, F, r, k0, k1) : 0u;
+#if !defined(HG_INTRA_NO_PAIR)
+                    if constexpr (!XfInline && CF == 1) {
+                        // the next record (lane + 1; none past this block): its Cr TB?
+                        const int nl = min(lane + 1, 63);
+                        const uint4 nb = make_uint4((uint32_t)__shfl((int)tblk.x, nl, 64), (uint32_t)__shfl((int)tblk.y, nl, 64),
+                                                    (uint32_t)__shfl((int)tblk.z, nl, 64), (uint32_t)__shfl((int)tblk.w, nl, 64));
+                        TuRec nq;
+                        __builtin_memcpy(&nq, &nb, sizeof(nq));
+                        const bool pair = (metav & TBM_OK) && lane < 63 && i + 1 < ntu && (q.flags & TU_CIDX_MASK) == 1 &&
+                                          q.log2 <= 3 && (nq.flags & TU_CIDX_MASK) == 2 && nq.x == q.x && nq.y == q.y &&
+                                          nq.log2 == q.log2 && nq.mode == q.mode && nq.ctu == q.ctu;
+                        metav |= pair ? TBM_PAIR : 0u;
+                    }
+#endif
                 }
                 const int sel = (int)(t - t0);
                 const uint4 r = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)tblk.x, sel),
@@ -925,17 +966,18 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                 }
                 wave_sync();
             }
-            const int cidx = tu.flags & TU_CIDX_MASK;
-            if (cidx >= ncomp || cidx < k0 || cidx >= k1) continue;
+            // this wave's component, a valid TB of CTB `cur` (tb_meta): its facts for 64 records
+            // were formed at the block load
+#if defined(HG_HOST_EMU)
+            const uint32_t m = tb_meta(tu, F, r, k0, k1);
+#else
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)metav, (int)(t - t0));
+#endif
+            if (!(m & TBM_OK)) continue;
+            const int cidx = tu.flags & TU_CIDX_MASK, zc = (int)((m >> 8) & 0xffu);
             // the TB's component window, formed here from the wave-uniform cidx and CTU
             Win<Pel> w = F.win(cidx, cur, r);
             const int PW = cidx ? cw : W, PH = cidx ? ch : H;
-            // a TB must lie inside the picture and inside its CTU window, with a mode
-            // of 8.4.2 (the parse keeps it so; the check keeps the tables in range)
-            if (tu.mode > 34 || tu.log2 < 2 || tu.log2 > 5 || tu.x + (1 << tu.log2) > PW || tu.y + (1 << tu.log2) > PH ||
-                tu.x < w.cx0 || tu.y < w.cy0 || tu.x + (1 << tu.log2) > w.cx0 + w.csx ||
-                tu.y + (1 << tu.log2) > w.cy0 + w.csy)
-                continue;
             if constexpr (XfInline) {
                 // the TB's residual, transformed by this wave into LDS (pitch n, origin the TB's)
                 if (tu.flags & TU_CBF) {
@@ -954,23 +996,15 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
 #if !defined(HG_HOST_EMU) && !defined(HG_INTRA_NO_PAIR)
             // a 4x4 / 8x8 Cb TB followed by its Cr TB (same TU; the next record of this 64-record block):
             // both in one pass
-            if (!XfInline && cidx == 1 && chroma == 1 && tu.log2 <= 3 && t + 1 < ntu && ((t + 1) & 63u) != 0) {
-                const int sel = (int)(t + 1 - t0);
-                const uint4 rn = make_uint4((uint32_t)__builtin_amdgcn_readlane((int)tblk.x, sel),
-                                            (uint32_t)__builtin_amdgcn_readlane((int)tblk.y, sel),
-                                            (uint32_t)__builtin_amdgcn_readlane((int)tblk.z, sel),
-                                            (uint32_t)__builtin_amdgcn_readlane((int)tblk.w, sel));
-                TuRec tr;
-                __builtin_memcpy(&tr, &rn, sizeof(tr));
-                if ((tr.flags & TU_CIDX_MASK) == 2 && tr.x == tu.x && tr.y == tu.y && tr.log2 == tu.log2 &&
-                    tr.mode == tu.mode && tr.ctu == tu.ctu) {
-                    predict_pair<Pel>(S, tu, tr, F.win(1, cur, r), F.win(2, cur, r), PW, PH, sp.bit_depth_c, lane);
-                    ++t;
-                    continue;
-                }
+            if (!XfInline && (m & TBM_PAIR)) {  // (the next record is its Cr TB: tb_meta)
+                TuRec tr = tu;  // same position, size, mode and CTU; the flags are the Cr TB's
+                tr.flags = (uint8_t)((uint32_t)__builtin_amdgcn_readlane((int)tblk.y, (int)(t + 1 - t0)) >> 8);
+                predict_pair<Pel>(S, tu, tr, F.win(1, cur, r), F.win(2, cur, r), PW, PH, sp.bit_depth_c, zc, lane);
+                ++t;
+                continue;
             }
 #endif
-            predict_tb<Pel, CF>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, lane);
+            predict_tb<Pel, CF>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, zc, lane);
         }
         if (gave_up) {  // (the waves below see it and give up too)
             hg_atomic_store(&progress[wave], kGaveUp);
