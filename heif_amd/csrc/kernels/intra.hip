@@ -260,7 +260,12 @@ struct Frame {
 // set by the caller): a 4x4 / 8x8 Cb TB whose next record is its Cr TB.
 // Bits 8-15: zc, the z-order index of the TB's first luma 4x4 block in its
 // CTU (6.4.1 availability).
-enum : uint32_t { TBM_OK = 1u, TBM_PAIR = 2u };
+// Bit 2 (TBM_FILT): the TB's neighbours are filtered (8.4.4.2.3: luma, or
+// chroma with 4:4:4; not DC, not 4x4; the mode farther from horizontal and
+// vertical than the size's threshold).  A second word per record (tb_angle)
+// holds intraPredAngle and invAngle (8.4.4.2.6), read by one vector load per
+// 64 records instead of two scalar loads from constant memory per TB.
+enum : uint32_t { TBM_OK = 1u, TBM_PAIR = 2u, TBM_FILT = 4u };
 template <typename Pel, int CF>
 __device__ __forceinline__ uint32_t tb_meta(const TuRec &q, const Frame<Pel, CF> &F, int r, int k0, int k1) {
     const int k = q.flags & TU_CIDX_MASK, n = 1 << q.log2;
@@ -272,7 +277,15 @@ __device__ __forceinline__ uint32_t tb_meta(const TuRec &q, const Frame<Pel, CF>
                     q.x + n <= PW && q.y + n <= PH && q.x >= cx0 && q.y >= cy0 && q.x + n <= cx0 + (1 << lcx) &&
                     q.y + n <= cy0 + (1 << lcy);
     const int zc = ok ? zidx((((int)q.x - cx0) << subx) >> 2, (((int)q.y - cy0) << suby) >> 2) : 0;
-    return (ok ? TBM_OK : 0u) | ((uint32_t)zc << 8);
+    const int dist = min(abs((int)q.mode - 26), abs((int)q.mode - 10));
+    const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
+    const bool filt = (k == 0 || CF == 3) && q.mode != 1 && n != 4 && dist > thr;
+    return (ok ? TBM_OK : 0u) | (filt ? TBM_FILT : 0u) | ((uint32_t)zc << 8);
+}
+// intraPredAngle (low byte, signed) and invAngle (high half, signed) of a record's mode
+__device__ __forceinline__ uint32_t tb_angle(const TuRec &q) {
+    const int m = q.mode <= 34 ? q.mode : 0;
+    return (uint32_t)(uint8_t)c_angle[m] | ((uint32_t)(uint16_t)c_inv_angle[m] << 16);
 }
 
 #if !defined(HG_HOST_EMU)
@@ -293,7 +306,7 @@ __device__ __forceinline__ int group_sum(int v, int m) {
 template <typename Pel, int CF>
 __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L, const TuRec &tu, const Win<Pel> &w,
                                                                  int PW, int PH, int cidx, int bd, bool strong,
-                                                                 int zc, int lane) {
+                                                                 int zc, bool filt, uint32_t am, int lane) {
     constexpr int chroma = CF;
     const int log2n = tu.log2, n = 1 << log2n, mode = tu.mode;
     const int x0 = tu.x, y0 = tu.y;
@@ -471,10 +484,8 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     wave_sync();
     // 3. filtering (8.4.4.2.3): luma, and chroma with 4:4:4
     const int16_t *lf = L->left, *tp = L->top;
-    if ((cidx == 0 || chroma == 3) && mode != 1 && n != 4) {
-        const int dist = min(abs(mode - 26), abs(mode - 10));
-        const int thr = n == 8 ? 7 : (n == 16 ? 1 : 0);
-        if (dist > thr) {
+    {
+        if (filt) {  // (tb_meta: luma or 4:4:4 chroma, not DC, not 4x4, the mode past the threshold)
             const int c = L->left[0];
             const bool bi = strong && cidx == 0 && n == 32 && abs(c + L->top[64] - 2 * L->top[32]) < (1 << (bd - 5)) &&
                             abs(c + L->left[64] - 2 * L->left[32]) < (1 << (bd - 5));
@@ -534,7 +545,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
                 else if (x == 0) pv = (lf[1 + y] + 3 * dc + 2) >> 2;
             }
         } else {
-            const int ang = c_angle[mode], inv = c_inv_angle[mode];
+            const int ang = (int)(int8_t)(am & 0xffu), inv = (int)(int16_t)(am >> 16);  // (tb_angle)
             const int16_t *main_ = mode >= 18 ? tp : lf, *side = mode >= 18 ? lf : tp;
             const int a = mode >= 18 ? x : y, b = mode >= 18 ? y : x;  // a along the main direction
             const int idx = ((b + 1) * ang) >> 5, fact = ((b + 1) * ang) & 31;
@@ -577,7 +588,7 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
 template <typename Pel>
 __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch *L, const TuRec &tb, const TuRec &tr,
                                                                    const Win<Pel> &wb, const Win<Pel> &wr, int PW,
-                                                                   int PH, int bd, int zc, int lane) {
+                                                                   int PH, int bd, int zc, uint32_t am, int lane) {
     // lanes 0-31 predict Cb and 32-63 Cr: the pairing needs a full 64-lane wave
     static_assert(kWave == 64, "predict_pair splits a 64-lane wave into two halves");
     const int log2n = tb.log2, n = 1 << log2n, mode = tb.mode;
@@ -669,7 +680,7 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     const int16_t *lf = left, *tp = top;
     const int maxv = (1 << bd) - 1;
     int dc = 0;
-    const int ang = c_angle[mode], inv = c_inv_angle[mode];
+    const int ang = (int)(int8_t)(am & 0xffu), inv = (int)(int16_t)(am >> 16);  // (tb_angle)
     const int16_t *main_ = mode >= 18 ? tp : lf, *side = mode >= 18 ? lf : tp;
     if (mode == 1) {  // each half sums its 2n <= 16 references in its lanes 0 .. 2n - 1
         const int sum = group_sum(sl < 2 * n ? (sl < n ? tp[1 + sl] : lf[1 + sl - n]) : 0, 2 * n);
@@ -797,7 +808,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
         int cur = -1;
 #if !defined(HG_HOST_EMU)
         uint4 tblk = make_uint4(0, 0, 0, 0);  // lane l: TuRec t0 + l (one coalesced load per 64 TBs)
-        uint32_t metav = 0;                   // lane l: tb_meta of that record
+        uint32_t metav = 0, anglev = 0;       // lane l: tb_meta and tb_angle of that record
         uint32_t t0 = 0;
 #endif
         for (uint32_t t = 0;; ++t) {
@@ -876,6 +887,7 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
                     TuRec q;
                     __builtin_memcpy(&q, &tblk, sizeof(q));
                     metav = i < ntu ? tb_meta(q, F, r, k0, k1) : 0u;
+                    anglev = tb_angle(q);
 #if !defined(HG_INTRA_NO_PAIR)
                     if constexpr (!XfInline && CF == 1) {
                         // the next record (lane + 1; none past this block): its Cr TB?
@@ -974,6 +986,11 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
             const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)metav, (int)(t - t0));
 #endif
             if (!(m & TBM_OK)) continue;
+#if defined(HG_HOST_EMU)
+            const uint32_t am = tb_angle(tu);
+#else
+            const uint32_t am = (uint32_t)__builtin_amdgcn_readlane((int)anglev, (int)(t - t0));
+#endif
             const int cidx = tu.flags & TU_CIDX_MASK, zc = (int)((m >> 8) & 0xffu);
             // the TB's component window, formed here from the wave-uniform cidx and CTU
             Win<Pel> w = F.win(cidx, cur, r);
@@ -999,12 +1016,13 @@ __device__ __attribute__((always_inline)) inline void intra_body(const BatchArgs
             if (!XfInline && (m & TBM_PAIR)) {  // (the next record is its Cr TB: tb_meta)
                 TuRec tr = tu;  // same position, size, mode and CTU; the flags are the Cr TB's
                 tr.flags = (uint8_t)((uint32_t)__builtin_amdgcn_readlane((int)tblk.y, (int)(t + 1 - t0)) >> 8);
-                predict_pair<Pel>(S, tu, tr, F.win(1, cur, r), F.win(2, cur, r), PW, PH, sp.bit_depth_c, zc, lane);
+                predict_pair<Pel>(S, tu, tr, F.win(1, cur, r), F.win(2, cur, r), PW, PH, sp.bit_depth_c, zc, am, lane);
                 ++t;
                 continue;
             }
 #endif
-            predict_tb<Pel, CF>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, zc, lane);
+            predict_tb<Pel, CF>(S, tu, w, PW, PH, cidx, cidx ? sp.bit_depth_c : sp.bit_depth_y, strong, zc,
+                                (m & TBM_FILT) != 0, am, lane);
         }
         if (gave_up) {  // (the waves below see it and give up too)
             hg_atomic_store(&progress[wave], kGaveUp);
