@@ -3,6 +3,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
+mkdir -p gpurun_out/r06
 timeout -k 10 600 bash tools/ab.sh full iabl_TB:HEIFGPU_LIBRARY=heif_amd/libheifgpu_iabl_TB.so iabl_GATHER:HEIFGPU_LIBRARY=heif_amd/libheifgpu_iabl_GATHER.so iabl_PRED:HEIFGPU_LIBRARY=heif_amd/libheifgpu_iabl_PRED.so &&
 cd /tmp && export TMPDIR=/tmp &&
 for v in full iabl_TB iabl_GATHER iabl_PRED; do
@@ -21,3 +22,4 @@ for v in ("full", "iabl_TB", "iabl_GATHER", "iabl_PRED"):
     n = max(1, len(nd))
     print(f"{v:>12} k_intra per launch: " + "  ".join(f"{k[9:]} {x / n / 1e9:.3f} G" for k, x in sorted(acc.items())))
 PY
+cd "$R" && timeout -k 10 600 python3 -u tools/r06/mixed_parse.py 16,16,1 24,8,1 32,16,1 32,32,2 16,48,2 > gpurun_out/r06/mixed_parse.log 2>&1; cat gpurun_out/r06/mixed_parse.log

@@ -9,6 +9,7 @@ This prints how the waves' end times spread (the kernel ends with its last
 wave), the passes and times of every wave composition (source tiles of the
 permuted halfmoonbay batch) and which waves shared a SIMD.
 """
+import collections
 import ctypes
 import json
 import os
@@ -96,11 +97,15 @@ def main():
                           "dur_ms_mean": round(statistics.mean(r["dur"] for r in v), 3),
                           "us_per_pass": round(1e3 * statistics.mean(r["dur"] for r in v) / max(v[0]["passes"], 1), 3)}
                          for k, v in by_comp],
+        # wave-index offsets of the waves sharing a SIMD (the dispatcher's pairing rule)
+        "simd_pair_offsets": dict(sorted(collections.Counter(
+            max(ws) - min(ws) for ws in simds.values() if len(ws) == 2).most_common(8))),
         "simd_pairs_top": [{"pair": [list(t) for t in k], "simds": c} for k, c in
                            sorted(pairs.items(), key=lambda kv: -kv[1])[:40]],
         "note": "s_memrealtime 100 MHz; tiles = source tiles of the wave's pictures (dealing order)",
     }
-    print(json.dumps({k: res[k] for k in ("wave_end_ms", "passes", "parse_ms_hip_events", "waves_per_simd")}))
+    print(json.dumps({k: res[k] for k in ("wave_end_ms", "passes", "parse_ms_hip_events", "waves_per_simd",
+                                          "simd_pair_offsets")}))
     if len(sys.argv) > 2:
         pathlib.Path(sys.argv[2]).write_text(json.dumps(res, indent=1) + "\n")
 
