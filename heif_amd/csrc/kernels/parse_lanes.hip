@@ -2286,7 +2286,10 @@ inline int lanes_pics_per_wave(int lane_rows, int n_pics) {
 // unsorted dealing).  (r06 A/B, DESIGN 5.13: dealing by WPP critical path, or
 // the lightest pictures beside each wave's heaviest, won only where a wave's
 // companions repeat one bitstream, on the permuted halfmoonbay shard; on
-// distinct tiles both were neutral or worse, so snake dealing stays.)
+// distinct tiles both were neutral or worse, so snake dealing stays.  The
+// dispatcher puts waves w and w + W/2 on one SIMD; pairing the heaviest wave
+// with the lightest moved nothing, and the heaviest pictures two per wave (the
+// rest four) lost 7.7 %: a wave's time is its heaviest picture's chain.)
 int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, std::vector<uint32_t> &order) {
     static const int on = [] {
         const char *e = std::getenv("HEIFGPU_PARSE_ORDER");
