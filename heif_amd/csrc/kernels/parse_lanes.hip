@@ -232,11 +232,13 @@ struct Lane {
 #endif
 };
 #if defined(HG_PARSE_PROF_SB) && !defined(HG_HOST_EMU)
-#define HG_SB_T(L, i, t0)                                      \
-    do {                                                       \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();      \
-        (L).psb[i] += t_ - (t0);                               \
-        (t0) = t_;                                             \
+// (the lowest active lane accumulates: in the lanes kernel the lanes running
+// the unit share one timeline, so the psb sums over lanes are the wave's time)
+#define HG_SB_T(L, i, t0)                                                            \
+    do {                                                                             \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                            \
+        if ((int)__lane_id() == __builtin_ctzll(__ballot(1))) (L).psb[i] += t_ - (t0); \
+        (t0) = t_;                                                                   \
     } while (0)
 #else
 #define HG_SB_T(L, i, t0) ((void)0)
@@ -1816,16 +1818,34 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
         const int cbase = CTX_SIG + (cidx ? 27 : 0);
         auto cb = [&](int i) { return ctx_ld(L, G, cbase + i); };
         uint64_t seq = G.seqw(L.rc_scan * 5 + (l2 == 2 ? 4 : pcs));  // slot per scan position
-        uint32_t c0, c1 = 0, c2 = 0;
+        uint32_t c0 = 0, c1 = 0, c2 = 0;
+        // vector engines: the sub-block's (up to 9) context states as 7-bit fields
+        // of one 64-bit word, slot k at bit 7k (a state byte is below 128:
+        // pStateIdx << 1 | valMps), so a slot is one 64-bit shift and mask each way.
+        // The 3-word byte cache the scalar engine keeps took two compares, two
+        // selects and a bit-field extract to read a slot and three selects to
+        // write it back.  r06 A/B (profiles/r06/ab/ab_cc7.txt): 22,805 -> 23,052
+        // Mpix/s at 128 images; in the scalar engine's 4x4 loop the same fields
+        // cost one image 24.88 -> 25.2 ms, so it keeps its byte word and slot 8
+        constexpr bool kCc7 = !EG::kSolo;
+        uint64_t cc = 0;
         int off = 0;
         if (l2 == 2) {
-            c0 = cb(0) | (cb(1) << 8) | (cb(2) << 16) | (cb(3) << 24);
-            c1 = cb(4) | (cb(5) << 8) | (cb(6) << 16) | (cb(7) << 24);
-            c2 = cb(8);
+            if constexpr (kCc7) {
+                for (int k = 0; k < 9; ++k) cc |= (uint64_t)cb(k) << (7 * k);
+            } else {
+                c0 = cb(0) | (cb(1) << 8) | (cb(2) << 16) | (cb(3) << 24);
+                c1 = cb(4) | (cb(5) << 8) | (cb(6) << 16) | (cb(7) << 24);
+                c2 = cb(8);
+            }
         } else {
             off = cidx == 0 ? ((xS | yS) ? 3 : 0) + (l2 == 3 ? (L.rc_scan == 0 ? 9 : 15) : 21) : (l2 == 3 ? 9 : 12);
             if ((xS | yS) == 0) seq &= ~0xfull;  // DC of the TB (scan position 0 of sub-block 0): sigCtx 0
-            c0 = cb(0) | (cb(off) << 8) | (cb(off + 1) << 16) | (cb(off + 2) << 24);
+            if constexpr (kCc7)
+                cc = (uint64_t)cb(0) | ((uint64_t)cb(off) << 7) | ((uint64_t)cb(off + 1) << 14) |
+                     ((uint64_t)cb(off + 2) << 21);
+            else
+                c0 = cb(0) | (cb(off) << 8) | (cb(off + 1) << 16) | (cb(off + 2) << 24);
         }
         HG_SB_T(L, 0, tsb);
         if constexpr (EG::kSolo) {
@@ -1874,10 +1894,18 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             // for the inferred DC at every position: parse alone 63.1 -> 59.9 ms,
             // 18,770 -> 19,260 Mpix/s at 128 images)
             auto dec_slot = [&](int slot) -> uint32_t {
-                uint32_t cs = cache_get(c0, c1, c2, slot);
-                const uint32_t bin = (uint32_t)dec_s(L, G, cs);
-                cache_put(c0, c1, c2, slot, cs);
-                return bin;
+                if constexpr (kCc7) {
+                    const uint32_t sh = (uint32_t)slot * 7u;
+                    uint32_t cs = (uint32_t)(cc >> sh) & 0x7fu;
+                    const uint32_t bin = (uint32_t)dec_s(L, G, cs);
+                    cc = (cc & ~(0x7full << sh)) | ((uint64_t)cs << sh);
+                    return bin;
+                } else {
+                    uint32_t cs = cache_get(c0, c1, c2, slot);
+                    const uint32_t bin = (uint32_t)dec_s(L, G, cs);
+                    cache_put(c0, c1, c2, slot, cs);
+                    return bin;
+                }
             };
             for (int nn = nstart; nn > 0; --nn) sig |= dec_slot((int)((seq >> (4 * nn)) & 15u)) << nn;
             if (nstart >= 0) {
@@ -1886,7 +1914,16 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             }
         }
         auto cw = [&](int i, uint32_t v) { ctx_st(L, G, cbase + i, v & 0xffu); };
-        if (l2 == 2) {
+        if constexpr (kCc7) {
+            if (l2 == 2) {
+                for (int k = 0; k < 9; ++k) cw(k, (uint32_t)(cc >> (7 * k)) & 0x7fu);
+            } else {
+                cw(0, (uint32_t)cc & 0x7fu);
+                cw(off, (uint32_t)(cc >> 7) & 0x7fu);
+                cw(off + 1, (uint32_t)(cc >> 14) & 0x7fu);
+                cw(off + 2, (uint32_t)(cc >> 21) & 0x7fu);
+            }
+        } else if (l2 == 2) {
             for (int k = 0; k < 4; ++k) cw(k, c0 >> (8 * k));
             for (int k = 0; k < 4; ++k) cw(4 + k, c1 >> (8 * k));
             cw(8, c2);
@@ -2611,6 +2648,9 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     s_prog[lane] = 0;
     const bool live = in && lane_init(L, P, ld, a, pic, row, pl * a.lane_rows, a.lane_rows);
     if (!live) L.st = U_DONE;
+#if defined(HG_PARSE_PROF_SB)
+    for (int k = 0; k < 6; ++k) L.psb[k] = 0;
+#endif
     __syncthreads();
     const Env E{&a, s_lds, s_prog, s_wctx, lane};
 #if defined(HG_NO_SCAN8)
@@ -2660,6 +2700,12 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     pf[0] = __builtin_amdgcn_s_memtime() - t_start;
     if (lane == 0)
         for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[k], (unsigned long long)pf[k]);
+#if defined(HG_PARSE_PROF_SB)
+    // the sub-block unit's phases (slots 8..13: header, sig loop, greater1/2,
+    // signs + remainders + record, sig bins, -), the wave's time: one lane per run
+    if (live)
+        for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[8 + k], (unsigned long long)L.psb[k]);
+#endif
     // per wave (the CTU-time slots, unused by this kernel): s_memrealtime at its start, its
     // duration and place, then the passes and its first three pictures (16 bits each; 0xffff: none)
     if (blockIdx.x < (unsigned)kCtuTimeCap) {

@@ -51,6 +51,24 @@ def main():
     parse_ms = ctx.stage_times()[0]
     lib.heifgpu_debug_counters(buf, 16)
     waves = geom["workgroups"] * geom["waves_per_workgroup"]
+    if "profsb" in str(_lib.LIB_PATH) and geom["mode"] == "lanes":
+        # `make prof-sb`, lanes kernel: the unit kinds (slots 0-7) and the sub-block
+        # unit's phases as the wave's time (slots 8-12, one lane per unit run)
+        names = LANES + ["sb_head", "sb_sig", "sb_g1", "sb_rest", "sig_bins"]
+        c = dict(zip(names, buf[:13]))
+        sb = max(c["sb"], 1)
+        res = {"images": n, "geometry": geom, "waves": waves, "parse_ms": round(parse_ms, 3),
+               "per_wave": {k2: round(c[k2] / waves, 1) for k2 in names},
+               "unit_cycle_share": {k2: round(c[k2] / max(c["cycles"], 1), 3) for k2 in ("ctu", "tree", "tb", "sb", "ctu_end")},
+               "sb_phase_share": {k2: round(c[k2] / sb, 3) for k2 in ("sb_head", "sb_sig", "sb_g1", "sb_rest")},
+               "sb_cycles_per_sig_bin_lane": round(c["sb_sig"] / max(c["sig_bins"], 1), 2),
+               "note": "s_memtime cycles of the counter build; sb phases: header (coded_sub_block_flag, context "
+                       "gather), sig_coeff_flag loop, greater1/2, signs + remainders + record store; the wave's "
+                       "time (one lane accumulates per unit run); sig_bins summed over lanes"}
+        print(json.dumps(res))
+        if len(sys.argv) > 2:
+            pathlib.Path(sys.argv[2]).write_text(json.dumps(res, indent=1) + "\n")
+        return
     if "profsb" in str(_lib.LIB_PATH):  # `make prof-sb`: solo / spread sub-block phases
         names = ["cycles", "wait", "sb_head", "sb_sig", "sb_g1", "sb_rest", "sig_bins", "coefs", "driver"]
         c = dict(zip(names, buf[:9]))
