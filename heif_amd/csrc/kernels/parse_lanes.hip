@@ -86,6 +86,9 @@ __device__ uint64_t g_prof_lanes[16];  // 8 used; 16 in the prof-sb build
 // the end of its U_CTU_END unit (heifgpu_debug_counters slots 8 on)
 constexpr int kCtuTimeCap = 1 << 17;
 __device__ uint64_t g_ctu_t[kCtuTimeCap][3];
+// k_parse_lanes (one wave per workgroup): records kWaveRec.. of g_ctu_t hold
+// each wave's own cycle breakdown, three records per wave (five in prof-sb)
+constexpr int kWaveRec = 4096, kWaveRecCap = 4096;
 #endif
 
 namespace {
@@ -102,20 +105,23 @@ HG_HD inline uint64_t state_row(int st) {
     return r | (lps_next << 32) | (mps_next << 40);
 }
 
-// Vector engines (lanes, rows): one row per context byte s = pStateIdx << 1 |
-// valMps, valMps folded in: rangeTabLps[4], the next context byte after an LPS
-// and after an MPS, then the bin an LPS and an MPS decode to (bits 48 / 56).
-// A decision indexes it by the byte itself and reads the new byte and the bin
-// from one shift (no valMps extraction, XOR or row-index masking; r05 A/B at
-// 128 images: 18,770 vs 18,590 Mpix/s)
-// (A/B r05: the decoded bin in bit 7 of the context byte, 256 rows, one shift
-// less per decision: 19,020 vs 19,200 Mpix/s, rejected)
+// Vector engines (lanes): one row per context byte s = pStateIdx << 1 |
+// valMps, valMps folded in: rangeTabLps[4], then the next context byte after
+// an LPS (bits 32-38) and after an MPS (bits 40-46), each with the bin that
+// path decodes to in its bit 7.  A decision indexes it by the byte itself and
+// reads the new byte and the bin from one shift (no valMps extraction, XOR or
+// row-index masking; r05 A/B at 128 images: 18,770 vs 18,590 Mpix/s); a
+// register cache inserts the shifted byte under a 7-bit mask (v_bfi), so the
+// bin bit costs no extra mask there (dec_t; r06 A/B: VALU 19.92 -> 19.60 G per
+// launch, 23,056 -> 23,108 Mpix/s, profiles/r06/ab/ab_bfi.txt).
+// (A/B r05: the decoded bin in bit 7 of the context byte itself, 256 rows:
+// 19,020 vs 19,200 Mpix/s, rejected)
 constexpr int kTabRows = 128;
 HG_HD inline uint64_t state_row_ctx(int s) {
     const uint64_t r = state_row(s >> 1);
     const uint64_t mps = (uint64_t)(s & 1);
-    return (r & 0xffffffffull) | ((((r >> 32) & 0xffu) ^ mps) << 32) | ((((r >> 40) & 0xffu) ^ mps) << 40) |
-           ((mps ^ 1u) << 48) | (mps << 56);
+    return (r & 0xffffffffull) | (((((r >> 32) & 0xffu) ^ mps) | ((mps ^ 1u) << 7)) << 32) |
+           (((((r >> 40) & 0xffu) ^ mps) | (mps << 7)) << 40);
 }
 
 constexpr uint32_t kProgDone = 0x7fffffffu;
@@ -735,23 +741,44 @@ HG_HD inline void engine_init(Lane &L, const EG &G, uint32_t start, uint32_t end
 // DecodeDecision (arithmetic.rs:97-144), branch-free: one row per pStateIdx
 // gives rangeTabLps and both transitions; the renormalisation of either path
 // is a shift by clz and lowers k.
+// (a & m) | (b & ~m) as one v_bfi_b32: written as C the compiler re-masks the
+// inserted value first (a bit-field extract of the row, then the OR)
+HG_HD inline uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b) {
+#if !defined(HG_HOST_EMU) && defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+#else
+    return (a & m) | (b & ~m);
+#endif
+}
+
+// (vector engines, state_row_ctx) a decision on context byte s; t receives
+// the new byte in bits 0-6 and the bin in bit 7, bits above are not cleared
+template <class EG>
+HG_HD inline int dec_t(Lane &L, const EG &G, uint32_t s, uint32_t &t) {
+    const uint64_t row = G.row(s);
+    const uint32_t lps = ((uint32_t)row >> ((L.range >> 3) & 24u)) & 0xffu;
+    const uint32_t rm = L.range - lps;
+    const uint32_t sr = rm << L.k;
+    const bool isl = L.value >= sr;
+    L.value -= isl ? sr : 0u;
+    const uint32_t rn = isl ? lps : rm;
+    const int nb = __builtin_clz(rn) - 23;
+    L.range = rn << nb;
+    L.k -= nb;
+    t = (uint32_t)(row >> (isl ? 32 : 40));
+    if (L.k < 8) vfill(L, G);
+    return (int)((t >> 7) & 1u);
+}
+
 template <class EG>
 HG_HD inline int dec_s(Lane &L, const EG &G, uint32_t &s) {
     if constexpr (EG::kRowCtx) {
-        const uint64_t row = G.row(s);
-        const uint32_t lps = ((uint32_t)row >> ((L.range >> 3) & 24u)) & 0xffu;
-        const uint32_t rm = L.range - lps;
-        const uint32_t sr = rm << L.k;
-        const bool isl = L.value >= sr;
-        L.value -= isl ? sr : 0u;
-        const uint32_t rn = isl ? lps : rm;
-        const int nb = __builtin_clz(rn) - 23;
-        L.range = rn << nb;
-        L.k -= nb;
-        const uint32_t t = (uint32_t)(row >> (isl ? 32 : 40));
-        s = t & 0xffu;
-        if (L.k < 8) vfill(L, G);
-        return (int)((t >> 16) & 1u);
+        uint32_t t;
+        const int bin = dec_t(L, G, s, t);
+        s = t & 0x7fu;
+        return bin;
     }
     const uint32_t st = s >> 1, mps = s & 1u;
     const uint64_t row = G.row(st);
@@ -1895,10 +1922,15 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
             // 18,770 -> 19,260 Mpix/s at 128 images)
             auto dec_slot = [&](int slot) -> uint32_t {
                 if constexpr (kCc7) {
+                    // the new byte goes in under the field's mask (v_bfi), which
+                    // also drops dec_t's bin bit
                     const uint32_t sh = (uint32_t)slot * 7u;
-                    uint32_t cs = (uint32_t)(cc >> sh) & 0x7fu;
-                    const uint32_t bin = (uint32_t)dec_s(L, G, cs);
-                    cc = (cc & ~(0x7full << sh)) | ((uint64_t)cs << sh);
+                    const uint64_t m = 0x7full << sh;
+                    uint32_t t;
+                    const uint32_t bin = (uint32_t)dec_t(L, G, (uint32_t)(cc >> sh) & 0x7fu, t);
+                    const uint64_t tv = (uint64_t)t << sh;
+                    cc = (uint64_t)bfi32((uint32_t)m, (uint32_t)tv, (uint32_t)cc) |
+                         ((uint64_t)bfi32((uint32_t)(m >> 32), (uint32_t)(tv >> 32), (uint32_t)(cc >> 32)) << 32);
                     return bin;
                 } else {
                     uint32_t cs = cache_get(c0, c1, c2, slot);
@@ -1907,7 +1939,17 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
                     return bin;
                 }
             };
-            for (int nn = nstart; nn > 0; --nn) sig |= dec_slot((int)((seq >> (4 * nn)) & 15u)) << nn;
+            if constexpr (kCc7) {
+                // the slot of position nn taken from the top nibble of a copy of
+                // seq shifted left one nibble per position (no per-lane shift count)
+                uint64_t sq = nstart > 0 ? seq << (4 * (15 - nstart)) : 0ull;
+                for (int nn = nstart; nn > 0; --nn) {
+                    sig |= dec_slot((int)(uint32_t)(sq >> 60)) << nn;
+                    sq <<= 4;
+                }
+            } else {
+                for (int nn = nstart; nn > 0; --nn) sig |= dec_slot((int)((seq >> (4 * nn)) & 15u)) << nn;
+            }
             if (nstart >= 0) {
                 if (infer_dc && sig == 0) sig |= 1u;
                 else sig |= dec_slot((int)(seq & 15u));
@@ -1974,9 +2016,10 @@ HG_HD inline void unit_sb(Lane &L, LaneLds &ld, LanePic &P, const EG &G) {
                 const int nn = msb32(m);
                 m &= ~(1u << nn);
                 const int gs = (c1 < 3 ? c1 : 3) * 8;
-                uint32_t cs = (gc >> gs) & 0xffu;
-                const int f = dec_s(L, G, cs);
-                gc = (gc & ~(0xffu << gs)) | (cs << gs);
+                const uint32_t gm = 0x7fu << gs;  // (bit 7 of every byte of gc stays 0)
+                uint32_t t;
+                const int f = dec_t(L, G, (gc >> gs) & 0xffu, t);
+                gc = bfi32(gm, t << gs, gc);
                 ++num_g1;
                 g1 |= (uint32_t)f << nn;
                 if (c1 > 0) c1 = f ? 0 : c1 + 1;
@@ -2663,10 +2706,20 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
     const uint64_t t_start = __builtin_amdgcn_s_memtime();
     const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
+#if defined(HG_PARSE_PROF)
+    uint64_t pw = 0;                                // the passes' start (pass_wait, q_refill)
+    uint32_t kc[U_CTU_END] = {0, 0, 0, 0, 0, 0, 0};  // passes that ran each unit kind
+#endif
     for (uint32_t pass = 0;; ++pass) {
         if (!__any(L.st != U_DONE)) break;
+#if defined(HG_PARSE_PROF)
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
         pass_wait();
         if (live) q_refill(L, G);
+#if defined(HG_PARSE_PROF)
+        pw += __builtin_amdgcn_s_memtime() - t0;
+#endif
         // one pass: every unit kind in syntax order, each run by the lanes in it
         // (a uniform loop: the units are never linearised into one divergent region)
         bool progressed = false;
@@ -2676,6 +2729,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
             if (!__any(mine)) continue;
             progressed = true;
 #if defined(HG_PARSE_PROF)
+            ++kc[kind - 1];
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
             pf[7] += (uint64_t)__popcll(__ballot(mine));  // lanes running a unit
 #endif
@@ -2703,8 +2757,13 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
 #if defined(HG_PARSE_PROF_SB)
     // the sub-block unit's phases (slots 8..13: header, sig loop, greater1/2,
     // signs + remainders + record, sig bins, -), the wave's time: one lane per run
-    if (live)
+    if (live) {
         for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long *)&g_prof_lanes[8 + k], (unsigned long long)L.psb[k]);
+        if (blockIdx.x < (unsigned)kWaveRecCap)  // and per wave (records 3 and 4 of the wave's breakdown)
+            for (int k = 0; k < 6; ++k)
+                atomicAdd((unsigned long long *)&g_ctu_t[kWaveRec + (3 + k / 3) * kWaveRecCap + blockIdx.x][k % 3],
+                          (unsigned long long)L.psb[k]);
+    }
 #endif
     // per wave (the CTU-time slots, unused by this kernel): s_memrealtime at its start, its
     // duration and place, then the passes and its first three pictures (16 bits each; 0xffff: none)
@@ -2723,6 +2782,20 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
                                      ((uint64_t)((hwid & 0xffffu) | ((xcc & 0xfu) << 16)) << 32);
             g_ctu_t[blockIdx.x][2] = (pf[1] & 0xffffu) | ((uint64_t)(p0 & 0xffffu) << 16) |
                                      ((uint64_t)(p1 & 0xffffu) << 32) | ((uint64_t)(p2 & 0xffffu) << 48);
+            // the wave's own breakdown (tools/wave_times.py): s_memtime cycles of the
+            // wave, per unit kind group (pf[2..6]), of the pass starts, the lanes x
+            // units / 4, and the passes that ran each unit kind (16 bits each)
+            if (blockIdx.x < (unsigned)kWaveRecCap) {
+                uint64_t *r = &g_ctu_t[kWaveRec + blockIdx.x][0];
+                uint64_t *r2 = &g_ctu_t[kWaveRec + kWaveRecCap + blockIdx.x][0];
+                uint64_t *r3 = &g_ctu_t[kWaveRec + 2 * kWaveRecCap + blockIdx.x][0];
+                r[0] = pf[0], r[1] = pf[2], r[2] = pf[3];
+                r2[0] = pf[4], r2[1] = pf[5], r2[2] = pf[6];
+                r3[0] = pw;
+                r3[1] = (uint64_t)kc[0] | ((uint64_t)kc[1] << 16) | ((uint64_t)kc[2] << 32) | ((uint64_t)kc[3] << 48);
+                r3[2] = (uint64_t)kc[4] | ((uint64_t)kc[5] << 16) | ((uint64_t)kc[6] << 32) |
+                        (std::min<uint64_t>(pf[7] >> 2, 0xffffu) << 48);
+            }
         }
     }
 #endif
@@ -2944,7 +3017,16 @@ extern "C" int heifgpu_debug_counters(uint64_t *out, int n) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_prof_lanes), zero, sizeof(zero)) != hipSuccess) return -1;
 #if defined(HG_PARSE_PROF_SB)
     for (int k = 0; k < n && k < 16; ++k) out[k] = tmp[k];
-    return n < 16 ? n : 16;
+    if (n <= 16) return n;
+    // slots 16 on: g_ctu_t as in the prof build (the per-wave records), then zeroed
+    {
+        const size_t m = std::min((size_t)(n - 16), (size_t)hg::kCtuTimeCap * 3);
+        if (hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(hg::g_ctu_t), m * sizeof(uint64_t)) != hipSuccess) return -1;
+        std::vector<uint64_t> z((size_t)hg::kCtuTimeCap * 3, 0);
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_ctu_t), z.data(), z.size() * sizeof(uint64_t)) != hipSuccess)
+            return -1;
+        return (int)(16 + m);
+    }
 #endif
     for (int k = 0; k < n && k < 8; ++k) out[k] = tmp[k];
     if (n <= 8) return 8;

@@ -27,6 +27,11 @@ from heif_amd import _lib  # noqa: E402
 from heif_amd.synthetic import permutation, permuted_heic  # noqa: E402
 
 
+# parse_lanes.hip kWaveRec / kWaveRecCap: the records of each wave's own breakdown
+WAVE_REC, WAVE_REC_CAP = 4096, 4096
+KINDS = ["ctu", "cqt", "cu", "tt", "tb", "sb", "ctu_end"]
+
+
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 128
     ppw = int(sys.argv[3]) if len(sys.argv) > 3 else 0
@@ -39,7 +44,9 @@ def main():
     geom = batch.parse_geometry()
     waves = geom["workgroups"]
     lib = _lib.lib
-    m = 8 + 3 * waves
+    sb = "profsb" in str(_lib.LIB_PATH)  # `make prof-sb`: 16 counter slots, the sub-block phases per wave
+    o = 16 if sb else 8
+    m = o + 3 * (WAVE_REC + 5 * WAVE_REC_CAP)
     buf = (ctypes.c_uint64 * m)()
     ctx.set_timing(True)
     batch.decode_async(outs)
@@ -62,12 +69,25 @@ def main():
 
     rec = []
     for w in range(waves):
-        t0, x1, x = buf[8 + 3 * w], buf[9 + 3 * w], buf[10 + 3 * w]
+        t0, x1, x = buf[o + 3 * w], buf[o + 1 + 3 * w], buf[o + 2 + 3 * w]
         dur, place = x1 & 0xffffffff, x1 >> 32
         pics = [p for p in ((x >> s) & 0xffff for s in (16, 32, 48)) if p != 0xffff]
         hw = place & 0xffff
         rec.append({"t0": t0, "dur": dur / 1e5, "passes": x & 0xffff, "tiles": [src_tile(p) for p in pics],
                     "simd": (place >> 16 & 0xf, hw >> 13 & 7, hw >> 12 & 1, hw >> 8 & 15, hw >> 4 & 3)})
+    for w, r in enumerate(rec):
+        if w >= WAVE_REC_CAP:
+            break
+        b = [buf[o + 3 * (WAVE_REC + j * WAVE_REC_CAP + w) + i] for j in range(5) for i in range(3)]
+        if b[0] == 0:
+            continue
+        kc = [(b[7] >> s) & 0xffff for s in (0, 16, 32, 48)] + [(b[8] >> s) & 0xffff for s in (0, 16, 32)]
+        r["cycles"] = {"wave": b[0], "ctu": b[1], "tree": b[2], "tb": b[3], "sb": b[4], "ctu_end": b[5],
+                       "pass_start": b[6]}
+        r["kind_passes"] = dict(zip(KINDS, kc))
+        r["lane_units"] = 4 * (b[8] >> 48)
+        if sb:  # header, sig loop, greater1/2, signs + remainders + record (cycles, one lane per run), sig bins
+            r["sb_phases"] = dict(zip(["head", "sig", "g1g2", "rest", "sig_bins"], b[9:14]))
     base = min(r["t0"] for r in rec)
     for r in rec:
         r["end"] = (r["t0"] - base) / 1e5 + r["dur"]
@@ -102,12 +122,31 @@ def main():
             max(ws) - min(ws) for ws in simds.values() if len(ws) == 2).most_common(8))),
         "simd_pairs_top": [{"pair": [list(t) for t in k], "simds": c} for k, c in
                            sorted(pairs.items(), key=lambda kv: -kv[1])[:40]],
+        # the 8 waves ending last and 8 around the median: their own s_memtime
+        # breakdown (cycles per unit kind group, pass starts) and the passes that
+        # ran each unit kind, i.e. the cycles per run of each kind
+        "slowest": [breakdown(r) for r in sorted(rec, key=lambda r: -r["end"])[:8] if "cycles" in r],
+        "median": [breakdown(r) for r in sorted(rec, key=lambda r: r["end"])[len(rec) // 2 - 4:len(rec) // 2 + 4]
+                   if "cycles" in r],
         "note": "s_memrealtime 100 MHz; tiles = source tiles of the wave's pictures (dealing order)",
     }
     print(json.dumps({k: res[k] for k in ("wave_end_ms", "passes", "parse_ms_hip_events", "waves_per_simd",
                                           "simd_pair_offsets")}))
     if len(sys.argv) > 2:
         pathlib.Path(sys.argv[2]).write_text(json.dumps(res, indent=1) + "\n")
+
+
+def breakdown(r):
+    c, kp = r["cycles"], r["kind_passes"]
+    runs = {"ctu": kp["ctu"], "tree": kp["cqt"] + kp["cu"] + kp["tt"], "tb": kp["tb"], "sb": kp["sb"],
+            "ctu_end": kp["ctu_end"]}
+    return {"tiles": r["tiles"], "end_ms": round(r["end"], 3), "passes": r["passes"],
+            "share": {k: round(v / max(c["wave"], 1), 3) for k, v in c.items() if k != "wave"},
+            "cycles_per_pass": round(c["wave"] / max(r["passes"], 1)), "kind_passes": kp,
+            "cycles_per_run": {k: round(c[k] / max(n, 1)) for k, n in runs.items()},
+            "lanes_per_pass": round(r["lane_units"] / max(r["passes"], 1), 2),
+            **({"sb_phase_cycles_per_run": {k: round(v / max(kp["sb"], 1)) for k, v in r["sb_phases"].items()}}
+               if "sb_phases" in r else {})}
 
 
 if __name__ == "__main__":
