@@ -352,8 +352,10 @@ def end_to_end(H, ctx, files, outs0, n_batches, threads, stream, info) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # (the round-end driver's K / W; the timed region holds the pipeline's fill and
+    # drain, about 40 ms at 128 images, so K moves ms_per_step: 68.4 at 10, 66.5 at 20)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
