@@ -118,6 +118,9 @@ __device__ __forceinline__ int zidx(int bx, int by) {  // bits of bx, by interle
     };
     return spread(bx) | (spread(by) << 1);
 }
+// (r06 A/B: as one expression of bitwise ands / ors with the z-index always
+// formed, k_intra VALU +0.45 G for SALU -0.2 G, the step not better: the early
+// returns stay)
 __device__ __forceinline__ bool nb_avail(int zc, int xl, int yl, int bx0, int by0, int csl) {
     const int lx = xl - bx0, ly = yl - by0;
     if (ly < 0) return true;
@@ -129,6 +132,8 @@ __device__ __forceinline__ bool nb_avail(int zc, int xl, int yl, int bx0, int by
 // ref[k] of 8.4.4.2.6 read in place: the main-side neighbour for k >= 0, the
 // projected side-side neighbour for k < 0 (only reached when
 // (nTbS * intraPredAngle) >> 5 < -1, exactly where the spec extends ref)
+// (r06 A/B: as an element index from one base, an integer select before one
+// load: VALU +0.18 G with the two rows below, the step -0.3 %; not taken)
 __device__ __forceinline__ const int16_t *ang_ref(const int16_t *main_, const int16_t *side, int inv, int k) {
     return k >= 0 ? main_ + k : side + ((k * inv + 128) >> 8);
 }
@@ -425,20 +430,15 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
     int val[3] = {0, 0, 0};
     uint64_t msk[3] = {0, 0, 0};
     for (int k = 0; k < nch; ++k) {
+        // (as the one-chunk path: positions and the source by selects)
         const int s = lane + 64 * k;
-        int xn, yn;
-        if (s < 2 * n) {
-            xn = x0 - 1;
-            yn = y0 + 2 * n - 1 - s;
-        } else if (s == 2 * n) {
-            xn = x0 - 1;
-            yn = y0 - 1;
-        } else {
-            xn = x0 + s - 2 * n - 1;
-            yn = y0 - 1;
-        }
-        bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH && nb_avail(zc, xn << subx, yn << suby, bx0, by0, csl);
-        val[k] = av ? w.fetch(xn, yn) : 0;
+        const int xn = s <= 2 * n ? x0 - 1 : x0 + s - 2 * n - 1;
+        const int yn = s < 2 * n ? y0 + 2 * n - 1 - s : y0 - 1;
+        const bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
+                        nb_avail(zc, xn << subx, yn << suby, bx0, by0, csl);
+        const int lx = xn - w.cx0, ly = yn - w.cy0;
+        const Pel *src = ly < 0 ? w.above + lx + 1 : (lx < 0 ? w.left + ly : w.cur + ly * w.csx + lx);
+        val[k] = av ? (int)*src : 0;
         msk[k] = __ballot(av);
     }
     // 2. substitution: nearest available predecessor in search order, else the first available
@@ -471,13 +471,9 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         const int v0 = __shfl(val[0], sl, 64), v1 = __shfl(val[1], sl, 64);
         const int v2 = nch > 2 ? __shfl(val[2], sl, 64) : 0;
         const int v = !any ? (1 << (bd - 1)) : (sc == 0 ? v0 : (sc == 1 ? v1 : v2));
-        if (s < 2 * n) L->left[2 * n - s] = (int16_t)v;
-        else if (s == 2 * n) {
-            L->left[0] = (int16_t)v;
-            L->top[0] = (int16_t)v;
-        } else if (s < ns) {
-            L->top[s - 2 * n] = (int16_t)v;
-        }
+        int16_t *dp = s < 2 * n ? L->left + (2 * n - s) : L->top + (s - 2 * n);
+        if (s < ns) *dp = (int16_t)v;
+        if (s == 2 * n) L->left[0] = (int16_t)v;
     }
     }
 #endif
@@ -489,25 +485,21 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
             const int c = L->left[0];
             const bool bi = strong && cidx == 0 && n == 32 && abs(c + L->top[64] - 2 * L->top[32]) < (1 << (bd - 5)) &&
                             abs(c + L->left[64] - 2 * L->left[32]) < (1 << (bd - 5));
+            // (selects, not a lane-dependent if / else chain: one exec-mask region
+            // per arm cost more scalar instructions than the arithmetic)
+            const int corner = (L->left[1] + 2 * c + L->top[1] + 2) >> 2;
             for (int i = lane; i <= 2 * n; i += kWave) {
                 int a, b;
-                if (bi) {
-                    if (i == 0) a = b = c;
-                    else if (i == 64) {
-                        a = L->left[64];
-                        b = L->top[64];
-                    } else {
-                        a = ((64 - i) * c + i * L->left[64] + 32) >> 6;
-                        b = ((64 - i) * c + i * L->top[64] + 32) >> 6;
-                    }
-                } else if (i == 0) {
-                    a = b = (L->left[1] + 2 * c + L->top[1] + 2) >> 2;
-                } else if (i == 2 * n) {
-                    a = L->left[i];
-                    b = L->top[i];
+                if (bi) {  // (uniform; i == 0 and i == 64 are the interpolation's end points)
+                    a = ((64 - i) * c + i * L->left[64] + 32) >> 6;
+                    b = ((64 - i) * c + i * L->top[64] + 32) >> 6;
                 } else {
-                    a = (L->left[i + 1] + 2 * L->left[i] + L->left[i - 1] + 2) >> 2;
-                    b = (L->top[i + 1] + 2 * L->top[i] + L->top[i - 1] + 2) >> 2;
+                    const int im = i > 0 ? i - 1 : 0, ip = i < 2 * n ? i + 1 : i;
+                    const int li = L->left[i], ti = L->top[i];
+                    a = (L->left[ip] + 2 * li + L->left[im] + 2) >> 2;
+                    b = (L->top[ip] + 2 * ti + L->top[im] + 2) >> 2;
+                    a = i == 0 ? corner : (i == 2 * n ? li : a);
+                    b = i == 0 ? corner : (i == 2 * n ? ti : b);
                 }
                 L->fl[i] = (int16_t)a;
                 L->ft[i] = (int16_t)b;
@@ -540,20 +532,31 @@ __device__ __attribute__((always_inline)) inline void predict_tb(IntraScratch *L
         } else if (mode == 1) {
             pv = dc;
             if (cidx == 0 && n < 32) {
-                if (x == 0 && y == 0) pv = (lf[1] + 2 * dc + tp[1] + 2) >> 2;
-                else if (y == 0) pv = (tp[1 + x] + 3 * dc + 2) >> 2;
-                else if (x == 0) pv = (lf[1 + y] + 3 * dc + 2) >> 2;
+                // the DC edge filter as selects over both reference reads (the
+                // lane-dependent if / else chain cost an exec-mask region per arm)
+                const int t = tp[1 + x], l = lf[1 + y];
+                const int e = (x == 0 ? l : t) + (x == 0 && y == 0 ? t : dc) + 2 * dc + 2;
+                pv = (x == 0 || y == 0) ? e >> 2 : dc;
             }
         } else {
             const int ang = (int)(int8_t)(am & 0xffu), inv = (int)(int16_t)(am >> 16);  // (tb_angle)
             const int16_t *main_ = mode >= 18 ? tp : lf, *side = mode >= 18 ? lf : tp;
             const int a = mode >= 18 ? x : y, b = mode >= 18 ? y : x;  // a along the main direction
             const int idx = ((b + 1) * ang) >> 5, fact = ((b + 1) * ang) & 31;
-            const int p0 = *ang_ref(main_, side, inv, a + idx + 1);
-            pv = fact ? ((32 - fact) * p0 + fact * *ang_ref(main_, side, inv, a + idx + 2) + 16) >> 5 : p0;
+            // both references read unconditionally (the second index is at most
+            // 2n + 1, inside the 66-entry arrays): with iFact 0 the weighted sum
+            // is the first reference exactly, so no lane-dependent branch
+            const int p0 = *ang_ref(main_, side, inv, a + idx + 1), p1 = *ang_ref(main_, side, inv, a + idx + 2);
+            pv = ((32 - fact) * p0 + fact * p1 + 16) >> 5;
             if (cidx == 0 && n < 32) {
-                if (mode == 26 && x == 0) pv = min(max(tp[1] + ((lf[1 + y] - lf[0]) >> 1), 0), maxv);
-                if (mode == 10 && y == 0) pv = min(max(lf[1] + ((tp[1 + x] - tp[0]) >> 1), 0), maxv);
+                if (mode == 26) {
+                    const int v = min(max(tp[1] + ((lf[1 + y] - lf[0]) >> 1), 0), maxv);
+                    pv = x == 0 ? v : pv;
+                }
+                if (mode == 10) {
+                    const int v = min(max(lf[1] + ((tp[1 + x] - tp[0]) >> 1), 0), maxv);
+                    pv = y == 0 ? v : pv;
+                }
             }
         }
         const int li = (ly0 + y) * w.csx + lx0 + x;
@@ -622,20 +625,14 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
     for (int k = 0; k < 2; ++k) {
         if (k >= nch) break;
         const int s = sl + 32 * k;
-        int xn, yn;
-        if (s < 2 * n) {
-            xn = x0 - 1;
-            yn = y0 + 2 * n - 1 - s;
-        } else if (s == 2 * n) {
-            xn = x0 - 1;
-            yn = y0 - 1;
-        } else {
-            xn = x0 + s - 2 * n - 1;
-            yn = y0 - 1;
-        }
+        // (positions and the source by selects, as predict_tb's one-chunk path)
+        const int xn = s <= 2 * n ? x0 - 1 : x0 + s - 2 * n - 1;
+        const int yn = s < 2 * n ? y0 + 2 * n - 1 - s : y0 - 1;
         const bool av = s < ns && xn >= 0 && yn >= 0 && xn < PW && yn < PH &&
                         nb_avail(zc, xn << 1, yn << 1, bx0, by0, csl);
-        const int vk = av ? w.fetch(xn, yn) : 0;
+        const int lx = xn - w.cx0, ly = yn - w.cy0;
+        const Pel *srcp = ly < 0 ? w.above + lx + 1 : (lx < 0 ? w.left + ly : w.cur + ly * w.csx + lx);
+        const int vk = av ? (int)*srcp : 0;
         const uint32_t hk = (uint32_t)(__ballot(av) >> (32 * h));
         if (k == 0) {
             val0 = vk;
@@ -668,13 +665,9 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
         const int v0 = __shfl(val0, 32 * h + src, 64);
         const int v1 = nch > 1 ? __shfl(val1, 32 * h + src, 64) : 0;
         const int v = !any ? (1 << (bd - 1)) : (sc == 0 ? v0 : v1);
-        if (s < 2 * n) left[2 * n - s] = (int16_t)v;
-        else if (s == 2 * n) {
-            left[0] = (int16_t)v;
-            top[0] = (int16_t)v;
-        } else if (s < ns) {
-            top[s - 2 * n] = (int16_t)v;
-        }
+        int16_t *dp = s < 2 * n ? left + (2 * n - s) : top + (s - 2 * n);
+        if (s < ns) *dp = (int16_t)v;
+        if (s == 2 * n) left[0] = (int16_t)v;
     }
     wave_sync();
     const int16_t *lf = left, *tp = top;
@@ -701,8 +694,9 @@ __device__ __attribute__((always_inline)) inline void predict_pair(IntraScratch 
             } else {
                 const int a = mode >= 18 ? x : y, b = mode >= 18 ? y : x;
                 const int idx = ((b + 1) * ang) >> 5, fact = ((b + 1) * ang) & 31;
-                const int p0 = *ang_ref(main_, side, inv, a + idx + 1);
-                pv = fact ? ((32 - fact) * p0 + fact * *ang_ref(main_, side, inv, a + idx + 2) + 16) >> 5 : p0;
+                // (both references unconditionally, as predict_tb: index <= 2n + 1 inside the half's 33)
+                const int p0 = *ang_ref(main_, side, inv, a + idx + 1), p1 = *ang_ref(main_, side, inv, a + idx + 2);
+                pv = ((32 - fact) * p0 + fact * p1 + 16) >> 5;
             }
             if (pcm) pv = 0;  // the residual is the PCM sample itself
             if (cbf) pv += it ? r1 : r0;
