@@ -257,10 +257,19 @@ __device__ __forceinline__ void transform_mfma(const int16_t *dT, int sn, int lo
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = (acc[i] << 8) + corr + rnd;
     acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(gl, b2, acc, 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    // rows y = (i & 3) + 8 (i >> 2) + 4h: all inside a 32x32 TB; inside a 16x16
+    // one exactly for i < 8, with the columns r < 16 (one lane-dependent region
+    // instead of a compare and an exec-mask region per store)
+    auto out = [&](int i) {
         const int y = (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (y < n && r < n) dst[y * pitch + r] = (int16_t)min(max(acc[i] >> bd2, -32768), 32767);
+        dst[y * pitch + r] = (int16_t)min(max(acc[i] >> bd2, -32768), 32767);
+    };
+    if (n == 32) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) out(i);
+    } else if (r < n) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) out(i);
     }
 }
 #endif
