@@ -1,6 +1,6 @@
-# r06: a library change against the HEAD build (libheifgpu_base.so): GPU suite on the new build, same-box
+# A library change against the HEAD build (libheifgpu_base.so): GPU suite on the new build, same-box
 # bench pairs at 128 images (and one image), and one SQ instruction-mix pass per kernel for both builds.
-# usage: bash tools/r06/ab_lib.sh <name> [extra ab.sh specs...]
+# usage: bash tools/ab_lib.sh <name> [extra ab.sh specs...]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"

@@ -1,4 +1,4 @@
-# r06 closing lines on the final code, after profiles/r06/ holds this round's counter files: the default
+# Closing lines on the final code, after profiles/<round>/ holds this round's counter files: the default
 # bench (config 4, with roofline.traffic and issue), one image, config 5 (cpu_baseline, traffic, issue),
 # the config-5 tile split at world 1 (per-rank parse, chain floor), the distinct-tile control, the GPU
 # suite and smoke()

@@ -2,7 +2,7 @@
 batch parsed by the spread engine (scalar unit), one by the lanes engine
 (vector unit), decoded alone and side by side.  Prints wall ms per decode.
 
-usage: python tools/r06/concurrent.py [n_spread n_lanes lanes_ppw] ...
+usage: python tools/mixed_parse.py [n_spread n_lanes lanes_ppw] ...
 """
 import pathlib
 import sys
