@@ -3005,37 +3005,57 @@ hipError_t launch_parse(const BatchArgs &a0, hipStream_t s) {
 
 }  // namespace hg
 
+#if !defined(HG_HOST_EMU) && defined(HG_PARSE_PROF)
+namespace hg {
+namespace {
+// this translation unit's counters (g_prof_lanes, g_ctu_t) copied out and zeroed
+int prof_read(uint64_t *out, int n) {
+    uint64_t tmp[16] = {};
+    if (hipMemcpyFromSymbol(tmp, HIP_SYMBOL(hg::g_prof_lanes), sizeof(tmp)) != hipSuccess) return -1;
+    const uint64_t zero[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_prof_lanes), zero, sizeof(zero)) != hipSuccess) return -1;
+#if defined(HG_PARSE_PROF_SB)
+    const int head = 16;  // slots 16 on: g_ctu_t as in the prof build (the per-wave records)
+#else
+    const int head = 8;   // slots 8 on: the per-CTU times (3 per CTU) and the per-wave records
+#endif
+    for (int k = 0; k < n && k < head; ++k) out[k] = tmp[k];
+    if (n <= head) return n < head ? n : head;
+    const size_t m = std::min((size_t)(n - head), (size_t)hg::kCtuTimeCap * 3);
+    if (hipMemcpyFromSymbol(out + head, HIP_SYMBOL(hg::g_ctu_t), m * sizeof(uint64_t)) != hipSuccess) return -1;
+    std::vector<uint64_t> z((size_t)hg::kCtuTimeCap * 3, 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_ctu_t), z.data(), z.size() * sizeof(uint64_t)) != hipSuccess) return -1;
+    return (int)(head + m);
+}
+}  // namespace
+}  // namespace hg
+// The library builds the solo / spread kernels as a translation unit of their
+// own (parse_solo.hip), whose device globals are a code object's own: their
+// counters are read through this entry and added in heifgpu_debug_counters
+#if defined(HG_PARSE_TU)
+extern "C" int hg_debug_counters_solo(uint64_t *out, int n);
+#if HG_PARSE_TU == 2
+extern "C" int hg_debug_counters_solo(uint64_t *out, int n) { return hg::prof_read(out, n); }
+#endif
+#endif
+#endif
+
 #if !defined(HG_HOST_EMU) && HG_PARSE_WANT_LANES
 // Tuning hook (include/heifgpu.h): copies out and zeroes k_parse_lanes'
 // per-wave s_memtime counters.  Returns the number of counters written, or 0
 // for the product library (counters compiled out; `make prof` has them).
 extern "C" int heifgpu_debug_counters(uint64_t *out, int n) {
 #if defined(HG_PARSE_PROF)
-    uint64_t tmp[16] = {};
-    if (hipMemcpyFromSymbol(tmp, HIP_SYMBOL(hg::g_prof_lanes), sizeof(tmp)) != hipSuccess) return -1;
-    const uint64_t zero[16] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_prof_lanes), zero, sizeof(zero)) != hipSuccess) return -1;
-#if defined(HG_PARSE_PROF_SB)
-    for (int k = 0; k < n && k < 16; ++k) out[k] = tmp[k];
-    if (n <= 16) return n;
-    // slots 16 on: g_ctu_t as in the prof build (the per-wave records), then zeroed
-    {
-        const size_t m = std::min((size_t)(n - 16), (size_t)hg::kCtuTimeCap * 3);
-        if (hipMemcpyFromSymbol(out + 16, HIP_SYMBOL(hg::g_ctu_t), m * sizeof(uint64_t)) != hipSuccess) return -1;
-        std::vector<uint64_t> z((size_t)hg::kCtuTimeCap * 3, 0);
-        if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_ctu_t), z.data(), z.size() * sizeof(uint64_t)) != hipSuccess)
-            return -1;
-        return (int)(16 + m);
+    const int r = hg::prof_read(out, n);
+#if defined(HG_PARSE_TU)
+    if (r > 0) {  // (one of the two kinds of kernel ran; the other's slots are zero)
+        std::vector<uint64_t> o2((size_t)r, 0);
+        const int r2 = hg_debug_counters_solo(o2.data(), r);
+        if (r2 < 0) return -1;
+        for (int k = 0; k < r2 && k < r; ++k) out[k] += o2[(size_t)k];
     }
 #endif
-    for (int k = 0; k < n && k < 8; ++k) out[k] = tmp[k];
-    if (n <= 8) return 8;
-    // slots 8 on: the per-CTU times (3 per CTU), then zeroed
-    const size_t m = std::min((size_t)(n - 8), (size_t)hg::kCtuTimeCap * 3);
-    if (hipMemcpyFromSymbol(out + 8, HIP_SYMBOL(hg::g_ctu_t), m * sizeof(uint64_t)) != hipSuccess) return -1;
-    std::vector<uint64_t> z((size_t)hg::kCtuTimeCap * 3, 0);
-    if (hipMemcpyToSymbol(HIP_SYMBOL(hg::g_ctu_t), z.data(), z.size() * sizeof(uint64_t)) != hipSuccess) return -1;
-    return (int)(8 + m);
+    return r;
 #else
     (void)out;
     (void)n;
