@@ -632,7 +632,7 @@ int heifgpu_batch_prepare_ex(heifgpu_ctx *ctx, const heifgpu_image *const *imgs,
         if (b->set[k].pending) HIP_TRY(hipStreamWaitEvent(ctx->upload, b->set[k].parsed, 0));
     if (G.pending) HIP_TRY(hipStreamWaitEvent(ctx->upload, G.done, 0));
     std::vector<uint32_t> order;
-    const int mode = parse_mode_for(int(mode_req), int(hb.pics.size()));
+    const int mode = parse_mode_for(int(mode_req), int(hb.pics.size()), hb.pics.data());
     const int solo_waves = solo_waves_for(hb.lane_rows);
     int parse_group = 1;
     if (mode == PARSE_SPREAD) {

@@ -72,7 +72,7 @@ int main(int argc, char **argv) {
     a.rbsp = rbsp.data();
     a.rsubs = rsubs.data();
     std::vector<uint32_t> order;
-    const int mode = parse_mode_for(PARSE_AUTO, int(hb.pics.size()));
+    const int mode = parse_mode_for(PARSE_AUTO, int(hb.pics.size()), hb.pics.data());
     const int solo_waves = solo_waves_for(hb.lane_rows);
     int parse_group = 1;
     if (mode == PARSE_SPREAD) spread_parse_order(hb.pics.data(), int(hb.pics.size()), order);

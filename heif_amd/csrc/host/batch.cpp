@@ -255,9 +255,42 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                 PicDesc pd{};
                 pd.bits_off = hb.bits_size;
                 pd.sub_first = uint32_t(hb.subs.size());
-                if (su.nseg > 1) {
-                    // a slice of several segments: their slice data back to back, one
-                    // substream-table entry per CTB row (SUB_* flags, desc.hpp)
+                std::vector<uint32_t> mids;  // data offsets of dependent segments starting inside a row
+                if (su.nseg > 1 && !ps.pps.entropy_coding_sync_enabled_flag) {
+                    // a slice of several segments without WPP: their slice data back
+                    // to back, one substream-table entry per CTB row for the CTU at its
+                    // start (a segment starting there: its data; otherwise the engine
+                    // runs on, SUB_CONTINUE), SUB_SEG_END on a row whose last CTU ends a
+                    // segment, and the data of each dependent segment starting inside a
+                    // row after the end entry (their count in PicDesc.flags, PD_NMID_SHIFT; the parse switches to the
+                    // next one where end_of_slice_segment_flag ends a segment inside a row)
+                    std::vector<uint32_t> seg_off, seg_addr;
+                    uint32_t off = 0;
+                    for (size_t j = su.seg; j < su.seg + su.nseg; ++j) {
+                        const SliceSeg &g = tj.segs[j];
+                        const uint32_t d0 = g.sh.slice_data_raw_offset;
+                        uint32_t d1 = uint32_t(g.payload_len);
+                        while (d1 >= d0 + 3 && g.payload[d1 - 1] == 3 && g.payload[d1 - 2] == 0 && g.payload[d1 - 3] == 0)
+                            d1 -= 3;  // (cabac_zero_words: see the WPP path below)
+                        hb.pieces.push_back({g.payload + d0, d1 - d0, hb.bits_size + off});
+                        seg_off.push_back(off);
+                        seg_addr.push_back(g.sh.slice_segment_address);
+                        if (j > su.seg && g.sh.slice_segment_address % uint32_t(pw)) mids.push_back(off);
+                        off += d1 - d0;
+                    }
+                    size_t cov = 0;  // the segment holding the row's first CTU
+                    for (int r = su.y0; r < su.y1; ++r) {
+                        const uint32_t a0 = uint32_t(r * pw), a1 = uint32_t((r + 1) * pw);
+                        while (cov + 1 < seg_addr.size() && seg_addr[cov + 1] <= a0) ++cov;
+                        uint32_t v = seg_addr[cov] == a0 ? seg_off[cov] : (seg_off[cov] | SUB_CONTINUE);
+                        if (std::find(seg_addr.begin() + 1, seg_addr.end(), a1) != seg_addr.end()) v |= SUB_SEG_END;
+                        hb.subs.push_back(v);
+                    }
+                    pd.bits_len = off;
+                    pd.n_sub = uint32_t(su.y1 - su.y0);
+                } else if (su.nseg > 1) {
+                    // a slice of several segments with WPP: their slice data back to back,
+                    // one substream-table entry per CTB row (SUB_* flags, desc.hpp)
                     const bool wpp = ps.pps.entropy_coding_sync_enabled_flag;
                     uint32_t off = 0;
                     for (size_t j = su.seg; j < su.seg + su.nseg; ++j) {
@@ -297,6 +330,9 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                     for (size_t k = 0; k + 1 < starts.size(); ++k) hb.subs.push_back(starts[k]);
                 }
                 hb.subs.push_back(pd.bits_len);
+                for (uint32_t m : mids) hb.subs.push_back(m);
+                if (mids.size() > PD_NMID_MAX) throw UnsupportedError("over 32767 slice segments starting inside CTB rows");
+                pd.flags |= uint32_t(mids.size()) << PD_NMID_SHIFT;
                 hb.bits_size = (hb.bits_size + pd.bits_len + 63) & ~size_t(63);
                 const int hctb = (sq.height + (1 << sq.log2_ctb) - 1) >> sq.log2_ctb;
                 if ((sq.flags & SP_WPP) && int(pd.n_sub) != hctb)

@@ -75,7 +75,11 @@ void check_segments(TileJob &job, const ParamSet &ps) {
                 throw UnsupportedError("several slice segments together with HEVC tiles filtered across tiles");
             continue;
         }
-        if (sh.slice_segment_address % pw) throw UnsupportedError("a slice segment starting inside a CTB row");
+        // a dependent segment inside a row of a picture without WPP continues its
+        // slice's one substream: the parse switches to its data there (batch.cpp)
+        if (sh.slice_segment_address % pw &&
+            (!sh.dependent_slice_segment_flag || pps.entropy_coding_sync_enabled_flag))
+            throw UnsupportedError("a slice segment starting inside a CTB row");
         if (sh.dependent_slice_segment_flag) continue;  // the loop-filter rules below are per slice
         size_t second = 1;  // the second slice
         while (job.segs[second].sh.dependent_slice_segment_flag) ++second;

@@ -126,7 +126,9 @@ struct StreamKnobs {
 StreamKnobs stream_knobs_from_env();
 bool intra_stream_for(int parse_mode, int n_pics, bool has_assembly, const StreamKnobs &k);
 // the parse mode a batch of n_pics pictures runs in (requested: PARSE_*)
-int parse_mode_for(int requested, int n_pics);
+// (pics: the batch's pictures; one with dependent slice segments starting inside a
+// CTB row (PicDesc.flags, PD_NMID_SHIFT) makes it a lanes parse: only that engine takes them)
+int parse_mode_for(int requested, int n_pics, const PicDesc *pics = nullptr);
 // spread mode's wave slots (row << 20 | picture); -1 if the batch exceeds the encoding
 int spread_parse_order(const PicDesc *pics, int n, std::vector<uint32_t> &order);
 int solo_waves_for(int lane_rows);

@@ -187,7 +187,15 @@ enum : uint32_t {
     F_STOP = 1u << 12,
     F_PCM = 1u << 13,     // the TB being recorded is a PCM block
     F_REINIT = 1u << 14,  // solo modes: engine re-initialisation at byte L.reinit before the next unit
+    // bits 16-31: the dependent segments started inside a row so far (kMsegOne
+    // each; in fl, not a register of its own: the lanes parse sits at its VGPR floor)
 };
+constexpr uint32_t kMsegShift = 16, kMsegOne = 1u << kMsegShift;
+// Lane.status bit, never reported (unit_ctu clears it): a dependent slice
+// segment starts at the next CTU, inside the row (lanes_nmid).  Carried in
+// status, which the CTU end's error branch writes anyway: set in fl there, the
+// flag cost the lanes parse 16 VGPRs of allocation (160 -> 176)
+constexpr uint32_t ST_SEGSW = 1u << 30;
 
 struct Lane {
     // arithmetic decoder (9.3.4.3): ivlOffset carried with k look-ahead bits,
@@ -1168,8 +1176,26 @@ HG_HD inline bool wpp_ready(const Lane &L, const LanePic &P, const Env &E) {
 
 // RBSP offset (absolute) at which a lane about to run U_CTU starts its
 // substream (engine and context initialisation, unit_ctu), or ~0u
+// dependent slice segments starting inside a CTB row of picture P (PicDesc.flags)
+HG_HD inline uint32_t lanes_nmid(const LanePic &P) { return (P.flags >> PD_NMID_SHIFT) & PD_NMID_MAX; }
+
+// (Mid: the lanes engine, which takes dependent segments starting inside a
+// row; the scalar engines do not, parse_mode_for gives such batches the lanes parse)
+template <bool Mid>
 HG_HD inline uint32_t substream_start(const Lane &L, const LanePic &P, const BatchArgs &a) {
-    if (L.c != 0) return ~0u;
+    if (L.c != 0) {
+        if constexpr (Mid) {
+            if (L.status & ST_SEGSW) {
+                // a dependent segment starting inside the row (no WPP: one substream,
+                // its row entries, the end entry, then these); past the picture's
+                // list (a corrupt stream, flagged by unit_ctu): the RBSP end
+                const uint32_t m = L.fl >> kMsegShift;
+                return P.bits_off +
+                       (a.rsubs[P.sub_first + (uint32_t)P.hctb + (m < lanes_nmid(P) ? 1u + m : 0u)] & SUB_OFFSET);
+            }
+        }
+        return ~0u;
+    }
     if ((L.fl & F_WPP) || L.row == 0)
         return P.bits_off + (a.rsubs[P.sub_first + ((L.fl & F_WPP) ? L.row : 0)] & SUB_OFFSET);
     if (P.flags & SP_ROW_SEGMENTS) {  // no WPP: a dependent slice segment may start at this row
@@ -1201,12 +1227,14 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
     if (!wpp_ready<EG>(L, P, E)) return;
     L.ctbx = L.c << P.log2ctb;
     L.ctby = L.row << P.log2ctb;
-    const uint32_t start = substream_start(L, P, *E.a);
+    const uint32_t start = substream_start<!EG::kSolo>(L, P, *E.a);
     if (start != ~0u) {
         // substream start: contexts (init; the WPP copy already in ld.ctx; or, a
         // dependent slice segment without WPP, the previous segment's final
-        // state, which the lane still holds: 9.3.2.4) + engine
-        const bool init = L.row == 0 || ((L.fl & F_WPP) && P.wctb < 2);
+        // state, which the lane still holds: 9.3.2.4) + engine.  A dependent
+        // segment starting inside a row (ST_SEGSW) keeps the contexts and qPY_PREV
+        const bool segsw = !EG::kSolo && (L.status & ST_SEGSW) != 0;
+        const bool init = !segsw && (L.row == 0 || ((L.fl & F_WPP) && P.wctb < 2));
         const bool wpp_copy = !init && (L.fl & F_WPP);
         if constexpr (EG::kCtxReg) {
 #if !defined(HG_HOST_EMU)
@@ -1239,7 +1267,13 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
             for (int k = 0; k < CTX_PAD / 4; ++k) dst[k] = EG::kSpread ? load_agent(src + k) : src[k];
         }
         engine_init(L, G, start, P.bits_end);
-        if (L.row == 0) L.fl |= F_FIRST_QG;
+        if (segsw) {
+            L.status &= ~ST_SEGSW;
+            if ((L.fl >> kMsegShift) >= lanes_nmid(P)) L.status |= ST_SUBSTREAM_END;  // no such segment
+            L.fl += kMsegOne;
+        } else if (L.row == 0) {
+            L.fl |= F_FIRST_QG;
+        }
     }
     if (P.saoL || P.saoC) {
         int ml = 0, mu = 0;
@@ -2155,7 +2189,14 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     const bool seg_end = !last_in_pic && L.c == P.wctb - 1 && (P.flags & SP_ROW_SEGMENTS) &&
                          (E.a->rsubs[P.sub_first + L.row] & SUB_SEG_END);
     const bool eos = (last_in_pic && !(P.flags & SP_SUBSET_END)) || seg_end;
-    if (term(L, G) != (eos ? 1 : 0)) L.status |= ST_SUBSTREAM_END;
+    // inside a row of a picture with dependent segments starting inside rows
+    // (no WPP), end_of_slice_segment_flag = 1 ends one: the next starts at the next CTU
+    if (term(L, G) != (eos ? 1 : 0)) {
+        // end_of_slice_segment_flag = 1 inside a row without WPP: a dependent
+        // segment starts at the next CTU (unit_ctu checks that the picture has one)
+        if constexpr (EG::kSolo) L.status |= ST_SUBSTREAM_END;
+        else L.status |= (!eos && !(L.fl & F_WPP) && L.c < P.wctb - 1) ? ST_SEGSW : (uint32_t)ST_SUBSTREAM_END;
+    }
     if (!eos && (last_in_pic || ((L.fl & F_WPP) && L.c == P.wctb - 1)) && !term(L, G)) L.status |= ST_SUBSTREAM_END;
     if (L.budget + L.k < 0) L.status |= ST_OVERRUN;  // read past the NAL unit
     ++L.c;
@@ -2193,7 +2234,9 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
         L.st = U_CTU;
         return;
     }
-    if (L.status) atomicOr(&E.a->status[P.pic], L.status);
+    // (ST_SEGSW: never reported; the scalar engines never set it)
+    const uint32_t st_rep = EG::kSolo ? L.status : (L.status & ~ST_SEGSW);
+    if (st_rep) atomicOr(&E.a->status[P.pic], st_rep);
     L.st = U_DONE;
 }
 
@@ -2227,6 +2270,9 @@ HG_HD inline bool ctu_ready(const Lane &L, const LanePic &P, const Env &E) { ret
 
 // lane setup: picture constants, outputs, first state.  Returns false for an idle lane.
 // `cap` lanes (waves, solo mode) at most per picture.
+// (Mid: the lanes engine, which keeps the picture's count of segment starts
+// inside rows in P.flags; the scalar engines do not take such pictures)
+template <bool Mid = true>
 HG_HD inline bool pic_init(LanePic &P, const BatchArgs &a, int pic, int lane0, int cap) {
     const PicDesc &pd = a.pics[pic];
     if (pd.flags & PD_ASSEMBLY) return false;  // no coded data of its own
@@ -2267,7 +2313,8 @@ HG_HD inline bool pic_init(LanePic &P, const BatchArgs &a, int pic, int lane0, i
     P.w8 = (sp.width + 7) >> 3;
     P.saoL = pd.sao_luma;
     P.saoC = pd.sao_chroma;
-    P.flags = sp.flags | (a.xntu ? PF_COHERENT : 0u);
+    // (bits 16-30: the picture's segment starts inside rows, PicDesc.flags; lanes_nmid)
+    P.flags = sp.flags | (a.xntu ? PF_COHERENT : 0u) | (Mid ? pd.flags & (PD_NMID_MAX << PD_NMID_SHIFT) : 0u);
     P.bits_off = (uint32_t)pd.bits_off;
     P.bits_end = (uint32_t)pd.bits_off + a.rsubs[pd.sub_first + pd.n_sub];  // RBSP end (k_rbsp)
     P.sub_first = pd.sub_first;
@@ -2291,7 +2338,7 @@ HG_HD inline void lane_start(Lane &L, const LanePic &P, LaneLds &ld, int row) {
     L.k = 8;
     L.ai = L.bv = L.fp = 0;
     L.lb = 0;
-    L.fl = (P.flags & SP_WPP) ? F_WPP : 0u;
+    L.fl = (P.flags & SP_WPP) ? F_WPP : 0u;  // (no segment started inside a row yet: bits 16-31)
     L.row = row;
     L.c = 0;
     L.qp_prev_last = P.sliceQp;
@@ -2299,9 +2346,10 @@ HG_HD inline void lane_start(Lane &L, const LanePic &P, LaneLds &ld, int row) {
     L.st = U_CTU;
 }
 
+template <bool Mid = true>
 HG_HD inline bool lane_init(Lane &L, LanePic &P, LaneLds &ld, const BatchArgs &a, int pic, int row, int lane0,
                             int cap) {
-    if (!pic_init(P, a, pic, lane0, cap) || row >= P.R) return false;
+    if (!pic_init<Mid>(P, a, pic, lane0, cap) || row >= P.R) return false;
     lane_start(L, P, ld, row);
     return true;
 }
@@ -2410,7 +2458,10 @@ int lanes_parse_order(const PicDesc *pics, int n, int lane_rows, int ppw_force, 
 // / 11,135; distinct tiles at 32 images 7,683 / 7,768.  So batches up to 1536
 // pictures (32 such images) take spread mode.  HEIFGPU_PARSE=lanes|solo|spread
 // forces a mode for every batch, HEIFGPU_SOLO_MAX_PICS moves the switch-over.
-int parse_mode_for(int requested, int n_pics) {
+int parse_mode_for(int requested, int n_pics, const PicDesc *pics) {
+    if (pics)
+        for (int i = 0; i < n_pics; ++i)
+            if (pics[i].flags >> PD_NMID_SHIFT) return PARSE_LANES;
     static const int env = [] {
         const char *e = std::getenv("HEIFGPU_PARSE");
         if (!e) return PARSE_AUTO;
@@ -2538,7 +2589,7 @@ void emu_parse_lanes(const BatchArgs &a) {
                 for (int l = 0; l < 64; ++l)
                     if (lanes[l].st != U_DONE) {
                         lanes[l].status |= ST_SUBSTREAM_END;
-                        atomicOr(&a.status[pics[l / a.lane_rows].pic], lanes[l].status);
+                        atomicOr(&a.status[pics[l / a.lane_rows].pic], lanes[l].status & ~ST_SEGSW);
                         lanes[l].st = U_DONE;
                     }
                 break;
@@ -2581,7 +2632,7 @@ void emu_parse_solo(const BatchArgs &a) {
         const int pic = a.pic0 + (int)(Spread ? (ent & 0xfffffu) : ent);
         for (int w = 0; w < NW; ++w) {
             prog[w] = 0;
-            if (!lane_init(lanes[(size_t)w], P, lds[(size_t)w], a, pic, w, 0, Spread ? (1 << 20) : NW))
+            if (!lane_init<false>(lanes[(size_t)w], P, lds[(size_t)w], a, pic, w, 0, Spread ? (1 << 20) : NW))
                 lanes[(size_t)w].st = U_DONE;
             wins[(size_t)w].w = &wbuf[(size_t)w * 192];
             wins[(size_t)w].f = &wbuf[(size_t)w * 192 + 128];
@@ -2601,7 +2652,7 @@ void emu_parse_solo(const BatchArgs &a) {
                 if (L.st == U_CTU && !ctu_ready<EG>(L, P, E)) continue;
                 progressed = true;
                 SoloWin &sw = wins[(size_t)w];
-                const uint32_t start = L.st == U_CTU ? substream_start(L, P, a) : ~0u;
+                const uint32_t start = L.st == U_CTU ? substream_start<false>(L, P, a) : ~0u;
                 if (start != ~0u) sw.restart(a.rbsp, start, lim, 0);
                 else sw.advance(a.rbsp, L.lb, lim, 0);
                 const EG G{lds[(size_t)w].ctx, 0u, 0u, seq, a.rbsp, lim, sw.view(), 0u, 0u, 0u};
@@ -2745,7 +2796,7 @@ __global__ void __launch_bounds__(64) HG_PARSE_ATTR k_parse_lanes(BatchArgs a) {
         if (!progressed || pass > (1u << 30)) {  // every live lane waits: cannot happen (the top row never waits)
             if (L.st != U_DONE) {
                 L.status |= ST_SUBSTREAM_END;
-                atomicOr(&a.status[P.pic], L.status);
+                atomicOr(&a.status[P.pic], L.status & ~ST_SEGSW);
             }
             break;
         }
@@ -2856,7 +2907,7 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
     Lane L;
     LaneLds &ld = s_lds[w < NW ? w : 0];
     LanePic &P = s_pic[0];
-    const bool live = in && w < NW && lane_init(L, P, ld, a, pic, row, 0, Spread ? (1 << 20) : NW);  // every lane alike
+    const bool live = in && w < NW && lane_init<false>(L, P, ld, a, pic, row, 0, Spread ? (1 << 20) : NW);  // every lane alike
     if (!live) L.st = U_DONE;
 #if defined(HG_PARSE_PROF_SB)
     for (int k = 0; k < 6; ++k) L.psb[k] = 0;
@@ -2893,7 +2944,7 @@ __global__ void __launch_bounds__(Spread ? 64 : 64 * kSoloMaxWaves) k_parse_solo
             if (run && lane == 0) g_ctu_t[tix][1] = now;
         }
 #endif
-        uint32_t start = run && st == U_CTU ? substream_start(L, P, a) : ~0u;
+        uint32_t start = run && st == U_CTU ? substream_start<false>(L, P, a) : ~0u;
         const uint32_t rd = L.lb;
         st = __builtin_amdgcn_readfirstlane(st);
         if (st == U_DONE) break;

@@ -64,7 +64,7 @@ void emu_rbsp(const BatchArgs &a) {
             else out[o++] = raw[i];
         }
         removed_before[len] = r;
-        for (uint32_t s = 0; s <= pd.n_sub; ++s) {
+        for (uint32_t s = 0; s <= pd.n_sub + (pd.flags >> PD_NMID_SHIFT); ++s) {
             const uint32_t e = a.subs[pd.sub_first + s] & SUB_OFFSET, fl = a.subs[pd.sub_first + s] & ~SUB_OFFSET;
             a.rsubs[pd.sub_first + s] = (e < len ? e - removed_before[e] : len - r) | fl;
         }
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(64) k_rbsp(BatchArgs a) {
     const uint8_t *raw = a.bits + pd.bits_off;
     uint8_t *out = a.rbsp + pd.bits_off;
     const uint32_t len = pd.bits_len;
-    const uint32_t nent = pd.n_sub + 1;
+    const uint32_t nent = pd.n_sub + 1 + (pd.flags >> PD_NMID_SHIFT);  // (segment starts inside rows after the end entry)
     const uint32_t *subs = a.subs + pd.sub_first;
     uint32_t *rsubs = a.rsubs + pd.sub_first;
     uint32_t run = 0;  // bytes removed before this step

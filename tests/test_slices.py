@@ -20,9 +20,12 @@ GPU: each slice of such a picture is decoded as its own picture
 segment ends or, without WPP, where the engine runs on); when every slice is
 filtered across its upper boundary (one set of deblocking values) the slices
 are children of an assembly picture filtered whole (desc.hpp PD_ASSEMBLY).
-Segments starting inside a CTB row, filtering across some slice boundaries
-only and segments starting inside an HEVC tile are HEIFGPU_E_UNSUPPORTED;
-slices of whole tiles decode as one sub-picture per tile.
+A dependent segment starting inside a CTB row of a picture without WPP is
+decoded in place (PicDesc.n_mid: the slice's one substream switches to its
+data after end_of_slice_segment_flag); independent slices starting inside a
+row, such segments with WPP, filtering across some slice boundaries only and
+segments starting inside an HEVC tile are HEIFGPU_E_UNSUPPORTED; slices of
+whole tiles decode as one sub-picture per tile.
 """
 import os
 import subprocess
@@ -76,6 +79,16 @@ DEP_CASES = [
     ("dep_crop_10b_dbk", dict(width=200, height=120, conf_right=6, conf_bottom=2, bit_depth=10, slice_ctus=14,
                               slice_dependent=1, wpp=1, slice_dbk_vary=1)),
     ("dep_alt_across", dict(width=128, height=192, slice_ctus=4, slice_dependent=2, wpp=1, slice_lf_across=1)),
+    # dependent segments starting inside CTB rows, no WPP (the slice's one
+    # substream switches to the next segment's data after end_of_slice_segment_flag;
+    # the lanes engine only: parse_mode_for makes such a batch a lanes parse
+    # whatever mode is asked, so the solo / spread cases below run lanes too)
+    ("dep_mid_nowpp", dict(slice_ctus=5, slice_dependent=1)),
+    ("dep_mid_1ctu_10b", dict(slice_ctus=1, slice_dependent=1, bit_depth=10)),
+    ("dep_mid_ctb16_pcm", dict(log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2, slice_ctus=7, slice_dependent=1,
+                               pcm=1, pcm_pct=20, pcm_log2_max=4)),
+    ("dep_mid_c444_across", dict(chroma_format=3, width=160, height=96, slice_ctus=3, slice_dependent=1,
+                                 slice_lf_across=1)),
 ]
 
 
@@ -175,7 +188,8 @@ def test_synth_writes_segments():
 
 @pytest.mark.parametrize("over,why", [
     (dict(slice_ctus=5), "a slice segment starting inside a CTB row"),
-    (dict(slice_ctus=6, slice_dependent=1), "a slice segment starting inside a CTB row"),
+    (dict(slice_ctus=6, slice_dependent=1, wpp=1), "a slice segment starting inside a CTB row"),
+    (dict(slice_ctus=5, slice_dependent=2), "a slice segment starting inside a CTB row"),
     (dict(slice_ctus=4, slice_lf_across=2), "slices filtered across some slice boundaries only"),
     (dict(slice_ctus=4, slice_lf_across=1, slice_dbk_vary=1), "with different deblocking values"),
     (dict(slice_ctus=8, tile_cols=2, tile_rows=1), "several slice segments together with HEVC tiles"),
@@ -228,7 +242,9 @@ def emu_check():
 @pytest.mark.parametrize("name,across", [("rows2_wpp_dbk", 0), ("crop_10b_wpp", 0), ("ctb16_rows2", 0),
                                          ("ctb16_rows2", 1), ("mono_rows", 1), ("dep_all_nowpp", 0),
                                          ("dep_alt_wpp", 0), ("dep_alt_nowpp_ctb16_pcm", 0),
-                                         ("dep_alt_across", 1), ("c422_rows_wpp", 1), ("c444_rows_10b", 0)])
+                                         ("dep_alt_across", 1), ("c422_rows_wpp", 1), ("c444_rows_10b", 0),
+                                         ("dep_mid_nowpp", 0), ("dep_mid_1ctu_10b", 1), ("dep_mid_ctb16_pcm", 0),
+                                         ("dep_mid_c444_across", 1)])
 def test_emulated_kernels_slices(emu_check, tmp_path, name, across, parse):
     """The kernels' source compiled for the host decodes a picture of row
     slices (one picture per slice, its dependent segments back to back;
