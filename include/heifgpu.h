@@ -90,7 +90,8 @@ typedef struct {
      * (src/heic/decoder.rs:98-119 decodes them one by one). */
     uint32_t tile_stride, tile_offset;
     /* CABAC parse mode: HEIFGPU_PARSE_AUTO picks by batch
-     * size (spread up to 1536 pictures, lanes above);
+     * size (spread up to 1536 pictures, lanes above; lanes whatever is asked
+     * for a batch with dependent slice segments starting inside a CTB row);
      * HEIFGPU_PARSE_LANES packs one substream per lane (throughput);
      * HEIFGPU_PARSE_SOLO runs one substream per wavefront, a picture's rows in
      * one workgroup; HEIFGPU_PARSE_SPREAD one substream per wavefront, every
