@@ -104,9 +104,10 @@ struct PicDesc {
 enum : uint32_t {
     PD_CHILD = 1u << 0,
     PD_ASSEMBLY = 1u << 1,
-    // bits 16-30: SP_ROW_SEGMENTS without WPP, the dependent slice segments starting
-    // inside a CTB row (their data offsets follow the end entry of the substream
-    // table; in flags, so PicDesc and the parse's LanePic keep their layout)
+    // bits 16-30: SP_ROW_SEGMENTS, the dependent slice segments starting inside a
+    // CTB row (their data offsets follow the end entry of the substream table, then
+    // with WPP one count per row of those starting in earlier rows; in flags, so
+    // PicDesc and the parse's LanePic keep their layout)
     PD_NMID_SHIFT = 16,
     PD_NMID_MAX = 0x7fffu,
 };

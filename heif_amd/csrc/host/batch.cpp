@@ -256,6 +256,7 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                 pd.bits_off = hb.bits_size;
                 pd.sub_first = uint32_t(hb.subs.size());
                 std::vector<uint32_t> mids;  // data offsets of dependent segments starting inside a row
+                std::vector<uint32_t> mid_prefix;  // WPP: per row, the mids starting in earlier rows
                 if (su.nseg > 1 && !ps.pps.entropy_coding_sync_enabled_flag) {
                     // a slice of several segments without WPP: their slice data back
                     // to back, one substream-table entry per CTB row for the CTU at its
@@ -290,10 +291,15 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                     pd.n_sub = uint32_t(su.y1 - su.y0);
                 } else if (su.nseg > 1) {
                     // a slice of several segments with WPP: their slice data back to back,
-                    // one substream-table entry per CTB row (SUB_* flags, desc.hpp)
-                    const bool wpp = ps.pps.entropy_coding_sync_enabled_flag;
+                    // one substream-table entry per CTB row (SUB_* flags, desc.hpp): the
+                    // data, or the entry point, of the segment holding the row's first
+                    // CTU.  Dependent segments starting inside a row: their data after
+                    // the end entry as without WPP, then per row the count of those
+                    // starting in earlier rows (where the row's lane starts counting)
                     uint32_t off = 0;
-                    for (size_t j = su.seg; j < su.seg + su.nseg; ++j) {
+                    std::vector<int> mid_rows;
+                    const size_t jend = su.seg + su.nseg;
+                    for (size_t j = su.seg; j < jend; ++j) {
                         const SliceSeg &g = tj.segs[j];
                         const uint32_t d0 = g.sh.slice_data_raw_offset;
                         uint32_t d1 = uint32_t(g.payload_len);
@@ -302,20 +308,38 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                         while (d1 >= d0 + 3 && g.payload[d1 - 1] == 3 && g.payload[d1 - 2] == 0 && g.payload[d1 - 3] == 0)
                             d1 -= 3;
                         hb.pieces.push_back({g.payload + d0, d1 - d0, hb.bits_size + off});
-                        const int r0 = int(g.sh.slice_segment_address) / pw;
-                        const int r1 = j + 1 < su.seg + su.nseg ? int(tj.segs[j + 1].sh.slice_segment_address) / pw
-                                                                : su.y1;
+                        const int a0 = int(g.sh.slice_segment_address);
+                        const int a1 = j + 1 < jend ? int(tj.segs[j + 1].sh.slice_segment_address) : su.y1 * pw;
+                        const int r0 = a0 / pw;
+                        if (j > su.seg && a0 % pw) {
+                            mids.push_back(off);
+                            mid_rows.push_back(r0);
+                        }
                         uint32_t e = off;  // the row's substream start within the concatenation
-                        for (int r = r0; r < r1; ++r) {
-                            if (wpp && r > r0) e += g.sh.entry_point_offset[size_t(r - r0 - 1)];
-                            uint32_t v = (wpp || r == r0) ? e : (off | SUB_CONTINUE);
-                            if (r + 1 == r1 && j + 1 < su.seg + su.nseg) v |= SUB_SEG_END;
+                        // the rows whose first CTU the segment holds: r * pw in [a0, a1)
+                        for (int r = r0; r * pw < a1; ++r) {
+                            if (r > r0) {
+                                if (size_t(r - r0 - 1) >= g.sh.entry_point_offset.size())
+                                    throw HeifError("WPP slice segment without one entry point per CTB row");
+                                e += g.sh.entry_point_offset[size_t(r - r0 - 1)];
+                            }
+                            if (r * pw < a0) continue;  // starts inside row r0
+                            uint32_t v = e;
+                            if ((r + 1) * pw == a1 && j + 1 < jend) v |= SUB_SEG_END;
                             hb.subs.push_back(v);
                         }
                         off += d1 - d0;
                     }
                     pd.bits_len = off;
                     pd.n_sub = uint32_t(su.y1 - su.y0);
+                    if (hb.subs.size() != pd.sub_first + pd.n_sub) throw HeifError("slice segments out of order");
+                    if (!mids.empty()) {  // after the end entry and the mids (pushed below)
+                        size_t k = 0;
+                        for (int r = su.y0; r < su.y1; ++r) {
+                            while (k < mid_rows.size() && mid_rows[k] < r) ++k;
+                            mid_prefix.push_back(uint32_t(k));
+                        }
+                    }
                 } else if (su.s0 > 0 || su.s1 + 1 < int(starts.size())) {
                     // a substream range alone (it starts after a nonzero byte: no EP state carries in)
                     const uint32_t r0 = starts[size_t(su.s0)], r1 = starts[size_t(su.s1)];
@@ -331,6 +355,7 @@ HostBatch build_batch(const ParsedImage *const *imgs, size_t n, uint32_t tile_st
                 }
                 hb.subs.push_back(pd.bits_len);
                 for (uint32_t m : mids) hb.subs.push_back(m);
+                for (uint32_t m : mid_prefix) hb.subs.push_back(m);  // raw only (k_rbsp remaps up to the mids)
                 if (mids.size() > PD_NMID_MAX) throw UnsupportedError("over 32767 slice segments starting inside CTB rows");
                 pd.flags |= uint32_t(mids.size()) << PD_NMID_SHIFT;
                 hb.bits_size = (hb.bits_size + pd.bits_len + 63) & ~size_t(63);

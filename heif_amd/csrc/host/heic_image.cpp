@@ -75,10 +75,9 @@ void check_segments(TileJob &job, const ParamSet &ps) {
                 throw UnsupportedError("several slice segments together with HEVC tiles filtered across tiles");
             continue;
         }
-        // a dependent segment inside a row of a picture without WPP continues its
-        // slice's one substream: the parse switches to its data there (batch.cpp)
-        if (sh.slice_segment_address % pw &&
-            (!sh.dependent_slice_segment_flag || pps.entropy_coding_sync_enabled_flag))
+        // a dependent segment inside a row continues its slice's substream there
+        // (the row's, with WPP): the parse switches to its data (batch.cpp)
+        if (sh.slice_segment_address % pw && !sh.dependent_slice_segment_flag)
             throw UnsupportedError("a slice segment starting inside a CTB row");
         if (sh.dependent_slice_segment_flag) continue;  // the loop-filter rules below are per slice
         size_t second = 1;  // the second slice
@@ -104,8 +103,9 @@ void check_segments(TileJob &job, const ParamSet &ps) {
         throw HeifError("tiled picture without one entry point per tile (per tile row with WPP)");
     if (pps.entropy_coding_sync_enabled_flag && !pps.tiles_enabled_flag)
         for (size_t k = 0; k < job.segs.size(); ++k) {
+            // the rows the segment's CTUs touch (it may start and end inside rows)
             const uint32_t r0 = job.segs[k].sh.slice_segment_address / pw;
-            const uint32_t r1 = k + 1 < job.segs.size() ? job.segs[k + 1].sh.slice_segment_address / pw
+            const uint32_t r1 = k + 1 < job.segs.size() ? (job.segs[k + 1].sh.slice_segment_address - 1) / pw + 1
                                                         : uint32_t(sps.pic_height_in_ctbs_y());
             if (uint32_t(job.segs[k].sh.num_entry_point_offsets) + 1 != r1 - r0)
                 throw HeifError("WPP slice without one entry point per CTB row");

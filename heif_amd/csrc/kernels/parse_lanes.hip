@@ -1186,8 +1186,8 @@ HG_HD inline uint32_t substream_start(const Lane &L, const LanePic &P, const Bat
     if (L.c != 0) {
         if constexpr (Mid) {
             if (L.status & ST_SEGSW) {
-                // a dependent segment starting inside the row (no WPP: one substream,
-                // its row entries, the end entry, then these); past the picture's
+                // a dependent segment starting inside the row (the picture's row
+                // entries, the end entry, then these); past the picture's
                 // list (a corrupt stream, flagged by unit_ctu): the RBSP end
                 const uint32_t m = L.fl >> kMsegShift;
                 return P.bits_off +
@@ -1271,8 +1271,16 @@ HG_HD inline void unit_ctu(Lane &L, LaneLds &ld, LanePic &P, const Env &E, const
             L.status &= ~ST_SEGSW;
             if ((L.fl >> kMsegShift) >= lanes_nmid(P)) L.status |= ST_SUBSTREAM_END;  // no such segment
             L.fl += kMsegOne;
-        } else if (L.row == 0) {
-            L.fl |= F_FIRST_QG;
+        } else {
+            if (L.row == 0) L.fl |= F_FIRST_QG;
+            if constexpr (!EG::kSolo) {
+                // WPP: this row's lane counts the segments started inside rows from
+                // those of earlier rows (batch.cpp: after the picture's mid list)
+                const uint32_t nm = lanes_nmid(P);
+                if ((L.fl & F_WPP) && nm)
+                    L.fl = (L.fl & (kMsegOne - 1)) |
+                           (E.a->subs[P.sub_first + (uint32_t)P.hctb + 1u + nm + L.row] << kMsegShift);
+            }
         }
     }
     if (P.saoL || P.saoC) {
@@ -2189,13 +2197,13 @@ HG_HD inline void unit_ctu_end(Lane &L, LaneLds &ld, LanePic &P, const Env &E, c
     const bool seg_end = !last_in_pic && L.c == P.wctb - 1 && (P.flags & SP_ROW_SEGMENTS) &&
                          (E.a->rsubs[P.sub_first + L.row] & SUB_SEG_END);
     const bool eos = (last_in_pic && !(P.flags & SP_SUBSET_END)) || seg_end;
-    // inside a row of a picture with dependent segments starting inside rows
-    // (no WPP), end_of_slice_segment_flag = 1 ends one: the next starts at the next CTU
+    // inside a row of a picture with dependent segments starting inside rows,
+    // end_of_slice_segment_flag = 1 ends one: the next starts at the next CTU
     if (term(L, G) != (eos ? 1 : 0)) {
-        // end_of_slice_segment_flag = 1 inside a row without WPP: a dependent
-        // segment starts at the next CTU (unit_ctu checks that the picture has one)
+        // end_of_slice_segment_flag = 1 inside a row: a dependent segment starts
+        // at the next CTU (unit_ctu checks that the picture has one)
         if constexpr (EG::kSolo) L.status |= ST_SUBSTREAM_END;
-        else L.status |= (!eos && !(L.fl & F_WPP) && L.c < P.wctb - 1) ? ST_SEGSW : (uint32_t)ST_SUBSTREAM_END;
+        else L.status |= (!eos && L.c < P.wctb - 1) ? ST_SEGSW : (uint32_t)ST_SUBSTREAM_END;
     }
     if (!eos && (last_in_pic || ((L.fl & F_WPP) && L.c == P.wctb - 1)) && !term(L, G)) L.status |= ST_SUBSTREAM_END;
     if (L.budget + L.k < 0) L.status |= ST_OVERRUN;  // read past the NAL unit

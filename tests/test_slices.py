@@ -89,6 +89,15 @@ DEP_CASES = [
                                pcm=1, pcm_pct=20, pcm_log2_max=4)),
     ("dep_mid_c444_across", dict(chroma_format=3, width=160, height=96, slice_ctus=3, slice_dependent=1,
                                  slice_lf_across=1)),
+    # with WPP: a segment starting inside a row continues that row's substream,
+    # its entry points start the rows below; each row's lane starts counting the
+    # mid-row segments from those of earlier rows (the tall one: 18 CTB rows, so
+    # lanes take a second row of the picture)
+    ("dep_mid_wpp", dict(slice_ctus=3, slice_dependent=1, wpp=1)),
+    ("dep_mid_wpp_10b_dbk", dict(width=200, height=120, conf_right=6, conf_bottom=2, bit_depth=10, slice_ctus=5,
+                                 slice_dependent=1, wpp=1, slice_dbk_vary=1)),
+    ("dep_mid_wpp_ctb16_tall", dict(width=64, height=288, log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2,
+                                    slice_ctus=7, slice_dependent=1, wpp=1)),
 ]
 
 
@@ -188,7 +197,7 @@ def test_synth_writes_segments():
 
 @pytest.mark.parametrize("over,why", [
     (dict(slice_ctus=5), "a slice segment starting inside a CTB row"),
-    (dict(slice_ctus=6, slice_dependent=1, wpp=1), "a slice segment starting inside a CTB row"),
+    (dict(slice_ctus=5, slice_dependent=2, wpp=1), "a slice segment starting inside a CTB row"),
     (dict(slice_ctus=5, slice_dependent=2), "a slice segment starting inside a CTB row"),
     (dict(slice_ctus=4, slice_lf_across=2), "slices filtered across some slice boundaries only"),
     (dict(slice_ctus=4, slice_lf_across=1, slice_dbk_vary=1), "with different deblocking values"),
@@ -244,7 +253,8 @@ def emu_check():
                                          ("dep_alt_wpp", 0), ("dep_alt_nowpp_ctb16_pcm", 0),
                                          ("dep_alt_across", 1), ("c422_rows_wpp", 1), ("c444_rows_10b", 0),
                                          ("dep_mid_nowpp", 0), ("dep_mid_1ctu_10b", 1), ("dep_mid_ctb16_pcm", 0),
-                                         ("dep_mid_c444_across", 1)])
+                                         ("dep_mid_c444_across", 1), ("dep_mid_wpp", 0), ("dep_mid_wpp", 1),
+                                         ("dep_mid_wpp_10b_dbk", 0), ("dep_mid_wpp_ctb16_tall", 0)])
 def test_emulated_kernels_slices(emu_check, tmp_path, name, across, parse):
     """The kernels' source compiled for the host decodes a picture of row
     slices (one picture per slice, its dependent segments back to back;
