@@ -20,12 +20,13 @@ GPU: each slice of such a picture is decoded as its own picture
 segment ends or, without WPP, where the engine runs on); when every slice is
 filtered across its upper boundary (one set of deblocking values) the slices
 are children of an assembly picture filtered whole (desc.hpp PD_ASSEMBLY).
-A dependent segment starting inside a CTB row of a picture without WPP is
-decoded in place (PicDesc.n_mid: the slice's one substream switches to its
-data after end_of_slice_segment_flag); independent slices starting inside a
-row, such segments with WPP, filtering across some slice boundaries only and
-segments starting inside an HEVC tile are HEIFGPU_E_UNSUPPORTED; slices of
-whole tiles decode as one sub-picture per tile.
+A dependent segment starting inside a CTB row is decoded in place (count in
+PicDesc.flags bits 16-30: the substream of its row switches to its data after
+end_of_slice_segment_flag; with WPP each row's lane starts from a per-row
+count of the earlier ones); independent slices starting inside a row,
+filtering across some slice boundaries only and segments starting inside an
+HEVC tile are HEIFGPU_E_UNSUPPORTED; slices of whole tiles decode as one
+sub-picture per tile.
 """
 import os
 import subprocess
@@ -98,6 +99,7 @@ DEP_CASES = [
                                  slice_dependent=1, wpp=1, slice_dbk_vary=1)),
     ("dep_mid_wpp_ctb16_tall", dict(width=64, height=288, log2_ctb=4, log2_max_tb=4, max_th_depth_intra=2,
                                     slice_ctus=7, slice_dependent=1, wpp=1)),
+    ("dep_mid_wpp_c422", dict(chroma_format=2, slice_ctus=6, slice_dependent=1, wpp=1)),
 ]
 
 
@@ -254,7 +256,8 @@ def emu_check():
                                          ("dep_alt_across", 1), ("c422_rows_wpp", 1), ("c444_rows_10b", 0),
                                          ("dep_mid_nowpp", 0), ("dep_mid_1ctu_10b", 1), ("dep_mid_ctb16_pcm", 0),
                                          ("dep_mid_c444_across", 1), ("dep_mid_wpp", 0), ("dep_mid_wpp", 1),
-                                         ("dep_mid_wpp_10b_dbk", 0), ("dep_mid_wpp_ctb16_tall", 0)])
+                                         ("dep_mid_wpp_10b_dbk", 0), ("dep_mid_wpp_ctb16_tall", 0),
+                                         ("dep_mid_wpp_c422", 1)])
 def test_emulated_kernels_slices(emu_check, tmp_path, name, across, parse):
     """The kernels' source compiled for the host decodes a picture of row
     slices (one picture per slice, its dependent segments back to back;
